@@ -1,0 +1,96 @@
+// Shared device helpers for libhiseg (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "hiseg.h"
+
+namespace hiseg {
+
+// bf16 is carried as raw 16-bit storage; arithmetic is always f32.
+struct bf16_t { uint16_t x; };
+
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+// Round-to-nearest-even, NaN kept a NaN (MI355X_MICROARCH.md "Correctness boundaries").
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+template <typename T> struct Elem;
+template <> struct Elem<float> {
+  static constexpr int kChunk = 4;  // elements per 16-B chunk
+  __device__ static __forceinline__ float load(const void* p, long long i) {
+    return reinterpret_cast<const float*>(p)[i];
+  }
+  __device__ static __forceinline__ void store(void* p, long long i, float v) {
+    reinterpret_cast<float*>(p)[i] = v;
+  }
+};
+template <> struct Elem<bf16_t> {
+  static constexpr int kChunk = 8;
+  __device__ static __forceinline__ float load(const void* p, long long i) {
+    return bf2f(reinterpret_cast<const uint16_t*>(p)[i]);
+  }
+  __device__ static __forceinline__ void store(void* p, long long i, float v) {
+    reinterpret_cast<uint16_t*>(p)[i] = f2bf(v);
+  }
+};
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  switch (act) {
+    case HISEG_ACT_RELU: return v > 0.f ? v : 0.f;
+    case HISEG_ACT_SIGMOID: return sigmoidf_(v);
+    case HISEG_ACT_SILU: return v * sigmoidf_(v);
+    default: return v;
+  }
+}
+
+// Unpack a 16-B chunk into f32 values / pack back.
+template <typename T> struct Chunk;
+template <> struct Chunk<float> {
+  static constexpr int N = 4;
+  __device__ static __forceinline__ void unpack(const uint4& c, float* v) {
+    v[0] = __uint_as_float(c.x); v[1] = __uint_as_float(c.y);
+    v[2] = __uint_as_float(c.z); v[3] = __uint_as_float(c.w);
+  }
+  __device__ static __forceinline__ uint4 pack(const float* v) {
+    return make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                      __float_as_uint(v[3]));
+  }
+};
+template <> struct Chunk<bf16_t> {
+  static constexpr int N = 8;
+  __device__ static __forceinline__ void unpack(const uint4& c, float* v) {
+    const uint32_t w[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  __device__ static __forceinline__ uint4 pack(const float* v) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  }
+};
+
+}  // namespace hiseg
+
+// Host-side error plumbing (defined in capi.cpp).
+void hiseg_set_error(const char* fmt, ...);
+int hiseg_check_launch(const char* what);
+
+#define HISEG_REQUIRE(cond, code, ...)  \
+  do {                                  \
+    if (!(cond)) {                      \
+      hiseg_set_error(__VA_ARGS__);     \
+      return (code);                    \
+    }                                   \
+  } while (0)

@@ -1,0 +1,367 @@
+// Implicit-GEMM convolution on CDNA4 MFMA (gfx950).
+//
+// GEMM view (see include/hiseg.h, hiseg_conv2d_fwd):   D[co][px] = sum_k W[co][k] * X[px][k]
+//   rows of the MFMA "A" operand  = output channels (weights, K-contiguous, packed by the host)
+//   cols of the MFMA "B" operand  = output pixels   (gathered on the fly from NHWC activations)
+// With this orientation every lane ends up holding 4 consecutive output channels of one
+// pixel (16x16 accumulator map: col = lane&15, row = 4*(lane>>4)+r), which is what the
+// channel-contiguous NHWC epilogue stores.
+//
+// bf16: v_mfma_f32_16x16x32_bf16 (8 k-values per lane per fragment = one 16-B chunk).
+// f32 : v_mfma_f32_16x16x4_f32 (exact f32, parity mode); a 16-B chunk holds 4 k-values and
+//       is consumed by 4 MFMAs (the k order inside a chunk is permuted identically for both
+//       operands, so the contraction is unchanged).
+//
+// Tiling: one workgroup = 256 threads = 4 waves, output tile BCO x BPX, K block = 8 chunks
+// (64 bf16 / 32 f32).  Both operand tiles are staged through LDS as 128-B rows of 8 chunks,
+// chunk c of row r stored at slot c ^ ((r>>1)&7): conflict-free for the ds_read_b128 lane
+// groups of the fragment reads (MI355X_MICROARCH.md §LDS) and for the row-wise stores.
+// Two LDS stages; the next K block is gathered into registers while the current one feeds
+// the MFMAs (register-staged double buffering, one barrier per K block).
+#include "common.h"
+
+namespace hiseg {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+struct ConvArgs {
+  hiseg_conv2d_desc d;
+  int M;       // GEMM rows
+  int Cin;     // Ca + Cb
+  int nK;      // K blocks
+  int Hs, Ws;  // src-A grid
+};
+
+template <typename T>
+__device__ __forceinline__ void load4(const void* base, long long idx, bool vec, int nvalid,
+                                      float* v) {
+  if (vec) {
+    if constexpr (sizeof(T) == 4) {
+      float4 q = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(base) + idx);
+      v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+    } else {
+      uint2 q = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(base) + idx);
+      v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
+      v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = (e < nvalid) ? Elem<T>::load(base, idx + e) : 0.f;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void store4(void* base, long long idx, bool vec, int nvalid,
+                                       const float* v) {
+  if (vec) {
+    if constexpr (sizeof(T) == 4) {
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(base) + idx) =
+          make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+      uint2 q;
+      q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      q.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(base) + idx) = q;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (e < nvalid) Elem<T>::store(base, idx + e, v[e]);
+  }
+}
+
+__device__ __forceinline__ int swz(int row, int c) { return row * 8 + (c ^ ((row >> 1) & 7)); }
+
+template <typename T, typename TO>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, int px, int co, floatx4 acc) {
+  const hiseg_conv2d_desc& d = a.d;
+  float v[4] = {acc[0], acc[1], acc[2], acc[3]};
+  const int ncol = d.Cout - co;
+  if (ncol <= 0) return;
+  const int nv = ncol < 4 ? ncol : 4;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (e < nv) v[e] = v[e] * d.scale[co + e] + d.shift[co + e];
+  }
+  long long op;  // output pixel index
+  int oc;        // output channel
+  if (d.convT) {
+    const int Cq = d.Cout >> 2;
+    const int q = co / Cq;
+    oc = co - q * Cq;
+    const int x = px % d.Wo;
+    const int t = px / d.Wo;
+    const int y = t % d.Ho;
+    const int n = t / d.Ho;
+    op = ((long long)n * (2 * d.Ho) + 2 * y + (q >> 1)) * (2 * d.Wo) + 2 * x + (q & 1);
+  } else {
+    op = px;
+    oc = co;
+  }
+  if (d.residual) {
+    float r[4];
+    const bool vec = (nv == 4) && ((d.r_cstride | d.r_coff | oc) & 3) == 0;
+    load4<T>(d.residual, op * d.r_cstride + d.r_coff + oc, vec, nv, r);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] += r[e];
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], d.act);
+  if (d.mul) {
+    float m[4];
+    const bool vec = (nv == 4) && ((d.m_cstride | d.m_coff | oc) & 3) == 0;
+    load4<T>(d.mul, op * d.m_cstride + d.m_coff + oc, vec, nv, m);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] *= m[e];
+  }
+  {
+    const bool vec = (nv == 4) && ((d.o_cstride | d.o_coff | oc) & 3) == 0;
+    store4<TO>(d.out, op * d.o_cstride + d.o_coff + oc, vec, nv, v);
+  }
+  if (d.out2) {
+    const bool vec = (nv == 4) && ((d.o2_cstride | d.o2_coff | oc) & 3) == 0;
+    store4<T>(d.out2, op * d.o2_cstride + d.o2_coff + oc, vec, nv, v);
+  }
+}
+
+template <typename T, typename TO, int BCO, int BPX, int WCO, int WPX>
+__global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
+  constexpr int KCH = Chunk<T>::N;
+  constexpr int BK = 8 * KCH;
+  constexpr int TM = BCO / (WCO * 16);
+  constexpr int TN = BPX / (WPX * 16);
+  constexpr int A_CH = (BPX * 8 + 255) / 256;
+  constexpr int W_CH = (BCO * 8 + 255) / 256;
+  constexpr int STAGE = (BCO + BPX) * 8;  // uint4 slots per stage
+  constexpr bool A_FULL = (BPX * 8) % 256 == 0;  // every thread owns A_CH act chunks
+  constexpr bool W_FULL = (BCO * 8) % 256 == 0;
+  static_assert(WCO * WPX == 4, "4 waves");
+  static_assert(TM >= 1 && TN >= 1, "tile");
+
+  extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+
+  const hiseg_conv2d_desc& d = a.d;
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  const int wco = wave / WPX;
+  const int wpx = wave % WPX;
+  const int px0 = blockIdx.x * BPX;
+  const int co0 = blockIdx.y * BCO;
+  const int c = t & 7;  // the chunk this thread stages, every row, every K block
+
+  // ---- per-row pixel decode for the activation gather ----
+  int rn[A_CH], riy[A_CH], rix[A_CH];
+#pragma unroll
+  for (int i = 0; i < A_CH; ++i) {
+    const int r = (t >> 3) + 32 * i;
+    const int m = px0 + r;
+    if ((A_FULL || r < BPX) && m < a.M) {
+      const int ox = m % d.Wo;
+      const int tt = m / d.Wo;
+      const int oy = tt % d.Ho;
+      rn[i] = tt / d.Ho;
+      riy[i] = oy * d.stride - d.pad;
+      rix[i] = ox * d.stride - d.pad;
+    } else {
+      rn[i] = -1; riy[i] = 0; rix[i] = 0;
+    }
+  }
+  // K state of this thread's chunk: k = kb*BK + c*KCH  ->  (ky, kx, ci)
+  int ci, ky, kx;
+  {
+    const int k = c * KCH;
+    const int tap = k / a.Cin;
+    ci = k - tap * a.Cin;
+    ky = tap / d.KW;
+    kx = tap - ky * d.KW;
+  }
+  const int Cin = a.Cin;
+  const int KW = d.KW;
+
+  uint4 ra[A_CH], rw[W_CH];
+#pragma unroll
+  for (int i = 0; i < W_CH; ++i) rw[i] = make_uint4(0u, 0u, 0u, 0u);
+
+  auto gather = [&](int kb) __attribute__((always_inline)) {
+    const bool kvalid = ky < d.KH;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (rn[i] >= 0 && kvalid) {
+        const int iy = riy[i] + ky, ix = rix[i] + kx;
+        if (iy >= 0 && iy < d.H && ix >= 0 && ix < d.W) {
+          if (ci < d.Ca) {
+            const int sy = d.a_up == 2 ? (iy >> 1) : iy;
+            const int sx = d.a_up == 2 ? (ix >> 1) : ix;
+            const long long off = (((long long)rn[i] * a.Hs + sy) * a.Ws + sx) * d.a_cstride + d.a_coff + ci;
+            v = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(d.srcA) + off);
+            if (d.in_scale) {
+              float f[KCH];
+              Chunk<T>::unpack(v, f);
+              const float* s = d.in_scale + (long long)rn[i] * d.Ca + ci;
+#pragma unroll
+              for (int e = 0; e < KCH; ++e) f[e] *= s[e];
+              v = Chunk<T>::pack(f);
+            }
+          } else {
+            const long long off = (((long long)rn[i] * d.H + iy) * d.W + ix) * d.b_cstride + d.b_coff + (ci - d.Ca);
+            v = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(d.srcB) + off);
+          }
+        }
+      }
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < W_CH; ++i) {
+      const int r = (t >> 3) + 32 * i;
+      if (W_FULL || r < BCO) {
+        const long long off = (long long)(co0 + r) * d.K_pad + (long long)kb * BK + c * KCH;
+        rw[i] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(d.weight) + off);
+      }
+    }
+  };
+  auto advance = [&]() __attribute__((always_inline)) {
+    ci += BK;
+    while (ci >= Cin) {
+      ci -= Cin;
+      if (++kx == KW) { kx = 0; ++ky; }
+    }
+  };
+  auto stage_store = [&](int s) __attribute__((always_inline)) {
+    uint4* sm = smem + s * STAGE;
+#pragma unroll
+    for (int i = 0; i < W_CH; ++i) {
+      const int r = (t >> 3) + 32 * i;
+      if (W_FULL || r < BCO) sm[swz(r, c)] = rw[i];
+    }
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int r = (t >> 3) + 32 * i;
+      if (A_FULL || r < BPX) sm[BCO * 8 + swz(r, c)] = ra[i];
+    }
+  };
+
+  floatx4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  gather(0);
+  stage_store(0);
+  __syncthreads();
+
+  const int nK = a.nK;
+  for (int kb = 0; kb < nK; ++kb) {
+    const int cur = kb & 1;
+    if (kb + 1 < nK) {
+      advance();
+      gather(kb + 1);
+    }
+    const uint4* sW = smem + cur * STAGE;
+    const uint4* sX = sW + BCO * 8;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ch = s * 4 + (lane >> 4);
+      uint4 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = sW[swz(wco * TM * 16 + i * 16 + (lane & 15), ch)];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = sX[swz(wpx * TN * 16 + j * 16 + (lane & 15), ch)];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (sizeof(T) == 2) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8_t, af[i]), __builtin_bit_cast(bf16x8_t, bfr[j]),
+                acc[i][j], 0, 0, 0);
+          } else {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[i].x), __uint_as_float(bfr[j].x), acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[i].y), __uint_as_float(bfr[j].y), acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[i].z), __uint_as_float(bfr[j].z), acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[i].w), __uint_as_float(bfr[j].w), acc[i][j], 0, 0, 0);
+          }
+        }
+      }
+    }
+    if (kb + 1 < nK) stage_store(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue ----
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int px = px0 + wpx * TN * 16 + j * 16 + (lane & 15);
+      const int co = co0 + wco * TM * 16 + i * 16 + (lane >> 4) * 4;
+      if (px < a.M) conv_epilogue<T, TO>(a, px, co, acc[i][j]);
+    }
+  }
+}
+
+template <typename T, typename TO, int BCO, int BPX, int WCO, int WPX>
+static int launch_cfg(const ConvArgs& a, hipStream_t s) {
+  dim3 grid((a.M + BPX - 1) / BPX, a.d.Cout_pad / BCO);
+  const size_t lds = 2u * (BCO + BPX) * 8u * 16u;
+  hipLaunchKernelGGL((conv_igemm_kernel<T, TO, BCO, BPX, WCO, WPX>), grid, dim3(256), lds, s, a);
+  return hiseg_check_launch("conv_igemm");
+}
+
+template <typename T, typename TO>
+static int launch_typed(const ConvArgs& a, hipStream_t s) {
+  const int cp = a.d.Cout_pad;
+  if (cp % 128 == 0) return launch_cfg<T, TO, 128, 128, 2, 2>(a, s);
+  if (cp % 64 == 0) return launch_cfg<T, TO, 64, 128, 2, 2>(a, s);
+  if (cp % 32 == 0) return launch_cfg<T, TO, 32, 256, 1, 4>(a, s);
+  return launch_cfg<T, TO, 16, 256, 1, 4>(a, s);
+}
+
+}  // namespace hiseg
+
+using namespace hiseg;
+
+static bool al16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+extern "C" int hiseg_conv2d_fwd(const hiseg_conv2d_desc* d, hiseg_stream_t stream) {
+  HISEG_REQUIRE(d != nullptr, HISEG_ERR_BAD_ARG, "conv2d: null descriptor");
+  HISEG_REQUIRE(d->dtype == HISEG_F32 || d->dtype == HISEG_BF16, HISEG_ERR_BAD_DTYPE, "conv2d: dtype %d", d->dtype);
+  HISEG_REQUIRE(d->out_dtype == HISEG_F32 || d->out_dtype == HISEG_BF16, HISEG_ERR_BAD_DTYPE, "conv2d: out_dtype %d", d->out_dtype);
+  HISEG_REQUIRE(d->srcA && d->weight && d->scale && d->shift && d->out, HISEG_ERR_BAD_ARG, "conv2d: null pointer");
+  HISEG_REQUIRE(d->N > 0 && d->H > 0 && d->W > 0 && d->Ho > 0 && d->Wo > 0, HISEG_ERR_BAD_SHAPE, "conv2d: empty grid");
+  HISEG_REQUIRE(d->KH > 0 && d->KW > 0 && d->stride > 0 && d->pad >= 0, HISEG_ERR_BAD_SHAPE, "conv2d: bad window");
+  HISEG_REQUIRE(d->a_up == 1 || d->a_up == 2, HISEG_ERR_BAD_SHAPE, "conv2d: a_up must be 1 or 2");
+  HISEG_REQUIRE(d->a_up == 1 || (d->H % 2 == 0 && d->W % 2 == 0), HISEG_ERR_BAD_SHAPE, "conv2d: upsampled grid must be even");
+  HISEG_REQUIRE(d->Cb == 0 || d->srcB, HISEG_ERR_BAD_ARG, "conv2d: Cb > 0 needs srcB");
+  HISEG_REQUIRE(d->Cout > 0 && d->Cout_pad >= d->Cout && d->Cout_pad % 16 == 0, HISEG_ERR_BAD_SHAPE,
+                "conv2d: Cout %d Cout_pad %d (must be multiple of 16)", d->Cout, d->Cout_pad);
+  const int kch = d->dtype == HISEG_BF16 ? 8 : 4;
+  const int bk = 8 * kch;
+  const int Cin = d->Ca + d->Cb;
+  HISEG_REQUIRE(d->Ca > 0 && d->Ca % kch == 0 && d->Cb % kch == 0 && d->a_cstride % kch == 0 &&
+                    d->a_coff % kch == 0 && (d->Cb == 0 || (d->b_cstride % kch == 0 && d->b_coff % kch == 0)),
+                HISEG_ERR_BAD_SHAPE, "conv2d: input channels/strides must be multiples of %d", kch);
+  HISEG_REQUIRE(d->K_pad % bk == 0 && d->K_pad >= d->KH * d->KW * Cin, HISEG_ERR_BAD_SHAPE,
+                "conv2d: K_pad %d must be a multiple of %d and >= %d", d->K_pad, bk, d->KH * d->KW * Cin);
+  HISEG_REQUIRE(al16(d->srcA) && al16(d->srcB) && al16(d->weight), HISEG_ERR_BAD_SHAPE, "conv2d: operands must be 16-B aligned");
+  HISEG_REQUIRE(!d->convT || (d->KH == 1 && d->KW == 1 && d->stride == 1 && d->pad == 0 && d->Cout % 16 == 0 &&
+                              d->Ho == d->H && d->Wo == d->W),
+                HISEG_ERR_BAD_SHAPE, "conv2d: convT requires a 1x1 GEMM with Cout = 4*C, C %% 4 == 0");
+  const long long M = (long long)d->N * d->Ho * d->Wo;
+  HISEG_REQUIRE(M < (1ll << 31), HISEG_ERR_BAD_SHAPE, "conv2d: too many pixels");
+  ConvArgs a;
+  a.d = *d;
+  a.M = (int)M;
+  a.Cin = Cin;
+  a.nK = d->K_pad / bk;
+  a.Hs = d->H / d->a_up;
+  a.Ws = d->W / d->a_up;
+  hipStream_t s = (hipStream_t)stream;
+  if (d->dtype == HISEG_BF16) {
+    return d->out_dtype == HISEG_BF16 ? launch_typed<bf16_t, bf16_t>(a, s) : launch_typed<bf16_t, float>(a, s);
+  }
+  return d->out_dtype == HISEG_BF16 ? launch_typed<float, bf16_t>(a, s) : launch_typed<float, float>(a, s);
+}

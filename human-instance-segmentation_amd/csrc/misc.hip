@@ -1,0 +1,556 @@
+// Memory-bound kernels of the hot path (pool, attention gates, depthwise conv, layout and
+// epilogue kernels).  All are vectorised on 16-B chunks of the NHWC channel dimension
+// (cdna_hip_programming.md Guideline 13) and grid-sized for 256 CUs.
+#include <float.h>
+#include "common.h"
+
+namespace hiseg {
+
+static inline unsigned nblocks(long long n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+// ------------------------------------------------------------------ MaxPool2d(2), NHWC
+template <typename T>
+__global__ void __launch_bounds__(256) maxpool2x2_kernel(const void* in, int N, int H, int W, int C, void* out) {
+  constexpr int K = Chunk<T>::N;
+  const int nch = C / K;
+  const int Ho = H / 2, Wo = W / 2;
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long total = (long long)N * Ho * Wo * nch;
+  if (gid >= total) return;
+  const int ch = (int)(gid % nch);
+  long long p = gid / nch;
+  const int x = (int)(p % Wo); p /= Wo;
+  const int y = (int)(p % Ho);
+  const int n = (int)(p / Ho);
+  const uint4* src = reinterpret_cast<const uint4*>(in);
+  float m[K], v[K];
+  for (int e = 0; e < K; ++e) m[e] = -FLT_MAX;
+#pragma unroll
+  for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+    for (int dx = 0; dx < 2; ++dx) {
+      const long long pix = ((long long)n * H + 2 * y + dy) * W + 2 * x + dx;
+      Chunk<T>::unpack(src[pix * nch + ch], v);
+#pragma unroll
+      for (int e = 0; e < K; ++e) m[e] = fmaxf(m[e], v[e]);
+    }
+  reinterpret_cast<uint4*>(out)[gid] = Chunk<T>::pack(m);
+}
+
+// ------------------------------------------------------------------ spatial attention
+// stats[p] = (mean_c x, max_c x); G lanes cooperate on one pixel.
+template <typename T>
+__global__ void __launch_bounds__(256) attn_stats_kernel(const void* x, long long P, int C, float* stats) {
+  constexpr int K = Chunk<T>::N;
+  constexpr int G = 16;
+  const int nch = C / K;
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long pix = gid / G;
+  const int l = (int)(gid % G);
+  float s = 0.f, m = -FLT_MAX, v[K];
+  if (pix < P) {
+    const uint4* src = reinterpret_cast<const uint4*>(x) + pix * nch;
+    for (int ch = l; ch < nch; ch += G) {
+      Chunk<T>::unpack(src[ch], v);
+#pragma unroll
+      for (int e = 0; e < K; ++e) { s += v[e]; m = fmaxf(m, v[e]); }
+    }
+  }
+#pragma unroll
+  for (int off = G / 2; off > 0; off >>= 1) {
+    s += __shfl_xor(s, off, G);
+    m = fmaxf(m, __shfl_xor(m, off, G));
+  }
+  if (pix < P && l == 0) {
+    stats[pix * 2] = s / (float)C;
+    stats[pix * 2 + 1] = m;
+  }
+}
+
+__global__ void __launch_bounds__(256) attn_map_kernel(const float* stats, int N, int H, int W, const float* w, int k,
+                                                       float* att) {
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long total = (long long)N * H * W;
+  if (gid >= total) return;
+  const int x = (int)(gid % W);
+  const long long t = gid / W;
+  const int y = (int)(t % H);
+  const int n = (int)(t / H);
+  const int r = k / 2;
+  float acc = 0.f;
+  for (int c = 0; c < 2; ++c)
+    for (int ky = 0; ky < k; ++ky) {
+      const int yy = y + ky - r;
+      if (yy < 0 || yy >= H) continue;
+      for (int kx = 0; kx < k; ++kx) {
+        const int xx = x + kx - r;
+        if (xx < 0 || xx >= W) continue;
+        acc += w[(c * k + ky) * k + kx] * stats[(((long long)n * H + yy) * W + xx) * 2 + c];
+      }
+    }
+  att[gid] = sigmoidf_(acc);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) pixel_scale_kernel(const void* x, long long P, int C, const float* att, void* out) {
+  constexpr int K = Chunk<T>::N;
+  const int nch = C / K;
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= P * nch) return;
+  const float a = att[gid / nch];
+  float v[K];
+  Chunk<T>::unpack(reinterpret_cast<const uint4*>(x)[gid], v);
+#pragma unroll
+  for (int e = 0; e < K; ++e) v[e] *= a;
+  reinterpret_cast<uint4*>(out)[gid] = Chunk<T>::pack(v);
+}
+
+// ------------------------------------------------------------------ GAP + SE gate
+template <typename T>
+__global__ void __launch_bounds__(256) gap_partial_kernel(const void* x, int HW, int C, int splits, float* partial) {
+  constexpr int K = Chunk<T>::N;
+  extern __shared__ __attribute__((aligned(16))) float red[];
+  const int n = blockIdx.x;
+  const int sp = blockIdx.y;
+  const int nch = C / K;
+  const int p0 = (int)((long long)HW * sp / splits), p1 = (int)((long long)HW * (sp + 1) / splits);
+  const uint4* src = reinterpret_cast<const uint4*>(x) + (long long)n * HW * nch;
+  const int t = threadIdx.x;
+  float* out = partial + ((long long)n * splits + sp) * C;
+  if (nch >= 256) {
+    for (int ch = t; ch < nch; ch += 256) {
+      float a[K], v[K];
+      for (int e = 0; e < K; ++e) a[e] = 0.f;
+      for (int p = p0; p < p1; ++p) {
+        Chunk<T>::unpack(src[(long long)p * nch + ch], v);
+#pragma unroll
+        for (int e = 0; e < K; ++e) a[e] += v[e];
+      }
+      for (int e = 0; e < K; ++e) out[ch * K + e] = a[e];
+    }
+    return;
+  }
+  const int pg = 256 / nch;
+  const int g = t / nch, ch = t % nch;
+  float a[K], v[K];
+  for (int e = 0; e < K; ++e) a[e] = 0.f;
+  if (g < pg) {
+    for (int p = p0 + g; p < p1; p += pg) {
+      Chunk<T>::unpack(src[(long long)p * nch + ch], v);
+#pragma unroll
+      for (int e = 0; e < K; ++e) a[e] += v[e];
+    }
+    for (int e = 0; e < K; ++e) red[(g * nch + ch) * K + e] = a[e];
+  }
+  __syncthreads();
+  for (int c = t; c < C; c += 256) {
+    float s = 0.f;
+    for (int gg = 0; gg < pg; ++gg) s += red[gg * C + c];
+    out[c] = s;
+  }
+}
+
+__global__ void __launch_bounds__(256) se_gate_kernel(const float* partial, int splits, int HW, int C, const float* w1,
+                                                      const float* b1, int Cr, const float* w2, const float* b2, int act,
+                                                      float* gate) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* mean = sm;
+  float* hid = sm + C;
+  const int n = blockIdx.x;
+  const int t = threadIdx.x;
+  for (int c = t; c < C; c += 256) {
+    float s = 0.f;
+    for (int sp = 0; sp < splits; ++sp) s += partial[((long long)n * splits + sp) * C + c];
+    mean[c] = s / (float)HW;
+  }
+  __syncthreads();
+  for (int r = t; r < Cr; r += 256) {
+    float s = b1 ? b1[r] : 0.f;
+    for (int c = 0; c < C; ++c) s += w1[(long long)r * C + c] * mean[c];
+    hid[r] = apply_act(s, act);
+  }
+  __syncthreads();
+  for (int c = t; c < C; c += 256) {
+    float s = b2 ? b2[c] : 0.f;
+    for (int r = 0; r < Cr; ++r) s += w2[(long long)c * Cr + r] * hid[r];
+    gate[(long long)n * C + c] = sigmoidf_(s);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) channel_scale_kernel(const void* x, int N, long long HW, int C, const float* gate,
+                                                            void* out) {
+  constexpr int K = Chunk<T>::N;
+  const int nch = C / K;
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long total = (long long)N * HW * nch;
+  if (gid >= total) return;
+  const int ch = (int)(gid % nch);
+  const long long n = gid / nch / HW;
+  float v[K];
+  Chunk<T>::unpack(reinterpret_cast<const uint4*>(x)[gid], v);
+  const float* g = gate + n * C + ch * K;
+#pragma unroll
+  for (int e = 0; e < K; ++e) v[e] *= g[e];
+  reinterpret_cast<uint4*>(out)[gid] = Chunk<T>::pack(v);
+}
+
+// ------------------------------------------------------------------ depthwise conv + BN + act
+template <typename T>
+__global__ void __launch_bounds__(256) dwconv_kernel(const void* in, int N, int H, int W, int C, int Kk, int stride,
+                                                     const float* w, const float* scale, const float* shift, int act,
+                                                     void* out, int Ho, int Wo) {
+  constexpr int K = Chunk<T>::N;
+  const int nch = C / K;
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long total = (long long)N * Ho * Wo * nch;
+  if (gid >= total) return;
+  const int ch = (int)(gid % nch);
+  long long p = gid / nch;
+  const int x = (int)(p % Wo); p /= Wo;
+  const int y = (int)(p % Ho);
+  const int n = (int)(p / Ho);
+  const int pad = Kk / 2;
+  float acc[K], v[K];
+#pragma unroll
+  for (int e = 0; e < K; ++e) acc[e] = 0.f;
+  const uint4* src = reinterpret_cast<const uint4*>(in);
+  for (int ky = 0; ky < Kk; ++ky) {
+    const int yy = y * stride - pad + ky;
+    if (yy < 0 || yy >= H) continue;
+    for (int kx = 0; kx < Kk; ++kx) {
+      const int xx = x * stride - pad + kx;
+      if (xx < 0 || xx >= W) continue;
+      Chunk<T>::unpack(src[(((long long)n * H + yy) * W + xx) * nch + ch], v);
+      const float* wp = w + (long long)(ky * Kk + kx) * C + ch * K;
+#pragma unroll
+      for (int e = 0; e < K; ++e) acc[e] += wp[e] * v[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < K; ++e) acc[e] = apply_act(acc[e] * scale[ch * K + e] + shift[ch * K + e], act);
+  reinterpret_cast<uint4*>(out)[gid] = Chunk<T>::pack(acc);
+}
+
+// ------------------------------------------------------------------ input prologue
+__device__ __forceinline__ unsigned ord_enc(float f) {
+  const unsigned u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord_dec(unsigned e) {
+  return __uint_as_float((e & 0x80000000u) ? (e & 0x7fffffffu) : ~e);
+}
+
+__global__ void reset_max_kernel(unsigned* buf) { *buf = 0u; }  // encodes below -FLT_MAX
+
+__global__ void __launch_bounds__(256) image_max_kernel(const float* x, long long n, unsigned* buf) {
+  float m = -FLT_MAX;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) m = fmaxf(m, x[i]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(buf, ord_enc(m));
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) input_norm_kernel(const float* x, int B, int C, int H, int W, const unsigned* maxbuf,
+                                                         const float* mean, const float* stdv, void* out, int cpad) {
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long plane = (long long)H * W;
+  if (gid >= (long long)B * plane) return;
+  const long long b = gid / plane, pp = gid % plane;
+  const bool div255 = ord_dec(*maxbuf) > 1.0f;
+  for (int c = 0; c < cpad; ++c) {
+    float v = 0.f;
+    if (c < C) {
+      v = x[(b * C + c) * plane + pp];
+      if (div255) v = __fdiv_rn(v, 255.0f);
+      v = __fdiv_rn(__fsub_rn(v, mean[c]), stdv[c]);
+    }
+    Elem<T>::store(out, gid * cpad + c, v);
+  }
+}
+
+// ------------------------------------------------------------------ hierarchical combine
+template <typename T>
+__global__ void __launch_bounds__(256) hier_combine_kernel(const float* low, int N, int h, int w, const void* tfeat, int Ct,
+                                                           const float* ut_w, const float* ut_scale, const float* ut_shift,
+                                                           int ut_act, const float* u1_w, const float* u1_b,
+                                                           const float* t_w, const float* t_b, float* logits, float* bgfg,
+                                                           float* tn) {
+  __shared__ float s_ut[2 * 32 * 4], s_us[32], s_ush[32], s_u1[64], s_tw[2 * 512];
+  const int t = threadIdx.x;
+  for (int i = t; i < 256; i += 256) s_ut[i] = ut_w[i];
+  if (t < 32) { s_us[t] = ut_scale[t]; s_ush[t] = ut_shift[t]; }
+  if (t < 64) s_u1[t] = u1_w[t];
+  for (int i = t; i < 2 * Ct; i += 256) s_tw[i] = t_w[i];
+  __syncthreads();
+  const int H = 2 * h, W = 2 * w;
+  const long long gid = (long long)blockIdx.x * 256 + t;
+  const long long total = (long long)N * H * W;
+  if (gid >= total) return;
+  const int X = (int)(gid % W);
+  const long long tt = gid / W;
+  const int Y = (int)(tt % H);
+  const int n = (int)(tt / H);
+  const int dy = Y & 1, dx = X & 1;
+  const float* lo = low + (((long long)n * h + (Y >> 1)) * w + (X >> 1)) * 2;
+  const float l0 = lo[0], l1 = lo[1];
+  float b0 = u1_b[0], b1 = u1_b[1];
+  for (int co = 0; co < 32; ++co) {
+    // ConvTranspose2d weight [ci][co][dy][dx]
+    float hsum = l0 * s_ut[((0 * 32 + co) * 2 + dy) * 2 + dx] + l1 * s_ut[((1 * 32 + co) * 2 + dy) * 2 + dx];
+    hsum = apply_act(hsum * s_us[co] + s_ush[co], ut_act);
+    b0 += s_u1[co] * hsum;
+    b1 += s_u1[32 + co] * hsum;
+  }
+  constexpr int K = Chunk<T>::N;
+  float t0 = t_b[0], t1 = t_b[1], v[K];
+  const uint4* tf = reinterpret_cast<const uint4*>(tfeat) + gid * (Ct / K);
+  for (int ch = 0; ch < Ct / K; ++ch) {
+    Chunk<T>::unpack(tf[ch], v);
+#pragma unroll
+    for (int e = 0; e < K; ++e) {
+      t0 += s_tw[ch * K + e] * v[e];
+      t1 += s_tw[Ct + ch * K + e] * v[e];
+    }
+  }
+  const float mx = fmaxf(b0, b1);
+  const float e0 = __expf(b0 - mx), e1 = __expf(b1 - mx);
+  const float pfg = e1 / (e0 + e1);
+  const long long plane = (long long)H * W;
+  const long long pp = (long long)Y * W + X;
+  float* L = logits + (long long)n * 3 * plane + pp;
+  L[0] = b0;
+  L[plane] = b1 + t0 * pfg;
+  L[2 * plane] = b1 + t1 * pfg;
+  if (bgfg) {
+    float* G = bgfg + (long long)n * 2 * plane + pp;
+    G[0] = b0; G[plane] = b1;
+  }
+  if (tn) {
+    float* Tn = tn + (long long)n * 2 * plane + pp;
+    Tn[0] = t0; Tn[plane] = t1;
+  }
+}
+
+// ------------------------------------------------------------------ layout helpers
+template <typename T>
+__global__ void __launch_bounds__(256) nhwc_to_nchw_kernel(const void* in, int N, int H, int W, int C, int cstride, int coff,
+                                                           float* out) {
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long plane = (long long)H * W;
+  const long long total = (long long)N * C * plane;
+  if (gid >= total) return;
+  const long long pp = gid % plane;
+  const long long nc = gid / plane;
+  const int c = (int)(nc % C);
+  const long long n = nc / C;
+  out[gid] = Elem<T>::load(in, (n * plane + pp) * cstride + coff + c);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) nchw_to_nhwc_kernel(const float* in, int N, int C, int H, int W, void* out, int cpad) {
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long plane = (long long)H * W;
+  if (gid >= (long long)N * plane) return;
+  const long long n = gid / plane, pp = gid % plane;
+  for (int c = 0; c < cpad; ++c) Elem<T>::store(out, gid * cpad + c, c < C ? in[(n * C + c) * plane + pp] : 0.f);
+}
+
+// ------------------------------------------------------------------ exported-contract masks
+__device__ __forceinline__ float p_target(const float* L, long long plane) {
+  const float a = L[0], b = L[plane], c = L[2 * plane];
+  const float m = fmaxf(a, fmaxf(b, c));
+  const float ea = __expf(a - m), eb = __expf(b - m), ec = __expf(c - m);
+  return eb / (ea + eb + ec);
+}
+
+__global__ void __launch_bounds__(256) instance_mask_kernel(const float* logits, int N, int mh, int mw, int dil, float* inst) {
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long plane = (long long)mh * mw;
+  if (gid >= (long long)N * plane) return;
+  const long long n = gid / plane, pp = gid % plane;
+  const int y = (int)(pp / mw), x = (int)(pp % mw);
+  const float* L = logits + n * 3 * plane;
+  float l0 = L[pp], l1 = L[plane + pp], l2 = L[2 * plane + pp];
+  if (dil > 0) {
+    const float p1 = p_target(L + pp, plane);
+    float mx = -FLT_MAX;
+    for (int yy = y - dil; yy <= y + dil; ++yy)
+      for (int xx = x - dil; xx <= x + dil; ++xx)
+        if (yy >= 0 && yy < mh && xx >= 0 && xx < mw) mx = fmaxf(mx, p_target(L + (long long)yy * mw + xx, plane));
+    if (mx - p1 > 0.1f) l1 += 2.0f;
+  }
+  // torch.argmax: first index of the maximum
+  int cls = 0;
+  float best = l0;
+  if (l1 > best) { cls = 1; best = l1; }
+  if (l2 > best) { cls = 2; }
+  inst[gid] = cls == 1 ? 1.f : 0.f;
+}
+
+__global__ void __launch_bounds__(256) binary_mask_kernel(const float* u, int cs, long long P, const float* w, const float* b,
+                                                          float* out) {
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= P) return;
+  const float v = u[gid * cs];
+  const float a0 = w[0] * v + b[0], a1 = w[1] * v + b[1];
+  const float m = fmaxf(a0, a1);
+  const float e0 = __expf(a0 - m), e1 = __expf(a1 - m);
+  out[gid] = e0 / (e0 + e1);
+}
+
+}  // namespace hiseg
+
+using namespace hiseg;
+
+#define DISPATCH_T(dtype, KERNEL, ...)                                                        \
+  do {                                                                                        \
+    if ((dtype) == HISEG_BF16) hipLaunchKernelGGL(KERNEL<bf16_t>, __VA_ARGS__);               \
+    else if ((dtype) == HISEG_F32) hipLaunchKernelGGL(KERNEL<float>, __VA_ARGS__);            \
+    else { hiseg_set_error("unsupported dtype %d", (int)(dtype)); return HISEG_ERR_BAD_DTYPE; } \
+  } while (0)
+
+static int chunk_of(int dtype) { return dtype == HISEG_BF16 ? 8 : 4; }
+
+extern "C" int hiseg_maxpool2x2_fwd(int dtype, const void* in, int N, int H, int W, int C, void* out, hiseg_stream_t stream) {
+  HISEG_REQUIRE(in && out && N > 0 && H >= 2 && W >= 2 && C > 0, HISEG_ERR_BAD_SHAPE, "maxpool2x2: bad args");
+  HISEG_REQUIRE(C % chunk_of(dtype) == 0, HISEG_ERR_BAD_SHAPE, "maxpool2x2: C must be chunk aligned");
+  const long long total = (long long)N * (H / 2) * (W / 2) * (C / chunk_of(dtype));
+  DISPATCH_T(dtype, maxpool2x2_kernel, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, in, N, H, W, C, out);
+  return hiseg_check_launch("maxpool2x2");
+}
+
+extern "C" int hiseg_attn_spatial_fwd(int dtype, const void* x, int N, int H, int W, int C, const float* w7, int k,
+                                      float* stats, float* att, void* out, hiseg_stream_t stream) {
+  HISEG_REQUIRE(x && w7 && stats && att && out && N > 0 && H > 0 && W > 0 && C > 0 && (k & 1), HISEG_ERR_BAD_ARG,
+                "attn_spatial: bad args");
+  HISEG_REQUIRE(C % chunk_of(dtype) == 0, HISEG_ERR_BAD_SHAPE, "attn_spatial: C must be chunk aligned");
+  hipStream_t s = (hipStream_t)stream;
+  const long long P = (long long)N * H * W;
+  DISPATCH_T(dtype, attn_stats_kernel, dim3(nblocks(P * 16, 256)), dim3(256), 0, s, x, P, C, stats);
+  hipLaunchKernelGGL(attn_map_kernel, dim3(nblocks(P, 256)), dim3(256), 0, s, stats, N, H, W, w7, k, att);
+  const long long tot = P * (C / chunk_of(dtype));
+  DISPATCH_T(dtype, pixel_scale_kernel, dim3(nblocks(tot, 256)), dim3(256), 0, s, x, P, C, att, out);
+  return hiseg_check_launch("attn_spatial");
+}
+
+extern "C" int hiseg_gap_splits(int HW) {
+  int s = HW / 512;
+  if (s < 1) s = 1;
+  if (s > 64) s = 64;
+  return s;
+}
+
+extern "C" int hiseg_se_gate_fwd(int dtype, const void* x, int N, int HW, int C, const float* w1, const float* b1, int Cr,
+                                 const float* w2, const float* b2, int act, float* partial, float* gate,
+                                 hiseg_stream_t stream) {
+  HISEG_REQUIRE(x && w1 && w2 && partial && gate && N > 0 && HW > 0 && C > 0 && Cr > 0, HISEG_ERR_BAD_ARG,
+                "se_gate: bad args");
+  const int K = chunk_of(dtype);
+  HISEG_REQUIRE(C % K == 0, HISEG_ERR_BAD_SHAPE, "se_gate: C must be chunk aligned");
+  const int nch = C / K;
+  const int splits = hiseg_gap_splits(HW);
+  const size_t lds = nch >= 256 ? 0 : (size_t)(256 / nch) * C * sizeof(float);
+  hipStream_t s = (hipStream_t)stream;
+  DISPATCH_T(dtype, gap_partial_kernel, dim3(N, splits), dim3(256), lds, s, x, HW, C, splits, partial);
+  hipLaunchKernelGGL(se_gate_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, partial, splits, HW, C, w1, b1,
+                     Cr, w2, b2, act, gate);
+  return hiseg_check_launch("se_gate");
+}
+
+extern "C" int hiseg_channel_scale_fwd(int dtype, const void* x, int N, int HW, int C, const float* gate, void* out,
+                                       hiseg_stream_t stream) {
+  HISEG_REQUIRE(x && gate && out && N > 0 && HW > 0 && C % chunk_of(dtype) == 0, HISEG_ERR_BAD_ARG, "channel_scale: bad args");
+  const long long total = (long long)N * HW * (C / chunk_of(dtype));
+  DISPATCH_T(dtype, channel_scale_kernel, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, x, N, (long long)HW,
+             C, gate, out);
+  return hiseg_check_launch("channel_scale");
+}
+
+extern "C" int hiseg_dwconv_fwd(int dtype, const void* in, int N, int H, int W, int C, int K, int stride, const float* w,
+                                const float* scale, const float* shift, int act, void* out, int Ho, int Wo,
+                                hiseg_stream_t stream) {
+  HISEG_REQUIRE(in && w && scale && shift && out && N > 0 && C % chunk_of(dtype) == 0 && (K & 1) && stride >= 1,
+                HISEG_ERR_BAD_ARG, "dwconv: bad args");
+  HISEG_REQUIRE(Ho == (H + 2 * (K / 2) - K) / stride + 1 && Wo == (W + 2 * (K / 2) - K) / stride + 1, HISEG_ERR_BAD_SHAPE,
+                "dwconv: output grid mismatch");
+  const long long total = (long long)N * Ho * Wo * (C / chunk_of(dtype));
+  DISPATCH_T(dtype, dwconv_kernel, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, in, N, H, W, C, K, stride, w,
+             scale, shift, act, out, Ho, Wo);
+  return hiseg_check_launch("dwconv");
+}
+
+extern "C" int hiseg_image_max_fwd(const float* x, long long n, float* maxbuf, hiseg_stream_t stream) {
+  HISEG_REQUIRE(x && maxbuf && n > 0, HISEG_ERR_BAD_ARG, "image_max: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  unsigned* buf = reinterpret_cast<unsigned*>(maxbuf);
+  hipLaunchKernelGGL(reset_max_kernel, dim3(1), dim3(1), 0, s, buf);
+  long long blocks = (n + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(image_max_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, n, buf);
+  return hiseg_check_launch("image_max");
+}
+
+extern "C" int hiseg_input_norm_fwd(int dtype, const float* x, int B, int C, int H, int W, const float* maxbuf,
+                                    const float* mean, const float* stdv, void* out, int cpad, hiseg_stream_t stream) {
+  HISEG_REQUIRE(x && maxbuf && mean && stdv && out && B > 0 && C > 0 && cpad >= C, HISEG_ERR_BAD_ARG, "input_norm: bad args");
+  const long long total = (long long)B * H * W;
+  DISPATCH_T(dtype, input_norm_kernel, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, x, B, C, H, W,
+             reinterpret_cast<const unsigned*>(maxbuf), mean, stdv, out, cpad);
+  return hiseg_check_launch("input_norm");
+}
+
+extern "C" int hiseg_hier_combine_fwd(int dtype, const float* low, int N, int h, int w, const void* tfeat, int Ct,
+                                      const float* ut_w, const float* ut_scale, const float* ut_shift, int ut_act,
+                                      const float* u1_w, const float* u1_b, const float* t_w, const float* t_b, float* logits,
+                                      float* bgfg, float* tn, hiseg_stream_t stream) {
+  HISEG_REQUIRE(low && tfeat && ut_w && ut_scale && ut_shift && u1_w && u1_b && t_w && t_b && logits, HISEG_ERR_BAD_ARG,
+                "hier_combine: null pointer");
+  HISEG_REQUIRE(N >= 0 && h > 0 && w > 0 && Ct > 0 && Ct <= 512 && Ct % chunk_of(dtype) == 0, HISEG_ERR_BAD_SHAPE,
+                "hier_combine: bad shape (Ct %d)", Ct);
+  if (N == 0) return HISEG_OK;
+  const long long total = (long long)N * 4 * h * w;
+  DISPATCH_T(dtype, hier_combine_kernel, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, low, N, h, w, tfeat,
+             Ct, ut_w, ut_scale, ut_shift, ut_act, u1_w, u1_b, t_w, t_b, logits, bgfg, tn);
+  return hiseg_check_launch("hier_combine");
+}
+
+extern "C" int hiseg_nhwc_to_nchw_fwd(int dtype, const void* in, int N, int H, int W, int C, int cstride, int coff, float* out,
+                                      hiseg_stream_t stream) {
+  HISEG_REQUIRE(in && out && N >= 0 && C > 0 && cstride >= coff + C, HISEG_ERR_BAD_ARG, "nhwc_to_nchw: bad args");
+  const long long total = (long long)N * C * H * W;
+  if (total == 0) return HISEG_OK;
+  DISPATCH_T(dtype, nhwc_to_nchw_kernel, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, in, N, H, W, C, cstride,
+             coff, out);
+  return hiseg_check_launch("nhwc_to_nchw");
+}
+
+extern "C" int hiseg_nchw_to_nhwc_fwd(int dtype, const float* in, int N, int C, int H, int W, void* out, int cpad,
+                                      hiseg_stream_t stream) {
+  HISEG_REQUIRE(in && out && N >= 0 && C > 0 && cpad >= C, HISEG_ERR_BAD_ARG, "nchw_to_nhwc: bad args");
+  const long long total = (long long)N * H * W;
+  if (total == 0) return HISEG_OK;
+  DISPATCH_T(dtype, nchw_to_nhwc_kernel, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, in, N, C, H, W, out, cpad);
+  return hiseg_check_launch("nchw_to_nhwc");
+}
+
+extern "C" int hiseg_instance_masks_fwd(const float* logits, int N, int mh, int mw, int dilation, float* instance,
+                                        hiseg_stream_t stream) {
+  HISEG_REQUIRE(logits && instance && N >= 0 && mh > 0 && mw > 0 && dilation >= 0, HISEG_ERR_BAD_ARG, "instance_masks: bad args");
+  const long long total = (long long)N * mh * mw;
+  if (total == 0) return HISEG_OK;
+  hipLaunchKernelGGL(instance_mask_kernel, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, logits, N, mh, mw,
+                     dilation, instance);
+  return hiseg_check_launch("instance_masks");
+}
+
+extern "C" int hiseg_binary_masks_fwd(int dtype, const void* u, int u_cstride, int B, int H, int W, const float* oc_w,
+                                      const float* oc_b, float* binary, hiseg_stream_t stream) {
+  HISEG_REQUIRE(dtype == HISEG_F32, HISEG_ERR_BAD_DTYPE, "binary_masks: the UNet logit map is f32");
+  HISEG_REQUIRE(u && oc_w && oc_b && binary && B > 0 && u_cstride >= 1, HISEG_ERR_BAD_ARG, "binary_masks: bad args");
+  const long long P = (long long)B * H * W;
+  hipLaunchKernelGGL(binary_mask_kernel, dim3(nblocks(P, 256)), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const float*>(u), u_cstride, P, oc_w, oc_b, binary);
+  return hiseg_check_launch("binary_masks");
+}

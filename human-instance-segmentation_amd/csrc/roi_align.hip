@@ -1,0 +1,127 @@
+// Dynamic RoIAlign forward (reference: src/human_edge_detection/dynamic_roi_align.py:56-171).
+//
+// One thread per output pixel (roi n, row i, col j); the sampling point and the four bilinear
+// weights are computed once and reused for every channel.  The coordinate arithmetic follows
+// the reference op for op in f32 with no FMA contraction (each product/sum rounded as torch
+// rounds it on the CPU):
+//   linspace(0,1,S)[j] = j < S/2 ? step*j : 1 - step*(S-1-j),  step = 1/(S-1)   (:110-111)
+//   fx = x1 + gx*(x2-x1), x1 = roi_x1*scale_w                                    (:83-93,133)
+//   nx = fx/(W-1)*2-1 (aligned) | fx/W*2-1                                       (:139-146)
+//   grid_sample unnormalise (CPU vectorised form): (nx+1)*((W-1)/2) | (nx+1)*(W/2)-0.5
+//   bilinear with zero padding: taps outside [0,W-1]x[0,H-1] contribute 0       (:163-169)
+// Feature maps are read in place through the roi's batch index; the reference's
+// index_select copy of N full maps (:156) is not materialised.
+#include "common.h"
+
+namespace hiseg {
+
+__device__ __forceinline__ float fmul(float a, float b) { return __fmul_rn(a, b); }
+__device__ __forceinline__ float fadd(float a, float b) { return __fadd_rn(a, b); }
+__device__ __forceinline__ float fsub(float a, float b) { return __fsub_rn(a, b); }
+
+__device__ __forceinline__ float linspace01(int idx, int steps) {
+  if (steps == 1) return 0.f;
+  const float step = __fdiv_rn(1.0f, (float)(steps - 1));
+  const int halfway = steps / 2;
+  if (idx < halfway) return fmul(step, (float)idx);
+  return fsub(1.0f, fmul(step, (float)(steps - idx - 1)));
+}
+
+// Returns the unnormalised source coordinate along one axis.
+__device__ __forceinline__ float src_coord(float lo, float len, float g, int size, int aligned) {
+  const float f = fadd(lo, fmul(g, len));
+  if (aligned) {
+    const float nrm = fsub(fmul(__fdiv_rn(f, (float)(size - 1)), 2.0f), 1.0f);
+    return fmul(fadd(nrm, 1.0f), __fdiv_rn((float)(size - 1), 2.0f));
+  }
+  const float nrm = fsub(fmul(__fdiv_rn(f, (float)size), 2.0f), 1.0f);
+  return fsub(fmul(fadd(nrm, 1.0f), __fdiv_rn((float)size, 2.0f)), 0.5f);
+}
+
+template <typename TO>
+__global__ void __launch_bounds__(256) roi_align_kernel(hiseg_roi_align_desc d) {
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long total = (long long)d.N * d.oh * d.ow;
+  if (gid >= total) return;
+  const int j = (int)(gid % d.ow);
+  const long long t = gid / d.ow;
+  const int i = (int)(t % d.oh);
+  const int n = (int)(t / d.oh);
+
+  const float* roi = d.rois + (long long)n * 5;
+  const float bf = roi[0];
+  const long long b = (long long)bf;  // .long(): truncation toward zero
+  const float x1 = fmul(roi[1], d.scale_w), y1 = fmul(roi[2], d.scale_h);
+  const float x2 = fmul(roi[3], d.scale_w), y2 = fmul(roi[4], d.scale_h);
+  const float ix = src_coord(x1, fsub(x2, x1), linspace01(j, d.ow), d.W, d.aligned);
+  const float iy = src_coord(y1, fsub(y2, y1), linspace01(i, d.oh), d.H, d.aligned);
+
+  const float xw = floorf(ix), yn = floorf(iy);
+  const float wgt_w = fsub(ix, xw), wgt_e = fsub(1.f, wgt_w);
+  const float wgt_n = fsub(iy, yn), wgt_s = fsub(1.f, wgt_n);
+  const float w_nw = fmul(wgt_s, wgt_e), w_ne = fmul(wgt_s, wgt_w);
+  const float w_sw = fmul(wgt_n, wgt_e), w_se = fmul(wgt_n, wgt_w);
+  // integer tap positions (clamped to a safe range before the int conversion)
+  const float xwc = fminf(fmaxf(xw, -2.f), (float)d.W + 1.f);
+  const float ync = fminf(fmaxf(yn, -2.f), (float)d.H + 1.f);
+  const int x0 = (int)xwc, y0 = (int)ync;
+  const bool bvalid = (b >= 0 && b < d.B) && (ix == ix) && (iy == iy);
+  const bool vx0 = x0 >= 0 && x0 < d.W, vx1 = x0 + 1 >= 0 && x0 + 1 < d.W;
+  const bool vy0 = y0 >= 0 && y0 < d.H, vy1 = y0 + 1 >= 0 && y0 + 1 < d.H;
+
+  const int Cout = d.aff_w ? d.n_aff : d.C;
+  const long long plane = (long long)d.H * d.W;
+  for (int c = 0; c < Cout; ++c) {
+    float v = 0.f;
+    if (bvalid) {
+      const float* src = d.feat + ((long long)b * d.C + (d.aff_w ? 0 : c)) * plane;
+      float aw = 1.f, ab = 0.f;
+      const bool aff = d.aff_w != nullptr;
+      if (aff) { aw = d.aff_w[c]; ab = d.aff_b ? d.aff_b[c] : 0.f; }
+      auto tap = [&](bool ok, int yy, int xx) -> float {
+        if (!ok) return 0.f;
+        const float u = src[(long long)yy * d.W + xx];
+        return aff ? fadd(fmul(aw, u), ab) : u;
+      };
+      const float v_nw = tap(vy0 && vx0, y0, x0);
+      const float v_ne = tap(vy0 && vx1, y0, x0 + 1);
+      const float v_sw = tap(vy1 && vx0, y0 + 1, x0);
+      const float v_se = tap(vy1 && vx1, y0 + 1, x0 + 1);
+      v = fadd(fadd(fadd(fmul(v_nw, w_nw), fmul(v_ne, w_ne)), fmul(v_sw, w_sw)), fmul(v_se, w_se));
+    }
+    if (d.o_nchw) {
+      reinterpret_cast<float*>(d.out)[(((long long)n * Cout + c) * d.oh + i) * d.ow + j] = v;
+    } else {
+      Elem<TO>::store(d.out, gid * d.o_cstride + d.o_coff + c, v);
+    }
+  }
+  if (!d.o_nchw) {
+    for (int c = Cout; c < d.zero_to; ++c) Elem<TO>::store(d.out, gid * d.o_cstride + d.o_coff + c, 0.f);
+  }
+}
+
+}  // namespace hiseg
+
+using namespace hiseg;
+
+extern "C" int hiseg_roi_align_fwd(const hiseg_roi_align_desc* d, hiseg_stream_t stream) {
+  HISEG_REQUIRE(d != nullptr, HISEG_ERR_BAD_ARG, "roi_align: null descriptor");
+  HISEG_REQUIRE(d->feat && d->rois && d->out, HISEG_ERR_BAD_ARG, "roi_align: null pointer");
+  HISEG_REQUIRE(d->B > 0 && d->C > 0 && d->H > 0 && d->W > 0 && d->oh > 0 && d->ow > 0 && d->N >= 0,
+                HISEG_ERR_BAD_SHAPE, "roi_align: bad shape");
+  HISEG_REQUIRE(!d->aligned || (d->H > 1 && d->W > 1), HISEG_ERR_BAD_SHAPE, "roi_align: aligned needs H,W > 1");
+  HISEG_REQUIRE(!d->aff_w || d->n_aff > 0, HISEG_ERR_BAD_ARG, "roi_align: n_aff");
+  HISEG_REQUIRE(!d->o_nchw || d->out_dtype == HISEG_F32, HISEG_ERR_BAD_DTYPE, "roi_align: NCHW output is f32 only");
+  const int Cout = d->aff_w ? d->n_aff : d->C;
+  HISEG_REQUIRE(d->o_nchw || d->o_cstride >= d->o_coff + (d->zero_to > Cout ? d->zero_to : Cout), HISEG_ERR_BAD_SHAPE,
+                "roi_align: o_cstride too small");
+  if (d->N == 0) return HISEG_OK;
+  const long long total = (long long)d->N * d->oh * d->ow;
+  dim3 grid((unsigned)((total + 255) / 256));
+  hipStream_t s = (hipStream_t)stream;
+  if (d->out_dtype == HISEG_BF16)
+    hipLaunchKernelGGL(roi_align_kernel<bf16_t>, grid, dim3(256), 0, s, *d);
+  else
+    hipLaunchKernelGGL(roi_align_kernel<float>, grid, dim3(256), 0, s, *d);
+  return hiseg_check_launch("roi_align");
+}
