@@ -400,6 +400,46 @@ __global__ void __launch_bounds__(256) binary_mask_kernel(const float* u, int cs
   out[gid] = e0 / (e0 + e1);
 }
 
+// ------------------------------------------------------------------ aux-map helpers
+__global__ void __launch_bounds__(256) resize_bilinear_kernel(const float* in, int NC, int H, int W, float* out, int Ho,
+                                                              int Wo) {
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long total = (long long)NC * Ho * Wo;
+  if (gid >= total) return;
+  const int x = (int)(gid % Wo);
+  const long long t = gid / Wo;
+  const int y = (int)(t % Ho);
+  const long long nc = t / Ho;
+  const float sh = (float)H / (float)Ho, sw = (float)W / (float)Wo;
+  float sy = (y + 0.5f) * sh - 0.5f;
+  float sx = (x + 0.5f) * sw - 0.5f;
+  sy = sy < 0.f ? 0.f : sy;
+  sx = sx < 0.f ? 0.f : sx;
+  const int y0 = (int)sy, x0 = (int)sx;
+  const int y1 = y0 + (y0 < H - 1 ? 1 : 0), x1 = x0 + (x0 < W - 1 ? 1 : 0);
+  const float ly = sy - y0, lx = sx - x0;
+  const float* p = in + nc * H * W;
+  const float v = (1.f - ly) * ((1.f - lx) * p[y0 * W + x0] + lx * p[y0 * W + x1]) +
+                  ly * ((1.f - lx) * p[y1 * W + x0] + lx * p[y1 * W + x1]);
+  out[gid] = v;
+}
+
+__global__ void __launch_bounds__(256) distance_mask_kernel(const float* x, long long n, const float* thr, float* out) {
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= n) return;
+  out[gid] = sigmoidf_((x[gid] - thr[0]) * 10.0f);
+}
+
+__global__ void __launch_bounds__(256) output_conv_kernel(const float* u, int B, long long plane, const float* w,
+                                                          const float* b, float* out) {
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= (long long)B * plane) return;
+  const long long n = gid / plane, p = gid % plane;
+  const float v = u[gid];
+  out[(n * 2) * plane + p] = w[0] * v + b[0];
+  out[(n * 2 + 1) * plane + p] = w[1] * v + b[1];
+}
+
 }  // namespace hiseg
 
 using namespace hiseg;
@@ -553,4 +593,31 @@ extern "C" int hiseg_binary_masks_fwd(int dtype, const void* u, int u_cstride, i
   hipLaunchKernelGGL(binary_mask_kernel, dim3(nblocks(P, 256)), dim3(256), 0, (hipStream_t)stream,
                      reinterpret_cast<const float*>(u), u_cstride, P, oc_w, oc_b, binary);
   return hiseg_check_launch("binary_masks");
+}
+
+extern "C" int hiseg_resize_bilinear_fwd(const float* in, int NC, int H, int W, float* out, int Ho, int Wo,
+                                         hiseg_stream_t stream) {
+  HISEG_REQUIRE(in && out && NC >= 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0, HISEG_ERR_BAD_ARG, "resize_bilinear: bad args");
+  const long long total = (long long)NC * Ho * Wo;
+  if (total == 0) return HISEG_OK;
+  hipLaunchKernelGGL(resize_bilinear_kernel, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, in, NC, H, W, out,
+                     Ho, Wo);
+  return hiseg_check_launch("resize_bilinear");
+}
+
+extern "C" int hiseg_distance_mask_fwd(const float* x, long long n, const float* threshold, float* out,
+                                       hiseg_stream_t stream) {
+  HISEG_REQUIRE(x && threshold && out && n >= 0, HISEG_ERR_BAD_ARG, "distance_mask: bad args");
+  if (n == 0) return HISEG_OK;
+  hipLaunchKernelGGL(distance_mask_kernel, dim3(nblocks(n, 256)), dim3(256), 0, (hipStream_t)stream, x, n, threshold, out);
+  return hiseg_check_launch("distance_mask");
+}
+
+extern "C" int hiseg_output_conv_fwd(const float* u, int B, int H, int W, const float* w, const float* b, float* out,
+                                     hiseg_stream_t stream) {
+  HISEG_REQUIRE(u && w && b && out && B > 0 && H > 0 && W > 0, HISEG_ERR_BAD_ARG, "output_conv: bad args");
+  const long long P = (long long)B * H * W;
+  hipLaunchKernelGGL(output_conv_kernel, dim3(nblocks(P, 256)), dim3(256), 0, (hipStream_t)stream, u, B, (long long)H * W, w,
+                     b, out);
+  return hiseg_check_launch("output_conv");
 }

@@ -106,6 +106,8 @@ using namespace hiseg;
 
 extern "C" int hiseg_roi_align_fwd(const hiseg_roi_align_desc* d, hiseg_stream_t stream) {
   HISEG_REQUIRE(d != nullptr, HISEG_ERR_BAD_ARG, "roi_align: null descriptor");
+  HISEG_REQUIRE(d->N >= 0, HISEG_ERR_BAD_SHAPE, "roi_align: negative N");
+  if (d->N == 0) return HISEG_OK;  // empty ROI list (empty tensors carry null pointers)
   HISEG_REQUIRE(d->feat && d->rois && d->out, HISEG_ERR_BAD_ARG, "roi_align: null pointer");
   HISEG_REQUIRE(d->B > 0 && d->C > 0 && d->H > 0 && d->W > 0 && d->oh > 0 && d->ow > 0 && d->N >= 0,
                 HISEG_ERR_BAD_SHAPE, "roi_align: bad shape");

@@ -1,3 +1,27 @@
-"""hiseg — MI355X-native ROI-hierarchical instance segmentation (drop-in for the RGB
-hierarchical path of PINTO0309/human-instance-segmentation).  See DESIGN.md."""
+"""hiseg — MI355X-native ROI-hierarchical instance segmentation.
+
+Drop-in for the RGB hierarchical path of PINTO0309/human-instance-segmentation
+(HierarchicalRGBSegmentationModelWithFullImagePretrainedUNet + RefinedHierarchicalSegmentationHead
+on a full-image EfficientNet-UNet).  Module tree and state_dict keys follow the reference;
+every forward runs on libhiseg (hand-written gfx950 HIP kernels, C ABI in include/hiseg.h).
+"""
+from .layers import (  # noqa: F401
+    ChannelAttentionModule, ContourDetectionBranch, DistanceTransformDecoder, EnhancedUNet,
+    ExtendedHierarchicalSegmentationHeadUNetV2, LayerNorm2d, RefinedHierarchicalSegmentationHead, ResidualBlock,
+    SpatialAttentionModule)
+from .effunet import EfficientNetUnet  # noqa: F401
+from .model import (  # noqa: F401
+    DynamicRoIAlign, HierarchicalRGBSegmentationModelWithFullImagePretrainedUNet, PreTrainedPeopleSegmentationUNet,
+    PreTrainedPeopleSegmentationUNetWrapper, RGBHierarchicalExportWrapper, create_rgb_hierarchical_model)
+
 __version__ = "0.1.0"
+
+
+def set_compute_dtype(model, dtype):
+    """Select the HIP compute precision of a model: torch.float32 (parity) or torch.bfloat16 (throughput)."""
+    import torch
+    if dtype not in (torch.float32, torch.bfloat16):
+        raise TypeError(dtype)
+    for m in model.modules():
+        m.hiseg_dtype = dtype
+    return model

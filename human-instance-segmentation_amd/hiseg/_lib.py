@@ -89,6 +89,9 @@ def _declare(lib):
         "hiseg_nchw_to_nhwc_fwd": ([c_int, P, c_int, c_int, c_int, c_int, P, c_int, P], c_int),
         "hiseg_instance_masks_fwd": ([P, c_int, c_int, c_int, c_int, P, P], c_int),
         "hiseg_binary_masks_fwd": ([c_int, P, c_int, c_int, c_int, c_int, P, P, P, P], c_int),
+        "hiseg_resize_bilinear_fwd": ([P, c_int, c_int, c_int, P, c_int, c_int, P], c_int),
+        "hiseg_distance_mask_fwd": ([P, c_ll, P, P, P], c_int),
+        "hiseg_output_conv_fwd": ([P, c_int, c_int, c_int, P, P, P, P], c_int),
     }
     for name, (argtypes, restype) in sigs.items():
         fn = getattr(lib, name)

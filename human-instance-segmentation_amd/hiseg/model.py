@@ -1,0 +1,228 @@
+"""Drop-in model surface of the RGB hierarchical path.
+
+Mirrors, module for module and parameter name for parameter name:
+  * PreTrainedPeopleSegmentationUNet / ...Wrapper  (advanced/hierarchical_segmentation_unet.py:1708-1993)
+  * DynamicRoIAlign                                (src/human_edge_detection/dynamic_roi_align.py:10-171)
+  * HierarchicalRGBSegmentationModelWithFullImagePretrainedUNet and create_rgb_hierarchical_model
+                                                   (advanced/hierarchical_segmentation_rgb.py:564-774, 925-1027)
+Forward passes execute on libhiseg (hiseg.engine); CPU tensors are rejected.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional, Tuple, Union
+
+import torch
+import torch.nn as nn
+
+from . import engine
+from .effunet import EfficientNetUnet
+from .layers import RefinedHierarchicalSegmentationHead, ResidualBlock, make_act, make_norm
+
+
+class DynamicRoIAlign(nn.Module):
+    """Bilinear ROI crop with a per-call output size (dynamic_roi_align.py:10-171)."""
+
+    def __init__(self, spatial_scale=(640, 640), sampling_ratio=-1, aligned=False):
+        super().__init__()
+        if isinstance(spatial_scale, (list, tuple)):
+            assert len(spatial_scale) == 2, "spatial_scale tuple must have 2 elements (height, width)"
+            self.spatial_scale_h, self.spatial_scale_w = spatial_scale
+        else:
+            self.spatial_scale_h = self.spatial_scale_w = spatial_scale
+        self.spatial_scale = spatial_scale
+        self.sampling_ratio = sampling_ratio  # unused, as in the reference (:37-38)
+        self.aligned = aligned
+
+    def forward(self, input_feature_map: torch.Tensor, rois: torch.Tensor, output_height, output_width):
+        return engine.roi_align_nchw(self, input_feature_map, rois, output_height, output_width)
+
+
+def _imagenet_or_half(path: str, mean, std):
+    if mean is not None and std is not None:
+        return list(mean), list(std)
+    if any(v in path.lower() for v in ("b0", "b1", "b7")):
+        return [0.485, 0.456, 0.406], [0.229, 0.224, 0.225]
+    return [0.5, 0.5, 0.5], [0.5, 0.5, 0.5]
+
+
+class PreTrainedPeopleSegmentationUNet(nn.Module):
+    """Frozen full-image person UNet (hierarchical_segmentation_unet.py:1708-1916)."""
+
+    def __init__(self, in_channels: int = 3, classes: int = 1,
+                 pretrained_weights_path: str = "ext_extractor/2020-09-23a.pth", mean=None, std=None,
+                 freeze_weights: bool = False, encoder_name: str = "timm-efficientnet-b3"):
+        super().__init__()
+        self.in_channels = in_channels
+        self.classes = classes
+        self.encoder_name = encoder_name
+        # normalisation chosen by weights-path substring (:1744-1758)
+        self.mean, self.std = _imagenet_or_half(pretrained_weights_path or "", mean, std)
+        self.model = EfficientNetUnet(encoder_name=encoder_name, classes=classes, encoder_weights=None)
+        if pretrained_weights_path and os.path.exists(pretrained_weights_path):
+            load_pretrained_unet(self.model, pretrained_weights_path)
+        if freeze_weights:
+            for p in self.model.parameters():
+                p.requires_grad = False
+            self.model.eval()
+            self._freeze_bn = True
+        else:
+            self._freeze_bn = False
+        self.register_buffer("norm_mean", torch.tensor(self.mean).view(1, 3, 1, 1))
+        self.register_buffer("norm_std", torch.tensor(self.std).view(1, 3, 1, 1))
+
+    def train(self, mode: bool = True):
+        super().train(mode)
+        if getattr(self, "_freeze_bn", False):
+            self.model.eval()
+        return self
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return engine.unet_logits_nchw(self, x)
+
+
+def load_pretrained_unet(model: nn.Module, path: str) -> Tuple[list, list]:
+    """Checkpoint loading of hierarchical_segmentation_unet.py:1781-1867 (prefix strip, strict=False).
+
+    Unlike the reference (weights_only=False) the file is read with the non-executing loader.
+    """
+    ckpt = torch.load(path, map_location="cpu", weights_only=True)
+    sd = ckpt
+    if isinstance(ckpt, dict):
+        for k in ("state_dict", "model_state_dict"):
+            if k in ckpt:
+                sd = ckpt[k]
+                break
+    first = next(iter(sd.keys()), "")
+    prefix = "model." if first.startswith("model.") else ("unet." if first.startswith("unet.") else "")
+    sd = {(k[len(prefix):] if prefix and k.startswith(prefix) else k): v for k, v in sd.items()}
+    missing, unexpected = model.load_state_dict(sd, strict=False)
+    return missing, unexpected
+
+
+class PreTrainedPeopleSegmentationUNetWrapper(nn.Module):
+    """UNet logit u -> trainable 1x1 conv 1->2 initialised [+1, -1] (hierarchical_segmentation_unet.py:1919-1993)."""
+
+    def __init__(self, in_channels: int, base_channels: int = 64, depth: int = 4, groups=None,
+                 normalization_type: str = "layernorm2d", normalization_groups: int = 8,
+                 pretrained_weights_path: str = "ext_extractor/2020-09-23a.pth", freeze_weights: bool = False,
+                 encoder_name: str = "timm-efficientnet-b3"):
+        super().__init__()
+        self.model = PreTrainedPeopleSegmentationUNet(in_channels=in_channels, classes=1,
+                                                      pretrained_weights_path=pretrained_weights_path,
+                                                      freeze_weights=freeze_weights, encoder_name=encoder_name)
+        self.output_conv = nn.Conv2d(1, 2, kernel_size=1)
+        with torch.no_grad():
+            self.output_conv.weight.data[0, 0, 0, 0] = 1.0
+            self.output_conv.weight.data[1, 0, 0, 0] = -1.0
+            self.output_conv.bias.data.zero_()
+
+    def forward(self, x: torch.Tensor):
+        return engine.unet_two_channel_nchw(self, x), []
+
+
+class HierarchicalRGBSegmentationModelWithFullImagePretrainedUNet(nn.Module):
+    """Full-image UNet -> 2x RoIAlign -> RGB conv stack -> 258->256 combiner -> refined hierarchical head."""
+
+    def __init__(self, roi_size: Union[int, Tuple[int, int]] = 28, mask_size: Union[int, Tuple[int, int]] = 56,
+                 pretrained_weights_path: str = "ext_extractor/2020-09-23a.pth", use_attention_module: bool = False,
+                 freeze_pretrained_weights: bool = False, use_boundary_refinement: bool = False,
+                 use_progressive_upsampling: bool = False, use_subpixel_conv: bool = False,
+                 use_contour_detection: bool = False, use_distance_transform: bool = False,
+                 normalization_type: str = "layernorm2d", normalization_groups: int = 8,
+                 activation_function: str = "relu", activation_beta: float = 1.0, **kwargs):
+        super().__init__()
+        base = kwargs.get("hierarchical_base_channels", 96)
+        depth = kwargs.get("hierarchical_depth", 3)
+        self.roi_size = (roi_size, roi_size) if isinstance(roi_size, int) else tuple(roi_size)
+        self.mask_size = (mask_size, mask_size) if isinstance(mask_size, int) else tuple(mask_size)
+        self.pretrained_unet = PreTrainedPeopleSegmentationUNetWrapper(
+            in_channels=3, pretrained_weights_path=pretrained_weights_path, freeze_weights=freeze_pretrained_weights,
+            encoder_name=kwargs.get("encoder_name", "timm-efficientnet-b3"))
+        # training semantics: normalised ROIs x 640 (rgb.py:636-647); export sets (H, W)
+        self.roi_align_mask = DynamicRoIAlign(spatial_scale=640.0, sampling_ratio=2, aligned=True)
+        self.roi_align_rgb = DynamicRoIAlign(spatial_scale=640.0, sampling_ratio=2, aligned=True)
+        fd = 256
+        norm, g, act, beta = normalization_type, normalization_groups, activation_function, activation_beta
+        self.rgb_feature_extractor = nn.Sequential(
+            nn.Conv2d(3, 64, 3, padding=1), make_norm(norm, 64, min(g, 64)), make_act(act, beta),
+            ResidualBlock(64, norm, min(g, 64), act, beta),
+            nn.Conv2d(64, 128, 3, padding=1), make_norm(norm, 128, min(g, 128)), make_act(act, beta),
+            ResidualBlock(128, norm, min(g, 128), act, beta),
+            nn.Conv2d(128, 256, 3, padding=1), make_norm(norm, 256, min(g, 256)), make_act(act, beta),
+            ResidualBlock(256, norm, min(g, 256), act, beta),
+            nn.Conv2d(256, fd, 1), make_norm(norm, fd, min(g, fd)), make_act(act, beta))
+        use_refinement = any([use_boundary_refinement, use_progressive_upsampling, use_subpixel_conv,
+                              use_contour_detection, use_distance_transform])
+        if not use_refinement:
+            raise NotImplementedError(
+                "PretrainedUNetGuidedSegmentationHead (no refinement flags) is not used by the measured configs; "
+                "hiseg builds the RefinedHierarchicalSegmentationHead path (SURVEY.md §0 item 4)")
+        self.feature_combiner = nn.Conv2d(fd + 2, fd, 1)
+        ms = self.mask_size[0] if self.mask_size[0] == self.mask_size[1] else self.mask_size
+        self.segmentation_head = RefinedHierarchicalSegmentationHead(
+            in_channels=fd, mid_channels=256, num_classes=3, mask_size=ms, use_attention_module=use_attention_module,
+            use_boundary_refinement=use_boundary_refinement, use_progressive_upsampling=use_progressive_upsampling,
+            use_subpixel_conv=use_subpixel_conv, use_contour_detection=use_contour_detection,
+            use_distance_transform=use_distance_transform, normalization_type=norm, normalization_groups=g,
+            activation_function=act, activation_beta=beta, hierarchical_base_channels=base,
+            hierarchical_depth=depth)
+        # compute precision of the HIP path: f32 (parity with the reference) or bf16 (throughput)
+        self.hiseg_dtype = torch.float32
+
+    def forward(self, images: torch.Tensor, rois: torch.Tensor) -> Tuple[torch.Tensor, Dict[str, torch.Tensor]]:
+        return engine.rgb_model_forward(self, images, rois, aux="full")
+
+    def infer(self, images: torch.Tensor, rois: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Logits [N,3,mh,mw] and the UNet logit map u [B,1,H,W], no aux tensors (serving path)."""
+        logits, aux = engine.rgb_model_forward(self, images, rois, aux="none")
+        return logits, aux["unet_logit"]
+
+
+class RGBHierarchicalExportWrapper(nn.Module):
+    """The exported ONNX contract (export_onnx_advanced.py:353-420, export_hierarchical_instance_peopleseg_onnx.py
+    :85-181): images [B,3,H,W] in [0,1], rois [N,5] -> instance_masks [N,1,mh,mw], binary_masks [B,1,H,W].
+
+    ROIAlign scales are set to (H, W) as _adjust_roi_align_spatial_scale does (:80-98).  The reference runs the
+    full-image UNet twice (once for binary_masks, once inside the model); both passes are the same deterministic
+    function of the image, so it is computed once here.
+    """
+
+    def __init__(self, model: HierarchicalRGBSegmentationModelWithFullImagePretrainedUNet, image_size=None,
+                 dilation_pixels: int = 0):
+        super().__init__()
+        self.model = model
+        self.image_size = image_size
+        self.dilation_pixels = dilation_pixels
+
+    def forward(self, images: torch.Tensor, rois: torch.Tensor):
+        H, W = images.shape[-2:] if self.image_size is None else self.image_size
+        for m in (self.model.roi_align_mask, self.model.roi_align_rgb):
+            m.spatial_scale = (H, W)
+            m.spatial_scale_h, m.spatial_scale_w = H, W
+        return engine.export_forward(self.model, images, rois, self.dilation_pixels)
+
+
+def create_rgb_hierarchical_model(roi_size=28, mask_size=56, multi_scale: bool = False,
+                                  activation_function: str = "relu", activation_beta: float = 1.0,
+                                  normalization_type: str = "layernorm2d", normalization_groups: int = 8,
+                                  **kwargs) -> nn.Module:
+    """Factory of advanced/hierarchical_segmentation_rgb.py:925-1027 (full-image pretrained-UNet branch)."""
+    use_attention_module = kwargs.pop("use_attention_module", False)
+    flags = {k: kwargs.pop(k, False) for k in ("use_boundary_refinement", "use_progressive_upsampling",
+                                               "use_subpixel_conv", "use_contour_detection", "use_distance_transform")}
+    use_pretrained_unet = kwargs.pop("use_pretrained_unet", False)
+    pretrained_weights_path = kwargs.pop("pretrained_weights_path", "")
+    freeze = kwargs.pop("freeze_pretrained_weights", False)
+    full_image = kwargs.pop("use_full_image_unet", False)
+    kwargs.pop("roi_sizes", None)
+    kwargs.pop("fusion_method", None)
+    if multi_scale or not (use_pretrained_unet and full_image):
+        raise NotImplementedError(
+            "hiseg implements the full-image pretrained-UNet RGB hierarchical model (the BASELINE.json hot path); "
+            "multi-scale / ROI-UNet / plain RGB variants are out of scope (SURVEY.md §2.1)")
+    return HierarchicalRGBSegmentationModelWithFullImagePretrainedUNet(
+        roi_size=roi_size, mask_size=mask_size, pretrained_weights_path=pretrained_weights_path,
+        use_attention_module=use_attention_module, freeze_pretrained_weights=freeze,
+        normalization_type=normalization_type, normalization_groups=normalization_groups,
+        activation_function=activation_function, activation_beta=activation_beta, **flags, **kwargs)

@@ -189,6 +189,21 @@ int hiseg_binary_masks_fwd(int dtype, const void* u, int u_cstride, int B, int H
                            const float* oc_w, const float* oc_b, float* binary,
                            hiseg_stream_t stream);
 
+/* Bilinear resize, align_corners=False (F.interpolate as used for the contour / distance aux
+ * maps, advanced/hierarchical_segmentation_refinement.py:775-800).  NCHW f32, NC planes. */
+int hiseg_resize_bilinear_fwd(const float* in, int NC, int H, int W, float* out, int Ho, int Wo,
+                              hiseg_stream_t stream);
+
+/* DistanceTransformDecoder mask (refinement.py:342): out = sigmoid((x - *threshold) * 10);
+ * `threshold` is a device pointer (the learnable parameter), n elements. */
+int hiseg_distance_mask_fwd(const float* x, long long n, const float* threshold, float* out,
+                            hiseg_stream_t stream);
+
+/* 1x1 conv 1 -> 2 of PreTrainedPeopleSegmentationUNetWrapper.output_conv
+ * (hierarchical_segmentation_unet.py:1963-1971,1990): u [B,1,H,W] -> out [B,2,H,W], f32. */
+int hiseg_output_conv_fwd(const float* u, int B, int H, int W, const float* w, const float* b, float* out,
+                          hiseg_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,47 @@
+"""The C-ABI library loads and exports every entry point include/hiseg.h declares (no GPU calls)."""
+import os
+import re
+
+from conftest import ROOT
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "hiseg.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(hiseg_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_the_hot_path():
+    fns = header_functions()
+    for must in ("hiseg_roi_align_fwd", "hiseg_conv2d_fwd", "hiseg_hier_combine_fwd", "hiseg_dwconv_fwd",
+                 "hiseg_se_gate_fwd", "hiseg_attn_spatial_fwd", "hiseg_instance_masks_fwd"):
+        assert must in fns
+
+
+def test_library_exports_every_declared_symbol():
+    from hiseg import _lib as L
+    lib = L.lib()
+    for name in header_functions():
+        assert hasattr(lib, name), name
+    assert lib.hiseg_version() >= 100
+    assert lib.hiseg_built_for_gfx950() == 1
+    # every symbol has a ctypes signature in the binding
+    assert set(header_functions()) <= set(L.EXPORTED)
+
+
+def test_invalid_descriptor_reports_an_error_without_touching_the_gpu():
+    import ctypes
+    from hiseg import _lib as L
+    d = L.Conv2dDesc()
+    d.dtype = 7  # unsupported
+    st = L.lib().hiseg_conv2d_fwd(ctypes.byref(d), None)
+    assert st == -3
+    assert b"dtype" in L.lib().hiseg_last_error_string()
+
+
+def test_product_path_refuses_cpu_tensors():
+    import pytest
+    import torch
+    from hiseg import DynamicRoIAlign
+    with pytest.raises(RuntimeError, match="GPU only"):
+        DynamicRoIAlign(640, aligned=True)(torch.zeros(1, 1, 4, 4), torch.zeros(1, 5), 2, 2)

@@ -1,0 +1,326 @@
+"""HIP path (libhiseg through the C ABI) against the oracle and the reference's golden vectors.
+
+Tolerances: f32 compute — the north-star bar of 1e-4 (relative to the output's magnitude);
+bf16 compute — 8-bit mantissa storage of every activation over ~70 layers: checked with a
+relative bound plus agreement of the exported instance masks (argmax == 1).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import filler
+from helpers import b0_kwargs, hiseg_kwargs, load, max_abs
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+F32_TOL = 1e-4
+
+
+def _rel(a, b):
+    a, b = torch.as_tensor(a).double().cpu(), torch.as_tensor(b).double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1.0)).item()
+
+
+# ------------------------------------------------------------------------------------------ RoIAlign
+def test_roi_align_kernel_matches_reference_golden():
+    from hiseg import DynamicRoIAlign
+    g = load("roi_align")
+    feat, rois = torch.from_numpy(g["feat"]).to(DEV), torch.from_numpy(g["rois"]).to(DEV)
+    for i in range(5):
+        oh, ow, sh, sw, al = g[f"c{i}_meta"]
+        m = DynamicRoIAlign((float(sh), float(sw)), aligned=bool(al))
+        out = m(feat, rois, int(oh), int(ow))
+        assert max_abs(out.cpu(), g[f"c{i}_out"]) < 1e-5, i
+    m = DynamicRoIAlign(20, aligned=True)
+    out = m(torch.from_numpy(g["feat2"]).to(DEV), torch.from_numpy(g["rois2"]).to(DEV), 6, 4)
+    assert max_abs(out.cpu(), g["out2"]) < 1e-5
+
+
+def test_roi_align_nhwc_affine_bf16_and_edge_cases():
+    from hiseg import ops
+    from oracle.roi_align import roi_align as roi_np
+    u = torch.from_numpy(filler.normal(3, (2, 1, 40, 56))).to(DEV)
+    rois = torch.from_numpy(filler.box_rois(4, 2, 5)).to(DEV)
+    rois = torch.cat([rois, torch.tensor([[1, 0.0, 0.0, 1.0, 1.0], [0, 0.3, 0.3, 0.3, 0.3]], device=DEV)])
+    w, b = torch.tensor([0.7, -1.3], device=DEV), torch.tensor([0.1, 0.2], device=DEV)
+    for dt in (torch.float32, torch.bfloat16):
+        a = ops.Act.new(rois.shape[0], 16, 12, 2, dt, DEV, zero=False)
+        a.t.fill_(float("nan"))
+        ops.roi_align(u, rois, 16, 12, 40, 56, True, out=a, aff_w=w, aff_b=b, zero_to=a.cstride)
+        got = a.to_nchw().cpu()
+        two = (w.view(1, 2, 1, 1) * u + b.view(1, 2, 1, 1)).cpu().numpy()
+        ref = roi_np(two, rois.cpu().numpy(), 16, 12, 40, 56, True)
+        tol = 1e-5 if dt == torch.float32 else 2e-2
+        assert max_abs(got, ref) < tol * max(1, np.abs(ref).max())
+        pads = a.t.view(-1, a.cstride)[:, 2:].float()
+        assert torch.all(pads == 0)
+    # empty ROI list is a no-op
+    a = ops.Act.new(0, 4, 4, 2, torch.float32, DEV)
+    ops.roi_align(u, torch.zeros(0, 5, device=DEV), 4, 4, 40, 56, True, out=a, zero_to=a.cstride)
+
+
+# ------------------------------------------------------------------------------------------ conv kernel
+def _conv_ref(x, w, b, stride, pad, act, res=None, mul=None):
+    y = F.conv2d(x.double(), w.double(), None if b is None else b.double(), stride=stride, padding=pad)
+    if res is not None:
+        y = y + res.double()
+    if act == 1:
+        y = F.relu(y)
+    elif act == 2:
+        y = torch.sigmoid(y)
+    elif act == 3:
+        y = F.silu(y)
+    if mul is not None:
+        y = y * mul.double()
+    return y.float()
+
+
+CONV_CASES = [
+    # N, Cin, Cout, H, W, k, stride, act
+    (2, 64, 64, 20, 18, 3, 1, 1), (2, 256, 256, 16, 12, 3, 1, 1), (3, 3, 64, 17, 13, 3, 1, 1),
+    (2, 128, 32, 15, 9, 3, 1, 2), (2, 32, 2, 15, 9, 1, 1, 0), (2, 24, 40, 31, 33, 3, 2, 3),
+    (1, 258, 256, 8, 6, 1, 1, 0), (2, 16, 96, 11, 7, 1, 1, 3), (1, 16, 1, 12, 20, 3, 1, 0),
+]
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_igemm_single_source(case, dt):
+    from hiseg import ops
+    N, Cin, Cout, H, W, k, s, act = case
+    torch.manual_seed(hash(case) % 1000)
+    x = torch.randn(N, Cin, H, W, device=DEV)
+    w = torch.randn(Cout, Cin, k, k, device=DEV) / (Cin * k * k) ** 0.5
+    b = torch.randn(Cout, device=DEV) * 0.1
+    p = ops.pack_conv(w, b, None, act, dt, DEV, stride=s, pad=k // 2)
+    y = ops.conv2d(p, ops.Act.from_nchw(x, dt)).to_nchw().cpu()
+    ref = _conv_ref(x.to(dt).float().cpu(), w.to(dt).float().cpu(), b.cpu(), s, k // 2, act)
+    tol = 2e-5 if dt == torch.float32 else 1e-2
+    assert _rel(y, ref) < tol
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_conv_igemm_fused_epilogue_two_sources_upsample(dt):
+    """split K over two loader sources, src A upsampled x2 (smp decoder), residual, mul, out2, f32 out."""
+    from hiseg import ops
+    torch.manual_seed(1)
+    N, Ca, Cb, H, W, Cout = 2, 32, 24, 12, 10, 48
+    xa = torch.randn(N, Ca, H // 2, W // 2, device=DEV)
+    xb = torch.randn(N, Cb, H, W, device=DEV)
+    res = torch.randn(N, Cout, H, W, device=DEV)
+    mul = torch.rand(N, Cout, H, W, device=DEV)
+    w = torch.randn(Cout, Ca + Cb, 3, 3, device=DEV) / ((Ca + Cb) * 9) ** 0.5
+    bn = torch.nn.BatchNorm2d(Cout).to(DEV).eval()
+    filler.fill_module(bn)
+    p = ops.pack_conv(w, None, bn, 1, dt, DEV, pad=1, split=(Ca, Cb))
+    A, B = ops.Act.from_nchw(xa, dt), ops.Act.from_nchw(xb, dt)
+    R, M = ops.Act.from_nchw(res, dt), ops.Act.from_nchw(mul, dt)
+    out2 = ops.Act.new(N, H, W, Cout, dt, DEV)
+    y = ops.conv2d(p, A, B, a_up=2, residual=R, mul=M, out2=out2, out_dtype=torch.float32)
+    cat = torch.cat([F.interpolate(xa.to(dt).float(), scale_factor=2, mode="nearest"), xb.to(dt).float()], 1)
+    z = F.conv2d(cat.double(), w.to(dt).double(), padding=1)
+    z = F.batch_norm(z, bn.running_mean.double(), bn.running_var.double(), bn.weight.double(), bn.bias.double(),
+                     False, 0.0, bn.eps)
+    ref = (F.relu(z + res.to(dt).double()) * mul.to(dt).double()).float().cpu()
+    tol = 2e-5 if dt == torch.float32 else 1e-2
+    assert _rel(y.to_nchw().cpu(), ref) < tol
+    assert _rel(out2.to_nchw().cpu(), ref) < tol
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_conv_transpose_and_in_scale(dt):
+    from hiseg import ops
+    torch.manual_seed(2)
+    x = torch.randn(3, 64, 7, 5, device=DEV)
+    w = torch.randn(64, 32, 2, 2, device=DEV) / 8
+    b = torch.randn(32, device=DEV) * 0.1
+    y = ops.conv2d(ops.pack_convT2x2(w, b, None, 1, dt, DEV), ops.Act.from_nchw(x, dt)).to_nchw().cpu()
+    ref = F.relu(F.conv_transpose2d(x.to(dt).double(), w.to(dt).double(), b.double(), stride=2)).float().cpu()
+    assert _rel(y, ref) < (2e-5 if dt == torch.float32 else 1e-2)
+    g = torch.rand(3, 64, device=DEV)
+    w1 = torch.randn(40, 64, 1, 1, device=DEV) / 8
+    y = ops.conv2d(ops.pack_conv(w1, None, None, 0, dt, DEV), ops.Act.from_nchw(x, dt), in_scale=g).to_nchw().cpu()
+    xs = (x.to(dt).float() * g[:, :, None, None])
+    if dt == torch.bfloat16:
+        xs = xs.to(dt).float()
+    ref = F.conv2d(xs.double(), w1.to(dt).double()).float().cpu()
+    assert _rel(y, ref) < (2e-5 if dt == torch.float32 else 1e-2)
+
+
+# ------------------------------------------------------------------------------------------ misc kernels
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_pointwise_kernels(dt):
+    from hiseg import ops
+    torch.manual_seed(3)
+    x = torch.randn(2, 64, 10, 8, device=DEV)
+    xq = x.to(dt).float()
+    A = ops.Act.from_nchw(x, dt)
+    tol = 1e-5 if dt == torch.float32 else 1e-2
+    assert _rel(ops.maxpool2x2(A).to_nchw().cpu(), F.max_pool2d(xq, 2).cpu()) < tol
+    w7 = torch.randn(1, 2, 7, 7, device=DEV) * 0.2
+    s = torch.cat([xq.mean(1, keepdim=True), xq.max(1, keepdim=True)[0]], 1)
+    ref = (xq * torch.sigmoid(F.conv2d(s, w7, padding=3))).cpu()
+    assert _rel(ops.attn_spatial(A, w7.contiguous()).to_nchw().cpu(), ref) < tol * 2
+    w1, w2 = torch.randn(8, 64, device=DEV) * 0.2, torch.randn(64, 8, device=DEV) * 0.2
+    b1, b2 = torch.randn(8, device=DEV) * 0.1, torch.randn(64, device=DEV) * 0.1
+    for act, bias in ((1, False), (3, True)):
+        gate = ops.se_gate(A, w1, b1 if bias else None, w2, b2 if bias else None, act)
+        m = xq.mean((2, 3))
+        h = m @ w1.t() + (b1 if bias else 0)
+        h = F.relu(h) if act == 1 else F.silu(h)
+        ref_g = torch.sigmoid(h @ w2.t() + (b2 if bias else 0))
+        assert _rel(gate.cpu(), ref_g.cpu()) < 1e-4
+        out = ops.channel_scale(A, gate).to_nchw().cpu()
+        assert _rel(out, (xq * gate[:, :, None, None]).cpu()) < tol
+    for k, stride in ((3, 1), (5, 2), (3, 2)):
+        wd = torch.randn(64, 1, k, k, device=DEV) * 0.3
+        sc, sh = torch.rand(64, device=DEV) + 0.5, torch.randn(64, device=DEV) * 0.1
+        out = ops.dwconv(A, wd.view(64, k * k).t().contiguous(), sc, sh, k, stride, 3).to_nchw().cpu()
+        ref = F.silu(F.conv2d(xq, wd, stride=stride, padding=k // 2, groups=64) * sc[:, None, None] + sh[:, None, None])
+        assert _rel(out, ref.cpu()) < tol * 2
+
+
+def test_input_norm_device_flag():
+    from hiseg import ops
+    mean = torch.tensor([0.485, 0.456, 0.406], device=DEV)
+    std = torch.tensor([0.229, 0.224, 0.225], device=DEV)
+    for scale in (1.0, 255.0):
+        img = torch.rand(2, 3, 8, 6, device=DEV) * scale
+        a = ops.input_norm(img, mean, std, torch.float32)
+        x = img / 255.0 if img.max() > 1 else img
+        ref = (x - mean.view(1, 3, 1, 1)) / std.view(1, 3, 1, 1)
+        assert max_abs(a.to_nchw().cpu(), ref.cpu()) < 1e-5
+        assert torch.all(a.t.view(-1, a.cstride)[:, 3:] == 0)
+
+
+def test_export_mask_kernels_match_oracle():
+    from hiseg import ops
+    from oracle import rgb_model as O
+    torch.manual_seed(4)
+    logits = torch.randn(5, 3, 16, 12, device=DEV) * 3
+    for dil in (0, 1, 2):
+        got = ops.instance_masks(logits, dil).cpu()
+        ref = O.instance_masks(logits.cpu(), dil)
+        assert torch.equal(got, ref), dil
+    u = torch.randn(2, 1, 9, 7, device=DEV) * 4
+    w, b = torch.tensor([1.0, -1.0], device=DEV), torch.tensor([0.0, 0.0], device=DEV)
+    sd = {"pretrained_unet.output_conv.weight": w.view(2, 1, 1, 1).cpu(), "pretrained_unet.output_conv.bias": b.cpu()}
+    assert max_abs(ops.binary_masks(u, w, b).cpu(), O.binary_masks(sd, u.cpu())) < 1e-6
+
+
+# ------------------------------------------------------------------------------------------ blocks / head / model
+def _filled(m):
+    return filler.fill_module(m).eval()
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_residual_block_and_enhanced_unet_match_golden(dt):
+    import hiseg
+    from hiseg.layers import EnhancedUNet, ResidualBlock
+    g = load("blocks")
+    blk = hiseg.set_compute_dtype(_filled(ResidualBlock(64, "batchnorm", 8, "relu")).to(DEV), dt)
+    y = blk(torch.from_numpy(g["res_x"]).to(DEV)).cpu()
+    tol = F32_TOL if dt == torch.float32 else 3e-2
+    assert _rel(y, g["res_y"]) < tol
+    un = hiseg.set_compute_dtype(_filled(EnhancedUNet(256, 64, 3, "batchnorm", 8, "relu")).to(DEV), dt)
+    y = un(torch.from_numpy(g["unet_x"]).to(DEV)).cpu()
+    assert _rel(y, g["unet_y"]) < (F32_TOL if dt == torch.float32 else 5e-2)
+
+
+def _model(dt):
+    import hiseg
+    from hiseg import create_rgb_hierarchical_model
+    m = _filled(create_rgb_hierarchical_model(**hiseg_kwargs(b0_kwargs()))).to(DEV)
+    return hiseg.set_compute_dtype(m, dt)
+
+
+def test_head_matches_golden_f32():
+    import hiseg
+    from hiseg.layers import RefinedHierarchicalSegmentationHead
+    kw = b0_kwargs()
+    g = load("head_b0")
+    head = _filled(RefinedHierarchicalSegmentationHead(
+        256, 256, 3, tuple(kw["mask_size"]), use_attention_module=True, use_contour_detection=True,
+        use_distance_transform=True, normalization_type="batchnorm", activation_function="relu",
+        hierarchical_base_channels=kw["hierarchical_base_channels"], hierarchical_depth=kw["hierarchical_depth"])).to(DEV)
+    hiseg.set_compute_dtype(head, torch.float32)
+    x = torch.from_numpy(filler.normal(31, (2, 256, 64, 48))).to(DEV)
+    logits, aux = head(x)
+    assert _rel(logits.cpu(), g["logits"]) < F32_TOL
+    for k in ("bg_fg_logits", "bg_fg_logits_low", "target_nontarget_logits", "contours", "distance_mask",
+              "distance_map"):
+        assert _rel(aux[k].cpu(), g["aux_" + k]) < F32_TOL, k
+    for k in ("fg_attention", "shared_features"):
+        assert _rel(aux[k].mean(dim=(0, 2, 3)).cpu(), g[f"aux_{k}__chmean"]) < F32_TOL, k
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_model_matches_reference_golden(dt):
+    from hiseg import engine
+    g = load("model_b0")
+    model = _model(dt)
+    for m in (model.roi_align_mask, model.roi_align_rgb):
+        m.spatial_scale_h, m.spatial_scale_w = 96, 128
+    images, rois, u = (torch.from_numpy(g[k]).to(DEV) for k in ("images", "rois", "u"))
+    logits, aux = engine.rgb_model_forward(model, images, rois, "full", unet_logit_override=u)
+    ref = torch.from_numpy(g["logits"])
+    if dt == torch.float32:
+        assert _rel(logits.cpu(), ref) < F32_TOL
+        for k in ("bg_fg_logits", "target_nontarget_logits", "full_image_logits", "roi_features", "roi_patches",
+                  "contours", "distance_map", "distance_mask", "bg_fg_logits_low"):
+            assert _rel(aux[k].cpu(), g["aux_" + k]) < F32_TOL, k
+    else:
+        assert _rel(logits.cpu(), ref) < 0.1
+        agree = (logits.argmax(1) == ref.to(DEV).argmax(1)).float().mean().item()
+        assert agree > 0.97, agree
+    # training-semantics scale (640 scalar) on 640x640 inputs
+    for m in (model.roi_align_mask, model.roi_align_rgb):
+        m.spatial_scale_h = m.spatial_scale_w = 640.0
+    images = torch.from_numpy(filler.uniform(43, (1, 3, 640, 640))).to(DEV)
+    u = torch.from_numpy(filler.normal(44, (1, 1, 640, 640)) * 2.0).to(DEV)
+    logits, _ = engine.rgb_model_forward(model, images, torch.from_numpy(g["rois640"]).to(DEV), "none",
+                                         unet_logit_override=u)
+    tol = F32_TOL if dt == torch.float32 else 0.1
+    assert _rel(logits.cpu(), g["logits640"]) < tol
+
+
+def test_full_pipeline_with_effunet_matches_oracle():
+    """Whole path incl. the EfficientNet-B0 UNet (parity of that sub-network vs the restated oracle only)."""
+    from oracle import rgb_model as O
+    from hiseg import RGBHierarchicalExportWrapper
+    model = _model(torch.float32)
+    sd = O.np_state(model)
+    cfg = O.cfg_from_kwargs(b0_kwargs())
+    images = torch.from_numpy(filler.uniform(51, (2, 3, 96, 128)))
+    rois = torch.from_numpy(filler.box_rois(52, 2, 2))
+    for m in (model.roi_align_mask, model.roi_align_rgb):
+        m.spatial_scale_h, m.spatial_scale_w = 96, 128
+    logits, aux = model(images.to(DEV), rois.to(DEV))
+    with torch.no_grad():
+        ref_logits, ref_aux, ref_u = O.rgb_model(sd, images, rois, cfg, (96, 128), "b0")
+    assert _rel(aux["full_image_logits"].cpu(), ref_aux["full_image_logits"]) < F32_TOL
+    assert _rel(logits.cpu(), ref_logits) < F32_TOL
+    wrap = RGBHierarchicalExportWrapper(model)
+    inst, binary = wrap(images.to(DEV), rois.to(DEV))
+    assert inst.shape == (4, 1, 128, 96) and binary.shape == (2, 1, 96, 128)
+    ref_inst = O.instance_masks(ref_logits)
+    assert (inst.cpu() == ref_inst).float().mean().item() > 0.999
+    assert max_abs(binary.cpu(), O.binary_masks(sd, ref_u)) < 1e-4
+
+
+def test_bf16_pipeline_instance_mask_agreement():
+    from oracle import rgb_model as O
+    from hiseg import RGBHierarchicalExportWrapper
+    model = _model(torch.bfloat16)
+    sd = O.np_state(model)
+    cfg = O.cfg_from_kwargs(b0_kwargs())
+    images = torch.from_numpy(filler.uniform(61, (2, 3, 96, 128)))
+    rois = torch.from_numpy(filler.box_rois(62, 2, 2))
+    inst, binary = RGBHierarchicalExportWrapper(model)(images.to(DEV), rois.to(DEV))
+    with torch.no_grad():
+        ref_logits, _, ref_u = O.rgb_model(sd, images, rois, cfg, (96, 128), "b0")
+    agree = (inst.cpu() == O.instance_masks(ref_logits)).float().mean().item()
+    assert agree > 0.97, agree
+    assert max_abs(binary.cpu(), O.binary_masks(sd, ref_u)) < 0.05

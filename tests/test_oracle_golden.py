@@ -1,0 +1,147 @@
+"""The CPU oracle against golden vectors produced by the reference itself (tests/golden/gen_golden.py)."""
+import numpy as np
+import pytest
+import torch
+
+import filler
+from helpers import b0_kwargs, load, max_abs
+from oracle import rgb_model as O
+from oracle.roi_align import roi_align as roi_np
+
+
+def test_roi_align_matches_reference():
+    # 1e-5 absolute on [0,1] features: torch's CPU linspace takes a vectorised arange path whose
+    # last-ulp rounding depends on the host SIMD width; the oracle uses the scalar two-sided formula.
+    g = load("roi_align")
+    for i in range(5):
+        oh, ow, sh, sw, al = g[f"c{i}_meta"]
+        out = roi_np(g["feat"], g["rois"], int(oh), int(ow), sh, sw, bool(al))
+        assert max_abs(out, g[f"c{i}_out"]) < 1e-5, i
+    out2 = roi_np(g["feat2"], g["rois2"], 6, 4, 20, 20, True)
+    assert max_abs(out2, g["out2"]) < 1e-5
+
+
+def test_roi_align_edge_cases():
+    feat = np.ones((1, 1, 4, 4), np.float32)
+    # output 1x1 samples the ROI's top-left (linspace(0,1,1) == [0])
+    out = roi_np(feat, np.array([[0, .5, .5, .9, .9]], np.float32), 1, 1, 4, 4, True)
+    assert out.shape == (1, 1, 1, 1) and out[0, 0, 0, 0] == pytest.approx(1.0)
+    # aligned: x=1.0 maps one column past the last pixel -> half the taps are zero padding
+    out = roi_np(feat, np.array([[0, 1.0, 0.0, 1.0, 0.0]], np.float32), 1, 1, 4, 4, True)
+    assert out[0, 0, 0, 0] == pytest.approx(0.0)
+    # batch index out of range -> zeros; empty ROI list -> empty output
+    assert roi_np(feat, np.array([[3, 0, 0, 1, 1]], np.float32), 2, 2, 4, 4, True).sum() == 0
+    assert roi_np(feat, np.zeros((0, 5), np.float32), 2, 2, 4, 4, True).shape == (0, 1, 2, 2)
+
+
+def _sd(module):
+    return O.np_state(filler.fill_module(module).eval())
+
+
+def test_blocks_match_reference():
+    from hiseg.layers import EnhancedUNet, ResidualBlock
+    g = load("blocks")
+    sd = {"b." + k: v for k, v in _sd(ResidualBlock(64, "batchnorm", 8, "relu")).items()}
+    y = O.residual(sd, "b", torch.from_numpy(g["res_x"]), "relu")
+    assert max_abs(y, g["res_y"]) < 1e-5
+    sd = {"u." + k: v for k, v in _sd(EnhancedUNet(256, 64, 3, "batchnorm", 8, "relu")).items()}
+    y = O.enhanced_unet(sd, "u", torch.from_numpy(g["unet_x"]), 3, "relu")
+    assert max_abs(y, g["unet_y"]) < 1e-4
+
+
+def _hiseg_head(kw):
+    from hiseg.layers import RefinedHierarchicalSegmentationHead
+    ms = tuple(kw["mask_size"])
+    return RefinedHierarchicalSegmentationHead(
+        256, 256, 3, ms if ms[0] != ms[1] else ms[0], use_attention_module=kw["use_attention_module"],
+        use_contour_detection=kw["use_contour_detection"], use_distance_transform=kw["use_distance_transform"],
+        normalization_type=kw["normalization_type"], normalization_groups=kw["normalization_groups"],
+        activation_function=kw["activation_function"], activation_beta=kw["activation_beta"],
+        hierarchical_base_channels=kw["hierarchical_base_channels"], hierarchical_depth=kw["hierarchical_depth"])
+
+
+def check_aux(aux, g, prefix="aux_", tol=2e-4):
+    for k, v in aux.items():
+        if prefix + k in g.files:
+            assert max_abs(v, g[prefix + k]) < tol * max(1.0, float(np.abs(g[prefix + k]).max())), k
+        elif prefix + k + "__chmean" in g.files:
+            v = torch.as_tensor(v)
+            assert max_abs(v.mean(dim=(0, 2, 3)), g[prefix + k + "__chmean"]) < tol, k
+            assert max_abs(v.reshape(-1)[::997], g[prefix + k + "__sample"]) < tol * 10, k
+        else:
+            raise AssertionError(f"aux key {k} missing from golden")
+
+
+def test_head_matches_reference():
+    kw = b0_kwargs()
+    g = load("head_b0")
+    head = _hiseg_head(kw)
+    sd = {"h." + k: v for k, v in _sd(head).items()}
+    cfg = O.cfg_from_kwargs(kw)
+    x = torch.from_numpy(filler.normal(31, (2, 256) + tuple(cfg["roi_hw"])))
+    with torch.no_grad():
+        logits, aux = O.hier_head(sd, "h", x, cfg)
+    assert max_abs(logits, g["logits"]) < 2e-4 * float(np.abs(g["logits"]).max())
+    check_aux(aux, g)
+
+
+def _hiseg_model(kw):
+    from hiseg import create_rgb_hierarchical_model
+    from helpers import hiseg_kwargs
+    return filler.fill_module(create_rgb_hierarchical_model(**hiseg_kwargs(kw))).eval()
+
+
+def test_model_from_unet_matches_reference():
+    kw = b0_kwargs()
+    g = load("model_b0")
+    sd = O.np_state(_hiseg_model(kw))
+    cfg = O.cfg_from_kwargs(kw)
+    with torch.no_grad():
+        logits, aux = O.rgb_model_from_unet(sd, torch.from_numpy(g["images"]), torch.from_numpy(g["rois"]),
+                                            torch.from_numpy(g["u"]), cfg, (96, 128))
+    assert max_abs(logits, g["logits"]) < 2e-4 * float(np.abs(g["logits"]).max())
+    check_aux(aux, g)
+    images = torch.from_numpy(filler.uniform(43, (1, 3, 640, 640)))
+    u = torch.from_numpy(filler.normal(44, (1, 1, 640, 640)) * 2.0)
+    with torch.no_grad():
+        logits, _ = O.rgb_model_from_unet(sd, images, torch.from_numpy(g["rois640"]), u, cfg, (640.0, 640.0))
+    assert max_abs(logits, g["logits640"]) < 2e-4 * float(np.abs(g["logits640"]).max())
+
+
+def test_state_dict_keys_match_reference():
+    import json
+    import os
+    from conftest import GOLDEN
+    ref_keys = json.load(open(os.path.join(GOLDEN, "state_keys_b0_head.json")))
+    ours = list(_hiseg_model(b0_kwargs()).state_dict().keys())
+    # the reference was built with a parameter-free smp stand-in: compare everything outside the smp.Unet
+    ours_no_unet = [k for k in ours if not k.startswith("pretrained_unet.model.model.")]
+    assert ours_no_unet == ref_keys
+    for k in ref_keys:
+        assert k in ours
+
+
+@pytest.mark.parametrize("variant,n_enc", [("b0", 358), ("b1", 506), ("b7", 1198)])
+def test_effunet_key_counts_match_reference_heuristics(variant, n_enc):
+    """hierarchical_segmentation_unet.py:1815-1828 classifies B0 <400, B1 <540, B7 >=700 encoder keys."""
+    from hiseg.effunet import EfficientNetUnet
+    sd = EfficientNetUnet(f"timm-efficientnet-{variant}").state_dict()
+    enc = [k for k in sd if "encoder" in k]
+    assert len(enc) == n_enc
+    assert "decoder.blocks.0.conv1.0.weight" in sd and "segmentation_head.0.weight" in sd
+
+
+def test_effunet_oracle_runs_and_shapes():
+    from hiseg.effunet import EfficientNetUnet
+    net = filler.fill_module(EfficientNetUnet("timm-efficientnet-b0")).eval()
+    sd = {"n." + k: v for k, v in O.np_state(net).items()}
+    x = torch.from_numpy(filler.normal(5, (1, 3, 64, 96)))
+    with torch.no_grad():
+        y = O.effunet_logits(sd, "n", x, "b0")
+    assert y.shape == (1, 1, 64, 96) and torch.isfinite(y).all()
+
+
+def test_instance_and_binary_mask_semantics():
+    logits = torch.tensor([[[[0.0, 1.0]], [[1.0, 1.0]], [[0.5, 1.0]]]])  # ties resolve to the first index
+    m = O.instance_masks(logits)
+    assert m.tolist() == [[[[1.0, 0.0]]]]
