@@ -1,0 +1,196 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ROI-masks/s of the exported RGB hierarchical contract on MI355X.
+
+Workload (BASELINE.json configs[1], "C2"): B0 EfficientNet-UNet + refined hierarchical head,
+640x480 images, batch 32 per GPU x 8 ROIs per image (256 ROI masks per step), ROI 64x48,
+mask 128x96, bf16 compute, synthetic data, deterministic random-init weights of that
+architecture.  One step = RGBHierarchicalExportWrapper forward: full-image UNet, 2x RoIAlign,
+ROI head, instance_masks [256,1,128,96] + binary_masks [32,1,480,640].
+
+Multi-GPU: one process per GPU (torch.distributed.run), each rank processes its own 32 images
+(weak scaling, no data-path collective); barrier + synchronize around the K timed steps and the
+max over ranks of the elapsed time.
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "human-instance-segmentation_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+
+import torch  # noqa: E402
+
+METRIC = "ROI-masks/sec (fwd) + train step/s, B0 640×480×8-ROI, 1/2/4/8 MI355X"
+B, R, H, W = 32, 8, 480, 640
+ROI_HW, MASK_HW = (64, 48), (128, 96)
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
+# Algorithmic work per ROI mask: head 53.1 GFLOP (inference graph) + B0 UNet 27.7/8
+GFLOP_PER_ROI_MASK = 53.1 + 27.7 / 8
+
+B0_KWARGS = dict(
+    roi_size=ROI_HW, mask_size=MASK_HW, multi_scale=False, use_attention_module=True,
+    use_boundary_refinement=False, use_progressive_upsampling=False, use_subpixel_conv=False,
+    use_contour_detection=True, use_distance_transform=True, normalization_type="batchnorm",
+    normalization_groups=8, activation_function="relu", activation_beta=1.0, use_pretrained_unet=True,
+    pretrained_weights_path="ext_extractor/best_model_b0_0.8741.pth", freeze_pretrained_weights=True,
+    use_full_image_unet=True, encoder_name="timm-efficientnet-b0", hierarchical_base_channels=64,
+    hierarchical_depth=3)
+
+
+def build_model(device, dtype):
+    import filler
+    import hiseg
+    model = hiseg.create_rgb_hierarchical_model(**B0_KWARGS)
+    filler.fill_module(model).eval()
+    model = model.to(device)
+    hiseg.set_compute_dtype(model, dtype)
+    return model
+
+
+def synthetic_batch(device, rank):
+    import filler
+    g = torch.Generator().manual_seed(rank)
+    images = torch.rand(B, 3, H, W, generator=g).to(device)
+    rois = torch.from_numpy(filler.box_rois(1 + 1000 * rank, B, R)).to(device)
+    return images, rois
+
+
+def dominant_select(d):
+    """The dominant launch class: 256->256 3x3 conv at the ROI grid (9 launches/step, ~60 % of FLOPs)."""
+    if d.KH == 3 and d.Ca == 256 and d.Cb == 0 and d.Cout == 256 and (d.Ho, d.Wo) == ROI_HW and not d.convT:
+        return "conv3x3_256x256_roi"
+    return None
+
+
+def cpu_baseline(seconds_budget=30.0):
+    """The oracle (float32 CPU restatement of the reference path) on a bounded sample of the same
+    workload: 1 image 480x640 with 8 ROIs through UNet + ROI head (exported contract)."""
+    import filler
+    from oracle import rgb_model as O
+    import hiseg
+    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    model = hiseg.create_rgb_hierarchical_model(**B0_KWARGS)
+    filler.fill_module(model).eval()
+    sd = O.np_state(model)
+    cfg = O.cfg_from_kwargs(B0_KWARGS)
+    images = torch.rand(1, 3, H, W, generator=torch.Generator().manual_seed(0))
+    rois = torch.from_numpy(filler.box_rois(1, 1, R))
+    times = []
+    with torch.no_grad():
+        for i in range(3):
+            t0 = time.perf_counter()
+            logits, _, u = O.rgb_model(sd, images, rois, cfg, (H, W), "b0")
+            O.instance_masks(logits)
+            O.binary_masks(sd, u)
+            times.append(time.perf_counter() - t0)
+            if sum(times) > seconds_budget:
+                break
+    t = min(times[1:]) if len(times) > 1 else times[0]
+    return {"value": round(R / t, 3), "unit": "ROI-masks/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle/rgb_model.py fp32 CPU, 1 image 480x640 x {R} ROIs (UNet B0 + head + export masks), "
+                      f"best of {len(times) - 1 if len(times) > 1 else 1} after 1 warm-up, {t:.2f} s/iter"}
+
+
+def load_traffic():
+    """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3 PMC summary, if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            return json.load(f).get("dominant_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+
+    import hiseg
+    from hiseg import ops
+    model = build_model(device, dtype)
+    wrapper = hiseg.RGBHierarchicalExportWrapper(model)
+    images, rois = synthetic_batch(device, rank)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            wrapper(images, rois)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        probe = ops.LaunchProbe(dominant_select)
+        ops.PROBE = probe
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            inst, binary = wrapper(images, rois)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        ops.PROBE = None
+    assert inst.shape == (B * R, 1) + MASK_HW and binary.shape == (B, 1, H, W)
+
+    if dist:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    n = world
+    ms_per_step = elapsed / args.steps * 1e3
+    value = n * B * R * args.steps / elapsed
+
+    summ = probe.summary().get("conv3x3_256x256_roi")
+    roofline = None
+    if summ:
+        achieved = summ["flops"] / (summ["avg_ms"] * 1e-3) / 1e12
+        roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": load_traffic(),
+                    "kernel": "conv_igemm_kernel<bf16,128x128> 256->256 3x3 @64x48 x256 ROIs",
+                    "launches_timed": summ["launches"], "avg_launch_ms": round(summ["avg_ms"], 4),
+                    "flop_per_launch": summ["flops"]}
+    pipeline_tflops = value * GFLOP_PER_ROI_MASK / 1e3
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "ROI-masks/s", "n_gpus": n, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if dtype == torch.bfloat16 else "f32",
+            "data": "synthetic (U[0,1) images, SURVEY §8d ROI boxes; deterministic random-init B0 weights)",
+            "config": {"workload": "C2: B0 inference 640x480, batch 32/GPU x 8 ROIs/img, ROI 64x48, mask 128x96",
+                       "global_batch": B * n, "rois_per_step": B * R * n, "seq_len": None,
+                       "parallelism": f"dp{n} (images sharded, model replicated, no collective)"},
+            "pipeline_tflops": round(pipeline_tflops, 1),
+            "roofline": roofline,
+        }
+        if n == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -129,6 +129,39 @@ def roi_align(feat: torch.Tensor, rois: torch.Tensor, oh: int, ow: int, scale_h:
 
 
 # ---------------------------------------------------------------------------------------- conv
+class LaunchProbe:
+    """Optional per-launch HIP-event timing of selected conv launches (used by bench.py's roofline).
+
+    ``select(desc) -> key or None`` picks launches; events are recorded on the launch stream.
+    """
+
+    def __init__(self, select):
+        self.select = select
+        self.events = []  # (key, start, end, flops)
+
+    def around(self, key, flops, launch):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        st = launch()
+        e.record()
+        self.events.append((key, s, e, flops))
+        return st
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for key, s, e, fl in self.events:
+            d = out.setdefault(key, {"launches": 0, "ms": 0.0, "flops": fl})
+            d["launches"] += 1
+            d["ms"] += s.elapsed_time(e)
+        for d in out.values():
+            d["avg_ms"] = d["ms"] / d["launches"]
+        return out
+
+
+PROBE: Optional[LaunchProbe] = None
+
+
 @dataclass
 class ConvPlan:
     """A conv (or ConvTranspose 2x2/s2) layer packed for hiseg_conv2d_fwd."""
@@ -255,6 +288,13 @@ def conv2d(p: ConvPlan, xa: Act, xb: Optional[Act] = None, out: Optional[Act] = 
         assert out2.dtype == dt
         d.out2, d.o2_cstride, d.o2_coff = out2.ptr(), out2.cstride, out2.coff
     d.convT = int(p.convT)
+    if PROBE is not None:
+        key = PROBE.select(d)
+        if key is not None:
+            flops = 2.0 * d.N * d.Ho * d.Wo * p.gemm_cols * p.kh * p.kw * (xa.C + (xb.C if xb is not None else 0))
+            L.check(PROBE.around(key, flops, lambda: L.lib().hiseg_conv2d_fwd(ctypes.byref(d), L.stream_ptr())),
+                    "conv2d")
+            return out
     L.check(L.lib().hiseg_conv2d_fwd(ctypes.byref(d), L.stream_ptr()), "conv2d")
     return out
 
