@@ -1,0 +1,110 @@
+// Shared pieces of the implicit-GEMM conv kernels (GEMM view, epilogue).
+#pragma once
+#include "common.h"
+
+namespace hiseg {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+struct ConvArgs {
+  hiseg_conv2d_desc d;
+  int M;       // GEMM rows
+  int Cin;     // Ca + Cb
+  int nK;      // K blocks
+  int Hs, Ws;  // src-A grid
+};
+
+template <typename T>
+__device__ __forceinline__ void load4(const void* base, long long idx, bool vec, int nvalid,
+                                      float* v) {
+  if (vec) {
+    if constexpr (sizeof(T) == 4) {
+      float4 q = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(base) + idx);
+      v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+    } else {
+      uint2 q = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(base) + idx);
+      v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
+      v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = (e < nvalid) ? Elem<T>::load(base, idx + e) : 0.f;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void store4(void* base, long long idx, bool vec, int nvalid,
+                                       const float* v) {
+  if (vec) {
+    if constexpr (sizeof(T) == 4) {
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(base) + idx) =
+          make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+      uint2 q;
+      q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      q.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(base) + idx) = q;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (e < nvalid) Elem<T>::store(base, idx + e, v[e]);
+  }
+}
+
+__device__ __forceinline__ int swz(int row, int c) { return row * 8 + (c ^ ((row >> 1) & 7)); }
+
+template <typename T, typename TO>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, int px, int co, floatx4 acc) {
+  const hiseg_conv2d_desc& d = a.d;
+  float v[4] = {acc[0], acc[1], acc[2], acc[3]};
+  const int ncol = d.Cout - co;
+  if (ncol <= 0) return;
+  const int nv = ncol < 4 ? ncol : 4;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (e < nv) v[e] = v[e] * d.scale[co + e] + d.shift[co + e];
+  }
+  long long op;  // output pixel index
+  int oc;        // output channel
+  if (d.convT) {
+    const int Cq = d.Cout >> 2;
+    const int q = co / Cq;
+    oc = co - q * Cq;
+    const int x = px % d.Wo;
+    const int t = px / d.Wo;
+    const int y = t % d.Ho;
+    const int n = t / d.Ho;
+    op = ((long long)n * (2 * d.Ho) + 2 * y + (q >> 1)) * (2 * d.Wo) + 2 * x + (q & 1);
+  } else {
+    op = px;
+    oc = co;
+  }
+  if (d.residual) {
+    float r[4];
+    const bool vec = (nv == 4) && ((d.r_cstride | d.r_coff | oc) & 3) == 0;
+    load4<T>(d.residual, op * d.r_cstride + d.r_coff + oc, vec, nv, r);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] += r[e];
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], d.act);
+  if (d.mul) {
+    float m[4];
+    const bool vec = (nv == 4) && ((d.m_cstride | d.m_coff | oc) & 3) == 0;
+    load4<T>(d.mul, op * d.m_cstride + d.m_coff + oc, vec, nv, m);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] *= m[e];
+  }
+  {
+    const bool vec = (nv == 4) && ((d.o_cstride | d.o_coff | oc) & 3) == 0;
+    store4<TO>(d.out, op * d.o_cstride + d.o_coff + oc, vec, nv, v);
+  }
+  if (d.out2) {
+    const bool vec = (nv == 4) && ((d.o2_cstride | d.o2_coff | oc) & 3) == 0;
+    store4<T>(d.out2, op * d.o2_cstride + d.o2_coff + oc, vec, nv, v);
+  }
+}
+
+}  // namespace hiseg

@@ -18,112 +18,9 @@
 // groups of the fragment reads (MI355X_MICROARCH.md §LDS) and for the row-wise stores.
 // Two LDS stages; the next K block is gathered into registers while the current one feeds
 // the MFMAs (register-staged double buffering, one barrier per K block).
-#include "common.h"
+#include "conv_common.h"
 
 namespace hiseg {
-
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef float floatx4 __attribute__((ext_vector_type(4)));
-
-struct ConvArgs {
-  hiseg_conv2d_desc d;
-  int M;       // GEMM rows
-  int Cin;     // Ca + Cb
-  int nK;      // K blocks
-  int Hs, Ws;  // src-A grid
-};
-
-template <typename T>
-__device__ __forceinline__ void load4(const void* base, long long idx, bool vec, int nvalid,
-                                      float* v) {
-  if (vec) {
-    if constexpr (sizeof(T) == 4) {
-      float4 q = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(base) + idx);
-      v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
-    } else {
-      uint2 q = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(base) + idx);
-      v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
-      v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
-    }
-  } else {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = (e < nvalid) ? Elem<T>::load(base, idx + e) : 0.f;
-  }
-}
-
-template <typename T>
-__device__ __forceinline__ void store4(void* base, long long idx, bool vec, int nvalid,
-                                       const float* v) {
-  if (vec) {
-    if constexpr (sizeof(T) == 4) {
-      *reinterpret_cast<float4*>(reinterpret_cast<float*>(base) + idx) =
-          make_float4(v[0], v[1], v[2], v[3]);
-    } else {
-      uint2 q;
-      q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-      q.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-      *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(base) + idx) = q;
-    }
-  } else {
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      if (e < nvalid) Elem<T>::store(base, idx + e, v[e]);
-  }
-}
-
-__device__ __forceinline__ int swz(int row, int c) { return row * 8 + (c ^ ((row >> 1) & 7)); }
-
-template <typename T, typename TO>
-__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, int px, int co, floatx4 acc) {
-  const hiseg_conv2d_desc& d = a.d;
-  float v[4] = {acc[0], acc[1], acc[2], acc[3]};
-  const int ncol = d.Cout - co;
-  if (ncol <= 0) return;
-  const int nv = ncol < 4 ? ncol : 4;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    if (e < nv) v[e] = v[e] * d.scale[co + e] + d.shift[co + e];
-  }
-  long long op;  // output pixel index
-  int oc;        // output channel
-  if (d.convT) {
-    const int Cq = d.Cout >> 2;
-    const int q = co / Cq;
-    oc = co - q * Cq;
-    const int x = px % d.Wo;
-    const int t = px / d.Wo;
-    const int y = t % d.Ho;
-    const int n = t / d.Ho;
-    op = ((long long)n * (2 * d.Ho) + 2 * y + (q >> 1)) * (2 * d.Wo) + 2 * x + (q & 1);
-  } else {
-    op = px;
-    oc = co;
-  }
-  if (d.residual) {
-    float r[4];
-    const bool vec = (nv == 4) && ((d.r_cstride | d.r_coff | oc) & 3) == 0;
-    load4<T>(d.residual, op * d.r_cstride + d.r_coff + oc, vec, nv, r);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] += r[e];
-  }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], d.act);
-  if (d.mul) {
-    float m[4];
-    const bool vec = (nv == 4) && ((d.m_cstride | d.m_coff | oc) & 3) == 0;
-    load4<T>(d.mul, op * d.m_cstride + d.m_coff + oc, vec, nv, m);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] *= m[e];
-  }
-  {
-    const bool vec = (nv == 4) && ((d.o_cstride | d.o_coff | oc) & 3) == 0;
-    store4<TO>(d.out, op * d.o_cstride + d.o_coff + oc, vec, nv, v);
-  }
-  if (d.out2) {
-    const bool vec = (nv == 4) && ((d.o2_cstride | d.o2_coff | oc) & 3) == 0;
-    store4<T>(d.out2, op * d.o2_cstride + d.o2_coff + oc, vec, nv, v);
-  }
-}
 
 template <typename T, typename TO, int BCO, int BPX, int WCO, int WPX>
 __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
@@ -322,11 +219,28 @@ static int launch_typed(const ConvArgs& a, hipStream_t s) {
 
 }  // namespace hiseg
 
+namespace hiseg {
+int conv_fast_try(const ConvArgs& a, hipStream_t s, int variant);
+int conv_halo_try(const ConvArgs& a, hipStream_t s, int variant);
+int conv_halo2_try(const ConvArgs& a, hipStream_t s, int variant);
+int conv_halo3_try(const ConvArgs& a, hipStream_t s, int variant);
+}
+
 using namespace hiseg;
 
 static bool al16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int variant);
+
 extern "C" int hiseg_conv2d_fwd(const hiseg_conv2d_desc* d, hiseg_stream_t stream) {
+  return conv2d_impl(d, stream, 0);
+}
+
+extern "C" int hiseg_conv2d_fwd_variant(const hiseg_conv2d_desc* d, int variant, hiseg_stream_t stream) {
+  return conv2d_impl(d, stream, variant);
+}
+
+static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int variant) {
   HISEG_REQUIRE(d != nullptr, HISEG_ERR_BAD_ARG, "conv2d: null descriptor");
   HISEG_REQUIRE(d->dtype == HISEG_F32 || d->dtype == HISEG_BF16, HISEG_ERR_BAD_DTYPE, "conv2d: dtype %d", d->dtype);
   HISEG_REQUIRE(d->out_dtype == HISEG_F32 || d->out_dtype == HISEG_BF16, HISEG_ERR_BAD_DTYPE, "conv2d: out_dtype %d", d->out_dtype);
@@ -360,6 +274,24 @@ extern "C" int hiseg_conv2d_fwd(const hiseg_conv2d_desc* d, hiseg_stream_t strea
   a.Hs = d->H / d->a_up;
   a.Ws = d->W / d->a_up;
   hipStream_t s = (hipStream_t)stream;
+  // Automatic choice (variant 0) = the fastest measured configuration per layer class
+  // (tools/conv_bench.py): LDS-DMA ring kernel, 128x128 tiles for Cout >= 128, 64x128 for 64.
+  // Experimental kernels (halo / halo2 / halo3) run only when forced by variant.
+  if (variant >= 30) {
+    const int r = conv_halo3_try(a, s, variant);
+    if (r != 0) return r < 0 ? r : HISEG_OK;
+  } else if (variant >= 20) {
+    const int r = conv_halo2_try(a, s, variant);
+    if (r != 0) return r < 0 ? r : HISEG_OK;
+  } else if (variant >= 10 && variant != 18 && variant != 19) {
+    const int r = conv_halo_try(a, s, variant);
+    if (r != 0) return r < 0 ? r : HISEG_OK;
+  } else if (variant >= 0) {
+    int v = variant;
+    if (v == 0) v = (d->Cout_pad % 128 == 0) ? 4 : 8;
+    const int r = conv_fast_try(a, s, v);
+    if (r != 0) return r < 0 ? r : HISEG_OK;
+  }
   if (d->dtype == HISEG_BF16) {
     return d->out_dtype == HISEG_BF16 ? launch_typed<bf16_t, bf16_t>(a, s) : launch_typed<bf16_t, float>(a, s);
   }

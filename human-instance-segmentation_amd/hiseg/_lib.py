@@ -55,6 +55,7 @@ class Conv2dDesc(ctypes.Structure):
         ("out", c_void_p), ("o_cstride", c_int), ("o_coff", c_int),
         ("out2", c_void_p), ("o2_cstride", c_int), ("o2_coff", c_int),
         ("convT", c_int),
+        ("weight_frag", c_void_p),
     ]
 
 
@@ -74,6 +75,7 @@ def _declare(lib):
         "hiseg_built_for_gfx950": ([], c_int),
         "hiseg_roi_align_fwd": ([ctypes.POINTER(RoiAlignDesc), P], c_int),
         "hiseg_conv2d_fwd": ([ctypes.POINTER(Conv2dDesc), P], c_int),
+        "hiseg_conv2d_fwd_variant": ([ctypes.POINTER(Conv2dDesc), c_int, P], c_int),
         "hiseg_maxpool2x2_fwd": ([c_int, P, c_int, c_int, c_int, c_int, P, P], c_int),
         "hiseg_attn_spatial_fwd": ([c_int, P, c_int, c_int, c_int, c_int, P, c_int, P, P, P, P], c_int),
         "hiseg_gap_splits": ([c_int], c_int),

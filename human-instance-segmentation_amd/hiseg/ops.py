@@ -180,6 +180,7 @@ class ConvPlan:
     k_pad: int
     act: int
     convT: bool = False
+    weight_frag: Optional[torch.Tensor] = None  # MFMA-fragment order (3x3 halo kernel), bf16 only
 
 
 def pack_conv(weight: torch.Tensor, bias: Optional[torch.Tensor], bn: Optional[torch.nn.BatchNorm2d], act: int,
@@ -209,8 +210,24 @@ def pack_conv(weight: torch.Tensor, bias: Optional[torch.Tensor], bn: Optional[t
     sc = torch.zeros(cout_pad, dtype=torch.float32, device=w.device)
     sh = torch.zeros(cout_pad, dtype=torch.float32, device=w.device)
     sc[:cout], sh[:cout] = scale, shift
+    frag = None
+    if dtype == torch.bfloat16 and kh == 3 and kw == 3 and stride == 1 and ca % 64 == 0 and cb % 64 == 0 and k == k_pad:
+        frag = frag_pack(wp, kh * kw, ca + cb).to(device=device, dtype=dtype).contiguous()
     return ConvPlan(wp.to(device=device, dtype=dtype).contiguous(), sc.to(device), sh.to(device), kh, kw, stride, pad,
-                    ca, cb, cout, cout, cout_pad, k_pad, act)
+                    ca, cb, cout, cout, cout_pad, k_pad, act, weight_frag=frag)
+
+
+def frag_pack(wp: torch.Tensor, taps: int, cin: int) -> torch.Tensor:
+    """[Cout_pad][taps*cin] -> MFMA A-fragment order [Cout_pad/16][cb][tap][s][lane(64)][8].
+
+    K blocks run channel-block-major, tap-minor (the halo kernel's loop order); inside a K block,
+    k-step s covers channels 32s..32s+31 and lane l holds row l&15, channels 8(l>>4)..+7
+    (v_mfma_f32_16x16x32_bf16 A-operand map, cdna_hip_programming.md §3).
+    """
+    cp = wp.shape[0]
+    v = wp.reshape(cp // 16, 16, taps, cin // 64, 2, 4, 8)      # ct, row, tap, cb, s, lg, e
+    v = v.permute(0, 3, 2, 4, 5, 1, 6)                           # ct, cb, tap, s, lg, row, e
+    return v.reshape(-1)
 
 
 def pack_convT2x2(weight: torch.Tensor, bias: Optional[torch.Tensor], bn, act: int, dtype, device) -> ConvPlan:
@@ -288,6 +305,8 @@ def conv2d(p: ConvPlan, xa: Act, xb: Optional[Act] = None, out: Optional[Act] = 
         assert out2.dtype == dt
         d.out2, d.o2_cstride, d.o2_coff = out2.ptr(), out2.cstride, out2.coff
     d.convT = int(p.convT)
+    if p.weight_frag is not None:
+        d.weight_frag = p.weight_frag.data_ptr()
     if PROBE is not None:
         key = PROBE.select(d)
         if key is not None:

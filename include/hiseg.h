@@ -110,8 +110,15 @@ typedef struct hiseg_conv2d_desc {
   void* out; int o_cstride, o_coff;
   void* out2; int o2_cstride, o2_coff;
   int convT;
+  /* Optional second copy of the weights in MFMA-fragment order ([Cout_pad/16][nK][2][64][8],
+   * nK = K_pad/64 K blocks in channel-block-major / tap-minor order) used by the 3x3 halo
+   * kernel that streams weights straight into registers; null disables that kernel. */
+  const void* weight_frag;
 } hiseg_conv2d_desc;
 int hiseg_conv2d_fwd(const hiseg_conv2d_desc* d, hiseg_stream_t stream);
+/* Tuning/test entry: variant -1 forces the generic kernel, 0 = automatic choice (as
+ * hiseg_conv2d_fwd), k > 0 selects pipelined-kernel configuration k when the layer qualifies. */
+int hiseg_conv2d_fwd_variant(const hiseg_conv2d_desc* d, int variant, hiseg_stream_t stream);
 
 /* MaxPool2d(2) on NHWC (hierarchical_segmentation_unet.py:331-332,391).
  * in [N, H, W, C] (cstride == C), out [N, H/2, W/2, C]. */

@@ -1,0 +1,124 @@
+"""A/B timing of libhiseg conv kernel variants on the path's conv shapes (developer tool, GPU).
+
+For every shape: checks each variant against the generic kernel (variant -1), then times all
+variants in interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24).
+Usage: python tools/conv_bench.py [--variants -1,0,1,2] [--reps 20] [--rounds 3]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "human-instance-segmentation_amd"))
+import torch  # noqa: E402
+
+from hiseg import _lib as L  # noqa: E402
+from hiseg import ops  # noqa: E402
+
+DEV = "cuda"
+# name: (N, Ca, Cb, Cout, H, W, k, residual)
+SHAPES = {
+    "res256_3x3_64x48": (256, 256, 0, 256, 64, 48, 3, True),
+    "res128_3x3_128x96": (256, 128, 0, 128, 128, 96, 3, True),
+    "c128to256_3x3_64x48": (256, 128, 0, 256, 64, 48, 3, False),
+    "res64_3x3_64x48": (256, 64, 0, 64, 64, 48, 3, True),
+    "dec_128+128to128_3x3_32x24": (256, 128, 128, 128, 32, 24, 3, False),
+    "c256to256_1x1_64x48": (256, 256, 0, 256, 64, 48, 1, False),
+    "c256to64_3x3_64x48": (256, 256, 0, 64, 64, 48, 3, False),
+    "res256_3x3_16x12": (256, 256, 0, 256, 16, 12, 3, True),
+}
+
+
+def make(shape, dt):
+    N, Ca, Cb, Cout, H, W, k, res = shape
+    g = torch.Generator(device=DEV).manual_seed(0)
+    xa = ops.Act.new(N, H, W, Ca, dt, DEV, zero=False)
+    xa.t.copy_(torch.randn(xa.t.numel(), device=DEV, generator=g))
+    xb = None
+    if Cb:
+        xb = ops.Act.new(N, H, W, Cb, dt, DEV, zero=False)
+        xb.t.copy_(torch.randn(xb.t.numel(), device=DEV, generator=g))
+    w = torch.randn(Cout, Ca + Cb, k, k, device=DEV, generator=g) / ((Ca + Cb) * k * k) ** 0.5
+    b = torch.randn(Cout, device=DEV, generator=g) * 0.1
+    p = ops.pack_conv(w, b, None, 1, dt, DEV, pad=k // 2, split=(Ca, Cb) if Cb else None)
+    r = None
+    if res:
+        r = ops.Act.new(N, H, W, Cout, dt, DEV, zero=False)
+        r.t.copy_(torch.randn(r.t.numel(), device=DEV, generator=g))
+    out = ops.Act.new(N, H, W, Cout, dt, DEV, zero=False)
+    return p, xa, xb, r, out
+
+
+def desc(p, xa, xb, r, out):
+    d = L.Conv2dDesc()
+    d.dtype = d.out_dtype = ops.hdtype(xa.dtype)
+    d.N, d.H, d.W, d.Ho, d.Wo = xa.N, xa.H, xa.W, xa.H, xa.W
+    d.KH, d.KW, d.stride, d.pad = p.kh, p.kw, 1, p.pad
+    d.srcA, d.a_cstride, d.a_coff, d.Ca, d.a_up = xa.ptr(), xa.cstride, 0, p.ca, 1
+    if xb is not None:
+        d.srcB, d.b_cstride, d.b_coff, d.Cb = xb.ptr(), xb.cstride, 0, p.cb
+    d.weight, d.Cout, d.Cout_pad, d.K_pad = p.weight.data_ptr(), p.gemm_cols, p.cout_pad, p.k_pad
+    d.scale, d.shift, d.act = p.scale.data_ptr(), p.shift.data_ptr(), p.act
+    if r is not None:
+        d.residual, d.r_cstride, d.r_coff = r.ptr(), r.cstride, 0
+    d.out, d.o_cstride, d.o_coff = out.ptr(), out.cstride, 0
+    if p.weight_frag is not None:
+        d.weight_frag = p.weight_frag.data_ptr()
+    return d
+
+
+def run(d, v):
+    L.check(L.lib().hiseg_conv2d_fwd_variant(ctypes.byref(d), v, L.stream_ptr()), f"conv variant {v}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="-1,0,1,2,4")
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--shapes", default=",".join(SHAPES))
+    args = ap.parse_args()
+    variants = [int(v) for v in args.variants.split(",")]
+    results = {}
+    for name in args.shapes.split(","):
+        shape = SHAPES[name]
+        N, Ca, Cb, Cout, H, W, k, res = shape
+        flops = 2.0 * N * H * W * Cout * k * k * (Ca + Cb)
+        p, xa, xb, r, out = make(shape, torch.bfloat16)
+        d = desc(p, xa, xb, r, out)
+        run(d, -1)
+        torch.cuda.synchronize()
+        ref = out.t.float().clone()
+        ok = {}
+        for v in variants:
+            out.t.fill_(float("nan"))
+            run(d, v)
+            torch.cuda.synchronize()
+            err = ((out.t.float() - ref).abs().max() / ref.abs().max()).item()
+            ok[v] = err
+        times = {v: [] for v in variants}
+        for _ in range(args.rounds):
+            for v in variants:
+                for _ in range(3):
+                    run(d, v)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(args.reps):
+                    run(d, v)
+                e1.record()
+                torch.cuda.synchronize()
+                times[v].append(e0.elapsed_time(e1) / args.reps)
+        row = {}
+        for v in variants:
+            ms = min(times[v])
+            row[str(v)] = {"ms": round(ms, 4), "tflops": round(flops / ms / 1e9, 1), "rel_err_vs_generic": ok[v]}
+        results[name] = row
+        print(name, json.dumps(row), flush=True)
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/conv_bench.json", "w") as f:
+        json.dump(results, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
