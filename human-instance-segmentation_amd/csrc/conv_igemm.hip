@@ -224,6 +224,7 @@ int conv_fast_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_halo_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_halo2_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_halo3_try(const ConvArgs& a, hipStream_t s, int variant);
+int conv_8ph_try(const ConvArgs& a, hipStream_t s, int variant);
 }
 
 using namespace hiseg;
@@ -277,7 +278,10 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
   // Automatic choice (variant 0) = the fastest measured configuration per layer class
   // (tools/conv_bench.py): LDS-DMA ring kernel, 128x128 tiles for Cout >= 128, 64x128 for 64.
   // Experimental kernels (halo / halo2 / halo3) run only when forced by variant.
-  if (variant >= 30) {
+  if (variant >= 40) {
+    const int r = conv_8ph_try(a, s, variant);
+    if (r != 0) return r < 0 ? r : HISEG_OK;
+  } else if (variant >= 30) {
     const int r = conv_halo3_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
   } else if (variant >= 20) {
