@@ -237,7 +237,7 @@ __global__ void __launch_bounds__(512) conv_8ph_kernel(ConvArgs a) {
   if constexpr (STAMP) st2 = stamp8();
 
   // ---- epilogue
-  const bool fast_ep = !d.convT && (d.Cout & 3) == 0 &&
+  const bool fast_ep = (!d.convT || ((d.Cout >> 2) & 3) == 0) && (d.Cout & 3) == 0 &&
                        ((d.o_cstride | d.o_coff) & 3) == 0 && (!d.out2 || ((d.o2_cstride | d.o2_coff) & 3) == 0) &&
                        (!d.residual || ((d.r_cstride | d.r_coff) & 3) == 0) &&
                        (!d.mul || ((d.m_cstride | d.m_coff) & 3) == 0) &&
@@ -256,12 +256,15 @@ __global__ void __launch_bounds__(512) conv_8ph_kernel(ConvArgs a) {
           const int cc = co < d.Cout ? co : 0;
           int px = px0 + wc * 64 + j * 16 + (lane & 15);
           px = px < a.M ? px : a.M - 1;
+          long long op;
+          int oc;
+          out_site(d, px, cc, op, oc);
           er[i][j] = make_uint2(0u, 0u);
           em[i][j] = make_uint2(0u, 0u);
           if (has_res)
-            er[i][j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(d.residual) + (long long)px * d.r_cstride + d.r_coff + cc);
+            er[i][j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(d.residual) + op * d.r_cstride + d.r_coff + oc);
           if (has_mul)
-            em[i][j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(d.mul) + (long long)px * d.m_cstride + d.m_coff + cc);
+            em[i][j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(d.mul) + op * d.m_cstride + d.m_coff + oc);
         }
 #pragma clang loop unroll(full)
       for (int i = 0; i < 4; ++i) {
@@ -273,6 +276,9 @@ __global__ void __launch_bounds__(512) conv_8ph_kernel(ConvArgs a) {
         for (int j = 0; j < 4; ++j) {
           const int px = px0 + wc * 64 + j * 16 + (lane & 15);
           if (px >= a.M || co >= d.Cout) continue;
+          long long op;
+          int oc;
+          out_site(d, px, co, op, oc);
           const floatx4 ac = acc[hh * 4 + i][j];
           float v[4] = {ac[0] * sc.x + sh.x, ac[1] * sc.y + sh.y, ac[2] * sc.z + sh.z, ac[3] * sc.w + sh.w};
           if (has_res) {
@@ -290,9 +296,9 @@ __global__ void __launch_bounds__(512) conv_8ph_kernel(ConvArgs a) {
           uint2 o;
           o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
           o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(d.out) + (long long)px * d.o_cstride + d.o_coff + co) = o;
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(d.out) + op * d.o_cstride + d.o_coff + oc) = o;
           if (out2)
-            *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out2) + (long long)px * d.o2_cstride + d.o2_coff + co) = o;
+            *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out2) + op * d.o2_cstride + d.o2_coff + oc) = o;
         }
       }
     }

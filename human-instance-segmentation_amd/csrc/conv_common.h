@@ -55,19 +55,9 @@ __device__ __forceinline__ void store4(void* base, long long idx, bool vec, int 
 
 __device__ __forceinline__ int swz(int row, int c) { return row * 8 + (c ^ ((row >> 1) & 7)); }
 
-template <typename T, typename TO>
-__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, int px, int co, floatx4 acc) {
-  const hiseg_conv2d_desc& d = a.d;
-  float v[4] = {acc[0], acc[1], acc[2], acc[3]};
-  const int ncol = d.Cout - co;
-  if (ncol <= 0) return;
-  const int nv = ncol < 4 ? ncol : 4;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    if (e < nv) v[e] = v[e] * d.scale[co + e] + d.shift[co + e];
-  }
-  long long op;  // output pixel index
-  int oc;        // output channel
+// Output site of GEMM element (px, co): (op, oc) = (px, co), or for a ConvTranspose 2x2/s2 GEMM
+// (columns q*Cout/4 + oc, q = 2*dy + dx) the scattered full-resolution pixel.
+__device__ __forceinline__ void out_site(const hiseg_conv2d_desc& d, int px, int co, long long& op, int& oc) {
   if (d.convT) {
     const int Cq = d.Cout >> 2;
     const int q = co / Cq;
@@ -81,6 +71,22 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, int px, int co,
     op = px;
     oc = co;
   }
+}
+
+template <typename T, typename TO>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, int px, int co, floatx4 acc) {
+  const hiseg_conv2d_desc& d = a.d;
+  float v[4] = {acc[0], acc[1], acc[2], acc[3]};
+  const int ncol = d.Cout - co;
+  if (ncol <= 0) return;
+  const int nv = ncol < 4 ? ncol : 4;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (e < nv) v[e] = v[e] * d.scale[co + e] + d.shift[co + e];
+  }
+  long long op;  // output pixel index
+  int oc;        // output channel
+  out_site(d, px, co, op, oc);
   if (d.residual) {
     float r[4];
     const bool vec = (nv == 4) && ((d.r_cstride | d.r_coff | oc) & 3) == 0;

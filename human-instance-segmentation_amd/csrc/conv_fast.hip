@@ -138,7 +138,7 @@ __global__ void __launch_bounds__(64 * WCO * WPX) conv_fast_kernel(ConvArgs a) {
   // latency hides under the K loop; issued as plain loads, they are older than every DMA of
   // the ring, and the loop's counted vmcnt waits stay exact (in-order return).  Fast path:
   // plain NHWC output (no convT scatter), Cout % 4 == 0, 8-B aligned channel views.
-  const bool fast_ep = !d.convT && (d.Cout & 3) == 0 &&
+  const bool fast_ep = (!d.convT || ((d.Cout >> 2) & 3) == 0) && (d.Cout & 3) == 0 &&
                        ((d.o_cstride | d.o_coff) & 3) == 0 && (!d.out2 || ((d.o2_cstride | d.o2_coff) & 3) == 0) &&
                        (!d.residual || ((d.r_cstride | d.r_coff) & 3) == 0) &&
                        (!d.mul || ((d.m_cstride | d.m_coff) & 3) == 0) &&
@@ -157,14 +157,17 @@ __global__ void __launch_bounds__(64 * WCO * WPX) conv_fast_kernel(ConvArgs a) {
       for (int j = 0; j < TN; ++j) {
         int px = px0 + wpx * TN * 16 + j * 16 + (lane & 15);
         px = px < a.M ? px : a.M - 1;
+        long long op;
+        int oc;
+        out_site(d, px, cc, op, oc);
         eres[i][j] = make_uint2(0u, 0u);
         emul[i][j] = make_uint2(0u, 0u);
         if (d.residual)
           eres[i][j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(d.residual) +
-                                                       (long long)px * d.r_cstride + d.r_coff + cc);
+                                                       op * d.r_cstride + d.r_coff + oc);
         if (d.mul)
           emul[i][j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(d.mul) +
-                                                       (long long)px * d.m_cstride + d.m_coff + cc);
+                                                       op * d.m_cstride + d.m_coff + oc);
       }
     }
   }
@@ -224,6 +227,9 @@ __global__ void __launch_bounds__(64 * WCO * WPX) conv_fast_kernel(ConvArgs a) {
         const int px = px0 + wpx * TN * 16 + j * 16 + (lane & 15);
         const int co = co0 + wco * TM * 16 + i * 16 + (lane >> 4) * 4;
         if (px >= a.M || co >= d.Cout) continue;
+        long long op;
+        int oc;
+        out_site(d, px, co, op, oc);
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * esc[i][e] + esh[i][e];
@@ -242,9 +248,9 @@ __global__ void __launch_bounds__(64 * WCO * WPX) conv_fast_kernel(ConvArgs a) {
         uint2 o;
         o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
         o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(d.out) + (long long)px * d.o_cstride + d.o_coff + co) = o;
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(d.out) + op * d.o_cstride + d.o_coff + oc) = o;
         if (out2)
-          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out2) + (long long)px * d.o2_cstride + d.o2_coff + co) = o;
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out2) + op * d.o2_cstride + d.o2_coff + oc) = o;
       }
   } else {
     ConvArgs ae = a;

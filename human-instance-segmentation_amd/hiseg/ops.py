@@ -160,6 +160,9 @@ class LaunchProbe:
 
 
 PROBE: Optional[LaunchProbe] = None
+# Developer hook (tools/layer_profile.py): when a list, every conv launch appends
+# (descriptor copy, tensors kept alive, flops).
+RECORD: Optional[list] = None
 
 
 @dataclass
@@ -268,8 +271,12 @@ def fold_affine(cout: int, bias: Optional[torch.Tensor], bn, device):
 
 def conv2d(p: ConvPlan, xa: Act, xb: Optional[Act] = None, out: Optional[Act] = None, *, a_up: int = 1,
            residual: Optional[Act] = None, mul: Optional[Act] = None, out2: Optional[Act] = None,
-           in_scale: Optional[torch.Tensor] = None, out_dtype: Optional[torch.dtype] = None) -> Act:
-    """hiseg_conv2d_fwd.  Returns the output Act (allocated when ``out`` is None)."""
+           in_scale: Optional[torch.Tensor] = None, out_dtype: Optional[torch.dtype] = None,
+           variant: int = 0) -> Act:
+    """hiseg_conv2d_fwd.  Returns the output Act (allocated when ``out`` is None).
+
+    ``variant`` != 0 forces a kernel variant (hiseg_conv2d_fwd_variant; -1 = generic kernel).
+    """
     dt = xa.dtype
     H, W = xa.H * a_up, xa.W * a_up
     if xb is not None:
@@ -307,6 +314,11 @@ def conv2d(p: ConvPlan, xa: Act, xb: Optional[Act] = None, out: Optional[Act] = 
     d.convT = int(p.convT)
     if p.weight_frag is not None:
         d.weight_frag = p.weight_frag.data_ptr()
+    if RECORD is not None:
+        dc = L.Conv2dDesc.from_buffer_copy(d)
+        keep = [t for t in (xa, xb, out, residual, mul, out2) if t is not None]
+        flops = 2.0 * d.N * d.Ho * d.Wo * p.gemm_cols * p.kh * p.kw * (xa.C + (xb.C if xb is not None else 0))
+        RECORD.append((dc, keep, p, flops))
     if PROBE is not None:
         key = PROBE.select(d)
         if key is not None:
@@ -314,7 +326,10 @@ def conv2d(p: ConvPlan, xa: Act, xb: Optional[Act] = None, out: Optional[Act] = 
             L.check(PROBE.around(key, flops, lambda: L.lib().hiseg_conv2d_fwd(ctypes.byref(d), L.stream_ptr())),
                     "conv2d")
             return out
-    L.check(L.lib().hiseg_conv2d_fwd(ctypes.byref(d), L.stream_ptr()), "conv2d")
+    if variant:
+        L.check(L.lib().hiseg_conv2d_fwd_variant(ctypes.byref(d), variant, L.stream_ptr()), "conv2d")
+    else:
+        L.check(L.lib().hiseg_conv2d_fwd(ctypes.byref(d), L.stream_ptr()), "conv2d")
     return out
 
 

@@ -149,6 +149,53 @@ def test_conv_transpose_and_in_scale(dt):
     assert _rel(y, ref) < (2e-5 if dt == torch.float32 else 1e-2)
 
 
+# Every bf16 kernel variant must reproduce the generic kernel bit for bit: same K order per
+# accumulator, same fp32 epilogue.  name: (N, Ca, Cb, Cout, H, W, k, convT, residual, mul, out2)
+VARIANT_CASES = {
+    "3x3_256_res_mul_out2": (3, 256, 0, 256, 13, 11, 3, False, True, True, True),
+    "3x3_128+128": (2, 128, 128, 128, 9, 7, 3, False, False, False, False),
+    "3x3_64_ragged": (3, 64, 0, 64, 7, 5, 3, False, True, False, False),
+    "1x1_256_cout120": (2, 256, 0, 120, 10, 9, 1, False, True, False, False),
+    "3x3_128_cout250": (2, 128, 0, 250, 9, 8, 3, False, True, False, True),
+    "convT_128_to_64": (2, 128, 0, 64, 6, 5, 1, True, False, False, False),
+    "convT_256_to_128_res": (2, 256, 0, 128, 5, 7, 1, True, True, False, False),
+}
+
+
+@pytest.mark.parametrize("name", list(VARIANT_CASES))
+def test_conv_kernel_variants_bit_identical(name):
+    from hiseg import ops
+    N, Ca, Cb, Cout, H, W, k, convT, res, mul, o2 = VARIANT_CASES[name]
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(7)
+    xa = ops.Act.from_nchw(torch.randn(N, Ca, H, W, device=DEV, generator=g), dt)
+    xb = ops.Act.from_nchw(torch.randn(N, Cb, H, W, device=DEV, generator=g), dt) if Cb else None
+    if convT:
+        w = torch.randn(Ca, Cout, 2, 2, device=DEV, generator=g) / Ca ** 0.5
+        p = ops.pack_convT2x2(w, torch.randn(Cout, device=DEV, generator=g), None, 1, dt, DEV)
+        oH, oW = 2 * H, 2 * W
+    else:
+        w = torch.randn(Cout, Ca + Cb, k, k, device=DEV, generator=g) / ((Ca + Cb) * k * k) ** 0.5
+        bn = torch.nn.BatchNorm2d(Cout).to(DEV).eval()
+        filler.fill_module(bn)
+        p = ops.pack_conv(w, None, bn, 1, dt, DEV, pad=k // 2, split=(Ca, Cb) if Cb else None)
+        oH, oW = H, W
+    R = ops.Act.from_nchw(torch.randn(N, Cout, oH, oW, device=DEV, generator=g), dt) if res else None
+    M = ops.Act.from_nchw(torch.rand(N, Cout, oH, oW, device=DEV, generator=g), dt) if mul else None
+    outs = {}
+    for v in (-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 40, 42, 43):
+        o2a = ops.Act.new(N, oH, oW, Cout, dt, DEV) if o2 else None
+        y = ops.conv2d(p, xa, xb, residual=R, mul=M, out2=o2a, variant=v)
+        torch.cuda.synchronize()
+        outs[v] = (y.t.clone(), None if o2a is None else o2a.t.clone())
+    ref, ref2 = outs[-1]
+    assert torch.isfinite(ref.float()).all()
+    for v, (y, y2) in outs.items():
+        assert torch.equal(y, ref), f"variant {v} differs from the generic kernel"
+        if o2:
+            assert torch.equal(y2, ref2), f"variant {v} out2 differs"
+
+
 # ------------------------------------------------------------------------------------------ misc kernels
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_pointwise_kernels(dt):
