@@ -113,4 +113,107 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, int px, int co,
   }
 }
 
+// 4 consecutive elements of T as one vector load / store.
+template <typename T> struct Quad;
+template <> struct Quad<bf16_t> {
+  typedef uint2 V;
+  __device__ static __forceinline__ V load(const void* p, long long i) {
+    return *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(p) + i);
+  }
+  __device__ static __forceinline__ float get(const V& v, int e) {
+    const uint32_t w = e < 2 ? v.x : v.y;
+    return (e & 1) ? __uint_as_float(w & 0xffff0000u) : __uint_as_float(w << 16);
+  }
+  __device__ static __forceinline__ V zero() { return make_uint2(0u, 0u); }
+  __device__ static __forceinline__ void store(void* p, long long i, const float* f) {
+    uint2 o;
+    o.x = (uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16);
+    o.y = (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16);
+    *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p) + i) = o;
+  }
+};
+template <> struct Quad<float> {
+  typedef float4 V;
+  __device__ static __forceinline__ V load(const void* p, long long i) {
+    return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p) + i);
+  }
+  __device__ static __forceinline__ float get(const V& v, int e) {
+    return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;
+  }
+  __device__ static __forceinline__ V zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  __device__ static __forceinline__ void store(void* p, long long i, const float* f) {
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(p) + i) = make_float4(f[0], f[1], f[2], f[3]);
+  }
+};
+
+// Epilogue of a TM x TN block of 16x16 accumulators whose lane owns 4 consecutive output channels
+// co[i] of pixel px[j].  prefetch() issues every scale / shift / residual load before the first
+// store, so the loads are not serialised behind the stores (out and residual may alias as far as
+// the compiler knows); call it early (e.g. before the K loop) to hide their latency.  Applies
+// when ok(): 4-aligned channel views and 4 | Cout (4 | Cout/4 for ConvTranspose); otherwise
+// use conv_epilogue per fragment.
+template <typename T, typename TO, int TM, int TN>
+struct TileEpi {
+  floatx4 sc[TM], sh[TM];
+  typename Quad<T>::V res[TM][TN];
+
+  __device__ static __forceinline__ bool ok(const hiseg_conv2d_desc& d) {
+    constexpr uintptr_t va = sizeof(T) == 2 ? 7 : 15, vo = sizeof(TO) == 2 ? 7 : 15;
+    return (!d.convT || ((d.Cout >> 2) & 3) == 0) && (d.Cout & 3) == 0 &&
+           ((d.o_cstride | d.o_coff) & 3) == 0 && (!d.out2 || ((d.o2_cstride | d.o2_coff) & 3) == 0) &&
+           (!d.residual || ((d.r_cstride | d.r_coff) & 3) == 0) &&
+           (!d.mul || ((d.m_cstride | d.m_coff) & 3) == 0) &&
+           (((uintptr_t)d.scale | (uintptr_t)d.shift) & 15) == 0 && ((uintptr_t)d.out & vo) == 0 &&
+           (((uintptr_t)d.out2 | (uintptr_t)d.residual | (uintptr_t)d.mul) & va) == 0;
+  }
+
+  __device__ __forceinline__ void prefetch(const hiseg_conv2d_desc& d, int M, const int (&px)[TN], const int (&co)[TM]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int cc = co[i] < d.Cout ? co[i] : 0;
+      sc[i] = *reinterpret_cast<const floatx4*>(d.scale + cc);
+      sh[i] = *reinterpret_cast<const floatx4*>(d.shift + cc);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        res[i][j] = Quad<T>::zero();
+        if (d.residual) {
+          long long op;
+          int oc;
+          out_site(d, px[j] < M ? px[j] : M - 1, cc, op, oc);
+          res[i][j] = Quad<T>::load(d.residual, op * d.r_cstride + d.r_coff + oc);
+        }
+      }
+    }
+  }
+
+  __device__ __forceinline__ void store(const hiseg_conv2d_desc& d, int M, const int (&px)[TN], const int (&co)[TM],
+                                        const floatx4 (&acc)[TM][TN], bool write_out2 = true) {
+#pragma clang loop unroll(full)
+    for (int i = 0; i < TM; ++i)
+#pragma clang loop unroll(full)
+      for (int j = 0; j < TN; ++j) {
+        if (px[j] >= M || co[i] >= d.Cout) continue;
+        long long op;
+        int oc;
+        out_site(d, px[j], co[i], op, oc);
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * sc[i][e] + sh[i][e];
+        if (d.residual) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += Quad<T>::get(res[i][j], e);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], d.act);
+        if (d.mul) {
+          const typename Quad<T>::V m = Quad<T>::load(d.mul, op * d.m_cstride + d.m_coff + oc);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] *= Quad<T>::get(m, e);
+        }
+        Quad<TO>::store(d.out, op * d.o_cstride + d.o_coff + oc, v);
+        if (write_out2 && d.out2) Quad<T>::store(d.out2, op * d.o2_cstride + d.o2_coff + oc, v);
+      }
+  }
+};
+
 }  // namespace hiseg

@@ -134,43 +134,17 @@ __global__ void __launch_bounds__(64 * WCO * WPX) conv_fast_kernel(ConvArgs a) {
     }
   };
 
-  // ---- epilogue operands (scale/shift, residual, mul) are fetched at kernel entry so their
-  // latency hides under the K loop; issued as plain loads, they are older than every DMA of
-  // the ring, and the loop's counted vmcnt waits stay exact (in-order return).  Fast path:
-  // plain NHWC output (no convT scatter), Cout % 4 == 0, 8-B aligned channel views.
-  const bool fast_ep = (!d.convT || ((d.Cout >> 2) & 3) == 0) && (d.Cout & 3) == 0 &&
-                       ((d.o_cstride | d.o_coff) & 3) == 0 && (!d.out2 || ((d.o2_cstride | d.o2_coff) & 3) == 0) &&
-                       (!d.residual || ((d.r_cstride | d.r_coff) & 3) == 0) &&
-                       (!d.mul || ((d.m_cstride | d.m_coff) & 3) == 0) &&
-                       (((uintptr_t)d.scale | (uintptr_t)d.shift) & 15) == 0 &&
-                       (((uintptr_t)d.out | (uintptr_t)d.out2 | (uintptr_t)d.residual | (uintptr_t)d.mul) & 7) == 0;
-  floatx4 esc[TM], esh[TM];
-  uint2 eres[TM][TN], emul[TM][TN];
-  if (fast_ep) {
+  // ---- epilogue operands (scale/shift, residual) are fetched at kernel entry so their latency
+  // hides under the K loop; issued as plain loads, they are older than every DMA of the ring,
+  // and the loop's counted vmcnt waits stay exact (in-order return).
+  int epx[TN], eco[TM];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int co = co0 + wco * TM * 16 + i * 16 + (lane >> 4) * 4;
-      const int cc = co < d.Cout ? co : 0;
-      esc[i] = *reinterpret_cast<const floatx4*>(d.scale + cc);
-      esh[i] = *reinterpret_cast<const floatx4*>(d.shift + cc);
+  for (int j = 0; j < TN; ++j) epx[j] = px0 + wpx * TN * 16 + j * 16 + (lane & 15);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        int px = px0 + wpx * TN * 16 + j * 16 + (lane & 15);
-        px = px < a.M ? px : a.M - 1;
-        long long op;
-        int oc;
-        out_site(d, px, cc, op, oc);
-        eres[i][j] = make_uint2(0u, 0u);
-        emul[i][j] = make_uint2(0u, 0u);
-        if (d.residual)
-          eres[i][j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(d.residual) +
-                                                       op * d.r_cstride + d.r_coff + oc);
-        if (d.mul)
-          emul[i][j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(d.mul) +
-                                                       op * d.m_cstride + d.m_coff + oc);
-      }
-    }
-  }
+  for (int i = 0; i < TM; ++i) eco[i] = co0 + wco * TM * 16 + i * 16 + (lane >> 4) * 4;
+  const bool fast_ep = TileEpi<bf16_t, bf16_t, TM, TN>::ok(d);
+  TileEpi<bf16_t, bf16_t, TM, TN> ep;
+  if (fast_ep) ep.prefetch(d, a.M, epx, eco);
 
   floatx4 acc[TM][TN];
 #pragma unroll
@@ -218,51 +192,15 @@ __global__ void __launch_bounds__(64 * WCO * WPX) conv_fast_kernel(ConvArgs a) {
 
   if constexpr (STAMP) st2 = stamp_now();
   if (fast_ep) {
-    const bool has_res = d.residual != nullptr, has_mul = d.mul != nullptr;
-    void* out2 = STAMP ? nullptr : d.out2;
-#pragma clang loop unroll(full)
-    for (int i = 0; i < TM; ++i)
-#pragma clang loop unroll(full)
-      for (int j = 0; j < TN; ++j) {
-        const int px = px0 + wpx * TN * 16 + j * 16 + (lane & 15);
-        const int co = co0 + wco * TM * 16 + i * 16 + (lane >> 4) * 4;
-        if (px >= a.M || co >= d.Cout) continue;
-        long long op;
-        int oc;
-        out_site(d, px, co, op, oc);
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * esc[i][e] + esh[i][e];
-        if (has_res) {
-          const uint2 q = eres[i][j];
-          v[0] += __uint_as_float(q.x << 16); v[1] += __uint_as_float(q.x & 0xffff0000u);
-          v[2] += __uint_as_float(q.y << 16); v[3] += __uint_as_float(q.y & 0xffff0000u);
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], d.act);
-        if (has_mul) {
-          const uint2 q = emul[i][j];
-          v[0] *= __uint_as_float(q.x << 16); v[1] *= __uint_as_float(q.x & 0xffff0000u);
-          v[2] *= __uint_as_float(q.y << 16); v[3] *= __uint_as_float(q.y & 0xffff0000u);
-        }
-        uint2 o;
-        o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-        o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(d.out) + op * d.o_cstride + d.o_coff + oc) = o;
-        if (out2)
-          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out2) + op * d.o2_cstride + d.o2_coff + oc) = o;
-      }
+    ep.store(d, a.M, epx, eco, acc, !STAMP);
   } else {
     ConvArgs ae = a;
     if constexpr (STAMP) ae.d.out2 = nullptr;
 #pragma clang loop unroll(full)
     for (int i = 0; i < TM; ++i)
 #pragma clang loop unroll(full)
-      for (int j = 0; j < TN; ++j) {
-        const int px = px0 + wpx * TN * 16 + j * 16 + (lane & 15);
-        const int co = co0 + wco * TM * 16 + i * 16 + (lane >> 4) * 4;
-        if (px < a.M) conv_epilogue<bf16_t, bf16_t>(ae, px, co, acc[i][j]);
-      }
+      for (int j = 0; j < TN; ++j)
+        if (epx[j] < a.M) conv_epilogue<bf16_t, bf16_t>(ae, epx[j], eco[i], acc[i][j]);
   }
   if constexpr (STAMP) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -114,8 +114,11 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
     for (int i = 0; i < W_CH; ++i) {
       const int r = (t >> 3) + 32 * i;
       if (W_FULL || r < BCO) {
-        const long long off = (long long)(co0 + r) * d.K_pad + (long long)kb * BK + c * KCH;
-        rw[i] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(d.weight) + off);
+        // the last Cout tile may overhang Cout_pad: clamp the row, zero the value
+        const int row = co0 + r < d.Cout_pad ? co0 + r : d.Cout_pad - 1;
+        const long long off = (long long)row * d.K_pad + (long long)kb * BK + c * KCH;
+        const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(d.weight) + off);
+        rw[i] = co0 + r < d.Cout_pad ? v : make_uint4(0u, 0u, 0u, 0u);
       }
     }
   };
@@ -189,31 +192,42 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
   }
 
   // ---- epilogue ----
+  int epx[TN], eco[TM];
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
+  for (int j = 0; j < TN; ++j) epx[j] = px0 + wpx * TN * 16 + j * 16 + (lane & 15);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int px = px0 + wpx * TN * 16 + j * 16 + (lane & 15);
-      const int co = co0 + wco * TM * 16 + i * 16 + (lane >> 4) * 4;
-      if (px < a.M) conv_epilogue<T, TO>(a, px, co, acc[i][j]);
+  for (int i = 0; i < TM; ++i) eco[i] = co0 + wco * TM * 16 + i * 16 + (lane >> 4) * 4;
+  if (TileEpi<T, TO, TM, TN>::ok(d)) {
+    TileEpi<T, TO, TM, TN> ep;
+    ep.prefetch(d, a.M, epx, eco);
+    ep.store(d, a.M, epx, eco, acc);
+  } else {
+#pragma clang loop unroll(full)
+    for (int i = 0; i < TM; ++i) {
+#pragma clang loop unroll(full)
+      for (int j = 0; j < TN; ++j) {
+        if (epx[j] < a.M) conv_epilogue<T, TO>(a, epx[j], eco[i], acc[i][j]);
+      }
     }
   }
 }
 
 template <typename T, typename TO, int BCO, int BPX, int WCO, int WPX>
 static int launch_cfg(const ConvArgs& a, hipStream_t s) {
-  dim3 grid((a.M + BPX - 1) / BPX, a.d.Cout_pad / BCO);
+  dim3 grid((a.M + BPX - 1) / BPX, (a.d.Cout_pad + BCO - 1) / BCO);
   const size_t lds = 2u * (BCO + BPX) * 8u * 16u;
   hipLaunchKernelGGL((conv_igemm_kernel<T, TO, BCO, BPX, WCO, WPX>), grid, dim3(256), lds, s, a);
   return hiseg_check_launch("conv_igemm");
 }
 
+// Tile choice: the widest Cout tile whose overhang past Cout_pad adds <= 1/6 to the MFMA work.
 template <typename T, typename TO>
 static int launch_typed(const ConvArgs& a, hipStream_t s) {
   const int cp = a.d.Cout_pad;
-  if (cp % 128 == 0) return launch_cfg<T, TO, 128, 128, 2, 2>(a, s);
-  if (cp % 64 == 0) return launch_cfg<T, TO, 64, 128, 2, 2>(a, s);
-  if (cp % 32 == 0) return launch_cfg<T, TO, 32, 256, 1, 4>(a, s);
+  auto fits = [&](int bco) { return ((cp + bco - 1) / bco) * bco * 6 <= cp * 7; };
+  if (cp >= 96 && fits(128)) return launch_cfg<T, TO, 128, 128, 2, 2>(a, s);
+  if (cp >= 48 && fits(64)) return launch_cfg<T, TO, 64, 128, 2, 2>(a, s);
+  if (fits(32)) return launch_cfg<T, TO, 32, 256, 1, 4>(a, s);
   return launch_cfg<T, TO, 16, 256, 1, 4>(a, s);
 }
 
@@ -225,6 +239,7 @@ int conv_halo_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_halo2_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_halo3_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_8ph_try(const ConvArgs& a, hipStream_t s, int variant);
+int conv_small_try(const ConvArgs& a, hipStream_t s, int variant);
 }
 
 using namespace hiseg;
@@ -278,7 +293,10 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
   // Automatic choice (variant 0) = the fastest measured configuration per layer class
   // (tools/conv_bench.py): LDS-DMA ring kernel, 128x128 tiles for Cout >= 128, 64x128 for 64.
   // Experimental kernels (halo / halo2 / halo3) run only when forced by variant.
-  if (variant >= 40) {
+  if (variant >= 50) {
+    const int r = conv_small_try(a, s, variant);
+    if (r != 0) return r < 0 ? r : HISEG_OK;
+  } else if (variant >= 40) {
     const int r = conv_8ph_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
   } else if (variant >= 30) {
@@ -295,6 +313,10 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
     if (v == 0) v = (d->Cout_pad % 128 == 0) ? 4 : 8;
     const int r = conv_fast_try(a, s, v);
     if (r != 0) return r < 0 ? r : HISEG_OK;
+    if (variant == 0) {   // narrow / ragged layers: halo-tiled direct kernel
+      const int r2 = conv_small_try(a, s, 0);
+      if (r2 != 0) return r2 < 0 ? r2 : HISEG_OK;
+    }
   }
   if (d->dtype == HISEG_BF16) {
     return d->out_dtype == HISEG_BF16 ? launch_typed<bf16_t, bf16_t>(a, s) : launch_typed<bf16_t, float>(a, s);

@@ -82,6 +82,7 @@ CONV_CASES = [
     (2, 64, 64, 20, 18, 3, 1, 1), (2, 256, 256, 16, 12, 3, 1, 1), (3, 3, 64, 17, 13, 3, 1, 1),
     (2, 128, 32, 15, 9, 3, 1, 2), (2, 32, 2, 15, 9, 1, 1, 0), (2, 24, 40, 31, 33, 3, 2, 3),
     (1, 258, 256, 8, 6, 1, 1, 0), (2, 16, 96, 11, 7, 1, 1, 3), (1, 16, 1, 12, 20, 3, 1, 0),
+    (2, 96, 112, 9, 11, 1, 1, 0), (2, 40, 240, 6, 7, 3, 1, 3), (2, 200, 672, 5, 4, 1, 1, 1),
 ]
 
 
@@ -159,6 +160,8 @@ VARIANT_CASES = {
     "3x3_128_cout250": (2, 128, 0, 250, 9, 8, 3, False, True, False, True),
     "convT_128_to_64": (2, 128, 0, 64, 6, 5, 1, True, False, False, False),
     "convT_256_to_128_res": (2, 256, 0, 128, 5, 7, 1, True, True, False, False),
+    "1x1_96_to_112_overhang": (2, 96, 0, 112, 9, 11, 1, False, True, False, False),
+    "3x3_40_to_240_overhang": (2, 40, 0, 240, 6, 7, 3, False, False, True, True),
 }
 
 
@@ -193,6 +196,50 @@ def test_conv_kernel_variants_bit_identical(name):
     for v, (y, y2) in outs.items():
         assert torch.equal(y, ref), f"variant {v} differs from the generic kernel"
         if o2:
+            assert torch.equal(y2, ref2), f"variant {v} out2 differs"
+
+
+# Narrow / ragged layers (full-resolution decoder, EfficientNet projections) on the halo-tiled
+# direct kernel (variants 50-58) vs the generic kernel, bit for bit.
+# name: (N, Ca, Cb, Cout, H, W, k, a_up, in_scale, residual, mul+out2, f32 out)
+NARROW_CASES = {
+    "up2_32_to_16": (2, 32, 0, 16, 10, 70, 3, 2, False, False, False, False),
+    "16_to_16_res": (2, 16, 0, 16, 9, 66, 3, 1, False, True, False, False),
+    "16_to_1_f32": (2, 16, 0, 1, 11, 40, 3, 1, False, False, False, True),
+    "up2_64+32_to_32": (2, 64, 32, 32, 12, 20, 3, 2, False, False, True, False),
+    "1x1_24_to_144_ins_res": (3, 24, 0, 144, 7, 9, 1, 1, True, True, False, False),
+    "1x1_16_to_96": (2, 16, 0, 96, 5, 130, 1, 1, False, False, False, False),
+    "3x3_8_to_64": (2, 8, 0, 64, 9, 13, 3, 1, False, False, False, False),
+    "3x3_64+8_to_64_ins": (2, 64, 8, 64, 6, 7, 3, 1, True, False, True, False),
+}
+
+
+@pytest.mark.parametrize("name", list(NARROW_CASES))
+def test_conv_small_kernel_bit_identical(name):
+    from hiseg import ops
+    N, Ca, Cb, Cout, H, W, k, up, ins, res, mul, f32o = NARROW_CASES[name]
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(11)
+    xa = ops.Act.from_nchw(torch.randn(N, Ca, H // up, W // up, device=DEV, generator=g), dt)
+    xb = ops.Act.from_nchw(torch.randn(N, Cb, H, W, device=DEV, generator=g), dt) if Cb else None
+    w = torch.randn(Cout, Ca + Cb, k, k, device=DEV, generator=g) / ((Ca + Cb) * k * k) ** 0.5
+    p = ops.pack_conv(w, torch.randn(Cout, device=DEV, generator=g) * 0.1, None, 1, dt, DEV, pad=k // 2,
+                      split=(Ca, Cb) if Cb else None)
+    gate = torch.rand(N, p.ca, device=DEV, generator=g) if ins else None
+    R = ops.Act.from_nchw(torch.randn(N, Cout, H, W, device=DEV, generator=g), dt) if res else None
+    M = ops.Act.from_nchw(torch.rand(N, Cout, H, W, device=DEV, generator=g), dt) if mul else None
+    outs = {}
+    for v in (-1, 0, 50, 51, 52, 54, 58):
+        o2 = ops.Act.new(N, H, W, Cout, dt, DEV) if mul else None
+        y = ops.conv2d(p, xa, xb, a_up=up, residual=R, mul=M, out2=o2, in_scale=gate,
+                       out_dtype=torch.float32 if f32o else None, variant=v)
+        torch.cuda.synchronize()
+        outs[v] = (y.t.clone(), None if o2 is None else o2.t.clone())
+    ref, ref2 = outs[-1]
+    assert torch.isfinite(ref.float()).all()
+    for v, (y, y2) in outs.items():
+        assert torch.equal(y, ref), f"variant {v} differs from the generic kernel"
+        if mul:
             assert torch.equal(y2, ref2), f"variant {v} out2 differs"
 
 

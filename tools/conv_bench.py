@@ -27,6 +27,9 @@ SHAPES = {
     "c256to256_1x1_64x48": (256, 256, 0, 256, 64, 48, 1, False),
     "c256to64_3x3_64x48": (256, 256, 0, 64, 64, 48, 3, False),
     "res256_3x3_16x12": (256, 256, 0, 256, 16, 12, 3, True),
+    "dec16_3x3_480x640": (32, 16, 0, 16, 480, 640, 3, False),
+    "dec32_3x3_240x320": (32, 32, 0, 32, 240, 320, 3, False),
+    "c16to96_1x1_240x320": (32, 16, 0, 96, 240, 320, 1, False),
 }
 
 
