@@ -2,7 +2,7 @@
 
 Functional form over a state_dict (keys exactly as the reference's modules), torch CPU ops.
 Citations are file:line in the reference (PINTO0309/human-instance-segmentation).
-Eval-mode semantics only (BatchNorm with running statistics, Dropout2d as identity).
+Eval-mode semantics by default (BatchNorm with running statistics, Dropout2d as identity);\noracle/train.py switches BatchNorm/RoIAlign to training semantics (Dropout stays identity: p = 0 in tests).
 """
 from __future__ import annotations
 
@@ -28,7 +28,11 @@ def conv(sd: SD, p: str, x, stride=1, pad=None):
 
 
 def bn(sd: SD, p: str, x, eps=1e-5):
-    """nn.BatchNorm2d eval (advanced/normalization_comparison.py:181-182)."""
+    """nn.BatchNorm2d (advanced/normalization_comparison.py:181-182): running statistics (eval), or
+    batch statistics + running-stat update inside oracle.train.train_mode()."""
+    from . import train as _T
+    if _T.is_train():
+        return _T.bn_train(sd, p, x, eps)
     return F.batch_norm(x, sd[p + ".running_mean"], sd[p + ".running_var"], sd[p + ".weight"], sd[p + ".bias"],
                         False, 0.0, eps)
 
@@ -54,7 +58,11 @@ def residual(sd: SD, p: str, x, a: str):
 
 
 def roi_align(feat: torch.Tensor, rois: torch.Tensor, oh: int, ow: int, scale_h, scale_w, aligned=True):
-    """dynamic_roi_align.py:56-171 (numpy restatement in oracle/roi_align.py)."""
+    """dynamic_roi_align.py:56-171 (numpy restatement in oracle/roi_align.py; differentiable torch
+    form oracle.train.roi_align_torch inside train_mode())."""
+    from . import train as _T
+    if _T.is_train():
+        return _T.roi_align_torch(feat, rois, oh, ow, scale_h, scale_w, aligned)
     out = _roi_align_np(feat.detach().numpy(), rois.detach().numpy(), oh, ow, scale_h, scale_w, aligned)
     return torch.from_numpy(out)
 

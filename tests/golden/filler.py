@@ -60,3 +60,21 @@ def box_rois(seed: int, n_images: int, per_image: int) -> np.ndarray:
             y1 = rng.uniform(0.0, 1.0 - h)
             out.append([b, x1, y1, x1 + w, y1 + h])
     return np.asarray(out, dtype=np.float32)
+
+
+def ellipse_targets(seed: int, n: int, mh: int, mw: int) -> np.ndarray:
+    """SURVEY.md §8d synthetic 3-class ROI targets (int64 [n, mh, mw]): class 1 = an ellipse filling
+    ~35 % of the ROI, class 2 = an offset ellipse ~15 % (drawn over class 1), 0 elsewhere."""
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:mh, 0:mw].astype(np.float32)
+    out = np.zeros((n, mh, mw), dtype=np.int64)
+    for i in range(n):
+        cy, cx = rng.uniform(0.35, 0.65) * mh, rng.uniform(0.35, 0.65) * mw
+        ry, rx = rng.uniform(0.30, 0.40) * mh, rng.uniform(0.28, 0.36) * mw
+        e1 = ((yy - cy) / ry) ** 2 + ((xx - cx) / rx) ** 2 <= 1.0
+        oy, ox = cy + rng.uniform(-0.3, 0.3) * mh, cx + rng.uniform(-0.35, 0.35) * mw
+        sy, sx = rng.uniform(0.18, 0.26) * mh, rng.uniform(0.16, 0.24) * mw
+        e2 = ((yy - oy) / sy) ** 2 + ((xx - ox) / sx) ** 2 <= 1.0
+        out[i][e1] = 1
+        out[i][e2] = 2
+    return out
