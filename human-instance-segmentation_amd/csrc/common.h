@@ -87,6 +87,8 @@ template <> struct Chunk<bf16_t> {
 void hiseg_set_error(const char* fmt, ...);
 int hiseg_check_launch(const char* what);
 
+static inline bool al16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
 #define HISEG_REQUIRE(cond, code, ...)  \
   do {                                  \
     if (!(cond)) {                      \

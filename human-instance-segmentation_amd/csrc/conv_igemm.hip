@@ -244,7 +244,6 @@ int conv_small_try(const ConvArgs& a, hipStream_t s, int variant);
 
 using namespace hiseg;
 
-static bool al16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int variant);
 

@@ -12,6 +12,7 @@
 // Feature maps are read in place through the roi's batch index; the reference's
 // index_select copy of N full maps (:156) is not materialised.
 #include "common.h"
+#include "hiseg_head_train.h"
 
 namespace hiseg {
 
@@ -100,9 +101,89 @@ __global__ void __launch_bounds__(256) roi_align_kernel(hiseg_roi_align_desc d) 
   }
 }
 
+// Backward into the output_conv affine (see hiseg_roi_align_bwd_affine): per sample, the same taps
+// and weights as the forward; partial sums [block][4] = (dw0, dw1, db0, db1), n_aff == 2.
+constexpr int kRoiBwdBlocks = 512;
+
+template <typename TG>
+__global__ void __launch_bounds__(256) roi_align_bwd_affine_kernel(hiseg_roi_align_desc d, const void* g, int gcs,
+                                                                   int gco, float* part) {
+  __shared__ float red[4][256];
+  const long long total = (long long)d.N * d.oh * d.ow;
+  float a0 = 0.f, a1 = 0.f, b0 = 0.f, b1 = 0.f;
+  for (long long gid = (long long)blockIdx.x * 256 + threadIdx.x; gid < total; gid += (long long)gridDim.x * 256) {
+    const int j = (int)(gid % d.ow);
+    const long long t = gid / d.ow;
+    const int i = (int)(t % d.oh);
+    const int n = (int)(t / d.oh);
+    const float* roi = d.rois + (long long)n * 5;
+    const long long b = (long long)roi[0];
+    const float x1 = fmul(roi[1], d.scale_w), y1 = fmul(roi[2], d.scale_h);
+    const float x2 = fmul(roi[3], d.scale_w), y2 = fmul(roi[4], d.scale_h);
+    const float ix = src_coord(x1, fsub(x2, x1), linspace01(j, d.ow), d.W, d.aligned);
+    const float iy = src_coord(y1, fsub(y2, y1), linspace01(i, d.oh), d.H, d.aligned);
+    const float xw = floorf(ix), yn = floorf(iy);
+    const float wgt_w = fsub(ix, xw), wgt_e = fsub(1.f, wgt_w);
+    const float wgt_n = fsub(iy, yn), wgt_s = fsub(1.f, wgt_n);
+    const int x0 = (int)fminf(fmaxf(xw, -2.f), (float)d.W + 1.f), y0 = (int)fminf(fmaxf(yn, -2.f), (float)d.H + 1.f);
+    if (!((b >= 0 && b < d.B) && (ix == ix) && (iy == iy))) continue;
+    const bool vx0 = x0 >= 0 && x0 < d.W, vx1 = x0 + 1 >= 0 && x0 + 1 < d.W;
+    const bool vy0 = y0 >= 0 && y0 < d.H, vy1 = y0 + 1 >= 0 && y0 + 1 < d.H;
+    const float* src = d.feat + (long long)b * d.C * d.H * d.W;
+    float vu = 0.f, ws = 0.f;
+    auto tap = [&](bool ok, int yy, int xx, float w) {
+      if (!ok) return;
+      vu += w * src[(long long)yy * d.W + xx];
+      ws += w;
+    };
+    tap(vy0 && vx0, y0, x0, fmul(wgt_s, wgt_e));
+    tap(vy0 && vx1, y0, x0 + 1, fmul(wgt_s, wgt_w));
+    tap(vy1 && vx0, y0 + 1, x0, fmul(wgt_n, wgt_e));
+    tap(vy1 && vx1, y0 + 1, x0 + 1, fmul(wgt_n, wgt_w));
+    const float g0 = Elem<TG>::load(g, gid * gcs + gco), g1 = Elem<TG>::load(g, gid * gcs + gco + 1);
+    a0 += g0 * vu; a1 += g1 * vu; b0 += g0 * ws; b1 += g1 * ws;
+  }
+  const int t = threadIdx.x;
+  red[0][t] = a0; red[1][t] = a1; red[2][t] = b0; red[3][t] = b1;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (t < s) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) red[k][t] += red[k][t + s];
+    }
+    __syncthreads();
+  }
+  if (t < 4) part[blockIdx.x * 4 + t] = red[t][0];
+}
+
+__global__ void roi_bwd_sum_kernel(const float* part, int nblk, float* dw, float* db) {
+  const int t = threadIdx.x;
+  if (t >= 4) return;
+  double s = 0;
+  for (int b = 0; b < nblk; ++b) s += part[b * 4 + t];
+  if (t < 2) dw[t] += (float)s;
+  else if (db) db[t - 2] += (float)s;
+}
+
 }  // namespace hiseg
 
 using namespace hiseg;
+
+extern "C" int hiseg_roi_align_ws(int N) { (void)N; return kRoiBwdBlocks * 4; }
+
+extern "C" int hiseg_roi_align_bwd_affine(const hiseg_roi_align_desc* d, const void* g, int g_dtype, int g_cstride,
+                                          int g_coff, float* ws, float* dw, float* db, hiseg_stream_t stream) {
+  HISEG_REQUIRE(d && g && ws && dw, HISEG_ERR_BAD_ARG, "roi_align_bwd_affine: null argument");
+  HISEG_REQUIRE(d->N > 0 && d->feat && d->rois && d->C == 1 && d->aff_w && d->n_aff == 2, HISEG_ERR_BAD_SHAPE,
+                "roi_align_bwd_affine: expects the 1->2 output_conv over a 1-channel map");
+  hipStream_t s = (hipStream_t)stream;
+  if (g_dtype == HISEG_BF16)
+    hipLaunchKernelGGL(roi_align_bwd_affine_kernel<bf16_t>, dim3(kRoiBwdBlocks), dim3(256), 0, s, *d, g, g_cstride, g_coff, ws);
+  else
+    hipLaunchKernelGGL(roi_align_bwd_affine_kernel<float>, dim3(kRoiBwdBlocks), dim3(256), 0, s, *d, g, g_cstride, g_coff, ws);
+  hipLaunchKernelGGL(roi_bwd_sum_kernel, dim3(1), dim3(64), 0, s, ws, kRoiBwdBlocks, dw, db);
+  return hiseg_check_launch("roi_align_bwd_affine");
+}
 
 extern "C" int hiseg_roi_align_fwd(const hiseg_roi_align_desc* d, hiseg_stream_t stream) {
   HISEG_REQUIRE(d != nullptr, HISEG_ERR_BAD_ARG, "roi_align: null descriptor");

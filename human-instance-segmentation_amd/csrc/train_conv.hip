@@ -1,0 +1,432 @@
+// Convolution backward on CDNA4 MFMA (gfx950): weight gradient, split reduction into the
+// reference parameter layouts, and the per-step weight packing of every layer in one launch.
+// (The data gradient reuses the forward implicit-GEMM kernels with packed dgrad weights.)
+//
+// Weight gradient GEMM (include/hiseg_train.h, hiseg_conv2d_wgrad):
+//   D[k][j] = sum_p X[p][k] * dY[p][j]        k: im2col column (tap, ci), j: GEMM output column
+// Both operands are pixel-major in HBM (NHWC), but MFMA wants each lane's 8 (bf16) / 4 (f32)
+// contraction elements -- here consecutive PIXELS -- in one register chunk.  Each staging task
+// therefore loads KCH pixels x one 16-B channel chunk (KCH coalesced 16-B loads, neighbouring
+// threads on neighbouring chunks of the same pixel rows), transposes the KCH x KCH block in
+// registers and writes KCH 16-B rows ("channel row, pixel chunk") into the same XOR-swizzled
+// 128-B-row LDS image the forward kernel uses, so the fragment reads and the MFMA loop are the
+// forward kernel's.  Register-staged double buffering, one barrier per pixel block.
+// The pixel dimension is split across workgroups (split-K); every split writes its own f32
+// partial tile (deterministic, no atomics) and hiseg_conv2d_wgrad_reduce sums them.
+#include "conv_common.h"
+#include "hiseg_train.h"
+
+namespace hiseg {
+
+struct WgradArgs {
+  hiseg_conv2d_desc d;  // forward descriptor (input side + geometry)
+  const void* dy; int dy_cs, dy_coff;
+  int M;          // GEMM rows of the forward conv (output pixels; input pixels for convT)
+  int Cin;        // Ca + Cb (padded)
+  int Ktot;       // KH*KW*Cin
+  int want_bias;
+  int Cg, Kg;
+  int splits, blocks_per_split;  // pixel blocks per split
+  float* ws;
+};
+
+// KCH x KCH transpose of 16-B chunks: in[i] = chunk of pixel i (KCH channels), out[e] = chunk of
+// channel e (KCH pixels).
+template <typename T> struct Tr;
+template <> struct Tr<bf16_t> {
+  __device__ static __forceinline__ void run(const uint4 (&in)[8], uint4 (&out)[8]) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      uint32_t w[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint4 a = in[2 * q], b = in[2 * q + 1];
+        const uint32_t wa = (e >> 1) == 0 ? a.x : (e >> 1) == 1 ? a.y : (e >> 1) == 2 ? a.z : a.w;
+        const uint32_t wb = (e >> 1) == 0 ? b.x : (e >> 1) == 1 ? b.y : (e >> 1) == 2 ? b.z : b.w;
+        w[q] = (e & 1) ? ((wa >> 16) | (wb & 0xffff0000u)) : ((wa & 0xffffu) | (wb << 16));
+      }
+      out[e] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+};
+template <> struct Tr<float> {
+  __device__ static __forceinline__ void run(const uint4 (&in)[4], uint4 (&out)[4]) {
+    out[0] = make_uint4(in[0].x, in[1].x, in[2].x, in[3].x);
+    out[1] = make_uint4(in[0].y, in[1].y, in[2].y, in[3].y);
+    out[2] = make_uint4(in[0].z, in[1].z, in[2].z, in[3].z);
+    out[3] = make_uint4(in[0].w, in[1].w, in[2].w, in[3].w);
+  }
+};
+
+template <typename T, int BK, int BC, int WK, int WC>
+__global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
+  constexpr int KCH = Chunk<T>::N;
+  constexpr int PB = 8 * KCH;             // pixels per block (one LDS stage row = 8 chunks)
+  constexpr int TM = BK / (WK * 16);
+  constexpr int TN = BC / (WC * 16);
+  constexpr int NXT = (BK / KCH) * 8;     // X staging tasks (row group x pixel group)
+  constexpr int NYT = (BC / KCH) * 8;
+  constexpr int NT = NXT + NYT;
+  constexpr int TPT = (NT + 255) / 256;   // tasks per thread
+  constexpr int STAGE = (BK + BC) * 8;
+  static_assert(WK * WC == 4 && TM >= 1 && TN >= 1, "tile");
+
+  extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+  const hiseg_conv2d_desc& d = a.d;
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  const int wk = wave / WC;
+  const int wc = wave % WC;
+  const int k0 = blockIdx.x * BK;
+  const int j0 = blockIdx.y * BC;
+  const int split = blockIdx.z;
+  const int pb_begin = split * a.blocks_per_split;
+  int pb_end = pb_begin + a.blocks_per_split;
+  const int nblocks = (a.M + PB - 1) / PB;
+  if (pb_end > nblocks) pb_end = nblocks;
+
+  // static per-task decode (row group, pixel group, operand)
+  int tk_row[TPT], tk_pg[TPT], tk_kind[TPT];  // kind: 0 = X, 1 = dY, -1 = none
+  int tk_tap_y[TPT], tk_tap_x[TPT], tk_ci[TPT];
+#pragma unroll
+  for (int i = 0; i < TPT; ++i) {
+    const int task = t + 256 * i;
+    tk_kind[i] = -1; tk_row[i] = 0; tk_pg[i] = 0; tk_tap_y[i] = 0; tk_tap_x[i] = 0; tk_ci[i] = 0;
+    if (task < NXT) {
+      tk_kind[i] = 0;
+      tk_row[i] = (task >> 3) * KCH;  // local k row
+      tk_pg[i] = task & 7;
+      const int k = k0 + tk_row[i];
+      const int tap = k / a.Cin;
+      tk_ci[i] = k - tap * a.Cin;
+      tk_tap_y[i] = tap / d.KW;
+      tk_tap_x[i] = tap - tk_tap_y[i] * d.KW;
+    } else if (task < NT) {
+      tk_kind[i] = 1;
+      const int tt = task - NXT;
+      tk_row[i] = (tt >> 3) * KCH;
+      tk_pg[i] = tt & 7;
+    }
+  }
+
+  uint4 reg[TPT][KCH];
+  auto gather = [&](int pb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < TPT; ++i) {
+      if (tk_kind[i] < 0) continue;
+      const int p0 = pb * PB + tk_pg[i] * KCH;
+      if (tk_kind[i] == 0) {
+        const int k = k0 + tk_row[i];
+        const bool is_bias = a.want_bias && k == a.Ktot;
+        const bool kvalid = k < a.Ktot;
+        int ox = p0 % d.Wo, tt = p0 / d.Wo;
+        int oy = tt % d.Ho, n = tt / d.Ho;
+#pragma unroll
+        for (int e = 0; e < KCH; ++e) {
+          uint4 v = make_uint4(0u, 0u, 0u, 0u);
+          const int p = p0 + e;
+          if (p < a.M) {
+            if (kvalid) {
+              const int iy = oy * d.stride - d.pad + tk_tap_y[i];
+              const int ix = ox * d.stride - d.pad + tk_tap_x[i];
+              if (iy >= 0 && iy < d.H && ix >= 0 && ix < d.W) {
+                const int ci = tk_ci[i];
+                if (ci < d.Ca) {
+                  const int Hs = d.H / d.a_up, Ws = d.W / d.a_up;
+                  const int sy = d.a_up == 2 ? (iy >> 1) : iy, sx = d.a_up == 2 ? (ix >> 1) : ix;
+                  const long long off = (((long long)n * Hs + sy) * Ws + sx) * d.a_cstride + d.a_coff + ci;
+                  v = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(d.srcA) + off);
+                } else {
+                  const long long off = (((long long)n * d.H + iy) * d.W + ix) * d.b_cstride + d.b_coff + (ci - d.Ca);
+                  v = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(d.srcB) + off);
+                }
+              }
+            } else if (is_bias) {
+              v = sizeof(T) == 2 ? make_uint4(0x3f80u, 0u, 0u, 0u) : make_uint4(0x3f800000u, 0u, 0u, 0u);
+            }
+          }
+          reg[i][e] = v;
+          if (++ox == d.Wo) { ox = 0; if (++oy == d.Ho) { oy = 0; ++n; } }
+        }
+      } else {
+        const int j = j0 + tk_row[i];
+        const bool jvalid = j < d.Cout;
+        int q = 0, co = j;
+        if (d.convT) { const int Cq = d.Cout >> 2; q = j / Cq; co = j - q * Cq; }
+        int ox = p0 % d.Wo, tt = p0 / d.Wo;
+        int oy = tt % d.Ho, n = tt / d.Ho;
+#pragma unroll
+        for (int e = 0; e < KCH; ++e) {
+          uint4 v = make_uint4(0u, 0u, 0u, 0u);
+          const int p = p0 + e;
+          if (p < a.M && jvalid) {
+            long long op = p;
+            if (d.convT) op = ((long long)n * (2 * d.Ho) + 2 * oy + (q >> 1)) * (2 * d.Wo) + 2 * ox + (q & 1);
+            v = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.dy) + op * a.dy_cs + a.dy_coff + co);
+          }
+          reg[i][e] = v;
+          if (++ox == d.Wo) { ox = 0; if (++oy == d.Ho) { oy = 0; ++n; } }
+        }
+      }
+    }
+  };
+  auto stage_store = [&](int s) __attribute__((always_inline)) {
+    uint4* sm = smem + s * STAGE;
+#pragma unroll
+    for (int i = 0; i < TPT; ++i) {
+      if (tk_kind[i] < 0) continue;
+      uint4 o[KCH];
+      Tr<T>::run(reg[i], o);
+      uint4* base = tk_kind[i] == 0 ? sm : sm + BK * 8;
+#pragma unroll
+      for (int e = 0; e < KCH; ++e) base[swz(tk_row[i] + e, tk_pg[i])] = o[e];
+    }
+  };
+
+  floatx4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  if (pb_begin < pb_end) {
+    gather(pb_begin);
+    stage_store(0);
+  }
+  __syncthreads();
+  for (int pb = pb_begin; pb < pb_end; ++pb) {
+    const int cur = (pb - pb_begin) & 1;
+    if (pb + 1 < pb_end) gather(pb + 1);
+    const uint4* sX = smem + cur * STAGE;
+    const uint4* sY = sX + BK * 8;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ch = s * 4 + (lane >> 4);
+      uint4 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = sX[swz(wk * TM * 16 + i * 16 + (lane & 15), ch)];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = sY[swz(wc * TN * 16 + j * 16 + (lane & 15), ch)];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (sizeof(T) == 2) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8_t, af[i]), __builtin_bit_cast(bf16x8_t, bfr[j]), acc[i][j], 0, 0, 0);
+          } else {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[i].x), __uint_as_float(bfr[j].x), acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[i].y), __uint_as_float(bfr[j].y), acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[i].z), __uint_as_float(bfr[j].z), acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(af[i].w), __uint_as_float(bfr[j].w), acc[i][j], 0, 0, 0);
+          }
+        }
+      }
+    }
+    if (pb + 1 < pb_end) stage_store(cur ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: lane holds rows k..k+3 (4*(lane>>4)+r) of column j (lane & 15) -> ws[split][j][k..k+3]
+  float* ws = a.ws + (long long)split * a.Cg * a.Kg;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int k = k0 + wk * TM * 16 + i * 16 + (lane >> 4) * 4;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int jj = j0 + wc * TN * 16 + j * 16 + (lane & 15);
+      if (k < a.Kg && jj < a.Cg)
+        *reinterpret_cast<floatx4*>(ws + (long long)jj * a.Kg + k) = acc[i][j];
+    }
+  }
+}
+
+template <typename T, int BK, int BC, int WK, int WC>
+static int wgrad_launch(const WgradArgs& a, hipStream_t s) {
+  constexpr int STAGE = (BK + BC) * 8;
+  const size_t lds = 2 * STAGE * sizeof(uint4);
+  dim3 grid((a.Kg + BK - 1) / BK, (a.Cg + BC - 1) / BC, a.splits);
+  hipLaunchKernelGGL((conv_wgrad_kernel<T, BK, BC, WK, WC>), grid, dim3(256), lds, s, a);
+  return hiseg_check_launch("conv_wgrad");
+}
+
+template <typename T>
+static int wgrad_typed(const WgradArgs& a, hipStream_t s) {
+  if (a.Cg >= 128) return wgrad_launch<T, 128, 128, 2, 2>(a, s);
+  if (a.Cg >= 64) return wgrad_launch<T, 128, 64, 2, 2>(a, s);
+  if (a.Cg >= 32) return wgrad_launch<T, 128, 32, 2, 2>(a, s);
+  return wgrad_launch<T, 64, 16, 4, 1>(a, s);
+}
+
+static int wgrad_geometry(const hiseg_conv2d_desc* d, int want_bias, int* Cg, int* Kg, int* splits, int* M,
+                          int* Cin, int* Ktot, int* bps) {
+  HISEG_REQUIRE(d != nullptr, HISEG_ERR_BAD_ARG, "wgrad: null descriptor");
+  HISEG_REQUIRE(d->dtype == HISEG_F32 || d->dtype == HISEG_BF16, HISEG_ERR_BAD_DTYPE, "wgrad: dtype %d", d->dtype);
+  const int kch = d->dtype == HISEG_BF16 ? 8 : 4;
+  *Cin = d->Ca + d->Cb;
+  HISEG_REQUIRE(d->Ca > 0 && d->Ca % kch == 0 && d->Cb % kch == 0, HISEG_ERR_BAD_SHAPE, "wgrad: channels");
+  HISEG_REQUIRE(d->Cout > 0 && d->Cout % kch == 0 && (!d->convT || (d->Cout / 4) % kch == 0), HISEG_ERR_BAD_SHAPE,
+                "wgrad: Cout %d must be a multiple of %d (per sub-pixel for convT)", d->Cout, kch);
+  *Ktot = d->KH * d->KW * (*Cin);
+  *Kg = (*Ktot + (want_bias ? 1 : 0) + 63) / 64 * 64;
+  *Cg = (d->Cout + 15) / 16 * 16;
+  const long long Mll = (long long)d->N * d->Ho * d->Wo;
+  HISEG_REQUIRE(Mll > 0 && Mll < (1ll << 31), HISEG_ERR_BAD_SHAPE, "wgrad: pixels");
+  *M = (int)Mll;
+  const int PB = 8 * kch;
+  const int nblocks = (*M + PB - 1) / PB;
+  const int BK = *Kg >= 128 ? 128 : 64;
+  const int BC = *Cg >= 128 ? 128 : *Cg >= 64 ? 64 : *Cg >= 32 ? 32 : 16;
+  const long long tiles = (long long)((*Kg + BK - 1) / BK) * ((*Cg + BC - 1) / BC);
+  int sp = (int)((1024 + tiles - 1) / tiles);
+  if (sp > nblocks) sp = nblocks;
+  if (sp < 1) sp = 1;
+  *bps = (nblocks + sp - 1) / sp;
+  *splits = (nblocks + *bps - 1) / *bps;
+  return HISEG_OK;
+}
+
+}  // namespace hiseg
+
+using namespace hiseg;
+
+extern "C" int hiseg_conv2d_wgrad_dims(const hiseg_conv2d_desc* fwd, int want_bias, int* Cg, int* Kg, int* splits) {
+  int M, Cin, Ktot, bps;
+  return wgrad_geometry(fwd, want_bias, Cg, Kg, splits, &M, &Cin, &Ktot, &bps);
+}
+
+extern "C" int hiseg_conv2d_wgrad(const hiseg_conv2d_desc* fwd, const void* dy, int dy_cstride, int dy_coff,
+                                  int want_bias, float* ws, int splits, hiseg_stream_t stream) {
+  WgradArgs a;
+  int sp;
+  const int r = wgrad_geometry(fwd, want_bias, &a.Cg, &a.Kg, &sp, &a.M, &a.Cin, &a.Ktot, &a.blocks_per_split);
+  if (r) return r;
+  HISEG_REQUIRE(splits == sp, HISEG_ERR_BAD_ARG, "wgrad: splits %d != %d from hiseg_conv2d_wgrad_dims", splits, sp);
+  HISEG_REQUIRE(dy && ws && fwd->srcA, HISEG_ERR_BAD_ARG, "wgrad: null pointer");
+  const int kch = fwd->dtype == HISEG_BF16 ? 8 : 4;
+  HISEG_REQUIRE(dy_cstride % kch == 0 && dy_coff % kch == 0, HISEG_ERR_BAD_SHAPE, "wgrad: dy view alignment");
+  HISEG_REQUIRE(al16(dy) && al16(fwd->srcA) && al16(fwd->srcB) && al16(ws), HISEG_ERR_BAD_SHAPE, "wgrad: alignment");
+  a.d = *fwd;
+  a.dy = dy; a.dy_cs = dy_cstride; a.dy_coff = dy_coff;
+  a.want_bias = want_bias;
+  a.splits = splits;
+  a.ws = ws;
+  hipStream_t s = (hipStream_t)stream;
+  return fwd->dtype == HISEG_BF16 ? wgrad_typed<bf16_t>(a, s) : wgrad_typed<float>(a, s);
+}
+
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* ws, int splits, hiseg_wgrad_map m, float* gw,
+                                                           float* gb, int acc) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  const int Cin = m.ca + m.cb;
+  const int Ktot = m.KH * m.KW * Cin;
+  const int ncol = Ktot + (m.want_bias ? 1 : 0);
+  if (idx >= (long long)m.Cout * ncol) return;
+  const int j = (int)(idx / ncol);
+  const int k = (int)(idx - (long long)j * ncol);
+  const long long plane = (long long)m.Cg * m.Kg;
+  if (k == Ktot) {  // bias column
+    if (!gb) return;
+    int co = j;
+    if (m.convT) {
+      const int C = m.Cout / 4;
+      if (j >= C) return;  // the q == 0 thread sums the 4 sub-pixel columns
+      co = j;
+    }
+    float s = 0.f;
+    const int nq = m.convT ? 4 : 1;
+    for (int q = 0; q < nq; ++q) {
+      const int jj = j + q * (m.convT ? m.Cout / 4 : 0);
+      for (int sp = 0; sp < splits; ++sp) s += ws[sp * plane + (long long)jj * m.Kg + k];
+    }
+    gb[co] = acc ? gb[co] + s : s;
+    return;
+  }
+  float s = 0.f;
+  for (int sp = 0; sp < splits; ++sp) s += ws[sp * plane + (long long)j * m.Kg + k];
+  long long dst;
+  if (m.convT) {
+    const int C = m.Cout / 4;
+    const int q = j / C, co = j - q * C;
+    if (k >= m.ca_real) return;
+    dst = (((long long)k * C + co) * 2 + (q >> 1)) * 2 + (q & 1);
+  } else {
+    const int tap = k / Cin, cp = k - tap * Cin;
+    int ci;
+    if (cp < m.ca) {
+      if (cp >= m.ca_real) return;
+      ci = cp;
+    } else {
+      const int b = cp - m.ca;
+      if (b >= m.cb_real) return;
+      ci = m.ca_real + b;
+    }
+    const int ky = tap / m.KW, kx = tap - ky * m.KW;
+    dst = (((long long)j * (m.ca_real + m.cb_real) + ci) * m.KH + ky) * m.KW + kx;
+  }
+  gw[dst] = acc ? gw[dst] + s : s;
+}
+
+extern "C" int hiseg_conv2d_wgrad_reduce(const float* ws, int splits, const hiseg_wgrad_map* map, float* gw, float* gb,
+                                         int accumulate, hiseg_stream_t stream) {
+  HISEG_REQUIRE(ws && map && gw && splits > 0, HISEG_ERR_BAD_ARG, "wgrad_reduce: null argument");
+  const hiseg_wgrad_map m = *map;
+  HISEG_REQUIRE(!m.convT || m.Cout % 4 == 0, HISEG_ERR_BAD_SHAPE, "wgrad_reduce: convT Cout");
+  const long long n = (long long)m.Cout * (m.KH * m.KW * (m.ca + m.cb) + (m.want_bias ? 1 : 0));
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ws,
+                     splits, m, gw, gb, accumulate);
+  return hiseg_check_launch("wgrad_reduce");
+}
+
+// ------------------------------------------------------------------------------------------ packing
+__device__ __forceinline__ int real_channel(const hiseg_pack_entry& e, int cp) {
+  if (cp < e.ca) return cp < e.ca_real ? cp : -1;
+  const int b = cp - e.ca;
+  return b < e.cb_real ? e.ca_real + b : -1;
+}
+
+__global__ void __launch_bounds__(256) pack_weights_kernel(const hiseg_pack_entry* table) {
+  const hiseg_pack_entry e = table[blockIdx.y];
+  for (long long idx = (long long)blockIdx.x * 256 + threadIdx.x; idx < e.total; idx += (long long)gridDim.x * 256) {
+    const int row = (int)(idx / e.K_pad);
+    const int k = (int)(idx - (long long)row * e.K_pad);
+    float v = 0.f;
+    const int cinp = e.ca + e.cb;
+    if (e.mode == 0) {            // conv forward: [co][tap*cinp + cp]
+      if (row < e.Cout && k < e.KH * e.KW * cinp) {
+        const int tap = k / cinp, ci = real_channel(e, k - tap * cinp);
+        if (ci >= 0) v = e.src[((long long)row * e.Cin_real + ci) * e.KH * e.KW + tap];
+      }
+    } else if (e.mode == 1) {     // conv dgrad: [cp_in][tap'*cop + co], taps flipped
+      const int ci = row < cinp ? real_channel(e, row) : -1;
+      if (ci >= 0 && k < e.KH * e.KW * e.cop) {
+        const int tap2 = k / e.cop, co = k - tap2 * e.cop;
+        if (co < e.Cout) {
+          const int ky = e.KH - 1 - tap2 / e.KW, kx = e.KW - 1 - (tap2 % e.KW);
+          v = e.src[(((long long)co * e.Cin_real + ci) * e.KH + ky) * e.KW + kx];
+        }
+      }
+    } else if (e.mode == 2) {     // convT forward: [q*C + co][ci], W [Cin][C][2][2]
+      if (row < 4 * e.Cout && k < e.Cin_real) {
+        const int q = row / e.Cout, co = row - q * e.Cout;
+        v = e.src[((long long)k * e.Cout + co) * 4 + q];
+      }
+    } else {                      // convT dgrad: 2x2/s2 conv [ci][tap*cop + co]
+      if (row < e.Cin_real && k < 4 * e.cop) {
+        const int tap = k / e.cop, co = k - tap * e.cop;
+        if (co < e.Cout) v = e.src[((long long)row * e.Cout + co) * 4 + tap];
+      }
+    }
+    if (e.dtype == HISEG_BF16) reinterpret_cast<uint16_t*>(e.dst)[idx] = f2bf(v);
+    else reinterpret_cast<float*>(e.dst)[idx] = v;
+  }
+}
+
+extern "C" int hiseg_pack_weights(const hiseg_pack_entry* table_dev, int n, int max_total, hiseg_stream_t stream) {
+  HISEG_REQUIRE(table_dev && n > 0 && max_total > 0, HISEG_ERR_BAD_ARG, "pack_weights: empty table");
+  int bx = (max_total + 255) / 256;
+  if (bx > 512) bx = 512;
+  hipLaunchKernelGGL(pack_weights_kernel, dim3(bx, n), dim3(256), 0, (hipStream_t)stream, table_dev);
+  return hiseg_check_launch("pack_weights");
+}

@@ -1,0 +1,797 @@
+// Training kernels of the refined hierarchical head's non-conv ops (gfx950):
+//   * SpatialAttentionModule (attention_modules.py:67-113) train forward (+ Dropout2d) / backward
+//   * ChannelAttentionModule (attention_modules.py:10-64) train forward (+ Dropout2d) / backward
+//   * upsample_bg_fg [ConvT 2->32, BatchNorm(train), ReLU, 1x1 32->2] + softmax + hierarchical
+//     combine + the target branch's last 1x1 (refinement.py:501-506,559-596) forward / backward
+//   * the target branch's last 1x1 conv (Ct -> 2) backward
+// All are HBM-streaming kernels; reductions go through deterministic per-block partials and a
+// finalize kernel (no atomics).
+#include <float.h>
+#include "common.h"
+#include "hiseg_train.h"
+#include "hiseg_head_train.h"
+
+namespace hiseg {
+
+template <typename T>
+__device__ __forceinline__ float ldT(const void* p, long long i) { return Elem<T>::load(p, i); }
+template <typename T>
+__device__ __forceinline__ void stT(void* p, long long i, float v) { Elem<T>::store(p, i, v); }
+
+static inline unsigned nb(long long n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+static inline unsigned capb(long long n) {
+  long long b = (n + 255) / 256;
+  return (unsigned)(b > 4096 ? 4096 : (b < 1 ? 1 : b));
+}
+
+// ======================================================================================= spatial attention
+// stats[p] = (mean_c x, max_c x), argmax[p] = first channel attaining the max.
+template <typename T>
+__global__ void __launch_bounds__(256) sa_stats_kernel(const void* x, long long P, int C, float* stats, int* argmax) {
+  constexpr int K = Chunk<T>::N;
+  constexpr int G = 16;
+  const int nch = C / K;
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long pix = gid / G;
+  const int l = (int)(gid % G);
+  float s = 0.f, m = -FLT_MAX, v[K];
+  int am = 0x7fffffff;
+  if (pix < P) {
+    const uint4* src = reinterpret_cast<const uint4*>(x) + pix * nch;
+    for (int ch = l; ch < nch; ch += G) {
+      Chunk<T>::unpack(src[ch], v);
+#pragma unroll
+      for (int e = 0; e < K; ++e) {
+        s += v[e];
+        if (v[e] > m) { m = v[e]; am = ch * K + e; }
+      }
+    }
+  }
+#pragma unroll
+  for (int off = G / 2; off > 0; off >>= 1) {
+    s += __shfl_xor(s, off, G);
+    const float mo = __shfl_xor(m, off, G);
+    const int ao = __shfl_xor(am, off, G);
+    if (mo > m || (mo == m && ao < am)) { m = mo; am = ao; }
+  }
+  if (pix < P && l == 0) {
+    stats[pix * 2] = s / (float)C;
+    stats[pix * 2 + 1] = m;
+    argmax[pix] = am;
+  }
+}
+
+__global__ void __launch_bounds__(256) sa_map_kernel(const float* stats, int N, int H, int W, const float* w, int k,
+                                                     float* att) {
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= (long long)N * H * W) return;
+  const int x = (int)(gid % W);
+  const long long t = gid / W;
+  const int y = (int)(t % H);
+  const int n = (int)(t / H);
+  const int r = k / 2;
+  float acc = 0.f;
+  for (int c = 0; c < 2; ++c)
+    for (int ky = 0; ky < k; ++ky) {
+      const int yy = y + ky - r;
+      if (yy < 0 || yy >= H) continue;
+      for (int kx = 0; kx < k; ++kx) {
+        const int xx = x + kx - r;
+        if (xx < 0 || xx >= W) continue;
+        acc += w[(c * k + ky) * k + kx] * stats[(((long long)n * H + yy) * W + xx) * 2 + c];
+      }
+    }
+  att[gid] = sigmoidf_(acc);
+}
+
+// out = x * att[p] * mul[n][c]
+template <typename T>
+__global__ void __launch_bounds__(256) sa_apply_kernel(const void* x, long long P, int HW, int C, const float* att,
+                                                       const float* mul, void* out) {
+  constexpr int K = Chunk<T>::N;
+  const int nch = C / K;
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= P * nch) return;
+  const long long p = gid / nch;
+  const int ch = (int)(gid - p * nch);
+  const float a = att[p];
+  float v[K];
+  Chunk<T>::unpack(reinterpret_cast<const uint4*>(x)[gid], v);
+  const float* m = mul ? mul + (p / HW) * C + ch * K : nullptr;
+#pragma unroll
+  for (int e = 0; e < K; ++e) v[e] *= m ? a * m[e] : a;
+  reinterpret_cast<uint4*>(out)[gid] = Chunk<T>::pack(v);
+}
+
+// dpre[p] = (sum_c dout*mul*x) * att * (1 - att)
+template <typename T>
+__global__ void __launch_bounds__(256) sa_bwd1_kernel(const void* x, const void* dout, long long P, int HW, int C,
+                                                      const float* att, const float* mul, float* dpre) {
+  constexpr int K = Chunk<T>::N;
+  constexpr int G = 16;
+  const int nch = C / K;
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long pix = gid / G;
+  const int l = (int)(gid % G);
+  float s = 0.f, v[K], g[K];
+  if (pix < P) {
+    const uint4* xs = reinterpret_cast<const uint4*>(x) + pix * nch;
+    const uint4* ds = reinterpret_cast<const uint4*>(dout) + pix * nch;
+    const float* m = mul ? mul + (pix / HW) * C : nullptr;
+    for (int ch = l; ch < nch; ch += G) {
+      Chunk<T>::unpack(xs[ch], v);
+      Chunk<T>::unpack(ds[ch], g);
+#pragma unroll
+      for (int e = 0; e < K; ++e) s += g[e] * v[e] * (m ? m[ch * K + e] : 1.f);
+    }
+  }
+#pragma unroll
+  for (int off = G / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, G);
+  if (pix < P && l == 0) {
+    const float a = att[pix];
+    dpre[pix] = s * a * (1.f - a);
+  }
+}
+
+// dstats[p][c] = sum_taps w[c][ky][kx] * dpre[y - ky + r][x - kx + r]   (adjoint of the 7x7 correlation)
+__global__ void __launch_bounds__(256) sa_bwd2_kernel(const float* dpre, int N, int H, int W, const float* w, int k,
+                                                      float* dstats) {
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= (long long)N * H * W) return;
+  const int x = (int)(gid % W);
+  const long long t = gid / W;
+  const int y = (int)(t % H);
+  const int n = (int)(t / H);
+  const int r = k / 2;
+  float a0 = 0.f, a1 = 0.f;
+  for (int ky = 0; ky < k; ++ky) {
+    const int yy = y - ky + r;
+    if (yy < 0 || yy >= H) continue;
+    for (int kx = 0; kx < k; ++kx) {
+      const int xx = x - kx + r;
+      if (xx < 0 || xx >= W) continue;
+      const float d = dpre[((long long)n * H + yy) * W + xx];
+      a0 += w[ky * k + kx] * d;
+      a1 += w[(k + ky) * k + kx] * d;
+    }
+  }
+  dstats[gid * 2] = a0;
+  dstats[gid * 2 + 1] = a1;
+}
+
+// dw partial per image row: part[(n*H + y)][c*k*k + ky*k + kx] = sum_x dpre[y][x] * stats[y+ky-r][x+kx-r][c]
+__global__ void __launch_bounds__(256) sa_dw_kernel(const float* dpre, const float* stats, int N, int H, int W, int k,
+                                                    float* part) {
+  const int row = blockIdx.x;  // n*H + y
+  const int n = row / H, y = row - n * H;
+  const int t = threadIdx.x;
+  const int nw = 2 * k * k;
+  if (t >= nw) return;
+  const int c = t / (k * k), ky = (t / k) % k, kx = t % k;
+  const int r = k / 2;
+  const int yy = y + ky - r;
+  float acc = 0.f;
+  if (yy >= 0 && yy < H) {
+    for (int x = 0; x < W; ++x) {
+      const int xx = x + kx - r;
+      if (xx < 0 || xx >= W) continue;
+      acc += dpre[((long long)n * H + y) * W + x] * stats[(((long long)n * H + yy) * W + xx) * 2 + c];
+    }
+  }
+  part[(long long)row * nw + t] = acc;
+}
+
+// out[c] (+)= sum_r part[r*ld + c], c < cols
+__global__ void __launch_bounds__(128) sum_rows_kernel(const float* part, int rows, int ld, int cols, float* out, int acc) {
+  const int c = blockIdx.x * 128 + threadIdx.x;
+  if (c >= cols) return;
+  double s = 0;
+  for (int r = 0; r < rows; ++r) s += part[(long long)r * ld + c];
+  out[c] = acc ? (float)(out[c] + s) : (float)s;
+}
+
+// dx = dout*mul*att + dstats0 / C + [c == argmax] * dstats1
+template <typename T>
+__global__ void __launch_bounds__(256) sa_bwd3_kernel(const void* dout, long long P, int HW, int C, const float* att,
+                                                      const float* mul, const float* dstats, const int* argmax, void* dx) {
+  constexpr int K = Chunk<T>::N;
+  const int nch = C / K;
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= P * nch) return;
+  const long long p = gid / nch;
+  const int ch = (int)(gid - p * nch);
+  const float a = att[p], d0 = dstats[p * 2] / (float)C, d1 = dstats[p * 2 + 1];
+  const int am = argmax[p];
+  const float* m = mul ? mul + (p / HW) * C + ch * K : nullptr;
+  float g[K];
+  Chunk<T>::unpack(reinterpret_cast<const uint4*>(dout)[gid], g);
+#pragma unroll
+  for (int e = 0; e < K; ++e) {
+    float v = g[e] * a * (m ? m[e] : 1.f) + d0;
+    if (ch * K + e == am) v += d1;
+    g[e] = v;
+  }
+  reinterpret_cast<uint4*>(dx)[gid] = Chunk<T>::pack(g);
+}
+
+// ======================================================================================= channel attention
+constexpr int kGapSplits = 16;
+
+// part[n][s][c] = sum_{p in split s of image n} x[p][c] (* dout[p][c] * mul[n][c] if dout)
+template <typename T>
+__global__ void __launch_bounds__(256) ca_gap_kernel(const void* x, const void* dout, const float* mul, int HW, int C,
+                                                     float* part) {
+  const int n = blockIdx.x, s = blockIdx.y;
+  const int p0 = (int)((long long)HW * s / kGapSplits), p1 = (int)((long long)HW * (s + 1) / kGapSplits);
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float acc = 0.f;
+    const float m = (dout && mul) ? mul[(long long)n * C + c] : 1.f;
+    for (int p = p0; p < p1; ++p) {
+      const long long i = ((long long)n * HW + p) * C + c;
+      float v = ldT<T>(x, i);
+      if (dout) v *= ldT<T>(dout, i) * m;
+      acc += v;
+    }
+    part[((long long)n * kGapSplits + s) * C + c] = acc;
+  }
+}
+
+__device__ __forceinline__ float act_f(float v, int act) { return apply_act(v, act); }
+__device__ __forceinline__ float act_d(float pre, int act) {
+  switch (act) {
+    case HISEG_ACT_RELU: return pre > 0.f ? 1.f : 0.f;
+    case HISEG_ACT_SILU: { const float s = sigmoidf_(pre); return s * (1.f + pre * (1.f - s)); }
+    case HISEG_ACT_SIGMOID: { const float s = sigmoidf_(pre); return s * (1.f - s); }
+    default: return 1.f;
+  }
+}
+
+// per image: gap, hidden pre-activation, gate
+__global__ void __launch_bounds__(256) ca_mlp_kernel(const float* part, int HW, int C, int Cr, const float* w1,
+                                                     const float* w2, int act, float* gap, float* hpre, float* gate) {
+  extern __shared__ float sm[];
+  float* g = sm;
+  float* h = sm + C;
+  const int n = blockIdx.x;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float s = 0.f;
+    for (int k = 0; k < kGapSplits; ++k) s += part[((long long)n * kGapSplits + k) * C + c];
+    g[c] = s / (float)HW;
+    gap[(long long)n * C + c] = g[c];
+  }
+  __syncthreads();
+  for (int r = threadIdx.x; r < Cr; r += 256) {
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) s += w1[(long long)r * C + c] * g[c];
+    hpre[(long long)n * Cr + r] = s;
+    h[r] = act_f(s, act);
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float s = 0.f;
+    for (int r = 0; r < Cr; ++r) s += w2[(long long)c * Cr + r] * h[r];
+    gate[(long long)n * C + c] = sigmoidf_(s);
+  }
+}
+
+// out = x * gate[n][c] * mul[n][c]   (NHWC, C channels contiguous)
+template <typename T>
+__global__ void __launch_bounds__(256) ca_apply_kernel(const void* x, int N, int HW, int C, const float* gate,
+                                                       const float* mul, void* out) {
+  constexpr int K = Chunk<T>::N;
+  const int nch = C / K;
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= (long long)N * HW * nch) return;
+  const int ch = (int)(gid % nch);
+  const long long n = gid / nch / HW;
+  float v[K];
+  Chunk<T>::unpack(reinterpret_cast<const uint4*>(x)[gid], v);
+  const float* g = gate + n * C + ch * K;
+  const float* m = mul ? mul + n * C + ch * K : nullptr;
+#pragma unroll
+  for (int e = 0; e < K; ++e) v[e] *= g[e] * (m ? m[e] : 1.f);
+  reinterpret_cast<uint4*>(out)[gid] = Chunk<T>::pack(v);
+}
+
+// per image: ds = dgate * g (1-g); dh; dgap; per-image weight-gradient rows
+__global__ void __launch_bounds__(256) ca_mlp_bwd_kernel(const float* part, int C, int Cr, const float* w1,
+                                                         const float* w2, int act, const float* gap, const float* hpre,
+                                                         const float* gate, float* dgap, float* wpart) {
+  extern __shared__ float sm[];
+  float* ds = sm;
+  float* dh = sm + C;
+  const int n = blockIdx.x;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float s = 0.f;
+    for (int k = 0; k < kGapSplits; ++k) s += part[((long long)n * kGapSplits + k) * C + c];
+    const float g = gate[(long long)n * C + c];
+    ds[c] = s * g * (1.f - g);
+  }
+  __syncthreads();
+  for (int r = threadIdx.x; r < Cr; r += 256) {
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) s += w2[(long long)c * Cr + r] * ds[c];
+    dh[r] = s * act_d(hpre[(long long)n * Cr + r], act);
+  }
+  __syncthreads();
+  float* wp = wpart + (long long)n * 2 * C * Cr;  // [dW1 (Cr x C)][dW2 (C x Cr)]
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float s = 0.f;
+    for (int r = 0; r < Cr; ++r) s += w1[(long long)r * C + c] * dh[r];
+    dgap[(long long)n * C + c] = s;
+  }
+  for (int i = threadIdx.x; i < C * Cr; i += 256) {
+    const int r = i / C, c = i - r * C;
+    wp[i] = dh[r] * gap[(long long)n * C + c];
+    const int c2 = i / Cr, r2 = i - c2 * Cr;
+    wp[C * Cr + i] = ds[c2] * act_f(hpre[(long long)n * Cr + r2], act);
+  }
+}
+
+// dx = dout*mul*gate + dgap/HW
+template <typename T>
+__global__ void __launch_bounds__(256) ca_dx_kernel(const void* dout, int N, int HW, int C, const float* gate,
+                                                    const float* mul, const float* dgap, void* dx) {
+  constexpr int K = Chunk<T>::N;
+  const int nch = C / K;
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= (long long)N * HW * nch) return;
+  const int ch = (int)(gid % nch);
+  const long long n = gid / nch / HW;
+  float v[K];
+  Chunk<T>::unpack(reinterpret_cast<const uint4*>(dout)[gid], v);
+  const float inv = 1.f / (float)HW;
+#pragma unroll
+  for (int e = 0; e < K; ++e) {
+    const long long i = n * C + ch * K + e;
+    v[e] = v[e] * gate[i] * (mul ? mul[i] : 1.f) + dgap[i] * inv;
+  }
+  reinterpret_cast<uint4*>(dx)[gid] = Chunk<T>::pack(v);
+}
+
+// ======================================================================================= upsample_bg_fg + combine
+struct UbfArgs {
+  const float* low; int N, h, w;
+  const float* ut_w; const float* ut_b;     // ConvT [2][32][2][2], bias [32]
+  const float* scale; const float* shift;   // BN(train) fold: a = relu(z*scale + shift)
+  const float* mean; const float* invstd; const float* gamma;
+  const float* u1_w; const float* u1_b;     // [2][32], [2]
+};
+
+__device__ __forceinline__ float ubf_z(const UbfArgs& u, float l0, float l1, int c, int q) {
+  return l0 * u.ut_w[(c * 2 + (q >> 1)) * 2 + (q & 1)] + l1 * u.ut_w[((32 + c) * 2 + (q >> 1)) * 2 + (q & 1)] + u.ut_b[c];
+}
+
+// BN statistics of z = ConvT(low) over all N*2h*2w pixels: partial [S][3][32] (Welford), block = 8 rows x 32 ch
+__global__ void __launch_bounds__(256) ubf_stats_kernel(UbfArgs u, float* partial) {
+  __shared__ float sn[256], sm[256], sq[256];
+  const int t = threadIdx.x, c = t & 31, r = t >> 5;
+  const long long P = (long long)u.N * u.h * u.w;
+  const long long b = P * blockIdx.x / gridDim.x, e = P * (blockIdx.x + 1) / gridDim.x;
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  for (long long p = b + r; p < e; p += 8) {
+    const float l0 = u.low[p * 2], l1 = u.low[p * 2 + 1];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float x = ubf_z(u, l0, l1, c, q);
+      n += 1.f;
+      const float d = x - mean;
+      mean += d / n;
+      m2 += d * (x - mean);
+    }
+  }
+  sn[t] = n; sm[t] = mean; sq[t] = m2;
+  __syncthreads();
+  if (r == 0) {
+    for (int rr = 1; rr < 8; ++rr) {
+      const int o = rr * 32 + c;
+      const float nb2 = sn[o];
+      if (nb2 == 0.f) continue;
+      const float nt = n + nb2, d = sm[o] - mean;
+      mean += d * (nb2 / nt);
+      m2 += sq[o] + d * d * (n * nb2 / nt);
+      n = nt;
+    }
+    float* out = partial + (long long)blockIdx.x * 96;
+    out[c] = n; out[32 + c] = mean; out[64 + c] = m2;
+  }
+}
+
+// per mask pixel: bg/fg logits, target logits (fused Ct->2 1x1), softmax, hierarchical combine
+template <typename T>
+__global__ void __launch_bounds__(256) ubf_fwd_kernel(UbfArgs u, const void* tfeat, int Ct, const float* t_w,
+                                                      const float* t_b, float* logits, float* bgfg, float* tn) {
+  __shared__ float s_tw[2 * 512];
+  for (int i = threadIdx.x; i < 2 * Ct; i += 256) s_tw[i] = t_w[i];
+  __syncthreads();
+  const int H = 2 * u.h, W = 2 * u.w;
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= (long long)u.N * H * W) return;
+  const int X = (int)(gid % W);
+  const long long tt = gid / W;
+  const int Y = (int)(tt % H);
+  const int n = (int)(tt / H);
+  const int q = (Y & 1) * 2 + (X & 1);
+  const float* lo = u.low + (((long long)n * u.h + (Y >> 1)) * u.w + (X >> 1)) * 2;
+  const float l0 = lo[0], l1 = lo[1];
+  float b0 = u.u1_b[0], b1 = u.u1_b[1];
+  for (int c = 0; c < 32; ++c) {
+    float a = ubf_z(u, l0, l1, c, q) * u.scale[c] + u.shift[c];
+    a = a > 0.f ? a : 0.f;
+    b0 += u.u1_w[c] * a;
+    b1 += u.u1_w[32 + c] * a;
+  }
+  constexpr int K = Chunk<T>::N;
+  float t0 = t_b[0], t1 = t_b[1], v[K];
+  const uint4* tf = reinterpret_cast<const uint4*>(tfeat) + gid * (Ct / K);
+  for (int ch = 0; ch < Ct / K; ++ch) {
+    Chunk<T>::unpack(tf[ch], v);
+#pragma unroll
+    for (int e = 0; e < K; ++e) {
+      t0 += s_tw[ch * K + e] * v[e];
+      t1 += s_tw[Ct + ch * K + e] * v[e];
+    }
+  }
+  const float mx = fmaxf(b0, b1);
+  const float e0 = __expf(b0 - mx), e1 = __expf(b1 - mx);
+  const float pf = e1 / (e0 + e1);
+  const long long plane = (long long)H * W, pp = (long long)Y * W + X;
+  float* L = logits + (long long)n * 3 * plane + pp;
+  L[0] = b0;
+  L[plane] = b1 + t0 * pf;
+  L[2 * plane] = b1 + t1 * pf;
+  float* G = bgfg + (long long)n * 2 * plane + pp;
+  G[0] = b0; G[plane] = b1;
+  float* Tn = tn + (long long)n * 2 * plane + pp;
+  Tn[0] = t0; Tn[plane] = t1;
+}
+
+// pass 1 (8 pixel rows x 32 channels per block): combine backward -> db, dtn per pixel (written by c == 0);
+// per channel: sum g, sum g*xhat, sum xhat (BN bwd), dW1[k][c] = sum db_k * a_c; db1.
+// partial layout per block: [32 g][32 gx][32 x][64 dW1][2 db1]  (162)
+__global__ void __launch_bounds__(256) ubf_bwd1_kernel(UbfArgs u, const float* dlogits, const float* dbgfg_ext,
+                                                       const float* dtn_ext, const float* bgfg, const float* tn,
+                                                       float* db_out, float* dtn_out, float* partial) {
+  __shared__ float red[8][162];
+  const int t = threadIdx.x, c = t & 31, r = t >> 5;
+  const int H = 2 * u.h, W = 2 * u.w;
+  const long long P = (long long)u.N * H * W, plane = (long long)H * W;
+  const long long b = P * blockIdx.x / gridDim.x, e = P * (blockIdx.x + 1) / gridDim.x;
+  const float mu = u.mean[c], inv = u.invstd[c], w0 = u.u1_w[c], w1 = u.u1_w[32 + c];
+  float sg = 0.f, sgx = 0.f, sx = 0.f, dw0 = 0.f, dw1 = 0.f, db0s = 0.f, db1s = 0.f;
+  for (long long p = b + r; p < e; p += 8) {
+    const int X = (int)(p % W);
+    const long long tt = p / W;
+    const int Y = (int)(tt % H);
+    const long long n = tt / H;
+    const long long pp = (long long)Y * W + X;
+    const float* G = bgfg + n * 2 * plane + pp;
+    const float* Tn = tn + n * 2 * plane + pp;
+    const float* dL = dlogits + n * 3 * plane + pp;
+    const float g0 = G[0], g1 = G[plane], t0 = Tn[0], t1 = Tn[plane];
+    const float dL0 = dL[0], dL1 = dL[plane], dL2 = dL[2 * plane];
+    const float mx = fmaxf(g0, g1);
+    const float ex0 = __expf(g0 - mx), ex1 = __expf(g1 - mx);
+    const float pf = ex1 / (ex0 + ex1);
+    const float dpf = dL1 * t0 + dL2 * t1;
+    const float dsg = dpf * pf * (1.f - pf);
+    float db0 = dL0 - dsg, db1 = dL1 + dL2 + dsg;
+    float dt0 = dL1 * pf, dt1 = dL2 * pf;
+    if (dbgfg_ext) { db0 += dbgfg_ext[n * 2 * plane + pp]; db1 += dbgfg_ext[n * 2 * plane + plane + pp]; }
+    if (dtn_ext) { dt0 += dtn_ext[n * 2 * plane + pp]; dt1 += dtn_ext[n * 2 * plane + plane + pp]; }
+    if (c == 0) {
+      db_out[p * 2] = db0; db_out[p * 2 + 1] = db1;
+      dtn_out[p * 2] = dt0; dtn_out[p * 2 + 1] = dt1;
+      db0s += db0; db1s += db1;
+    }
+    const int q = (Y & 1) * 2 + (X & 1);
+    const float* lo = u.low + ((n * u.h + (Y >> 1)) * u.w + (X >> 1)) * 2;
+    const float z = ubf_z(u, lo[0], lo[1], c, q);
+    float a = z * u.scale[c] + u.shift[c];
+    a = a > 0.f ? a : 0.f;
+    const float g = a > 0.f ? (w0 * db0 + w1 * db1) : 0.f;
+    const float xh = (z - mu) * inv;
+    sg += g; sgx += g * xh; sx += xh;
+    dw0 += db0 * a; dw1 += db1 * a;
+  }
+  red[r][c] = sg; red[r][32 + c] = sgx; red[r][64 + c] = sx; red[r][96 + c] = dw0; red[r][128 + c] = dw1;
+  if (c == 0) { red[r][160] = db0s; red[r][161] = db1s; }
+  __syncthreads();
+  if (t < 162) {
+    float s = 0.f;
+    for (int rr = 0; rr < 8; ++rr) s += red[rr][t];
+    partial[(long long)blockIdx.x * 162 + t] = s;
+  }
+}
+
+// finalize 1: BN coefficients + dgamma/dbeta/dW1/db1 (accumulate into the parameter gradients)
+// coef: [32 k][32 mean g][32 mean gx]
+__global__ void ubf_fin1_kernel(UbfArgs u, const float* partial, int nblk, long long P, float* coef, float* dgamma,
+                                float* dbeta, float* du1_w, float* du1_b, float* dut_b_analytic) {
+  const int t = threadIdx.x;
+  if (t >= 162) return;
+  double s = 0;
+  for (int b = 0; b < nblk; ++b) s += partial[(long long)b * 162 + t];
+  __shared__ double S[162];
+  S[t] = s;
+  __syncthreads();
+  if (t < 32) {
+    const double k = (u.gamma ? u.gamma[t] : 1.0) * u.invstd[t];
+    coef[t] = (float)k;
+    coef[32 + t] = (float)(S[t] / P);
+    coef[64 + t] = (float)(S[32 + t] / P);
+    dgamma[t] += (float)S[32 + t];
+    dbeta[t] += (float)S[t];
+    if (dut_b_analytic) dut_b_analytic[t] += (float)(k * (S[t] - P * (S[t] / P) - S[64 + t] * (S[32 + t] / P)));
+  }
+  if (t >= 96 && t < 160) du1_w[t - 96] += (float)S[t];
+  if (t >= 160) du1_b[t - 160] += (float)S[t];
+}
+
+// pass 2 (per low pixel, 8 rows x 32 channels): dz of the 4 children, dlow, dWt partial [ci][c][q] (256)
+__global__ void __launch_bounds__(256) ubf_bwd2_kernel(UbfArgs u, const float* db_in, const float* coef, float* dlow,
+                                                       float* partial) {
+  __shared__ float red[8][256];
+  const int t = threadIdx.x, c = t & 31, r = t >> 5;
+  const long long PL = (long long)u.N * u.h * u.w;
+  const long long b = PL * blockIdx.x / gridDim.x, e = PL * (blockIdx.x + 1) / gridDim.x;
+  const float k = coef[c], m1 = coef[32 + c], m2 = coef[64 + c], mu = u.mean[c], inv = u.invstd[c];
+  const float w0 = u.u1_w[c], w1 = u.u1_w[32 + c];
+  const int W = 2 * u.w;
+  float dw[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) dw[i] = 0.f;
+  for (long long p = b + r; p < e; p += 8) {
+    const int x = (int)(p % u.w);
+    const long long tt = p / u.w;
+    const int y = (int)(tt % u.h);
+    const long long n = tt / u.h;
+    const float l0 = u.low[p * 2], l1 = u.low[p * 2 + 1];
+    float dl0 = 0.f, dl1 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const long long P = (n * (2 * u.h) + 2 * y + (q >> 1)) * W + 2 * x + (q & 1);
+      const float z = ubf_z(u, l0, l1, c, q);
+      const float a = z * u.scale[c] + u.shift[c];
+      const float g = a > 0.f ? (w0 * db_in[P * 2] + w1 * db_in[P * 2 + 1]) : 0.f;
+      const float dz = k * (g - m1 - (z - mu) * inv * m2);
+      const float wa = u.ut_w[(c * 2 + (q >> 1)) * 2 + (q & 1)];
+      const float wb = u.ut_w[((32 + c) * 2 + (q >> 1)) * 2 + (q & 1)];
+      dl0 += wa * dz;
+      dl1 += wb * dz;
+      dw[q] += l0 * dz;
+      dw[4 + q] += l1 * dz;
+    }
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) {
+      dl0 += __shfl_xor(dl0, off, 32);
+      dl1 += __shfl_xor(dl1, off, 32);
+    }
+    if (c == 0) { dlow[p * 2] = dl0; dlow[p * 2 + 1] = dl1; }
+  }
+  // layout [ci][c][q] -> index (ci*32 + c)*4 + q
+#pragma unroll
+  for (int q = 0; q < 4; ++q) { red[r][(0 * 32 + c) * 4 + q] = dw[q]; red[r][(1 * 32 + c) * 4 + q] = dw[4 + q]; }
+  __syncthreads();
+  float s = 0.f;
+  for (int rr = 0; rr < 8; ++rr) s += red[rr][t];
+  partial[(long long)blockIdx.x * 256 + t] = s;
+}
+
+// ======================================================================================= last 1x1 (Ct -> 2) backward
+// dt[p][c] = sum_k dtn[p][k] * w[k][c]; dW[k][c] = sum_p dtn[p][k] * t[p][c]; db[k] = sum_p dtn[p][k]
+// block: 16 pixel rows x (Ct/K) chunk lanes
+template <typename T>
+__global__ void __launch_bounds__(256) pw2_bwd_kernel(const void* tfeat, long long P, int Ct, const float* dtn,
+                                                      const float* w, void* dt, float* partial) {
+  constexpr int K = Chunk<T>::N;
+  extern __shared__ float red[];  // [R][2*Ct + 2]
+  const int nch = Ct / K;
+  const int R = 256 / nch;
+  const int t = threadIdx.x, ch = t % nch, r = t / nch;
+  const long long b = P * blockIdx.x / gridDim.x, e = P * (blockIdx.x + 1) / gridDim.x;
+  float a0[K], a1[K], v[K], wk0[K], wk1[K];
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int i = 0; i < K; ++i) { a0[i] = 0.f; a1[i] = 0.f; wk0[i] = w[ch * K + i]; wk1[i] = w[Ct + ch * K + i]; }
+  if (r < R) {
+    for (long long p = b + r; p < e; p += R) {
+      const float d0 = dtn[p * 2], d1 = dtn[p * 2 + 1];
+      Chunk<T>::unpack(reinterpret_cast<const uint4*>(tfeat)[p * nch + ch], v);
+      float o[K];
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        a0[i] += d0 * v[i];
+        a1[i] += d1 * v[i];
+        o[i] = d0 * wk0[i] + d1 * wk1[i];
+      }
+      reinterpret_cast<uint4*>(dt)[p * nch + ch] = Chunk<T>::pack(o);
+      if (ch == 0) { s0 += d0; s1 += d1; }
+    }
+  }
+  const int cols = 2 * Ct + 2;
+  if (r < R) {
+#pragma unroll
+    for (int i = 0; i < K; ++i) { red[r * cols + ch * K + i] = a0[i]; red[r * cols + Ct + ch * K + i] = a1[i]; }
+    if (ch == 0) { red[r * cols + 2 * Ct] = s0; red[r * cols + 2 * Ct + 1] = s1; }
+  }
+  __syncthreads();
+  for (int i = t; i < cols; i += 256) {
+    float s = 0.f;
+    for (int rr = 0; rr < R; ++rr) s += red[rr * cols + i];
+    partial[(long long)blockIdx.x * cols + i] = s;
+  }
+}
+
+}  // namespace hiseg
+
+using namespace hiseg;
+
+#define DISPATCH_T(dtype, ...)        \
+  do {                                \
+    if ((dtype) == HISEG_BF16) {      \
+      using T = bf16_t;               \
+      __VA_ARGS__;                    \
+    } else {                          \
+      using T = float;                \
+      __VA_ARGS__;                    \
+    }                                 \
+  } while (0)
+
+static int chunk_of(int dtype) { return dtype == HISEG_BF16 ? 8 : 4; }
+
+extern "C" int hiseg_attn_spatial_train_fwd(int dtype, const void* x, int N, int H, int W, int C, const float* w7, int k,
+                                            const float* chan_mul, float* stats, int* argmax, float* att, void* out,
+                                            hiseg_stream_t stream) {
+  HISEG_REQUIRE(x && w7 && stats && argmax && att && out && N > 0 && H > 0 && W > 0 && (k & 1), HISEG_ERR_BAD_ARG,
+                "attn_spatial_train_fwd: bad args");
+  HISEG_REQUIRE(C > 0 && C % chunk_of(dtype) == 0, HISEG_ERR_BAD_SHAPE, "attn_spatial_train_fwd: C alignment");
+  hipStream_t s = (hipStream_t)stream;
+  const long long P = (long long)N * H * W;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(sa_stats_kernel<T>, dim3(nb(P * 16, 256)), dim3(256), 0, s, x, P, C, stats, argmax));
+  hipLaunchKernelGGL(sa_map_kernel, dim3(nb(P, 256)), dim3(256), 0, s, stats, N, H, W, w7, k, att);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(sa_apply_kernel<T>, dim3(nb(P * (C / chunk_of(dtype)), 256)), dim3(256), 0, s, x,
+                                       P, H * W, C, att, chan_mul, out));
+  return hiseg_check_launch("attn_spatial_train_fwd");
+}
+
+extern "C" int hiseg_attn_spatial_ws(int N, int H, int W, int k) {
+  // floats: dpre [P] + dstats [2P] + dw partial [N*H][2k^2]
+  const long long P = (long long)N * H * W;
+  return (int)(3 * P + (long long)N * H * 2 * k * k);
+}
+
+extern "C" int hiseg_attn_spatial_bwd(int dtype, const void* x, int N, int H, int W, int C, const float* w7, int k,
+                                      const float* chan_mul, const float* stats, const int* argmax, const float* att,
+                                      const void* dout, void* dx, float* ws, float* dw7, hiseg_stream_t stream) {
+  HISEG_REQUIRE(x && w7 && stats && argmax && att && dout && dx && ws && dw7, HISEG_ERR_BAD_ARG, "attn_spatial_bwd: null");
+  HISEG_REQUIRE(C > 0 && C % chunk_of(dtype) == 0 && (k & 1) && 2 * k * k <= 256, HISEG_ERR_BAD_SHAPE,
+                "attn_spatial_bwd: shape");
+  hipStream_t s = (hipStream_t)stream;
+  const long long P = (long long)N * H * W;
+  float* dpre = ws;
+  float* dstats = ws + P;
+  float* part = ws + 3 * P;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(sa_bwd1_kernel<T>, dim3(nb(P * 16, 256)), dim3(256), 0, s, x, dout, P, H * W, C,
+                                       att, chan_mul, dpre));
+  hipLaunchKernelGGL(sa_bwd2_kernel, dim3(nb(P, 256)), dim3(256), 0, s, dpre, N, H, W, w7, k, dstats);
+  hipLaunchKernelGGL(sa_dw_kernel, dim3(N * H), dim3(256), 0, s, dpre, stats, N, H, W, k, part);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(nb(2 * k * k, 128)), dim3(128), 0, s, part, N * H, 2 * k * k, 2 * k * k, dw7, 1);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(sa_bwd3_kernel<T>, dim3(nb(P * (C / chunk_of(dtype)), 256)), dim3(256), 0, s,
+                                       dout, P, H * W, C, att, chan_mul, dstats, argmax, dx));
+  return hiseg_check_launch("attn_spatial_bwd");
+}
+
+extern "C" int hiseg_attn_channel_ws(int N, int C, int Cr) {
+  return N * kGapSplits * C + N * C + N * 2 * C * Cr;  // floats: gap partials, dgap, per-image weight grads
+}
+
+extern "C" int hiseg_attn_channel_train_fwd(int dtype, const void* x, int N, int HW, int C, const float* w1, int Cr,
+                                            const float* w2, int act, const float* chan_mul, float* ws, float* gap,
+                                            float* hpre, float* gate, void* out, hiseg_stream_t stream) {
+  HISEG_REQUIRE(x && w1 && w2 && ws && gap && hpre && gate && out && N > 0 && HW > 0 && Cr > 0, HISEG_ERR_BAD_ARG,
+                "attn_channel_train_fwd: bad args");
+  HISEG_REQUIRE(C > 0 && C % chunk_of(dtype) == 0, HISEG_ERR_BAD_SHAPE, "attn_channel_train_fwd: C alignment");
+  hipStream_t s = (hipStream_t)stream;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_gap_kernel<T>, dim3(N, kGapSplits), dim3(256), 0, s, x, nullptr, nullptr, HW,
+                                       C, ws));
+  hipLaunchKernelGGL(ca_mlp_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, ws, HW, C, Cr, w1, w2, act,
+                     gap, hpre, gate);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_apply_kernel<T>, dim3(nb((long long)N * HW * (C / chunk_of(dtype)), 256)),
+                                       dim3(256), 0, s, x, N, HW, C, gate, chan_mul, out));
+  return hiseg_check_launch("attn_channel_train_fwd");
+}
+
+extern "C" int hiseg_attn_channel_bwd(int dtype, const void* x, int N, int HW, int C, const float* w1, int Cr,
+                                      const float* w2, int act, const float* chan_mul, const float* gap,
+                                      const float* hpre, const float* gate, const void* dout, void* dx, float* ws,
+                                      float* dw1, float* dw2, hiseg_stream_t stream) {
+  HISEG_REQUIRE(x && w1 && w2 && gap && hpre && gate && dout && dx && ws && dw1 && dw2, HISEG_ERR_BAD_ARG,
+                "attn_channel_bwd: null");
+  HISEG_REQUIRE(C > 0 && C % chunk_of(dtype) == 0, HISEG_ERR_BAD_SHAPE, "attn_channel_bwd: C alignment");
+  hipStream_t s = (hipStream_t)stream;
+  float* part = ws;
+  float* dgap = ws + (long long)N * kGapSplits * C;
+  float* wpart = dgap + (long long)N * C;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_gap_kernel<T>, dim3(N, kGapSplits), dim3(256), 0, s, x, dout, chan_mul, HW, C,
+                                       part));
+  hipLaunchKernelGGL(ca_mlp_bwd_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, part, C, Cr, w1, w2, act,
+                     gap, hpre, gate, dgap, wpart);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(nb(C * Cr, 128)), dim3(128), 0, s, wpart, N, 2 * C * Cr, C * Cr, dw1, 1);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(nb(C * Cr, 128)), dim3(128), 0, s, wpart + C * Cr, N, 2 * C * Cr, C * Cr, dw2, 1);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_dx_kernel<T>, dim3(nb((long long)N * HW * (C / chunk_of(dtype)), 256)),
+                                       dim3(256), 0, s, dout, N, HW, C, gate, chan_mul, dgap, dx));
+  return hiseg_check_launch("attn_channel_bwd");
+}
+
+static UbfArgs ubf_args(const hiseg_ubf_desc* d) {
+  UbfArgs u;
+  u.low = d->low; u.N = d->N; u.h = d->h; u.w = d->w;
+  u.ut_w = d->ut_w; u.ut_b = d->ut_b;
+  u.scale = d->scale; u.shift = d->shift; u.mean = d->mean; u.invstd = d->invstd; u.gamma = d->gamma;
+  u.u1_w = d->u1_w; u.u1_b = d->u1_b;
+  return u;
+}
+
+static const int kUbfBlocks = 512;
+
+extern "C" int hiseg_ubf_ws(void) { return hiseg_bn_partials() * 96 + kUbfBlocks * 256 + 96; }
+
+extern "C" int hiseg_ubf_train_fwd(const hiseg_ubf_desc* d, float eps, float momentum, float* running_mean,
+                                   float* running_var, float* ws, hiseg_stream_t stream) {
+  HISEG_REQUIRE(d && d->low && d->ut_w && d->ut_b && d->u1_w && d->u1_b && d->tfeat && d->t_w && d->t_b && d->logits &&
+                    d->bgfg && d->tn && ws && d->scale && d->shift && d->mean && d->invstd,
+                HISEG_ERR_BAD_ARG, "ubf_train_fwd: null argument");
+  HISEG_REQUIRE(d->Ct > 0 && d->Ct <= 512 && d->Ct % chunk_of(d->dtype) == 0, HISEG_ERR_BAD_SHAPE, "ubf: Ct");
+  hipStream_t s = (hipStream_t)stream;
+  const UbfArgs u = ubf_args(d);
+  const int S = hiseg_bn_partials();
+  hipLaunchKernelGGL(ubf_stats_kernel, dim3(S), dim3(256), 0, s, u, ws);
+  const long long Pm = (long long)d->N * 4 * d->h * d->w;
+  int r = hiseg_bn_finalize(ws, 32, Pm, d->gamma, d->beta, eps, momentum, running_mean, running_var,
+                            const_cast<float*>(d->mean), const_cast<float*>(d->invstd), const_cast<float*>(d->scale),
+                            const_cast<float*>(d->shift), stream);
+  if (r) return r;
+  DISPATCH_T(d->dtype, hipLaunchKernelGGL(ubf_fwd_kernel<T>, dim3(nb(Pm, 256)), dim3(256), 0, s, u, d->tfeat, d->Ct,
+                                          d->t_w, d->t_b, d->logits, d->bgfg, d->tn));
+  return hiseg_check_launch("ubf_train_fwd");
+}
+
+extern "C" int hiseg_ubf_train_bwd(const hiseg_ubf_desc* d, const float* dlogits, const float* dbgfg_ext,
+                                   const float* dtn_ext, float* db_buf, float* dtn_out, float* dlow, float* ws,
+                                   const hiseg_ubf_grads* g, hiseg_stream_t stream) {
+  HISEG_REQUIRE(d && dlogits && db_buf && dtn_out && dlow && ws && g && g->dut_w && g->dut_b && g->dgamma && g->dbeta &&
+                    g->du1_w && g->du1_b,
+                HISEG_ERR_BAD_ARG, "ubf_train_bwd: null argument");
+  hipStream_t s = (hipStream_t)stream;
+  const UbfArgs u = ubf_args(d);
+  const long long Pm = (long long)d->N * 4 * d->h * d->w, PL = (long long)d->N * d->h * d->w;
+  float* part = ws;                          // [kUbfBlocks][256]
+  float* coef = ws + (long long)kUbfBlocks * 256;
+  hipLaunchKernelGGL(ubf_bwd1_kernel, dim3(kUbfBlocks), dim3(256), 0, s, u, dlogits, dbgfg_ext, dtn_ext, d->bgfg, d->tn,
+                     db_buf, dtn_out, part);
+  hipLaunchKernelGGL(ubf_fin1_kernel, dim3(1), dim3(192), 0, s, u, part, kUbfBlocks, Pm, coef, g->dgamma, g->dbeta,
+                     g->du1_w, g->du1_b, g->dut_b);
+  hipLaunchKernelGGL(ubf_bwd2_kernel, dim3(kUbfBlocks), dim3(256), 0, s, u, db_buf, coef, dlow, part);
+  // dWt [ci][c][q] in the ConvTranspose2d layout [2][32][2][2] == (ci*32 + c)*4 + q
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(2), dim3(128), 0, s, part, kUbfBlocks, 256, 256, g->dut_w, 1);
+  (void)PL;
+  return hiseg_check_launch("ubf_train_bwd");
+}
+
+static const int kPw2Blocks = 512;
+extern "C" int hiseg_pw2_ws(int Ct) { return kPw2Blocks * (2 * Ct + 2); }
+
+extern "C" int hiseg_pw2_bwd(int dtype, const void* tfeat, long long P, int Ct, const float* dtn, const float* w,
+                             void* dt, float* ws, float* dw, float* db, hiseg_stream_t stream) {
+  HISEG_REQUIRE(tfeat && dtn && w && dt && ws && dw && db && P > 0, HISEG_ERR_BAD_ARG, "pw2_bwd: null argument");
+  HISEG_REQUIRE(Ct % chunk_of(dtype) == 0 && Ct / chunk_of(dtype) <= 256, HISEG_ERR_BAD_SHAPE, "pw2_bwd: Ct");
+  hipStream_t s = (hipStream_t)stream;
+  const int nch = Ct / chunk_of(dtype);
+  const int R = 256 / nch;
+  const size_t lds = (size_t)R * (2 * Ct + 2) * sizeof(float);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(pw2_bwd_kernel<T>, dim3(kPw2Blocks), dim3(256), lds, s, tfeat, P, Ct, dtn, w, dt, ws));
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(nb(2 * Ct, 128)), dim3(128), 0, s, ws, kPw2Blocks, 2 * Ct + 2, 2 * Ct, dw, 1);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(128), 0, s, ws + 2 * Ct, kPw2Blocks, 2 * Ct + 2, 2, db, 1);
+  return hiseg_check_launch("pw2_bwd");
+}

@@ -1,0 +1,489 @@
+// Train-mode BatchNorm, Dropout2d masks and the element-wise backward kernels of the ROI path
+// (gfx950).  All of them are HBM-streaming passes over NHWC activations: f32 arithmetic,
+// storage in the compute dtype, statistics as deterministic per-split partials (no atomics)
+// combined in double precision by a one-thread-per-channel finalize.
+#include "common.h"
+#include "hiseg_train.h"
+
+namespace hiseg {
+
+constexpr int kBnSplits = 480;  // pixel splits of the statistics passes (~2 blocks per CU)
+
+template <typename T>
+__device__ __forceinline__ float ld(const void* p, long long i) { return Elem<T>::load(p, i); }
+template <typename T>
+__device__ __forceinline__ void st(void* p, long long i, float v) { Elem<T>::store(p, i, v); }
+
+__device__ __forceinline__ float act_grad(float y, int act) {
+  switch (act) {
+    case HISEG_ACT_RELU: return y > 0.f ? 1.f : 0.f;
+    case HISEG_ACT_SIGMOID: return y * (1.f - y);
+    default: return 1.f;
+  }
+}
+
+// Pixel range of split s.
+__device__ __forceinline__ void split_range(long long P, int s, int S, long long& b, long long& e) {
+  b = P * s / S;
+  e = P * (s + 1) / S;
+}
+
+// ---------------------------------------------------------------------------------------- stats
+// Block layout: CT = min(C, 256) channel lanes x R = 256/CT pixel rows; channel block blockIdx.y.
+template <typename T>
+__global__ void __launch_bounds__(256) bn_stats_kernel(const void* z, long long P, int C, int cs, int coff,
+                                                       float* partial) {
+  __shared__ float sh_n[256], sh_m[256], sh_q[256];
+  const int CT = C < 256 ? C : 256;
+  const int R = 256 / CT;
+  const int t = threadIdx.x;
+  const int cl = t % CT, r = t / CT;
+  const int c = blockIdx.y * 256 + cl;
+  long long b, e;
+  split_range(P, blockIdx.x, gridDim.x, b, e);
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  if (r < R && c < C) {
+    for (long long p = b + r; p < e; p += R) {
+      const float x = ld<T>(z, p * cs + coff + c);
+      n += 1.f;
+      const float d = x - mean;
+      mean += d / n;
+      m2 += d * (x - mean);
+    }
+  }
+  sh_n[t] = n; sh_m[t] = mean; sh_q[t] = m2;
+  __syncthreads();
+  if (r == 0 && c < C) {
+    for (int rr = 1; rr < R; ++rr) {
+      const int o = rr * CT + cl;
+      const float nb = sh_n[o];
+      if (nb == 0.f) continue;
+      const float na = n, nt = na + nb;
+      const float d = sh_m[o] - mean;
+      mean += d * (nb / nt);
+      m2 += sh_q[o] + d * d * (na * nb / nt);
+      n = nt;
+    }
+    float* out = partial + (long long)blockIdx.x * 3 * C;
+    out[c] = n; out[C + c] = mean; out[2 * C + c] = m2;
+  }
+}
+
+__global__ void bn_finalize_kernel(const float* partial, int S, int C, long long P, const float* gamma,
+                                   const float* beta, float eps, float momentum, float* rm, float* rv, float* mean_o,
+                                   float* invstd_o, float* scale, float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double n = 0, mean = 0, m2 = 0;
+  for (int s = 0; s < S; ++s) {
+    const float* p = partial + (long long)s * 3 * C;
+    const double nb = p[c];
+    if (nb == 0) continue;
+    const double d = p[C + c] - mean, nt = n + nb;
+    mean += d * nb / nt;
+    m2 += p[2 * C + c] + d * d * n * nb / nt;
+    n = nt;
+  }
+  const double var = m2 / n;
+  const double inv = 1.0 / sqrt(var + (double)eps);
+  const float g = gamma ? gamma[c] : 1.f, bb = beta ? beta[c] : 0.f;
+  mean_o[c] = (float)mean;
+  invstd_o[c] = (float)inv;
+  scale[c] = (float)(g * inv);
+  shift[c] = (float)(bb - mean * g * inv);
+  if (rm) rm[c] = (float)((1.0 - momentum) * rm[c] + momentum * mean);
+  if (rv) rv[c] = (float)((1.0 - momentum) * rv[c] + momentum * (P > 1 ? var * (double)P / (double)(P - 1) : var));
+}
+
+// ---------------------------------------------------------------------------------------- apply
+template <typename T>
+__global__ void __launch_bounds__(256) bn_apply_kernel(hiseg_bn_apply_desc d) {
+  const long long n = d.P * d.C;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const long long p = i / d.C;
+    const int c = (int)(i - p * d.C);
+    float v = ld<T>(d.z, p * d.z_cstride + d.z_coff + c) * d.scale[c] + d.shift[c];
+    if (d.residual) v += ld<T>(d.residual, p * d.r_cstride + d.r_coff + c);
+    v = apply_act(v, d.act);
+    if (d.chan_mul) v *= d.chan_mul[(p / d.HW) * d.C + c];
+    st<T>(d.y, p * d.y_cstride + d.y_coff + c, v);
+  }
+}
+
+// ---------------------------------------------------------------------------------------- backward
+template <typename T>
+__device__ __forceinline__ float bn_g(const hiseg_bn_bwd_desc& d, long long p, int c) {
+  float g = ld<T>(d.dy, p * d.dy_cstride + d.dy_coff + c);
+  if (d.chan_mul) g *= d.chan_mul[(p / d.HW) * d.C + c];
+  if (d.act != HISEG_ACT_NONE) g *= act_grad(ld<T>(d.y, p * d.y_cstride + d.y_coff + c), d.act);
+  return g;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(hiseg_bn_bwd_desc d) {
+  __shared__ float sa[256], sb[256], sc[256];
+  const int C = d.C;
+  const int CT = C < 256 ? C : 256;
+  const int R = 256 / CT;
+  const int t = threadIdx.x;
+  const int cl = t % CT, r = t / CT;
+  const int c = blockIdx.y * 256 + cl;
+  long long b, e;
+  split_range(d.P, blockIdx.x, gridDim.x, b, e);
+  float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (r < R && c < C) {
+    const float mu = d.mean[c], inv = d.invstd[c];
+    for (long long p = b + r; p < e; p += R) {
+      const float g = bn_g<T>(d, p, c);
+      const float xh = (ld<T>(d.z, p * d.z_cstride + d.z_coff + c) - mu) * inv;
+      s1 += g; s2 += g * xh; s3 += xh;
+    }
+  }
+  sa[t] = s1; sb[t] = s2; sc[t] = s3;
+  __syncthreads();
+  if (r == 0 && c < C) {
+    for (int rr = 1; rr < R; ++rr) {
+      s1 += sa[rr * CT + cl]; s2 += sb[rr * CT + cl]; s3 += sc[rr * CT + cl];
+    }
+    float* out = d.partial + (long long)blockIdx.x * 3 * C;
+    out[c] = s1; out[C + c] = s2; out[2 * C + c] = s3;
+  }
+}
+
+__global__ void bn_bwd_finalize_kernel(hiseg_bn_bwd_desc d, int S) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int C = d.C;
+  if (c >= C) return;
+  double s1 = 0, s2 = 0, s3 = 0;
+  for (int s = 0; s < S; ++s) {
+    const float* p = d.partial + (long long)s * 3 * C;
+    s1 += p[c]; s2 += p[C + c]; s3 += p[2 * C + c];
+  }
+  const double P = (double)d.P;
+  const double k = (d.gamma ? d.gamma[c] : 1.0) * d.invstd[c];
+  float* coef = d.partial + (long long)S * 3 * C;  // [3][C]: k, mean(g), mean(g*xhat)
+  coef[c] = (float)k;
+  coef[C + c] = (float)(s1 / P);
+  coef[2 * C + c] = (float)(s2 / P);
+  if (d.dgamma) d.dgamma[c] = (float)(d.accumulate_params ? d.dgamma[c] + s2 : s2);
+  if (d.dbeta) d.dbeta[c] = (float)(d.accumulate_params ? d.dbeta[c] + s1 : s1);
+  if (d.dconv_bias) {
+    const double sdz = k * (s1 - P * (s1 / P) - s3 * (s2 / P));
+    d.dconv_bias[c] = (float)(d.accumulate_params ? d.dconv_bias[c] + sdz : sdz);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(hiseg_bn_bwd_desc d, int S) {
+  const int C = d.C;
+  const float* coef = d.partial + (long long)S * 3 * C;
+  const long long n = d.P * C;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const long long p = i / C;
+    const int c = (int)(i - p * C);
+    const float g = bn_g<T>(d, p, c);
+    const float xh = (ld<T>(d.z, p * d.z_cstride + d.z_coff + c) - d.mean[c]) * d.invstd[c];
+    st<T>(d.dz, p * d.dz_cstride + d.dz_coff + c, coef[c] * (g - coef[C + c] - xh * coef[2 * C + c]));
+    if (d.dres) {
+      const long long o = p * d.dres_cstride + d.dres_coff + c;
+      st<T>(d.dres, o, d.dres_accumulate ? ld<T>(d.dres, o) + g : g);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------- dropout
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__global__ void dropout2d_mask_kernel(int n, float p, unsigned long long seed, float* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float u = (float)(splitmix64(seed ^ splitmix64((unsigned long long)i)) >> 40) * (1.0f / 16777216.0f);
+  out[i] = u < p ? 0.f : 1.f / (1.f - p);
+}
+
+// ---------------------------------------------------------------------------------------- element-wise
+#define EW_LOOP(P, C)                                                                                   \
+  const long long n_ = (P) * (C);                                                                      \
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n_; i += (long long)gridDim.x * 256)
+
+__device__ __forceinline__ long long vi(const hiseg_ew_view& v, long long p, int c) { return p * v.cstride + v.coff + c; }
+
+template <typename T>
+__global__ void __launch_bounds__(256) relu_bwd_kernel(long long P, int HW, int C, hiseg_ew_view dy, hiseg_ew_view y,
+                                                       const float* mul, hiseg_ew_view dz) {
+  EW_LOOP(P, C) {
+    const long long p = i / C;
+    const int c = (int)(i - p * C);
+    float g = ld<T>(dy.p, vi(dy, p, c));
+    if (mul) g *= mul[(p / HW) * C + c];
+    st<T>(dz.p, vi(dz, p, c), ld<T>(y.p, vi(y, p, c)) > 0.f ? g : 0.f);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) sigmoid_bwd_kernel(long long P, int C, hiseg_ew_view dy, hiseg_ew_view s,
+                                                          hiseg_ew_view dz) {
+  EW_LOOP(P, C) {
+    const long long p = i / C;
+    const int c = (int)(i - p * C);
+    const float v = ld<T>(s.p, vi(s, p, c));
+    st<T>(dz.p, vi(dz, p, c), ld<T>(dy.p, vi(dy, p, c)) * v * (1.f - v));
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) gate_fwd_kernel(long long P, int C, hiseg_ew_view a, hiseg_ew_view g,
+                                                       hiseg_ew_view out) {
+  EW_LOOP(P, C) {
+    const long long p = i / C;
+    const int c = (int)(i - p * C);
+    st<T>(out.p, vi(out, p, c), ld<T>(a.p, vi(a, p, c)) * ld<T>(g.p, vi(g, p, c)));
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) gate_bwd_kernel(long long P, int C, hiseg_ew_view dy, hiseg_ew_view a,
+                                                       hiseg_ew_view g, hiseg_ew_view da, int acc, hiseg_ew_view dzg) {
+  EW_LOOP(P, C) {
+    const long long p = i / C;
+    const int c = (int)(i - p * C);
+    const float gy = ld<T>(dy.p, vi(dy, p, c));
+    const float gv = ld<T>(g.p, vi(g, p, c));
+    const float av = ld<T>(a.p, vi(a, p, c));
+    if (da.p) {
+      const long long o = vi(da, p, c);
+      st<T>(da.p, o, acc ? ld<T>(da.p, o) + gy * gv : gy * gv);
+    }
+    if (dzg.p) st<T>(dzg.p, vi(dzg, p, c), gy * av * gv * (1.f - gv));
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) act_bwd_cvt_kernel(long long P, int C, hiseg_ew_view dy, hiseg_ew_view y, int act,
+                                                          hiseg_ew_view dz, int acc) {
+  EW_LOOP(P, C) {
+    const long long p = i / C;
+    const int c = (int)(i - p * C);
+    float g = ld<float>(dy.p, vi(dy, p, c));
+    if (act != HISEG_ACT_NONE) g *= act_grad(ld<float>(y.p, vi(y, p, c)), act);
+    const long long o = vi(dz, p, c);
+    st<T>(dz.p, o, acc ? ld<T>(dz.p, o) + g : g);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) add_kernel(long long P, int C, hiseg_ew_view dst, hiseg_ew_view src) {
+  EW_LOOP(P, C) {
+    const long long p = i / C;
+    const int c = (int)(i - p * C);
+    const long long o = vi(dst, p, c);
+    st<T>(dst.p, o, ld<T>(dst.p, o) + ld<T>(src.p, vi(src, p, c)));
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) maxpool_bwd_kernel(const void* x, int N, int H, int W, int C, const void* dy,
+                                                          void* dx, int acc) {
+  const int Ho = H / 2, Wo = W / 2;
+  const long long n_ = (long long)N * Ho * Wo * C;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n_; i += (long long)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const long long q = i / C;
+    const int ox = (int)(q % Wo);
+    const long long t2 = q / Wo;
+    const int oy = (int)(t2 % Ho);
+    const long long n = t2 / Ho;
+    long long idx[4];
+    float best = -INFINITY;
+    int arg = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      idx[k] = ((n * H + 2 * oy + (k >> 1)) * W + 2 * ox + (k & 1)) * C + c;
+      const float v = ld<T>(x, idx[k]);
+      if (v > best || v != v) { best = v; arg = k; }
+    }
+    const float g = ld<T>(dy, q * C + c);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float add = k == arg ? g : 0.f;
+      st<T>(dx, idx[k], acc ? ld<T>(dx, idx[k]) + add : add);
+    }
+  }
+}
+
+// PyTorch bilinear (align_corners=False) source index of output o: max(0, (o+0.5)*scale-0.5).
+__device__ __forceinline__ void bl_src(int o, float scale, int in, int& i0, int& i1, float& l1) {
+  float s = scale * (o + 0.5f) - 0.5f;
+  if (s < 0.f) s = 0.f;
+  i0 = (int)s;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l1 = s - i0;
+}
+
+__global__ void __launch_bounds__(256) resize_bwd_kernel(const float* dy, int NC, int h, int w, int H, int W, float* dx) {
+  const long long n_ = (long long)NC * h * w;
+  const float sh = (float)h / H, sw = (float)w / W;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n_; i += (long long)gridDim.x * 256) {
+    const int ix = (int)(i % w);
+    const int iy = (int)((i / w) % h);
+    const long long pl = i / ((long long)h * w);
+    const int oy_lo = max(0, (int)floorf((iy - 1.5f) / sh)), oy_hi = min(H - 1, (int)ceilf((iy + 1.5f) / sh));
+    const int ox_lo = max(0, (int)floorf((ix - 1.5f) / sw)), ox_hi = min(W - 1, (int)ceilf((ix + 1.5f) / sw));
+    float acc = 0.f;
+    for (int oy = oy_lo; oy <= oy_hi; ++oy) {
+      int y0, y1; float ly;
+      bl_src(oy, sh, h, y0, y1, ly);
+      const float wy = (y0 == iy ? 1.f - ly : 0.f) + (y1 == iy ? ly : 0.f);
+      if (wy == 0.f) continue;
+      for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+        int x0, x1; float lx;
+        bl_src(ox, sw, w, x0, x1, lx);
+        const float wx = (x0 == ix ? 1.f - lx : 0.f) + (x1 == ix ? lx : 0.f);
+        if (wx != 0.f) acc += wy * wx * dy[(pl * H + oy) * W + ox];
+      }
+    }
+    dx[i] = acc;
+  }
+}
+
+inline unsigned ew_blocks(long long n) {
+  long long b = (n + 255) / 256;
+  return (unsigned)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
+}
+
+}  // namespace hiseg
+
+using namespace hiseg;
+
+#define DISPATCH_T(dtype, ...)                       \
+  do {                                               \
+    if ((dtype) == HISEG_BF16) {                     \
+      using T = bf16_t;                              \
+      __VA_ARGS__;                                   \
+    } else {                                         \
+      using T = float;                               \
+      __VA_ARGS__;                                   \
+    }                                                \
+  } while (0)
+
+extern "C" int hiseg_bn_partials(void) { return kBnSplits; }
+
+static int splits_for(long long P) { return (int)(P < kBnSplits ? (P > 0 ? P : 1) : kBnSplits); }
+
+extern "C" int hiseg_bn_stats(int dtype, const void* z, long long P, int C, int cstride, int coff, float* partial,
+                              hiseg_stream_t stream) {
+  HISEG_REQUIRE(z && partial && P > 0 && C > 0 && cstride >= C, HISEG_ERR_BAD_ARG, "bn_stats: bad arguments");
+  HISEG_REQUIRE(dtype == HISEG_F32 || dtype == HISEG_BF16, HISEG_ERR_BAD_DTYPE, "bn_stats: dtype");
+  const int S = kBnSplits;  // fixed count: empty splits write n = 0
+  dim3 grid(S, (C + 255) / 256);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(bn_stats_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream, z, P, C, cstride,
+                                       coff, partial));
+  return hiseg_check_launch("bn_stats");
+}
+
+extern "C" int hiseg_bn_finalize(const float* partial, int C, long long P, const float* gamma, const float* beta,
+                                 float eps, float momentum, float* running_mean, float* running_var, float* mean,
+                                 float* invstd, float* scale, float* shift, hiseg_stream_t stream) {
+  HISEG_REQUIRE(partial && mean && invstd && scale && shift && C > 0, HISEG_ERR_BAD_ARG, "bn_finalize: null");
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, partial, kBnSplits, C,
+                     P, gamma, beta, eps, momentum, running_mean, running_var, mean, invstd, scale, shift);
+  return hiseg_check_launch("bn_finalize");
+}
+
+extern "C" int hiseg_bn_apply(const hiseg_bn_apply_desc* d, hiseg_stream_t stream) {
+  HISEG_REQUIRE(d && d->z && d->y && d->scale && d->shift && d->P > 0 && d->C > 0 && d->HW > 0, HISEG_ERR_BAD_ARG,
+                "bn_apply: bad arguments");
+  DISPATCH_T(d->dtype, hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(ew_blocks(d->P * d->C)), dim3(256), 0,
+                                          (hipStream_t)stream, *d));
+  return hiseg_check_launch("bn_apply");
+}
+
+extern "C" int hiseg_bn_bwd(const hiseg_bn_bwd_desc* d, hiseg_stream_t stream) {
+  HISEG_REQUIRE(d && d->dy && d->z && d->dz && d->mean && d->invstd && d->partial && d->P > 0 && d->C > 0 && d->HW > 0,
+                HISEG_ERR_BAD_ARG, "bn_bwd: bad arguments");
+  HISEG_REQUIRE(d->act == HISEG_ACT_NONE || d->y, HISEG_ERR_BAD_ARG, "bn_bwd: activation needs y");
+  hipStream_t s = (hipStream_t)stream;
+  const int S = kBnSplits;
+  DISPATCH_T(d->dtype, hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(S, (d->C + 255) / 256), dim3(256), 0, s, *d));
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((d->C + 63) / 64), dim3(64), 0, s, *d, S);
+  DISPATCH_T(d->dtype, hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(ew_blocks(d->P * d->C)), dim3(256), 0, s, *d, S));
+  return hiseg_check_launch("bn_bwd");
+}
+
+extern "C" int hiseg_dropout2d_mask(int N, int C, float p, unsigned long long seed, float* out, hiseg_stream_t stream) {
+  HISEG_REQUIRE(out && N > 0 && C > 0 && p >= 0.f && p < 1.f, HISEG_ERR_BAD_ARG, "dropout2d_mask: bad arguments");
+  const int n = N * C;
+  hipLaunchKernelGGL(dropout2d_mask_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, n, p, seed, out);
+  return hiseg_check_launch("dropout2d_mask");
+}
+
+extern "C" int hiseg_relu_bwd(int dtype, long long P, int HW, int C, hiseg_ew_view dy, hiseg_ew_view y,
+                              const float* chan_mul, hiseg_ew_view dz, hiseg_stream_t stream) {
+  HISEG_REQUIRE(dy.p && y.p && dz.p && P > 0 && C > 0 && HW > 0, HISEG_ERR_BAD_ARG, "relu_bwd: bad arguments");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(relu_bwd_kernel<T>, dim3(ew_blocks(P * C)), dim3(256), 0, (hipStream_t)stream,
+                                       P, HW, C, dy, y, chan_mul, dz));
+  return hiseg_check_launch("relu_bwd");
+}
+
+extern "C" int hiseg_sigmoid_bwd(int dtype, long long P, int C, hiseg_ew_view dy, hiseg_ew_view s, hiseg_ew_view dz,
+                                 hiseg_stream_t stream) {
+  HISEG_REQUIRE(dy.p && s.p && dz.p && P > 0 && C > 0, HISEG_ERR_BAD_ARG, "sigmoid_bwd: bad arguments");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(sigmoid_bwd_kernel<T>, dim3(ew_blocks(P * C)), dim3(256), 0,
+                                       (hipStream_t)stream, P, C, dy, s, dz));
+  return hiseg_check_launch("sigmoid_bwd");
+}
+
+extern "C" int hiseg_gate_fwd(int dtype, long long P, int C, hiseg_ew_view a, hiseg_ew_view g, hiseg_ew_view out,
+                              hiseg_stream_t stream) {
+  HISEG_REQUIRE(a.p && g.p && out.p && P > 0 && C > 0, HISEG_ERR_BAD_ARG, "gate_fwd: bad arguments");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(gate_fwd_kernel<T>, dim3(ew_blocks(P * C)), dim3(256), 0, (hipStream_t)stream,
+                                       P, C, a, g, out));
+  return hiseg_check_launch("gate_fwd");
+}
+
+extern "C" int hiseg_gate_bwd(int dtype, long long P, int C, hiseg_ew_view dy, hiseg_ew_view a, hiseg_ew_view g,
+                              hiseg_ew_view da, int da_accumulate, hiseg_ew_view dzg, hiseg_stream_t stream) {
+  HISEG_REQUIRE(dy.p && a.p && g.p && P > 0 && C > 0, HISEG_ERR_BAD_ARG, "gate_bwd: bad arguments");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(gate_bwd_kernel<T>, dim3(ew_blocks(P * C)), dim3(256), 0, (hipStream_t)stream,
+                                       P, C, dy, a, g, da, da_accumulate, dzg));
+  return hiseg_check_launch("gate_bwd");
+}
+
+extern "C" int hiseg_act_bwd_cvt(int dtype, long long P, int C, hiseg_ew_view dy, hiseg_ew_view y, int act,
+                                 hiseg_ew_view dz, int accumulate, hiseg_stream_t stream) {
+  HISEG_REQUIRE(dy.p && dz.p && P > 0 && C > 0 && (act == HISEG_ACT_NONE || y.p), HISEG_ERR_BAD_ARG,
+                "act_bwd_cvt: bad arguments");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(act_bwd_cvt_kernel<T>, dim3(ew_blocks(P * C)), dim3(256), 0, (hipStream_t)stream,
+                                       P, C, dy, y, act, dz, accumulate));
+  return hiseg_check_launch("act_bwd_cvt");
+}
+
+extern "C" int hiseg_add_inplace(int dtype, long long P, int C, hiseg_ew_view dst, hiseg_ew_view src,
+                                 hiseg_stream_t stream) {
+  HISEG_REQUIRE(dst.p && src.p && P > 0 && C > 0, HISEG_ERR_BAD_ARG, "add_inplace: bad arguments");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(add_kernel<T>, dim3(ew_blocks(P * C)), dim3(256), 0, (hipStream_t)stream, P, C,
+                                       dst, src));
+  return hiseg_check_launch("add_inplace");
+}
+
+extern "C" int hiseg_maxpool2x2_bwd(int dtype, const void* x, int N, int H, int W, int C, const void* dy, void* dx,
+                                    int accumulate, hiseg_stream_t stream) {
+  HISEG_REQUIRE(x && dy && dx && N > 0 && H % 2 == 0 && W % 2 == 0 && C > 0, HISEG_ERR_BAD_ARG,
+                "maxpool2x2_bwd: bad arguments");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(ew_blocks((long long)N * H * W * C / 4)), dim3(256),
+                                       0, (hipStream_t)stream, x, N, H, W, C, dy, dx, accumulate));
+  return hiseg_check_launch("maxpool2x2_bwd");
+}
+
+extern "C" int hiseg_resize_bilinear_bwd(const float* dy, int NC, int h, int w, int H, int W, float* dx,
+                                         hiseg_stream_t stream) {
+  HISEG_REQUIRE(dy && dx && NC > 0 && h > 0 && w > 0 && H > 0 && W > 0, HISEG_ERR_BAD_ARG, "resize_bwd: bad arguments");
+  hipLaunchKernelGGL(resize_bwd_kernel, dim3(ew_blocks((long long)NC * h * w)), dim3(256), 0, (hipStream_t)stream, dy,
+                     NC, h, w, H, W, dx);
+  return hiseg_check_launch("resize_bilinear_bwd");
+}

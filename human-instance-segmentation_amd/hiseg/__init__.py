@@ -14,7 +14,10 @@ from .model import (  # noqa: F401
     DynamicRoIAlign, HierarchicalRGBSegmentationModelWithFullImagePretrainedUNet, PreTrainedPeopleSegmentationUNet,
     PreTrainedPeopleSegmentationUNetWrapper, RGBHierarchicalExportWrapper, create_rgb_hierarchical_model)
 
-__version__ = "0.1.0"
+from .losses import RefinedHierarchicalLoss  # noqa: F401,E402
+from .optim import FusedAdamW, cosine_lr  # noqa: F401,E402
+
+__version__ = "0.2.0"
 
 
 def set_compute_dtype(model, dtype):

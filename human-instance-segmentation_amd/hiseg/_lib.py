@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("HISEG_LIB", os.path.join(_HERE, "libhiseg.so"))
 HISEG_F32 = 0
 HISEG_BF16 = 1
 ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_SILU = 0, 1, 2, 3
+LOSS_NOUT = 15  # include/hiseg_loss.h HISEG_LOSS_NOUT
 
 c_int = ctypes.c_int
 c_float = ctypes.c_float
@@ -59,6 +60,64 @@ class Conv2dDesc(ctypes.Structure):
     ]
 
 
+class WgradMap(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in ("Cout", "KH", "KW", "ca", "ca_real", "cb", "cb_real", "convT", "Cg", "Kg",
+                                     "want_bias")]
+
+
+class PackEntry(ctypes.Structure):
+    _fields_ = [("src", c_void_p), ("dst", c_void_p), ("dtype", c_int), ("mode", c_int),
+                ("Cout", c_int), ("Cin_real", c_int), ("KH", c_int), ("KW", c_int),
+                ("ca", c_int), ("ca_real", c_int), ("cb", c_int), ("cb_real", c_int),
+                ("rows", c_int), ("K_pad", c_int), ("cop", c_int), ("total", c_int)]
+
+
+class BnApplyDesc(ctypes.Structure):
+    _fields_ = [("dtype", c_int), ("P", c_ll), ("HW", c_int), ("C", c_int),
+                ("z", c_void_p), ("z_cstride", c_int), ("z_coff", c_int),
+                ("scale", c_void_p), ("shift", c_void_p),
+                ("residual", c_void_p), ("r_cstride", c_int), ("r_coff", c_int),
+                ("act", c_int), ("chan_mul", c_void_p),
+                ("y", c_void_p), ("y_cstride", c_int), ("y_coff", c_int)]
+
+
+class BnBwdDesc(ctypes.Structure):
+    _fields_ = [("dtype", c_int), ("P", c_ll), ("HW", c_int), ("C", c_int),
+                ("dy", c_void_p), ("dy_cstride", c_int), ("dy_coff", c_int),
+                ("y", c_void_p), ("y_cstride", c_int), ("y_coff", c_int),
+                ("z", c_void_p), ("z_cstride", c_int), ("z_coff", c_int),
+                ("chan_mul", c_void_p), ("act", c_int),
+                ("mean", c_void_p), ("invstd", c_void_p), ("gamma", c_void_p),
+                ("partial", c_void_p),
+                ("dgamma", c_void_p), ("dbeta", c_void_p), ("dconv_bias", c_void_p), ("accumulate_params", c_int),
+                ("dz", c_void_p), ("dz_cstride", c_int), ("dz_coff", c_int),
+                ("dres", c_void_p), ("dres_cstride", c_int), ("dres_coff", c_int), ("dres_accumulate", c_int)]
+
+
+class EwView(ctypes.Structure):
+    _fields_ = [("p", c_void_p), ("cstride", c_int), ("coff", c_int)]
+
+
+class UbfDesc(ctypes.Structure):
+    _fields_ = [("dtype", c_int), ("low", c_void_p), ("N", c_int), ("h", c_int), ("w", c_int),
+                ("ut_w", c_void_p), ("ut_b", c_void_p), ("gamma", c_void_p), ("beta", c_void_p),
+                ("mean", c_void_p), ("invstd", c_void_p), ("scale", c_void_p), ("shift", c_void_p),
+                ("u1_w", c_void_p), ("u1_b", c_void_p),
+                ("tfeat", c_void_p), ("Ct", c_int), ("t_w", c_void_p), ("t_b", c_void_p),
+                ("logits", c_void_p), ("bgfg", c_void_p), ("tn", c_void_p)]
+
+
+class UbfGrads(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in ("dut_w", "dut_b", "dgamma", "dbeta", "du1_w", "du1_b")]
+
+
+class LossCfg(ctypes.Structure):
+    _fields_ = [(n, c_float) for n in ("bg_weight", "fg_weight", "target_weight", "consistency_weight", "dice_weight",
+                                       "ce_weight", "boundary_aware_weight", "contour_weight", "distance_weight")] + \
+               [(n, c_int) for n in ("use_dynamic_weights", "use_boundary_aware", "use_contour", "use_distance",
+                                     "contour_ks")]
+
+
 class HisegError(RuntimeError):
     """Raised when a libhiseg entry point returns a non-zero status."""
 
@@ -94,6 +153,49 @@ def _declare(lib):
         "hiseg_resize_bilinear_fwd": ([P, c_int, c_int, c_int, P, c_int, c_int, P], c_int),
         "hiseg_distance_mask_fwd": ([P, c_ll, P, P, P], c_int),
         "hiseg_output_conv_fwd": ([P, c_int, c_int, c_int, P, P, P, P], c_int),
+        # ---- training (include/hiseg_train.h, hiseg_head_train.h, hiseg_loss.h)
+        "hiseg_conv2d_wgrad_dims": ([ctypes.POINTER(Conv2dDesc), c_int, P, P, P], c_int),
+        "hiseg_conv2d_wgrad": ([ctypes.POINTER(Conv2dDesc), P, c_int, c_int, c_int, P, c_int, P], c_int),
+        "hiseg_conv2d_wgrad_reduce": ([P, c_int, ctypes.POINTER(WgradMap), P, P, c_int, P], c_int),
+        "hiseg_pack_weights": ([P, c_int, c_int, P], c_int),
+        "hiseg_bn_partials": ([], c_int),
+        "hiseg_bn_stats": ([c_int, P, c_ll, c_int, c_int, c_int, P, P], c_int),
+        "hiseg_bn_finalize": ([P, c_int, c_ll, P, P, c_float, c_float, P, P, P, P, P, P, P], c_int),
+        "hiseg_bn_apply": ([ctypes.POINTER(BnApplyDesc), P], c_int),
+        "hiseg_bn_bwd": ([ctypes.POINTER(BnBwdDesc), P], c_int),
+        "hiseg_dropout2d_mask": ([c_int, c_int, c_float, ctypes.c_ulonglong, P, P], c_int),
+        "hiseg_relu_bwd": ([c_int, c_ll, c_int, c_int, EwView, EwView, P, EwView, P], c_int),
+        "hiseg_sigmoid_bwd": ([c_int, c_ll, c_int, EwView, EwView, EwView, P], c_int),
+        "hiseg_gate_fwd": ([c_int, c_ll, c_int, EwView, EwView, EwView, P], c_int),
+        "hiseg_gate_bwd": ([c_int, c_ll, c_int, EwView, EwView, EwView, EwView, c_int, EwView, P], c_int),
+        "hiseg_add_inplace": ([c_int, c_ll, c_int, EwView, EwView, P], c_int),
+        "hiseg_act_bwd_cvt": ([c_int, c_ll, c_int, EwView, EwView, c_int, EwView, c_int, P], c_int),
+        "hiseg_maxpool2x2_bwd": ([c_int, P, c_int, c_int, c_int, c_int, P, P, c_int, P], c_int),
+        "hiseg_resize_bilinear_bwd": ([P, c_int, c_int, c_int, c_int, c_int, P, P], c_int),
+        "hiseg_attn_spatial_train_fwd": ([c_int, P, c_int, c_int, c_int, c_int, P, c_int, P, P, P, P, P, P], c_int),
+        "hiseg_attn_spatial_ws": ([c_int, c_int, c_int, c_int], c_int),
+        "hiseg_attn_spatial_bwd": ([c_int, P, c_int, c_int, c_int, c_int, P, c_int, P, P, P, P, P, P, P, P, P], c_int),
+        "hiseg_attn_channel_ws": ([c_int, c_int, c_int], c_int),
+        "hiseg_attn_channel_train_fwd": ([c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, P, P, P, P, P, P],
+                                         c_int),
+        "hiseg_attn_channel_bwd": ([c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, P, P, P, P, P, P, P, P, P],
+                                   c_int),
+        "hiseg_ubf_ws": ([], c_int),
+        "hiseg_ubf_train_fwd": ([ctypes.POINTER(UbfDesc), c_float, c_float, P, P, P, P], c_int),
+        "hiseg_ubf_train_bwd": ([ctypes.POINTER(UbfDesc), P, P, P, P, P, P, P, ctypes.POINTER(UbfGrads), P], c_int),
+        "hiseg_pw2_ws": ([c_int], c_int),
+        "hiseg_pw2_bwd": ([c_int, P, c_ll, c_int, P, P, P, P, P, P, P], c_int),
+        "hiseg_roi_align_ws": ([c_int], c_int),
+        "hiseg_roi_align_bwd_affine": ([ctypes.POINTER(RoiAlignDesc), P, c_int, c_int, c_int, P, P, P, P], c_int),
+        "hiseg_loss_state_init": ([P, P], c_int),
+        "hiseg_loss_ws": ([c_int, c_int, c_int], c_ll),
+        "hiseg_loss_fwd": ([ctypes.POINTER(LossCfg), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P], c_int),
+        "hiseg_loss_bwd": ([ctypes.POINTER(LossCfg), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
+                           c_int),
+        "hiseg_optim_blocks": ([], c_int),
+        "hiseg_grad_norm_partials": ([P, c_ll, P, P], c_int),
+        "hiseg_adamw_step": ([P, P, P, P, c_ll, c_float, c_float, c_float, c_float, c_float, c_float, c_float, P,
+                              c_float, P, P], c_int),
     }
     for name, (argtypes, restype) in sigs.items():
         fn = getattr(lib, name)

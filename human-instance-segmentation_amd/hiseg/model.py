@@ -171,6 +171,9 @@ class HierarchicalRGBSegmentationModelWithFullImagePretrainedUNet(nn.Module):
         self.hiseg_dtype = torch.float32
 
     def forward(self, images: torch.Tensor, rois: torch.Tensor) -> Tuple[torch.Tensor, Dict[str, torch.Tensor]]:
+        if self.training:  # train-mode BatchNorm / Dropout + hand-written backward (hiseg.train_engine)
+            from . import train_engine
+            return train_engine.train_forward(self, images, rois)
         return engine.rgb_model_forward(self, images, rois, aux="full")
 
     def infer(self, images: torch.Tensor, rois: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -1,0 +1,91 @@
+"""Fused optimiser step on the flat parameter space of a hiseg model.
+
+Replaces the reference's ``clip_grad_norm_(model.parameters(), 1.0)`` + ``torch.optim.AdamW(lr=1e-4,
+weight_decay=0.01)`` pair (train_advanced.py:733-740, 1111-1143): two launches over the contiguous
+parameter / gradient / moment buffers (gradient-norm partials, then clip + AdamW), no host sync.
+Arithmetic follows torch.optim.AdamW (decoupled weight decay, bias-corrected moments, eps outside the
+square root) and clip_grad_norm_ (coef = min(1, max_norm / (norm + 1e-6)), gradients scaled in place).
+``torch.optim.AdamW`` over the same parameters keeps working too: they are ordinary nn.Parameters.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from . import _lib as L
+
+
+def flat_params_of(model: torch.nn.Module):
+    S = model.__dict__.get("_hiseg_train")
+    if S is None:
+        raise RuntimeError("hiseg optimiser: run one training forward first (it lays the parameters out flat)")
+    return S.flat
+
+
+class FusedAdamW:
+    """AdamW + optional global-norm clipping over a model's FlatParams (param_groups: one, as the reference)."""
+
+    def __init__(self, model: torch.nn.Module, lr: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.01, max_grad_norm: Optional[float] = 1.0):
+        self.model = model
+        self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
+        self.max_grad_norm = max_grad_norm
+        self.step_count = 0
+        self._flat = None
+        self.exp_avg = self.exp_avg_sq = None
+        self.partial = None
+        self.last_norm: Optional[torch.Tensor] = None
+        self.param_groups = [{"lr": lr, "betas": betas, "eps": eps, "weight_decay": weight_decay}]
+
+    def _init(self):
+        if self._flat is None:
+            self._flat = flat_params_of(self.model)
+            f = self._flat
+            self.exp_avg = torch.zeros_like(f.data)
+            self.exp_avg_sq = torch.zeros_like(f.data)
+            self.partial = torch.empty(L.lib().hiseg_optim_blocks(), dtype=torch.float32, device=f.data.device)
+            self.last_norm = torch.zeros(1, dtype=torch.float32, device=f.data.device)
+
+    def zero_grad(self, set_to_none: bool = False):
+        self._init()
+        self._flat.grad.zero_()
+        self._flat.attach_grads()
+
+    @torch.no_grad()
+    def step(self):
+        """Returns the pre-clip total gradient norm as a device tensor (like clip_grad_norm_)."""
+        self._init()
+        f = self._flat
+        f.prepare_backward()  # adopt any .grad tensors replaced since the backward
+        lib = L.lib()
+        self.step_count += 1
+        lr = self.param_groups[0]["lr"]
+        b1, b2 = self.betas
+        bc1, bc2 = 1.0 - b1 ** self.step_count, 1.0 - b2 ** self.step_count
+        s = L.stream_ptr()
+        clip = self.max_grad_norm is not None and self.max_grad_norm > 0
+        L.check(lib.hiseg_grad_norm_partials(f.grad.data_ptr(), f.numel, self.partial.data_ptr(), s), "grad_norm")
+        L.check(lib.hiseg_adamw_step(f.data.data_ptr(), f.grad.data_ptr(), self.exp_avg.data_ptr(),
+                                     self.exp_avg_sq.data_ptr(), f.numel, float(lr), float(b1), float(b2),
+                                     float(self.eps), float(self.weight_decay), float(bc1), float(bc2),
+                                     self.partial.data_ptr(), float(self.max_grad_norm) if clip else 0.0,
+                                     self.last_norm.data_ptr(), s), "adamw_step")
+        return self.last_norm
+
+    def state_dict(self):
+        return {"step": self.step_count, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
+                "param_groups": self.param_groups}
+
+    def load_state_dict(self, sd):
+        self._init()
+        self.step_count = int(sd["step"])
+        self.exp_avg.copy_(sd["exp_avg"])
+        self.exp_avg_sq.copy_(sd["exp_avg_sq"])
+        self.param_groups = sd["param_groups"]
+
+
+def cosine_lr(base_lr: float, epoch: int, total_epochs: int, min_lr: float = 1e-6) -> float:
+    """CosineAnnealingLR(T_max=num_epochs, eta_min=min_lr) value at an epoch (train_advanced.py:1126-1131)."""
+    return min_lr + (base_lr - min_lr) * 0.5 * (1 + math.cos(math.pi * epoch / total_epochs))

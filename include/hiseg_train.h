@@ -1,0 +1,161 @@
+/*
+ * hiseg_train.h — C ABI of libhiseg's TRAINING kernels (backward passes, train-mode
+ * BatchNorm, dropout, the refined hierarchical loss and the AdamW update) for the
+ * ROI-hierarchical path of PINTO0309/human-instance-segmentation.  Conventions as in hiseg.h:
+ * caller-owned device pointers, NHWC activations with 16-B channel padding, stream-ordered,
+ * no host synchronisation, 0 / negative hiseg_status return.
+ *
+ * The reference trains with PyTorch autograd (train_advanced.py:680-762: autocast forward,
+ * scaled backward, clip_grad_norm_, AdamW); every entry below replaces the backward (or the
+ * train-mode forward) of one op class on that path, cited per function.
+ */
+#ifndef HISEG_TRAIN_H_
+#define HISEG_TRAIN_H_
+
+#include "hiseg.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ----------------------------------------------------------------------------------------
+ * Convolution weight gradient (nn.Conv2d / nn.ConvTranspose2d backward w.r.t. weight and
+ * bias; autograd of every conv site listed at hiseg_conv2d_fwd).
+ * `fwd` describes the FORWARD conv exactly as passed to hiseg_conv2d_fwd (sources, geometry,
+ * Cout = GEMM columns, convT); only its input-side fields are read.  `dy` is the gradient of
+ * the forward GEMM output (NHWC, dtype fwd->dtype, channel stride dy_cstride, offset dy_coff;
+ * for convT the full-resolution output).  Computes, for one split s of the output pixels,
+ *   ws[s][j][k] = sum_{p in split s} dy[p][j] * X[p][k]       (k < Ktot = KH*KW*(Ca+Cb))
+ *   ws[s][j][Ktot] = sum_{p in split s} dy[p][j]                (if want_bias)
+ * as f32, j < Cg = round_up(Cout, 16), k < Kg (hiseg_conv2d_wgrad_dims).  MFMA bf16 / f32.
+ * -------------------------------------------------------------------------------------- */
+int hiseg_conv2d_wgrad_dims(const hiseg_conv2d_desc* fwd, int want_bias, int* Cg, int* Kg, int* splits);
+int hiseg_conv2d_wgrad(const hiseg_conv2d_desc* fwd, const void* dy, int dy_cstride, int dy_coff,
+                       int want_bias, float* ws, int splits, hiseg_stream_t stream);
+
+/* Sum the split partials and scatter into the reference parameter layouts (f32):
+ *   conv : gw[co][ci][ky][kx]  ([Cout][Cin][KH][KW], Cin = ca_real + cb_real), gb[co]
+ *   convT: gw[ci][co][dy][dx]  ([Cin][Cout/4][2][2]),                          gb[co] (sum of the 4 sub-pixel columns)
+ * ca/cb are the padded source channel counts of the packed K layout.  accumulate != 0 adds
+ * to gw/gb (gradient accumulation), else overwrites.  gb may be null. */
+typedef struct hiseg_wgrad_map {
+  int Cout, KH, KW, ca, ca_real, cb, cb_real, convT, Cg, Kg, want_bias;
+} hiseg_wgrad_map;
+int hiseg_conv2d_wgrad_reduce(const float* ws, int splits, const hiseg_wgrad_map* map, float* gw, float* gb,
+                              int accumulate, hiseg_stream_t stream);
+
+/* ----------------------------------------------------------------------------------------
+ * Weight packing after every optimiser step, all layers in one launch.  Each table entry
+ * (device memory) packs one f32 parameter in the reference layout into the implicit-GEMM
+ * operand of the forward conv (mode 0: conv, 2: convT) or of its data-gradient conv
+ * (mode 1: conv -> flipped taps, Cin/Cout swapped; mode 3: convT -> 2x2/s2 conv).
+ * -------------------------------------------------------------------------------------- */
+typedef struct hiseg_pack_entry {
+  const float* src; void* dst; int dtype; int mode;
+  int Cout, Cin_real, KH, KW;   /* reference dims (convT: Cin_real = in, Cout = out channels)  */
+  int ca, ca_real, cb, cb_real; /* padded / real channel split of the forward K layout         */
+  int rows, K_pad;              /* packed [rows][K_pad]                                       */
+  int cop;                      /* dgrad modes: padded channel count of the output gradient   */
+  int total;                    /* rows * K_pad                                               */
+} hiseg_pack_entry;
+int hiseg_pack_weights(const hiseg_pack_entry* table_dev, int n, int max_total, hiseg_stream_t stream);
+
+/* ----------------------------------------------------------------------------------------
+ * Train-mode BatchNorm2d (advanced/normalization_comparison.py:181-182; nn.BatchNorm2d
+ * eps 1e-5, momentum 0.1): batch statistics over N*H*W, running-stat update with the
+ * unbiased variance, then y = act(z*scale + shift [+ residual]) * chan_mul[n][c].
+ * -------------------------------------------------------------------------------------- */
+int hiseg_bn_partials(void);   /* number of pixel splits used by the statistics kernels */
+int hiseg_bn_stats(int dtype, const void* z, long long P, int C, int cstride, int coff, float* partial,
+                   hiseg_stream_t stream);
+/* partial [splits][3][C] -> mean/invstd [C], scale/shift [C] (fold of gamma/beta), running update. */
+int hiseg_bn_finalize(const float* partial, int C, long long P, const float* gamma, const float* beta, float eps,
+                      float momentum, float* running_mean, float* running_var, float* mean, float* invstd,
+                      float* scale, float* shift, hiseg_stream_t stream);
+typedef struct hiseg_bn_apply_desc {
+  int dtype; long long P; int HW; int C;
+  const void* z; int z_cstride, z_coff;
+  const float* scale; const float* shift;
+  const void* residual; int r_cstride, r_coff;
+  int act;
+  const float* chan_mul;          /* [N][C] or null (Dropout2d mask, 0 or 1/(1-p)) */
+  void* y; int y_cstride, y_coff;
+} hiseg_bn_apply_desc;
+int hiseg_bn_apply(const hiseg_bn_apply_desc* d, hiseg_stream_t stream);
+
+/* Backward.  g = dy * chan_mul * act'(y) (ReLU: y > 0; none: 1), xhat = (z - mean)*invstd:
+ *   reduce : dgamma[c] (+)= sum g*xhat, dbeta[c] (+)= sum g ; partial [splits][2][C]
+ *   apply  : dz = gamma*invstd*(g - sum(g)/P - xhat*sum(g*xhat)/P)     (to dz, dtype)
+ *            dres (+)= g  (the residual input's gradient, if dres != null; accumulate flag)
+ * dconv_bias (+)= sum dz (analytically ~0; conv bias before BN) if non-null. */
+typedef struct hiseg_bn_bwd_desc {
+  int dtype; long long P; int HW; int C;
+  const void* dy; int dy_cstride, dy_coff;
+  const void* y; int y_cstride, y_coff;
+  const void* z; int z_cstride, z_coff;
+  const float* chan_mul;
+  int act;
+  const float* mean; const float* invstd; const float* gamma;
+  float* partial;
+  float* dgamma; float* dbeta; float* dconv_bias; int accumulate_params;
+  void* dz; int dz_cstride, dz_coff;
+  void* dres; int dres_cstride, dres_coff; int dres_accumulate;
+} hiseg_bn_bwd_desc;
+int hiseg_bn_bwd(const hiseg_bn_bwd_desc* d, hiseg_stream_t stream);
+
+/* Dropout2d mask (nn.Dropout2d in refinement.py:484,486,519,525,540): per (n, c) 0 with
+ * probability p else 1/(1-p), from a counter-based hash of (seed, n*C + c). */
+int hiseg_dropout2d_mask(int N, int C, float p, unsigned long long seed, float* out, hiseg_stream_t stream);
+
+/* ----------------------------------------------------------------------------------------
+ * Element-wise backward helpers (NHWC views, dtype = compute dtype, f32 math).
+ *   relu_bwd : dz = dy * chan_mul * (y > 0)                       (activation without BN)
+ *   sigmoid_bwd: dz = dy * s * (1 - s)
+ *   gate_fwd : out = a * g                                          (fg_gate / bottleneck gate)
+ *   gate_bwd : da (+)= dy * g ;  dzg = dy * a * g * (1 - g)         (g = sigmoid output)
+ *   add      : dst += src
+ * -------------------------------------------------------------------------------------- */
+typedef struct hiseg_ew_view { void* p; int cstride, coff; } hiseg_ew_view;
+int hiseg_relu_bwd(int dtype, long long P, int HW, int C, hiseg_ew_view dy, hiseg_ew_view y, const float* chan_mul,
+                   hiseg_ew_view dz, hiseg_stream_t stream);
+int hiseg_sigmoid_bwd(int dtype, long long P, int C, hiseg_ew_view dy, hiseg_ew_view s, hiseg_ew_view dz,
+                      hiseg_stream_t stream);
+int hiseg_gate_fwd(int dtype, long long P, int C, hiseg_ew_view a, hiseg_ew_view g, hiseg_ew_view out,
+                   hiseg_stream_t stream);
+int hiseg_gate_bwd(int dtype, long long P, int C, hiseg_ew_view dy, hiseg_ew_view a, hiseg_ew_view g,
+                   hiseg_ew_view da, int da_accumulate, hiseg_ew_view dzg, hiseg_stream_t stream);
+/* dz (dtype, += if accumulate) = dy * act'(y) with dy, y f32 views (the 1/2-channel f32 heads:
+ * contour sigmoid, distance map, EnhancedUNet's f32 logits). act: NONE or SIGMOID (y = output). */
+int hiseg_act_bwd_cvt(int dtype, long long P, int C, hiseg_ew_view dy, hiseg_ew_view y, int act, hiseg_ew_view dz,
+                      int accumulate, hiseg_stream_t stream);
+int hiseg_add_inplace(int dtype, long long P, int C, hiseg_ew_view dst, hiseg_ew_view src, hiseg_stream_t stream);
+
+/* MaxPool2d(2) backward (EnhancedUNet, hierarchical_segmentation_unet.py:366,384): dx (+)= dy
+ * routed to the first maximum of each 2x2 window (PyTorch's tie rule). */
+int hiseg_maxpool2x2_bwd(int dtype, const void* x, int N, int H, int W, int C, const void* dy, void* dx,
+                         int accumulate, hiseg_stream_t stream);
+
+/* F.interpolate(bilinear, align_corners=False) backward for the aux heads' up-sampling
+ * (refinement.py:775-800): NCHW f32 planes, dx = adjoint of resize (h,w) -> (H,W). */
+int hiseg_resize_bilinear_bwd(const float* dy, int NC, int h, int w, int H, int W, float* dx, hiseg_stream_t stream);
+
+/* ----------------------------------------------------------------------------------------
+ * Optimiser step over a flat f32 parameter space (all trainable parameters of the model are
+ * views into one buffer, their gradients into another): torch.nn.utils.clip_grad_norm_ +
+ * torch.optim.AdamW (train_advanced.py:733-740 clip 1.0; :1111-1143 AdamW lr 1e-4, wd 0.01).
+ *   hiseg_grad_norm_partials: partial[b] = sum of g^2 over block b's slice (b < hiseg_optim_blocks())
+ *   hiseg_adamw_step: total = sqrt(sum partial) (written to norm_out by block 0 if non-null);
+ *     coef = min(1, max_norm / (total + 1e-6)) if max_norm > 0 (grads scaled in place, as
+ *     clip_grad_norm_ does); then AdamW with bias corrections bc1 = 1-beta1^t, bc2 = 1-beta2^t.
+ * -------------------------------------------------------------------------------------- */
+int hiseg_optim_blocks(void);
+int hiseg_grad_norm_partials(const float* g, long long n, float* partial, hiseg_stream_t stream);
+int hiseg_adamw_step(float* p, float* g, float* m, float* v, long long n, float lr, float beta1, float beta2, float eps,
+                     float weight_decay, float bc1, float bc2, const float* partial, float max_norm, float* norm_out,
+                     hiseg_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif  /* HISEG_TRAIN_H_ */

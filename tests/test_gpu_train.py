@@ -1,0 +1,413 @@
+"""Training path on the GPU (libhiseg backward / train-mode kernels through the C ABI).
+
+Each op is run through hiseg.train_engine (forward + tape backward) on seeded inputs and checked
+against torch autograd of the same op in float64 on the GPU (the reference semantics; the oracle's
+functional forms where the op is the reference's composite).  Tolerances: f32 compute 1e-4
+relative to the tensor's max magnitude (2e-4 for reductions over > 1e5 terms); bf16 compute 3e-2.
+The whole-model step is additionally compared with the CPU oracle (oracle/train.py) and the loss
+kernel with the reference's golden vectors (tests/golden/train_loss.npz).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+import filler
+from helpers import b0_kwargs, hiseg_kwargs, load
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel(a, b):
+    a, b = torch.as_tensor(a).double().cpu(), torch.as_tensor(b).double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-12)).item()
+
+
+def rel2(a, b):
+    a, b = torch.as_tensor(a).double().cpu(), torch.as_tensor(b).double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+def err(dt):
+    """f32: max-abs error relative to the tensor's max (1e-4 bar).  bf16: relative L2 error -- a ReLU whose
+    pre-activation rounds across zero in bf16 flips single gradient elements by their full size, so the
+    element-wise maximum is not a meaningful bf16 metric."""
+    return rel if dt == torch.float32 else rel2
+
+
+def tol(dt):
+    return 1e-4 if dt == torch.float32 else 3e-2
+
+
+class _Holder(nn.Module):
+    def __init__(self, **mods):
+        super().__init__()
+        for k, v in mods.items():
+            setattr(self, k, v)
+
+
+def engine(module, dt):
+    from hiseg import train_engine as TE
+    module = module.to(DEV)
+    S = TE.TrainState(module, dt, torch.device(DEV))
+    return TE, S, TE.Tape(S)
+
+
+def inject(T, y, g_nchw, dt):
+    from hiseg.ops import Act
+    ga = Act.from_nchw(g_nchw.to(DEV), dt)
+    if ga.cstride != y.cstride:  # match the activation's padded layout
+        full = Act.new(y.N, y.H, y.W, y.C, dt, DEV, cpad=y.cstride, zero=True)
+        full.t.view(-1, y.cstride)[:, :y.C].copy_(ga.t.view(-1, ga.cstride)[:, :y.C])
+        ga = full
+    T.grads[id(y)] = ga
+    T.mark(y)
+
+
+def grad_nchw(T, a):
+    g, _ = T.grad(a)
+    return g.to_nchw()
+
+
+# ------------------------------------------------------------------------------------------ conv wgrad / dgrad
+CONV_CASES = [  # (cin, cout, k, H, W, N, bias, two-source split)
+    (64, 64, 3, 12, 10, 3, True, None),
+    (256, 256, 3, 16, 12, 2, False, None),
+    (258, 256, 1, 8, 6, 2, True, (256, 2)),
+    (3, 64, 3, 16, 12, 2, True, None),
+    (128, 2, 1, 8, 6, 3, True, None),
+    (128, 64, 3, 8, 6, 2, True, (64, 64)),
+]
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_backward_matches_autograd(case, dt):
+    from hiseg.ops import Act
+    cin, cout, k, H, W, N, bias, split = case
+    conv = nn.Conv2d(cin, cout, k, padding=k // 2, bias=bias)
+    filler.fill_module(conv, seed=7)
+    TE, S, T = engine(_Holder(c=conv), dt)
+    x = torch.from_numpy(filler.normal(1, (N, cin, H, W))).to(DEV)
+    if split is None:
+        xa, xb = Act.from_nchw(x, dt), None
+    else:
+        xa, xb = Act.from_nchw(x[:, :split[0]], dt), Act.from_nchw(x[:, split[0]:], dt)
+    y = TE.conv_plain(T, conv, TE.ACT_NONE, xa, xb, split=split)
+    g = torch.from_numpy(filler.normal(2, (N, cout, H, W))).to(DEV)
+    inject(T, y, g, dt)
+    S.flat.prepare_backward()
+    T.run_backward()
+    xr = x.double().requires_grad_(True)
+    wr = conv.weight.detach().double().requires_grad_(True)
+    br = conv.bias.detach().double().requires_grad_(True) if bias else None
+    yr = F.conv2d(xr, wr, br, padding=k // 2)
+    (yr * g.double()).sum().backward()
+    assert err(dt)(y.to_nchw(), yr.detach()) < tol(dt)
+    assert err(dt)(conv.weight.grad, wr.grad) < tol(dt) * 2
+    if bias:
+        assert err(dt)(conv.bias.grad, br.grad) < tol(dt) * 2
+    if split is None:
+        assert err(dt)(grad_nchw(T, xa), xr.grad) < tol(dt)
+    else:
+        assert err(dt)(grad_nchw(T, xa), xr.grad[:, :split[0]]) < tol(dt)
+        assert err(dt)(grad_nchw(T, xb), xr.grad[:, split[0]:]) < tol(dt)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_convT_backward_matches_autograd(dt):
+    from hiseg.ops import Act
+    conv = nn.ConvTranspose2d(256, 128, 2, stride=2)
+    filler.fill_module(conv, seed=9)
+    TE, S, T = engine(_Holder(c=conv), dt)
+    x = torch.from_numpy(filler.normal(3, (2, 256, 8, 6))).to(DEV)
+    xa = Act.from_nchw(x, dt)
+    y = TE.conv_plain(T, conv, TE.ACT_NONE, xa, convT=True)
+    g = torch.from_numpy(filler.normal(4, (2, 128, 16, 12))).to(DEV)
+    inject(T, y, g, dt)
+    S.flat.prepare_backward()
+    T.run_backward()
+    xr = x.double().requires_grad_(True)
+    wr = conv.weight.detach().double().requires_grad_(True)
+    br = conv.bias.detach().double().requires_grad_(True)
+    yr = F.conv_transpose2d(xr, wr, br, stride=2)
+    (yr * g.double()).sum().backward()
+    assert err(dt)(y.to_nchw(), yr.detach()) < tol(dt)
+    assert err(dt)(conv.weight.grad, wr.grad) < tol(dt) * 2
+    assert err(dt)(conv.bias.grad, br.grad) < tol(dt) * 2
+    assert err(dt)(grad_nchw(T, xa), xr.grad) < tol(dt)
+
+
+# ------------------------------------------------------------------------------------------ BN / residual / dropout
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_residual_block_train_matches_reference(dt):
+    """ResidualBlock(64) train forward/backward against the reference's golden vectors (train_blocks.npz)."""
+    from hiseg.layers import ResidualBlock
+    from hiseg.ops import Act
+    g = load("train_blocks")
+    blk = filler.fill_module(ResidualBlock(64, "batchnorm", 8, "relu")).train()
+    rm0 = blk.norm1.running_mean.clone()
+    TE, S, T = engine(_Holder(b=blk), dt)
+    x = torch.from_numpy(filler.normal(71, tuple(g["res_gx"].shape))).to(DEV)
+    xa = Act.from_nchw(x, dt)
+    y = TE.residual_block(T, blk, xa)
+    gy = torch.from_numpy(filler.normal(81, tuple(g["res_y"].shape)))
+    inject(T, y, gy, dt)
+    S.flat.prepare_backward()
+    T.run_backward()
+    t = tol(dt)
+    assert err(dt)(y.to_nchw(), g["res_y"]) < t
+    assert err(dt)(grad_nchw(T, xa), g["res_gx"]) < t * 2
+    names = list(g["res_names"])
+    for j, n in enumerate(names):
+        p = dict(blk.named_parameters())[n]
+        sq = float((p.grad.double() ** 2).sum())
+        ref = float(g["res_sumsq"][j])
+        if n.endswith(".bias") and n.replace("bias", "weight") in names and \
+                ref < 1e-6 * float(g["res_sumsq"][names.index(n.replace("bias", "weight"))]):
+            continue
+        assert sq == pytest.approx(ref, rel=4 * t), n
+    # running statistics moved with momentum 0.1 (unbiased variance)
+    assert not torch.equal(blk.norm1.running_mean.cpu(), rm0.cpu())
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_bn_dropout_residual_vs_autograd(dt):
+    """conv -> BN(train) -> +residual -> ReLU -> Dropout2d mask, against float64 autograd with the same mask."""
+    from hiseg.ops import Act
+    conv = nn.Conv2d(64, 64, 3, padding=1)
+    bn = nn.BatchNorm2d(64)
+    filler.fill_module(_Holder(c=conv, b=bn), seed=11)
+    TE, S, T = engine(_Holder(c=conv, b=bn), dt)
+    x = torch.from_numpy(filler.normal(5, (3, 64, 10, 8))).to(DEV)
+    r = torch.from_numpy(filler.normal(6, (3, 64, 10, 8))).to(DEV)
+    xa, ra = Act.from_nchw(x, dt), Act.from_nchw(r, dt)
+    drop = nn.Dropout2d(0.3)
+    mask = TE.dropout_mask(T, drop, 3, 64, DEV)
+    keep = (mask > 0).float().mean().item()
+    assert 0.4 < keep < 0.95 and torch.all((mask == 0) | ((mask - 1 / 0.7).abs() < 1e-6))
+    y = TE.conv_bn_act(T, conv, bn, TE.ACT_RELU, xa, residual=ra, drop=mask)
+    g = torch.from_numpy(filler.normal(7, (3, 64, 10, 8))).to(DEV)
+    inject(T, y, g, dt)
+    S.flat.prepare_backward()
+    T.run_backward()
+    xr, rr = x.double().requires_grad_(True), r.double().requires_grad_(True)
+    wr = conv.weight.detach().double().requires_grad_(True)
+    br = conv.bias.detach().double().requires_grad_(True)
+    gam = bn.weight.detach().double().requires_grad_(True)
+    bet = bn.bias.detach().double().requires_grad_(True)
+    z = F.conv2d(xr, wr, br, padding=1)
+    zn = F.batch_norm(z, None, None, gam, bet, True, 0.1, 1e-5)
+    yr = F.relu(zn + rr) * mask.double().view(3, 64, 1, 1)
+    (yr * g.double()).sum().backward()
+    t = tol(dt)
+    assert err(dt)(y.to_nchw(), yr.detach()) < t
+    assert err(dt)(grad_nchw(T, xa), xr.grad) < 2 * t
+    assert err(dt)(grad_nchw(T, ra), rr.grad) < t
+    assert err(dt)(conv.weight.grad, wr.grad) < 2 * t
+    assert err(dt)(bn.weight.grad, gam.grad) < 2 * t
+    assert err(dt)(bn.bias.grad, bet.grad) < 2 * t
+    assert conv.bias.grad.abs().max().item() < 1e-3 * bn.bias.grad.abs().max().item() + 1e-6
+
+
+# ------------------------------------------------------------------------------------------ attention / gates / pool
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_attention_modules_train_match_reference(dt):
+    from hiseg.layers import ChannelAttentionModule, SpatialAttentionModule
+    from hiseg.ops import Act
+    g = load("train_blocks")
+    t = tol(dt)
+    for i, key, mod in ((1, "sa", SpatialAttentionModule(7)), (2, "ca", ChannelAttentionModule(128, 8, act="relu"))):
+        m = filler.fill_module(mod)
+        TE, S, T = engine(_Holder(m=m), dt)
+        x = torch.from_numpy(filler.normal(71 + i, tuple(g[f"{key}_gx"].shape))).to(DEV)
+        xa = Act.from_nchw(x, dt)
+        y = TE.spatial_attention(T, m, xa, None) if key == "sa" else TE.channel_attention(T, m, xa, None)
+        inject(T, y, torch.from_numpy(filler.normal(81 + i, tuple(g[f"{key}_y"].shape))), dt)
+        S.flat.prepare_backward()
+        T.run_backward()
+        assert err(dt)(y.to_nchw(), g[f"{key}_y"]) < t, key
+        assert err(dt)(grad_nchw(T, xa), g[f"{key}_gx"]) < 2 * t, key
+        for j, n in enumerate(g[f"{key}_names"]):
+            p = dict(m.named_parameters())[n]
+            assert float((p.grad.double() ** 2).sum()) == pytest.approx(float(g[f"{key}_sumsq"][j]), rel=6 * t), (key, n)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_enhanced_unet_train_matches_reference(dt):
+    """EnhancedUNet(256, 64, depth 3) train forward/backward vs the reference's golden vectors: maxpool,
+    sigmoid bottleneck gate, ConvTranspose up-path with skip concatenation, f32 final logits."""
+    from hiseg.layers import EnhancedUNet
+    from hiseg.ops import Act
+    g = load("train_blocks")
+    u = filler.fill_module(EnhancedUNet(256, 64, 3, "batchnorm", 8, "relu")).train()
+    TE, S, T = engine(_Holder(m=u), dt)
+    x = torch.from_numpy(filler.normal(74, tuple(g["unet_gx"].shape))).to(DEV)
+    xa = Act.from_nchw(x, dt)
+    low, low_t = TE.enhanced_unet(T, u, xa)
+    gy = torch.from_numpy(filler.normal(84, tuple(g["unet_y"].shape))).to(DEV)
+    inject(T, low, gy, torch.float32)
+    S.flat.prepare_backward()
+    T.run_backward()
+    t = 1e-3 if dt == torch.float32 else 1e-1  # 20 train-mode BN layers over 4x16x12 pixels
+    assert err(dt)(low.to_nchw(), g["unet_y"]) < t
+    assert err(dt)(grad_nchw(T, xa), g["unet_gx"]) < 3 * t
+    names = list(g["unet_names"])
+    mine = np.array([float((dict(u.named_parameters())[n].grad.double() ** 2).sum()) for n in names])
+    ref = g["unet_sumsq"]
+    assert abs(mine.sum() / ref.sum() - 1) < 3 * t
+
+
+# ------------------------------------------------------------------------------------------ loss
+@pytest.mark.parametrize("case", ["a", "b", "c", "d", "e"])
+def test_loss_kernel_matches_reference_golden(case):
+    import hiseg
+    from test_oracle_train import loss_inputs, loss_targets
+    g = load("train_loss")
+    keys = list(g["dict_keys"])
+    names = sorted({k.split("_")[0] for k in g.files if k.endswith("_meta")})
+    loss_fn = hiseg.RefinedHierarchicalLoss(bg_weight=1.5, fg_weight=1.5, target_weight=1.2, consistency_weight=0.3,
+                                            use_dynamic_weights=True, dice_weight=1.0, ce_weight=1.0,
+                                            boundary_aware_weight=0.1, contour_loss_weight=0.1,
+                                            distance_loss_weight=0.1, use_boundary_aware_loss=True,
+                                            use_contour_detection=True, use_distance_transform=True)
+    for key in [n for n in names if n[0] == case]:
+        seed, n, mh, mw = (int(v) for v in g[f"{key}_meta"])
+        ins = [t.to(DEV).requires_grad_(True) for t in loss_inputs(seed, n, mh, mw)]
+        tgt = loss_targets(str(g[f"{key}_kind"]), seed, n, mh, mw).to(DEV)
+        aux = {"bg_fg_logits": ins[1], "target_nontarget_logits": ins[2], "contours": ins[3], "distance_map": ins[4]}
+        loss, d = loss_fn(ins[0], tgt, aux)
+        loss.backward()
+        assert loss.item() == pytest.approx(float(g[f"{key}_loss"]), rel=1e-5, abs=1e-6), key
+        for k, rv in zip(keys, g[f"{key}_dict"]):
+            if np.isnan(rv):
+                assert k not in d, (key, k)
+            else:
+                assert d[k] == pytest.approx(float(rv), rel=1e-4, abs=1e-6), (key, k)
+        for i, nm in enumerate(["pred", "bgfg", "tn", "cont", "dist"]):
+            ref = torch.from_numpy(g[f"{key}_grad_{nm}"])
+            got = ins[i].grad.cpu()
+            if ref.numel() == 0:
+                assert not got.any(), (key, nm)
+                continue
+            assert (got - ref).abs().max().item() <= 1e-7 + 1e-4 * ref.abs().max().item(), (key, nm)
+
+
+# ------------------------------------------------------------------------------------------ optimiser
+def test_fused_adamw_matches_torch():
+    import hiseg
+    from hiseg import train_engine as TE
+    torch.manual_seed(0)
+    m = nn.Sequential(nn.Conv2d(8, 16, 3), nn.Conv2d(16, 4, 1)).to(DEV)
+    ref = [p.detach().clone().requires_grad_(True) for p in m.parameters()]
+    S = TE.TrainState(m, torch.float32, torch.device(DEV))
+    m.__dict__["_hiseg_train"] = S
+    opt = hiseg.FusedAdamW(m, lr=1e-3, weight_decay=0.01, max_grad_norm=1.0)
+    ropt = torch.optim.AdamW(ref, lr=1e-3, weight_decay=0.01)
+    for step in range(3):
+        grads = [torch.randn_like(p) * (3.0 if step == 1 else 0.1) for p in ref]
+        for p, g in zip(m.parameters(), grads):
+            p.grad.copy_(g)
+        for p, g in zip(ref, grads):
+            p.grad = g.clone()
+        norm = opt.step()
+        rn = torch.nn.utils.clip_grad_norm_(ref, 1.0)
+        ropt.step()
+        assert norm.item() == pytest.approx(rn.item(), rel=1e-5)
+        for p, r in zip(m.parameters(), ref):
+            assert (p.detach() - r.detach()).abs().max().item() < 1e-6
+
+
+# ------------------------------------------------------------------------------------------ whole model
+def _model(dt, p_drop_zero=True):
+    import hiseg
+    m = hiseg.create_rgb_hierarchical_model(**hiseg_kwargs(b0_kwargs()))
+    filler.fill_module(m)
+    if p_drop_zero:
+        for mod in m.modules():
+            if isinstance(mod, (nn.Dropout, nn.Dropout2d)):
+                mod.p = 0.0
+    hiseg.set_compute_dtype(m, dt)
+    return m
+
+
+def test_train_step_f32_matches_oracle():
+    """B0-std train forward + RefinedHierarchicalLoss + backward in f32 against the CPU oracle (torch autograd
+    of the restated model, oracle/train.py) on the same inputs.  Loss and logits: 1e-4 relative.  Gradients:
+    the ~50-layer train-mode BN stack at initialisation amplifies 1e-7 input changes into ~5 % gradient changes
+    (tests/test_oracle_train.py), so parameter gradients are compared by cosine similarity (> 0.99 for every
+    tensor with a non-negligible gradient) and the total gradient norm (2 %)."""
+    import hiseg
+    from oracle import rgb_model as O
+    from oracle import train as OT
+    m = _model(torch.float32)
+    sd = OT.params_of(m)
+    m = m.to(DEV).train()
+    cfg = O.cfg_from_kwargs(hiseg_kwargs(b0_kwargs()))
+    images = torch.from_numpy(filler.uniform(61, (2, 3, 96, 128)))
+    u = torch.from_numpy(filler.normal(62, (2, 1, 96, 128)) * 2.0)
+    rois = torch.tensor([[0, .10, .10, .40, .90], [1, .35, .15, .80, .95], [0, .55, .05, .95, .70]])
+    for mm in (m.roi_align_mask, m.roi_align_rgb):
+        mm.spatial_scale_h, mm.spatial_scale_w = 96, 128
+    tgt = torch.from_numpy(filler.ellipse_targets(63, 3, *cfg["mask_hw"]))
+    from hiseg import train_engine as TE
+    logits, aux = TE.train_forward(m, images.to(DEV), rois.to(DEV), u_override=u.to(DEV))
+    loss_fn = hiseg.RefinedHierarchicalLoss(use_boundary_aware_loss=True, use_contour_detection=True,
+                                            use_distance_transform=True, boundary_aware_weight=0.1,
+                                            contour_loss_weight=0.1, distance_loss_weight=0.1)
+    loss, d = loss_fn(logits, tgt.to(DEV), aux)
+    loss.backward()
+    rlog, raux = OT.forward_train(sd, images, rois, u, cfg, (96, 128))
+    rloss, rd = OT.RefinedHierarchicalLoss()(rlog, tgt, raux)
+    rloss.backward()
+    assert rel(logits.detach(), rlog.detach()) < 1e-3
+    assert loss.item() == pytest.approx(rloss.item(), rel=1e-4)
+    for k in ("bg_fg_loss", "final_loss", "dice_loss", "boundary_aware", "contour", "distance_transform"):
+        assert d[k] == pytest.approx(rd[k], rel=1e-3), k
+    tot_m, tot_r = 0.0, 0.0
+    for n, p in m.named_parameters():
+        if n not in sd or not sd[n].requires_grad:
+            continue
+        rg = sd[n].grad
+        if rg is None:
+            assert p.grad is None or not p.grad.any(), n
+            continue
+        mg = p.grad.detach().cpu().double().reshape(-1)
+        rg = rg.double().reshape(-1)
+        tot_m += float((mg ** 2).sum())
+        tot_r += float((rg ** 2).sum())
+        if rg.norm() < 1e-6 * (1 + rg.numel()) ** 0.5 or (n.endswith(".bias") and rg.norm() < 1e-4):
+            continue
+        cos = float((mg * rg).sum() / (mg.norm() * rg.norm()))
+        assert cos > 0.99, (n, cos)
+    assert abs(tot_m / tot_r - 1) < 4e-2
+
+
+def test_train_loop_bf16_decreases_loss():
+    """bf16 training with the fused AdamW: five steps on one batch (dropout on) lower the loss."""
+    import hiseg
+    m = _model(torch.bfloat16, p_drop_zero=False).to(DEV).train()
+    images = torch.from_numpy(filler.uniform(91, (4, 3, 160, 192))).to(DEV)
+    rois = torch.from_numpy(filler.box_rois(92, 4, 1)).to(DEV)
+    for mm in (m.roi_align_mask, m.roi_align_rgb):
+        mm.spatial_scale_h, mm.spatial_scale_w = 160, 192
+    tgt = torch.from_numpy(filler.ellipse_targets(93, 4, 128, 96)).to(DEV)
+    loss_fn = hiseg.RefinedHierarchicalLoss(use_boundary_aware_loss=True, use_contour_detection=True,
+                                            use_distance_transform=True, boundary_aware_weight=0.1,
+                                            contour_loss_weight=0.1, distance_loss_weight=0.1)
+    opt = None
+    losses = []
+    for step in range(6):
+        logits, aux = m(images, rois)
+        loss, d = loss_fn(logits, tgt, aux)
+        if opt is None:
+            opt = hiseg.FusedAdamW(m, lr=5e-4)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert all(np.isfinite(losses)), losses
+    assert losses[-1] < losses[0], losses
+    assert set(d.keys()) >= {"bg_fg_loss", "final_loss", "dice_loss", "contour", "distance_transform"}
