@@ -11,7 +11,14 @@ Multi-GPU: one process per GPU (torch.distributed.run), each rank processes its 
 (weak scaling, no data-path collective); barrier + synchronize around the K timed steps and the
 max over ranks of the elapsed time.
 
-Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+Second measurement, reported under "train" in the same JSON line (the metric's "train step/s"): one
+training step of the same B0-std model on the same 32-image x 8-ROI batch per GPU -- frozen full-image
+UNet forward, train-mode ROI path (batch-statistics BN, Dropout2d), RefinedHierarchicalLoss with the
+boundary/contour/distance terms, the hand-written backward, FusedAdamW (clip 1.0) -- with the gradients
+averaged over the ranks by hiseg.distributed (bucketed RCCL all-reduce overlapped with the backward) when
+N > 1.
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--no-train]
 """
 import argparse
 import json
@@ -31,6 +38,8 @@ ROI_HW, MASK_HW = (64, 48), (128, 96)
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
 # Algorithmic work per ROI mask: head 53.1 GFLOP (inference graph) + B0 UNet 27.7/8
 GFLOP_PER_ROI_MASK = 53.1 + 27.7 / 8
+# Algorithmic work per training sample: B0-std head fwd+bwd 173.5 GFLOP + UNet fwd per ROI
+GFLOP_PER_TRAIN_ROI = 173.5 + 27.7 / 8
 
 B0_KWARGS = dict(
     roi_size=ROI_HW, mask_size=MASK_HW, multi_scale=False, use_attention_module=True,
@@ -65,6 +74,66 @@ def dominant_select(d):
     if d.KH == 3 and d.Ca == 256 and d.Cb == 0 and d.Cout == 256 and (d.Ho, d.Wo) == ROI_HW and not d.convT:
         return "conv3x3_256x256_roi"
     return None
+
+
+def train_bench(device, dtype, rank, world, dist, steps, warmup):
+    """Train steps/s of the B0-std ROI model on the C2-shaped batch (module docstring)."""
+    import filler
+    import hiseg
+    from hiseg import distributed as HD
+    model = build_model(device, dtype).train()
+    for m in (model.roi_align_mask, model.roi_align_rgb):
+        m.spatial_scale_h, m.spatial_scale_w = H, W
+    images, rois = synthetic_batch(device, rank)
+    tgt = torch.from_numpy(filler.ellipse_targets(7 + rank, B * R, *MASK_HW)).to(device)
+    loss_fn = hiseg.RefinedHierarchicalLoss(use_boundary_aware_loss=True, use_contour_detection=True,
+                                            use_distance_transform=True, boundary_aware_weight=0.1,
+                                            contour_loss_weight=0.1, distance_loss_weight=0.1)
+    if world > 1:
+        HD.enable_grad_sync(model)
+    state = {"opt": None}
+
+    def step():
+        logits, aux = model(images, rois)
+        loss, _ = loss_fn(logits, tgt, aux)
+        if state["opt"] is None:
+            state["opt"] = hiseg.FusedAdamW(model, lr=1e-4, weight_decay=0.01, max_grad_norm=1.0)
+        state["opt"].zero_grad()
+        loss.backward()
+        state["opt"].step()
+        return loss
+
+    for _ in range(warmup):
+        loss = step()
+    torch.cuda.synchronize()
+    first = float(loss.detach())
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    last = float(loss.detach())
+    if not (first == first and last == last):
+        raise RuntimeError("train bench: non-finite loss")
+    sps = steps / elapsed
+    return {"metric": "train step/s", "value": round(sps, 3), "unit": "steps/s", "ms_per_step": round(1e3 / sps, 2),
+            "steps": steps, "warmup": warmup, "samples_per_s": round(sps * B * R * world, 1),
+            "pipeline_tflops": round(sps * B * R * world * GFLOP_PER_TRAIN_ROI / 1e3, 1),
+            "loss_first_last": [round(first, 4), round(last, 4)],
+            "config": {"workload": "B0-std train step: 32 img 640x480 x 8 ROIs/GPU (256 ROI samples), ROI 64x48, "
+                                   "mask 128x96, frozen UNet fwd + ROI path fwd/bwd + RefinedHierarchicalLoss + "
+                                   "FusedAdamW", "global_batch": B * world, "roi_samples_per_step": B * R * world,
+                       "parallelism": f"dp{world} (DDP, bucketed RCCL grad all-reduce)" if world > 1 else "dp1"}}
 
 
 def cpu_baseline(seconds_budget=30.0):
@@ -115,6 +184,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--no-train", action="store_true")
+    ap.add_argument("--train-only", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -128,6 +199,22 @@ def main():
     device = torch.device("cuda", local)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
 
+    import hiseg  # noqa: F401
+    out = {}
+    if not args.train_only:
+        out = infer_bench(args, device, dtype, rank, world, dist)
+    if not args.no_train:
+        torch.cuda.empty_cache()
+        out["train"] = train_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), max(2, args.warmup))
+    if rank == 0:
+        if world == 1 and not args.no_cpu_baseline and not args.train_only:
+            out["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
+def infer_bench(args, device, dtype, rank, world, dist):
     import hiseg
     from hiseg import ops
     model = build_model(device, dtype)
@@ -172,24 +259,18 @@ def main():
                     "launches_timed": summ["launches"], "avg_launch_ms": round(summ["avg_ms"], 4),
                     "flop_per_launch": summ["flops"]}
     pipeline_tflops = value * GFLOP_PER_ROI_MASK / 1e3
-
-    if rank == 0:
-        out = {
-            "metric": METRIC, "value": round(value, 2), "unit": "ROI-masks/s", "n_gpus": n, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if dtype == torch.bfloat16 else "f32",
-            "data": "synthetic (U[0,1) images, SURVEY §8d ROI boxes; deterministic random-init B0 weights)",
-            "config": {"workload": "C2: B0 inference 640x480, batch 32/GPU x 8 ROIs/img, ROI 64x48, mask 128x96",
-                       "global_batch": B * n, "rois_per_step": B * R * n, "seq_len": None,
-                       "parallelism": f"dp{n} (images sharded, model replicated, no collective)"},
-            "pipeline_tflops": round(pipeline_tflops, 1),
-            "roofline": roofline,
-        }
-        if n == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline()
-        print(json.dumps(out))
-    if dist:
-        dist.destroy_process_group()
+    del wrapper, model
+    return {
+        "metric": METRIC, "value": round(value, 2), "unit": "ROI-masks/s", "n_gpus": n, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if dtype == torch.bfloat16 else "f32",
+        "data": "synthetic (U[0,1) images, SURVEY §8d ROI boxes; deterministic random-init B0 weights)",
+        "config": {"workload": "C2: B0 inference 640x480, batch 32/GPU x 8 ROIs/img, ROI 64x48, mask 128x96",
+                   "global_batch": B * n, "rois_per_step": B * R * n, "seq_len": None,
+                   "parallelism": f"dp{n} (images sharded, model replicated, no collective)"},
+        "pipeline_tflops": round(pipeline_tflops, 1),
+        "roofline": roofline,
+    }
 
 
 if __name__ == "__main__":

@@ -160,6 +160,8 @@ class TrainState:
         self.max_total = 0
         self.seed = itertools.count(int(torch.initial_seed()) & 0xFFFFFFFF)
         self.cached: Dict = {}
+        self.sync = None          # hiseg.distributed.GradBucketSync (data-parallel gradient exchange)
+        self.op_index: Optional[int] = None
 
     # -- plans
     def conv(self, conv: nn.Module, split=None, convT: bool = False) -> TConv:
@@ -234,6 +236,9 @@ class TrainState:
                 _copy_bias(p.shift, p.conv.bias.detach(), p.cout, p.convT)
 
     def grad(self, p: nn.Parameter) -> torch.Tensor:
+        """Gradient slice of p; during a backward also tells the gradient exchange which tape op writes it."""
+        if self.sync is not None:
+            self.sync.record(p, self.op_index)
         return self.flat.grad_view(p)
 
     def next_seed(self) -> int:
@@ -278,8 +283,19 @@ class Tape:
         return self.written.get(id(a), False)
 
     def run_backward(self):
-        for fn in reversed(self.ops):
+        S, ops = self.S, self.ops[::-1]
+        sync = S.sync
+        if sync is not None:
+            sync.attach(S)
+            sync.begin(len(ops))
+        for i, fn in enumerate(ops):
+            S.op_index = i
             fn()
+            if sync is not None:
+                sync.after_op(i)
+        S.op_index = None
+        if sync is not None:
+            sync.end(len(ops))
         self.ops.clear()
 
 
@@ -979,6 +995,7 @@ def train_forward(model: nn.Module, images: torch.Tensor, rois: torch.Tensor, u_
     if S is None or S.dtype != dtype or S.device != dev:
         S = TrainState(model, dtype, dev)
         model.__dict__["_hiseg_train"] = S
+    S.sync = model.__dict__.get("_hiseg_grad_sync")
     images = images.contiguous().float()
     rois = rois.to(device=dev, dtype=torch.float32).contiguous()
     pre = model.pretrained_unet
