@@ -7,7 +7,7 @@
 
 namespace hiseg {
 
-constexpr int kBnSplits = 480;  // pixel splits of the statistics passes (~2 blocks per CU)
+constexpr int kBnSplits = 1024;  // pixel splits of the statistics passes (4 blocks per CU)
 
 template <typename T>
 __device__ __forceinline__ float ld(const void* p, long long i) { return Elem<T>::load(p, i); }
@@ -69,32 +69,6 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const void* z, long long 
   }
 }
 
-__global__ void bn_finalize_kernel(const float* partial, int S, int C, long long P, const float* gamma,
-                                   const float* beta, float eps, float momentum, float* rm, float* rv, float* mean_o,
-                                   float* invstd_o, float* scale, float* shift) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double n = 0, mean = 0, m2 = 0;
-  for (int s = 0; s < S; ++s) {
-    const float* p = partial + (long long)s * 3 * C;
-    const double nb = p[c];
-    if (nb == 0) continue;
-    const double d = p[C + c] - mean, nt = n + nb;
-    mean += d * nb / nt;
-    m2 += p[2 * C + c] + d * d * n * nb / nt;
-    n = nt;
-  }
-  const double var = m2 / n;
-  const double inv = 1.0 / sqrt(var + (double)eps);
-  const float g = gamma ? gamma[c] : 1.f, bb = beta ? beta[c] : 0.f;
-  mean_o[c] = (float)mean;
-  invstd_o[c] = (float)inv;
-  scale[c] = (float)(g * inv);
-  shift[c] = (float)(bb - mean * g * inv);
-  if (rm) rm[c] = (float)((1.0 - momentum) * rm[c] + momentum * mean);
-  if (rv) rv[c] = (float)((1.0 - momentum) * rv[c] + momentum * (P > 1 ? var * (double)P / (double)(P - 1) : var));
-}
-
 // ---------------------------------------------------------------------------------------- apply
 template <typename T>
 __global__ void __launch_bounds__(256) bn_apply_kernel(hiseg_bn_apply_desc d) {
@@ -150,29 +124,6 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(hiseg_bn_bwd_desc d)
   }
 }
 
-__global__ void bn_bwd_finalize_kernel(hiseg_bn_bwd_desc d, int S) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  const int C = d.C;
-  if (c >= C) return;
-  double s1 = 0, s2 = 0, s3 = 0;
-  for (int s = 0; s < S; ++s) {
-    const float* p = d.partial + (long long)s * 3 * C;
-    s1 += p[c]; s2 += p[C + c]; s3 += p[2 * C + c];
-  }
-  const double P = (double)d.P;
-  const double k = (d.gamma ? d.gamma[c] : 1.0) * d.invstd[c];
-  float* coef = d.partial + (long long)S * 3 * C;  // [3][C]: k, mean(g), mean(g*xhat)
-  coef[c] = (float)k;
-  coef[C + c] = (float)(s1 / P);
-  coef[2 * C + c] = (float)(s2 / P);
-  if (d.dgamma) d.dgamma[c] = (float)(d.accumulate_params ? d.dgamma[c] + s2 : s2);
-  if (d.dbeta) d.dbeta[c] = (float)(d.accumulate_params ? d.dbeta[c] + s1 : s1);
-  if (d.dconv_bias) {
-    const double sdz = k * (s1 - P * (s1 / P) - s3 * (s2 / P));
-    d.dconv_bias[c] = (float)(d.accumulate_params ? d.dconv_bias[c] + sdz : sdz);
-  }
-}
-
 template <typename T>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(hiseg_bn_bwd_desc d, int S) {
   const int C = d.C;
@@ -187,6 +138,291 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(hiseg_bn_bwd_desc d, 
     if (d.dres) {
       const long long o = p * d.dres_cstride + d.dres_coff + c;
       st<T>(d.dres, o, d.dres_accumulate ? ld<T>(d.dres, o) + g : g);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------- vectorised
+// The same passes with one 16-B chunk (8 bf16 / 4 f32 channels) per thread per pixel: a wavefront
+// reads 64 x 16 B = 1 KiB per load instruction, pixel rows of a block are contiguous in HBM (NHWC),
+// so every pass streams at HBM rate.  Block = CT chunk lanes x R pixel rows (CT = min(C/VEC, 256)).
+// Used whenever channels, strides and offsets are multiples of the chunk (all hiseg activations).
+template <typename T>
+__device__ __forceinline__ void ldv(const void* p, long long i, float* v) {
+  Chunk<T>::unpack(*reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(p) + i), v);
+}
+template <typename T>
+__device__ __forceinline__ void stv(void* p, long long i, const float* v) {
+  *reinterpret_cast<uint4*>(reinterpret_cast<T*>(p) + i) = Chunk<T>::pack(v);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bn_stats_vec_kernel(const void* z, long long P, int C, int cs, int coff,
+                                                           float* partial) {
+  constexpr int V = Chunk<T>::N;
+  __shared__ float sh[256 * (2 * V + 1)];
+  const int NCH = C / V;
+  const int CT = NCH < 256 ? NCH : 256;
+  const int R = 256 / CT;
+  const int t = threadIdx.x;
+  const int cl = t % CT, r = t / CT;
+  const int ch = blockIdx.y * 256 + cl;
+  const bool live = r < R && ch < NCH;
+  long long b, e;
+  split_range(P, blockIdx.x, gridDim.x, b, e);
+  float n = 0.f, mean[V], m2[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) mean[k] = m2[k] = 0.f;
+  if (live) {
+    for (long long p = b + r; p < e; p += R) {
+      float x[V];
+      ldv<T>(z, p * cs + coff + ch * V, x);
+      n += 1.f;
+      const float rn = 1.f / n;
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        const float d = x[k] - mean[k];
+        mean[k] += d * rn;
+        m2[k] += d * (x[k] - mean[k]);
+      }
+    }
+  }
+  float* my = sh + t * (2 * V + 1);
+  my[0] = n;
+#pragma unroll
+  for (int k = 0; k < V; ++k) { my[1 + k] = mean[k]; my[1 + V + k] = m2[k]; }
+  __syncthreads();
+  if (r == 0 && ch < NCH) {
+    for (int rr = 1; rr < R; ++rr) {
+      const float* o = sh + (rr * CT + cl) * (2 * V + 1);
+      const float nb = o[0];
+      if (nb == 0.f) continue;
+      const float na = n, nt = na + nb;
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        const float d = o[1 + k] - mean[k];
+        mean[k] += d * (nb / nt);
+        m2[k] += o[1 + V + k] + d * d * (na * nb / nt);
+      }
+      n = nt;
+    }
+    float* out = partial + (long long)blockIdx.x * 3 * C + ch * V;
+#pragma unroll
+    for (int k = 0; k < V; ++k) { out[k] = n; out[C + k] = mean[k]; out[2 * C + k] = m2[k]; }
+  }
+}
+
+// One block per channel: 256 threads merge the S split partials (Chan, double), tree-combined in LDS.
+__global__ void __launch_bounds__(256) bn_finalize_par_kernel(const float* partial, int S, int C, long long P,
+                                                              const float* gamma, const float* beta, float eps,
+                                                              float momentum, float* rm, float* rv, float* mean_o,
+                                                              float* invstd_o, float* scale, float* shift) {
+  __shared__ double sn[256], sm[256], sq[256];
+  const int c = blockIdx.x, t = threadIdx.x;
+  double n = 0, mean = 0, m2 = 0;
+  for (int s = t; s < S; s += 256) {
+    const float* p = partial + (long long)s * 3 * C;
+    const double nb = p[c];
+    if (nb == 0) continue;
+    const double d = p[C + c] - mean, nt = n + nb;
+    mean += d * nb / nt;
+    m2 += p[2 * C + c] + d * d * n * nb / nt;
+    n = nt;
+  }
+  sn[t] = n; sm[t] = mean; sq[t] = m2;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) {
+      const double na = sn[t], nb = sn[t + w];
+      if (nb > 0) {
+        const double nt = na + nb, d = sm[t + w] - sm[t];
+        sm[t] += d * nb / nt;
+        sq[t] += sq[t + w] + d * d * na * nb / nt;
+        sn[t] = nt;
+      }
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    const double var = sq[0] / sn[0];
+    const double inv = 1.0 / sqrt(var + (double)eps);
+    const double mu = sm[0];
+    const float g = gamma ? gamma[c] : 1.f, bb = beta ? beta[c] : 0.f;
+    mean_o[c] = (float)mu;
+    invstd_o[c] = (float)inv;
+    scale[c] = (float)(g * inv);
+    shift[c] = (float)(bb - mu * g * inv);
+    if (rm) rm[c] = (float)((1.0 - momentum) * rm[c] + momentum * mu);
+    if (rv) rv[c] = (float)((1.0 - momentum) * rv[c] + momentum * (P > 1 ? var * (double)P / (double)(P - 1) : var));
+  }
+}
+
+// Element-wise passes: block = CT chunk lanes x R pixel rows (as the reductions), blocks stride over pixel
+// rows; 32-bit pixel indices (P < 2^31, checked on the host), no per-element 64-bit division.
+template <typename T>
+__global__ void __launch_bounds__(256) bn_apply_vec_kernel(hiseg_bn_apply_desc d) {
+  constexpr int V = Chunk<T>::N;
+  const int NCH = d.C / V;
+  const int CT = NCH < 256 ? NCH : 256;
+  const int R = 256 / CT;
+  const int t = threadIdx.x;
+  const int cl = t % CT, r = t / CT;
+  const int ch = blockIdx.y * 256 + cl;
+  if (r >= R || ch >= NCH) return;
+  const int c = ch * V;
+  const int P = (int)d.P;
+  float sc[V], sf[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) { sc[k] = d.scale[c + k]; sf[k] = d.shift[c + k]; }
+  for (int p = blockIdx.x * R + r; p < P; p += gridDim.x * R) {
+    float v[V], rr[V];
+    ldv<T>(d.z, (long long)p * d.z_cstride + d.z_coff + c, v);
+    if (d.residual) ldv<T>(d.residual, (long long)p * d.r_cstride + d.r_coff + c, rr);
+    const float* cm = d.chan_mul ? d.chan_mul + (long long)(p / d.HW) * d.C + c : nullptr;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      float x = v[k] * sc[k] + sf[k];
+      if (d.residual) x += rr[k];
+      x = apply_act(x, d.act);
+      if (cm) x *= cm[k];
+      v[k] = x;
+    }
+    stv<T>(d.y, (long long)p * d.y_cstride + d.y_coff + c, v);
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void bn_gv(const hiseg_bn_bwd_desc& d, long long p, int c, float* g) {
+  constexpr int V = Chunk<T>::N;
+  ldv<T>(d.dy, p * d.dy_cstride + d.dy_coff + c, g);
+  if (d.chan_mul) {
+    const float* cm = d.chan_mul + (long long)((int)p / d.HW) * d.C + c;
+#pragma unroll
+    for (int k = 0; k < V; ++k) g[k] *= cm[k];
+  }
+  if (d.act != HISEG_ACT_NONE) {
+    float y[V];
+    ldv<T>(d.y, p * d.y_cstride + d.y_coff + c, y);
+#pragma unroll
+    for (int k = 0; k < V; ++k) g[k] *= act_grad(y[k], d.act);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bn_bwd_reduce_vec_kernel(hiseg_bn_bwd_desc d) {
+  constexpr int V = Chunk<T>::N;
+  __shared__ float sh[256 * 3 * V];
+  const int C = d.C;
+  const int NCH = C / V;
+  const int CT = NCH < 256 ? NCH : 256;
+  const int R = 256 / CT;
+  const int t = threadIdx.x;
+  const int cl = t % CT, r = t / CT;
+  const int ch = blockIdx.y * 256 + cl;
+  const int c = ch * V;
+  long long b, e;
+  split_range(d.P, blockIdx.x, gridDim.x, b, e);
+  float s1[V], s2[V], s3[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) s1[k] = s2[k] = s3[k] = 0.f;
+  if (r < R && ch < NCH) {
+    float mu[V], inv[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) { mu[k] = d.mean[c + k]; inv[k] = d.invstd[c + k]; }
+    for (long long p = b + r; p < e; p += R) {
+      float g[V], z[V];
+      bn_gv<T>(d, p, c, g);
+      ldv<T>(d.z, p * d.z_cstride + d.z_coff + c, z);
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        const float xh = (z[k] - mu[k]) * inv[k];
+        s1[k] += g[k]; s2[k] += g[k] * xh; s3[k] += xh;
+      }
+    }
+  }
+  float* my = sh + t * 3 * V;
+#pragma unroll
+  for (int k = 0; k < V; ++k) { my[k] = s1[k]; my[V + k] = s2[k]; my[2 * V + k] = s3[k]; }
+  __syncthreads();
+  if (r == 0 && ch < NCH) {
+    for (int rr = 1; rr < R; ++rr) {
+      const float* o = sh + (rr * CT + cl) * 3 * V;
+#pragma unroll
+      for (int k = 0; k < V; ++k) { s1[k] += o[k]; s2[k] += o[V + k]; s3[k] += o[2 * V + k]; }
+    }
+    float* out = d.partial + (long long)blockIdx.x * 3 * C + c;
+#pragma unroll
+    for (int k = 0; k < V; ++k) { out[k] = s1[k]; out[C + k] = s2[k]; out[2 * C + k] = s3[k]; }
+  }
+}
+
+__global__ void __launch_bounds__(256) bn_bwd_finalize_par_kernel(hiseg_bn_bwd_desc d, int S) {
+  __shared__ double a1[256], a2[256], a3[256];
+  const int c = blockIdx.x, t = threadIdx.x, C = d.C;
+  double s1 = 0, s2 = 0, s3 = 0;
+  for (int s = t; s < S; s += 256) {
+    const float* p = d.partial + (long long)s * 3 * C;
+    s1 += p[c]; s2 += p[C + c]; s3 += p[2 * C + c];
+  }
+  a1[t] = s1; a2[t] = s2; a3[t] = s3;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) { a1[t] += a1[t + w]; a2[t] += a2[t + w]; a3[t] += a3[t + w]; }
+    __syncthreads();
+  }
+  if (t == 0) {
+    s1 = a1[0]; s2 = a2[0]; s3 = a3[0];
+    const double P = (double)d.P;
+    const double k = (d.gamma ? d.gamma[c] : 1.0) * d.invstd[c];
+    float* coef = d.partial + (long long)S * 3 * C;
+    coef[c] = (float)k;
+    coef[C + c] = (float)(s1 / P);
+    coef[2 * C + c] = (float)(s2 / P);
+    if (d.dgamma) d.dgamma[c] = (float)(d.accumulate_params ? d.dgamma[c] + s2 : s2);
+    if (d.dbeta) d.dbeta[c] = (float)(d.accumulate_params ? d.dbeta[c] + s1 : s1);
+    if (d.dconv_bias) {
+      const double sdz = k * (s1 - P * (s1 / P) - s3 * (s2 / P));
+      d.dconv_bias[c] = (float)(d.accumulate_params ? d.dconv_bias[c] + sdz : sdz);
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bn_bwd_apply_vec_kernel(hiseg_bn_bwd_desc d, int S) {
+  constexpr int V = Chunk<T>::N;
+  const int C = d.C;
+  const int NCH = C / V;
+  const int CT = NCH < 256 ? NCH : 256;
+  const int R = 256 / CT;
+  const int t = threadIdx.x;
+  const int cl = t % CT, r = t / CT;
+  const int ch = blockIdx.y * 256 + cl;
+  if (r >= R || ch >= NCH) return;
+  const int c = ch * V;
+  const float* coef = d.partial + (long long)S * 3 * C;
+  float k0[V], k1[V], k2[V], mu[V], inv[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    k0[k] = coef[c + k]; k1[k] = coef[C + c + k]; k2[k] = coef[2 * C + c + k];
+    mu[k] = d.mean[c + k]; inv[k] = d.invstd[c + k];
+  }
+  const int P = (int)d.P;
+  for (int p = blockIdx.x * R + r; p < P; p += gridDim.x * R) {
+    float g[V], z[V], o[V];
+    bn_gv<T>(d, p, c, g);
+    ldv<T>(d.z, (long long)p * d.z_cstride + d.z_coff + c, z);
+#pragma unroll
+    for (int k = 0; k < V; ++k) o[k] = k0[k] * (g[k] - k1[k] - (z[k] - mu[k]) * inv[k] * k2[k]);
+    stv<T>(d.dz, (long long)p * d.dz_cstride + d.dz_coff + c, o);
+    if (d.dres) {
+      const long long off = (long long)p * d.dres_cstride + d.dres_coff + c;
+      if (d.dres_accumulate) {
+        float r[V];
+        ldv<T>(d.dres, off, r);
+#pragma unroll
+        for (int k = 0; k < V; ++k) g[k] += r[k];
+      }
+      stv<T>(d.dres, off, g);
     }
   }
 }
@@ -373,6 +609,21 @@ using namespace hiseg;
 
 extern "C" int hiseg_bn_partials(void) { return kBnSplits; }
 
+// 16-B chunk path eligibility: channel count, strides and offsets in whole chunks, aligned base.
+static bool vec_ok(int dtype, int C, const void* p, int cs, int coff) {
+  const int v = dtype == HISEG_BF16 ? 8 : 4;
+  return p == nullptr || (C % v == 0 && cs % v == 0 && coff % v == 0 && al16(p));
+}
+
+// Grid of the element-wise passes: pixel-row blocks (<= 2048 -> 8 waves per SIMD), channel groups in y.
+static dim3 vec_grid(long long P, int C, int dtype) {
+  const int nch = C / (dtype == HISEG_BF16 ? 8 : 4);
+  const int ct = nch < 256 ? nch : 256, R = 256 / ct;
+  long long bx = (P + R - 1) / R;
+  if (bx > 2048) bx = 2048;
+  return dim3((unsigned)(bx < 1 ? 1 : bx), (unsigned)((nch + 255) / 256));
+}
+
 static int splits_for(long long P) { return (int)(P < kBnSplits ? (P > 0 ? P : 1) : kBnSplits); }
 
 extern "C" int hiseg_bn_stats(int dtype, const void* z, long long P, int C, int cstride, int coff, float* partial,
@@ -380,6 +631,13 @@ extern "C" int hiseg_bn_stats(int dtype, const void* z, long long P, int C, int 
   HISEG_REQUIRE(z && partial && P > 0 && C > 0 && cstride >= C, HISEG_ERR_BAD_ARG, "bn_stats: bad arguments");
   HISEG_REQUIRE(dtype == HISEG_F32 || dtype == HISEG_BF16, HISEG_ERR_BAD_DTYPE, "bn_stats: dtype");
   const int S = kBnSplits;  // fixed count: empty splits write n = 0
+  if (vec_ok(dtype, C, z, cstride, coff)) {
+    const int V = dtype == HISEG_BF16 ? 8 : 4;
+    dim3 grid(S, (C / V + 255) / 256);
+    DISPATCH_T(dtype, hipLaunchKernelGGL(bn_stats_vec_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream, z, P, C,
+                                         cstride, coff, partial));
+    return hiseg_check_launch("bn_stats");
+  }
   dim3 grid(S, (C + 255) / 256);
   DISPATCH_T(dtype, hipLaunchKernelGGL(bn_stats_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream, z, P, C, cstride,
                                        coff, partial));
@@ -390,7 +648,7 @@ extern "C" int hiseg_bn_finalize(const float* partial, int C, long long P, const
                                  float eps, float momentum, float* running_mean, float* running_var, float* mean,
                                  float* invstd, float* scale, float* shift, hiseg_stream_t stream) {
   HISEG_REQUIRE(partial && mean && invstd && scale && shift && C > 0, HISEG_ERR_BAD_ARG, "bn_finalize: null");
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, partial, kBnSplits, C,
+  hipLaunchKernelGGL(bn_finalize_par_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, partial, kBnSplits, C,
                      P, gamma, beta, eps, momentum, running_mean, running_var, mean, invstd, scale, shift);
   return hiseg_check_launch("bn_finalize");
 }
@@ -398,6 +656,13 @@ extern "C" int hiseg_bn_finalize(const float* partial, int C, long long P, const
 extern "C" int hiseg_bn_apply(const hiseg_bn_apply_desc* d, hiseg_stream_t stream) {
   HISEG_REQUIRE(d && d->z && d->y && d->scale && d->shift && d->P > 0 && d->C > 0 && d->HW > 0, HISEG_ERR_BAD_ARG,
                 "bn_apply: bad arguments");
+  HISEG_REQUIRE(d->P < (1ll << 31), HISEG_ERR_BAD_SHAPE, "bn_apply: too many pixels");
+  if (vec_ok(d->dtype, d->C, d->z, d->z_cstride, d->z_coff) && vec_ok(d->dtype, d->C, d->y, d->y_cstride, d->y_coff) &&
+      vec_ok(d->dtype, d->C, d->residual, d->r_cstride, d->r_coff)) {
+    DISPATCH_T(d->dtype, hipLaunchKernelGGL(bn_apply_vec_kernel<T>, vec_grid(d->P, d->C, d->dtype), dim3(256),
+                                            0, (hipStream_t)stream, *d));
+    return hiseg_check_launch("bn_apply");
+  }
   DISPATCH_T(d->dtype, hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(ew_blocks(d->P * d->C)), dim3(256), 0,
                                           (hipStream_t)stream, *d));
   return hiseg_check_launch("bn_apply");
@@ -407,10 +672,21 @@ extern "C" int hiseg_bn_bwd(const hiseg_bn_bwd_desc* d, hiseg_stream_t stream) {
   HISEG_REQUIRE(d && d->dy && d->z && d->dz && d->mean && d->invstd && d->partial && d->P > 0 && d->C > 0 && d->HW > 0,
                 HISEG_ERR_BAD_ARG, "bn_bwd: bad arguments");
   HISEG_REQUIRE(d->act == HISEG_ACT_NONE || d->y, HISEG_ERR_BAD_ARG, "bn_bwd: activation needs y");
+  HISEG_REQUIRE(d->P < (1ll << 31), HISEG_ERR_BAD_SHAPE, "bn_bwd: too many pixels");
   hipStream_t s = (hipStream_t)stream;
   const int S = kBnSplits;
+  const int dt = d->dtype, C = d->C;
+  if (vec_ok(dt, C, d->dy, d->dy_cstride, d->dy_coff) && vec_ok(dt, C, d->y, d->y_cstride, d->y_coff) &&
+      vec_ok(dt, C, d->z, d->z_cstride, d->z_coff) && vec_ok(dt, C, d->dz, d->dz_cstride, d->dz_coff) &&
+      vec_ok(dt, C, d->dres, d->dres_cstride, d->dres_coff)) {
+    const int V = dt == HISEG_BF16 ? 8 : 4;
+    DISPATCH_T(dt, hipLaunchKernelGGL(bn_bwd_reduce_vec_kernel<T>, dim3(S, (C / V + 255) / 256), dim3(256), 0, s, *d));
+    hipLaunchKernelGGL(bn_bwd_finalize_par_kernel, dim3(C), dim3(256), 0, s, *d, S);
+    DISPATCH_T(dt, hipLaunchKernelGGL(bn_bwd_apply_vec_kernel<T>, vec_grid(d->P, C, dt), dim3(256), 0, s, *d, S));
+    return hiseg_check_launch("bn_bwd");
+  }
   DISPATCH_T(d->dtype, hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(S, (d->C + 255) / 256), dim3(256), 0, s, *d));
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((d->C + 63) / 64), dim3(64), 0, s, *d, S);
+  hipLaunchKernelGGL(bn_bwd_finalize_par_kernel, dim3(C), dim3(256), 0, s, *d, S);
   DISPATCH_T(d->dtype, hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(ew_blocks(d->P * d->C)), dim3(256), 0, s, *d, S));
   return hiseg_check_launch("bn_bwd");
 }
