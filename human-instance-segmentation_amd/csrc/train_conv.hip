@@ -13,6 +13,8 @@
 // forward kernel's.  Register-staged double buffering, one barrier per pixel block.
 // The pixel dimension is split across workgroups (split-K); every split writes its own f32
 // partial tile (deterministic, no atomics) and hiseg_conv2d_wgrad_reduce sums them.
+#include <cstdlib>
+
 #include "conv_common.h"
 #include "hiseg_train.h"
 
@@ -242,6 +244,220 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------ wgrad, bf16 fast path
+// Same GEMM, no register transposes: both operands go HBM -> LDS by LDS-DMA in their natural NHWC
+// orientation (rows = pixels, 128 bf16 = 256 B per row), and the MFMA fragments, which need 8
+// consecutive PIXELS per lane, are read with gfx950's transposing LDS read ds_read_b64_tr_b16
+// (cdna_hip_programming.md T10): per 16-lane group a 4-pixel x 16-column block arrives column-major,
+// two reads give one 16x16x32 operand.  Image layout (T10 (b)): chunk ch of row r at byte
+// 256 r + 16 (ch ^ (((r & 3) << 2) | ((r >> 2) & 3))) -- conflict-free for these transposed reads;
+// applied on the DMA source side (the DMA writes lane-linear).  Im2col halo and tails cost nothing:
+// an out-of-image tap or a pixel past M gets a voffset beyond the buffer range and the DMA writes 0.
+// STAGES-deep ring with counted vmcnt + raw s_barrier, as conv_fast.
+typedef short v4s_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s_t lds_v4s_t;
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+__device__ __forceinline__ unsigned trswz(int row, int ch) {
+  return 256u * (unsigned)row + 16u * (unsigned)(ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+__device__ __forceinline__ void wg_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned lds_addr, unsigned voff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :: "s"(lds_addr), "v"(voff), "s"(rsrc) : "memory");
+}
+
+__device__ __forceinline__ v4s_t tr_read(unsigned byte_addr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)(uintptr_t)byte_addr);
+}
+
+template <int BC, int WK, int WC, int STAGES>
+__global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
+  constexpr int BK = 128, PB = 64;
+  constexpr int TM = BK / (WK * 16), TN = BC / (WC * 16);
+  constexpr int IMG = PB * 256;            // bytes of one operand image
+  constexpr int STAGE = 2 * IMG;           // X image, then dY image
+  constexpr int NL = 8;                    // DMA instructions per wave per stage (4 X + 4 dY)
+  static_assert(WK * WC == 4 && TM >= 1 && TN >= 1, "tile");
+  extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+  const hiseg_conv2d_desc& d = a.d;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wk = w / WC, wc = w % WC;
+  const int k0 = blockIdx.x * BK, j0 = blockIdx.y * BC, split = blockIdx.z;
+  const int pb_begin = split * a.blocks_per_split;
+  const int nblocks = (a.M + PB - 1) / PB;
+  int pb_end = pb_begin + a.blocks_per_split;
+  if (pb_end > nblocks) pb_end = nblocks;
+  const int nit = pb_end > pb_begin ? pb_end - pb_begin : 0;
+
+  // K tile source (wave-uniform by eligibility: one source per 128-column tile)
+  const int ci_tile = k0 % a.Cin;
+  const bool fromA = d.Cb == 0 || ci_tile < d.Ca;
+  const int cs = fromA ? d.a_cstride : d.b_cstride;
+  const int coff = fromA ? d.a_coff : d.b_coff - d.Ca;
+  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(fromA ? d.srcA : d.srcB),
+                                                                       (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rY = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.dy), (short)0, 0x7fffffff,
+                                                                       0x00020000);
+  const unsigned OOB = 0x80000000u;
+
+  // per-lane DMA state: instruction i fills rows 4(w + 4i) .. +3; this lane row (lane >> 4), slot lane & 15
+  int xo[4], ky[4], kx[4], yo[4];       // X channel offset (or -1 = zero column), tap; dY column offset (or -1)
+  int pn[4], py[4], px[4], pp[4];       // pixel (n, oy, ox) and flat index of the lane's row
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 4 * (w + 4 * i) + (lane >> 4);
+    const int c = (lane & 15) ^ (((r & 3) << 2) | ((r >> 2) & 3));
+    const int k = k0 + 8 * c;
+    const int tap = k / a.Cin;
+    const int ci = k - tap * a.Cin;
+    xo[i] = k < a.Ktot ? coff + ci : -1;
+    ky[i] = tap / d.KW;
+    kx[i] = tap - ky[i] * d.KW;
+    const int j = j0 + 8 * c;
+    yo[i] = j < d.Cout ? a.dy_coff + j : -1;
+    const int p = pb_begin * PB + r;
+    pp[i] = p;
+    px[i] = p % d.Wo;
+    const int tt = p / d.Wo;
+    py[i] = tt % d.Ho;
+    pn[i] = tt / d.Ho;
+  }
+  const int adv_x = PB % d.Wo, adv_y = PB / d.Wo;
+  const unsigned lds_base = (unsigned)(uintptr_t)(lds_void_t*)smem;
+
+  auto issue = [&](int s) __attribute__((always_inline)) {
+    const unsigned sb = lds_base + (unsigned)(s * STAGE);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const unsigned row_base = 256u * (unsigned)(4 * (w + 4 * i));
+      const int iy = py[i] * d.stride - d.pad + ky[i];
+      const int ix = px[i] * d.stride - d.pad + kx[i];
+      const bool okx = xo[i] >= 0 && pp[i] < a.M && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+      const unsigned offx = okx ? (unsigned)((((pn[i] * d.H + iy) * d.W + ix) * cs + xo[i]) * 2) : OOB;
+      wg_dma16(rX, sb + row_base, offx);
+      const bool oky = yo[i] >= 0 && pp[i] < a.M;
+      const unsigned offy = oky ? (unsigned)((pp[i] * a.dy_cs + yo[i]) * 2) : OOB;
+      wg_dma16(rY, sb + IMG + row_base, offy);
+      // advance this row by PB pixels
+      pp[i] += PB;
+      px[i] += adv_x;
+      py[i] += adv_y;
+      if (px[i] >= d.Wo) { px[i] -= d.Wo; ++py[i]; }
+      while (py[i] >= d.Ho) { py[i] -= d.Ho; ++pn[i]; }
+    }
+  };
+
+  floatx4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read addressing: group g = lane >> 4 takes pixel rows 8g..8g+7 of a 32-pixel k-step;
+  // lane 4q+p of the group addresses row q, columns 4p..4p+3 of its 16-column block
+  const int g = lane >> 4, q = (lane & 15) >> 2, pq = lane & 3;
+
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nit) issue(s);
+
+  for (int it = 0; it < nit; ++it) {
+    if (it + STAGES - 2 < nit) {
+      if constexpr (STAGES == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if constexpr (STAGES == 3) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NL) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NL) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (it + STAGES - 1 < nit) issue((it + STAGES - 1) % STAGES);
+
+    const unsigned sX = lds_base + (unsigned)((it % STAGES) * STAGE);
+    const unsigned sY = sX + IMG;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int r0 = ks * 32 + 8 * g + q;
+      bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int ch = (wk * TM * 16 + i * 16) / 8 + (pq >> 1);
+        const v4s_t lo = tr_read(sX + trswz(r0, ch) + 8u * (pq & 1));
+        const v4s_t hi = tr_read(sX + trswz(r0 + 4, ch) + 8u * (pq & 1));
+        af[i] = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int ch = (wc * TN * 16 + j * 16) / 8 + (pq >> 1);
+        const v4s_t lo = tr_read(sY + trswz(r0, ch) + 8u * (pq & 1));
+        const v4s_t hi = tr_read(sY + trswz(r0 + 4, ch) + 8u * (pq & 1));
+        bfr[j] = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  float* ws = a.ws + (long long)split * a.Cg * a.Kg;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int k = k0 + wk * TM * 16 + i * 16 + (lane >> 4) * 4;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int jj = j0 + wc * TN * 16 + j * 16 + (lane & 15);
+      if (k < a.Kg && jj < a.Cg)
+        *reinterpret_cast<floatx4*>(ws + (long long)jj * a.Kg + k) = acc[i][j];
+    }
+  }
+}
+
+template <int BC, int WK, int WC, int STAGES>
+static int wgrad_tr_launch(const WgradArgs& a, hipStream_t s) {
+  const size_t lds = (size_t)STAGES * 2 * 64 * 256;
+  auto kern = conv_wgrad_tr_kernel<BC, WK, WC, STAGES>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  dim3 grid((a.Kg + 127) / 128, (a.Cg + BC - 1) / BC, a.splits);
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a);
+  return hiseg_check_launch("conv_wgrad_tr");
+}
+
+// developer knob: HISEG_WGRAD_TR=0 forces the register-transpose kernel
+static int wgrad_tr_mode() {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("HISEG_WGRAD_TR");
+    mode = e ? atoi(e) : 1;
+  }
+  return mode;
+}
+
+// 1 = launched, 0 = layer not eligible (caller uses the generic kernel)
+static int wgrad_tr_try(const WgradArgs& a, hipStream_t s) {
+  const hiseg_conv2d_desc& d = a.d;
+  if (!wgrad_tr_mode()) return 0;
+  if (d.dtype != HISEG_BF16 || d.convT || d.a_up != 1 || a.want_bias) return 0;
+  if (!(d.Cb == 0 || (d.Ca % 128 == 0 && d.Cb % 128 == 0))) return 0;
+  if (a.Cin % 8 || a.dy_cs % 8 || a.dy_coff % 8 || d.a_cstride % 8 || d.a_coff % 8) return 0;
+  if (d.Cb && (d.b_cstride % 8 || d.b_coff % 8)) return 0;
+  if (a.Cg < 64) return 0;
+  const long long span_a = (long long)d.N * d.H * d.W * d.a_cstride * 2;
+  const long long span_b = d.Cb ? (long long)d.N * d.H * d.W * d.b_cstride * 2 : 0;
+  const long long span_y = ((long long)a.M * a.dy_cs + a.dy_coff + a.Cg) * 2;
+  if (span_a >= 0x7fffffffll || span_b >= 0x7fffffffll || span_y >= 0x7fffffffll) return 0;
+  const int r = a.Cg >= 128 ? wgrad_tr_launch<128, 2, 2, 2>(a, s) : wgrad_tr_launch<64, 4, 1, 2>(a, s);
+  return r < 0 ? r : 1;
+}
+
 template <typename T, int BK, int BC, int WK, int WC>
 static int wgrad_launch(const WgradArgs& a, hipStream_t s) {
   constexpr int STAGE = (BK + BC) * 8;
@@ -313,6 +529,8 @@ extern "C" int hiseg_conv2d_wgrad(const hiseg_conv2d_desc* fwd, const void* dy, 
   a.splits = splits;
   a.ws = ws;
   hipStream_t s = (hipStream_t)stream;
+  const int rt = wgrad_tr_try(a, s);
+  if (rt != 0) return rt < 0 ? rt : HISEG_OK;
   return fwd->dtype == HISEG_BF16 ? wgrad_typed<bf16_t>(a, s) : wgrad_typed<float>(a, s);
 }
 
