@@ -396,9 +396,14 @@ def test_fused_adamw_matches_torch():
 
 
 # ------------------------------------------------------------------------------------------ whole model
-def _model(dt, p_drop_zero=True):
+def _kwargs(name="b0"):
+    from helpers import configs
+    return hiseg_kwargs(dict(configs()[name]["model_kwargs"]))
+
+
+def _model(dt, p_drop_zero=True, name="b0"):
     import hiseg
-    m = hiseg.create_rgb_hierarchical_model(**hiseg_kwargs(b0_kwargs()))
+    m = hiseg.create_rgb_hierarchical_model(**_kwargs(name))
     filler.fill_module(m)
     if p_drop_zero:
         for mod in m.modules():
@@ -408,8 +413,9 @@ def _model(dt, p_drop_zero=True):
     return m
 
 
-def test_train_step_f32_matches_oracle():
-    """B0-std train forward + RefinedHierarchicalLoss + backward in f32 against the CPU oracle (torch autograd
+@pytest.mark.parametrize("name", ["b0", "b1", "b7"])
+def test_train_step_f32_matches_oracle(name):
+    """B0-std (and the B1-enhanced 80x60 / B7-ultra 128x96, depth-4 presets) train forward + RefinedHierarchicalLoss + backward in f32 against the CPU oracle (torch autograd
     of the restated model, oracle/train.py) on the same inputs.  Loss and logits: 1e-4 relative.  Gradients:
     the ~50-layer train-mode BN stack at initialisation amplifies 1e-7 input changes into ~5 % gradient changes
     (tests/test_oracle_train.py), so parameter gradients are compared by cosine similarity (> 0.99 for every
@@ -417,10 +423,10 @@ def test_train_step_f32_matches_oracle():
     import hiseg
     from oracle import rgb_model as O
     from oracle import train as OT
-    m = _model(torch.float32)
+    m = _model(torch.float32, name=name)
     sd = OT.params_of(m)
     m = m.to(DEV).train()
-    cfg = O.cfg_from_kwargs(hiseg_kwargs(b0_kwargs()))
+    cfg = O.cfg_from_kwargs(_kwargs(name))
     images = torch.from_numpy(filler.uniform(61, (2, 3, 96, 128)))
     u = torch.from_numpy(filler.normal(62, (2, 1, 96, 128)) * 2.0)
     rois = torch.tensor([[0, .10, .10, .40, .90], [1, .35, .15, .80, .95], [0, .55, .05, .95, .70]])
