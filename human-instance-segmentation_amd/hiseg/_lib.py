@@ -118,6 +118,15 @@ class LossCfg(ctypes.Structure):
                                      "contour_ks")]
 
 
+class DistillCfg(ctypes.Structure):
+    """include/hiseg_distill.h hiseg_distill_cfg"""
+    _fields_ = [(n, c_float) for n in ("temperature", "kl_weight", "task_weight", "pos_weight")] + \
+               [(n, c_int) for n in ("distill_terms", "distill_in_total", "use_dice", "has_target")]
+
+
+DISTILL_NOUT = 5  # include/hiseg_distill.h HISEG_DISTILL_NOUT
+
+
 class HisegError(RuntimeError):
     """Raised when a libhiseg entry point returns a non-zero status."""
 
@@ -192,6 +201,9 @@ def _declare(lib):
         "hiseg_loss_fwd": ([ctypes.POINTER(LossCfg), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P], c_int),
         "hiseg_loss_bwd": ([ctypes.POINTER(LossCfg), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
                            c_int),
+        "hiseg_distill_ws": ([c_int, c_int, c_int], c_ll),
+        "hiseg_distill_loss_fwd": ([ctypes.POINTER(DistillCfg), c_int, c_int, c_int, P, P, P, P, P, P], c_int),
+        "hiseg_distill_loss_bwd": ([ctypes.POINTER(DistillCfg), c_int, c_int, c_int, P, P, P, P, P, P, P], c_int),
         "hiseg_optim_blocks": ([], c_int),
         "hiseg_grad_norm_partials": ([P, c_ll, P, P], c_int),
         "hiseg_adamw_step": ([P, P, P, P, c_ll, c_float, c_float, c_float, c_float, c_float, c_float, c_float, P,

@@ -1,0 +1,183 @@
+"""B7 -> B0 UNet knowledge distillation on libhiseg (advanced/unet_decoder_distillation.py,
+train_distillation_staged.py).
+
+Same surface as the reference module: ``UNetDistillationLoss`` (temperature schedule, adaptive
+distillation weight, ``forward(student, teacher, masks) -> (total, loss_dict)``), ``UNetDecoderOnly``,
+``DistillationUNetWrapper`` (student + frozen teacher, progressive encoder unfreezing) and
+``create_unet_distillation_model``.  The loss terms, reductions and the gradient run as HIP kernels
+(include/hiseg_distill.h); the schedule state stays on the host exactly as in the reference (it is
+updated once per epoch), and ``loss_dict`` is materialised lazily (one device->host copy on first
+access instead of the reference's five ``.item()`` calls).  NaN/Inf fallbacks of the reference
+(:540-548, :640-650) are not reproduced: the kernels clamp exactly as the reference does, so a
+non-finite value can only come from non-finite logits.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from collections.abc import Mapping
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _lib as L
+
+_DICT_KEYS = ("total_loss", "kl_loss", "mse_loss", "bce_loss", "dice_loss")
+
+
+class _LazyDict(Mapping):
+    def __init__(self, out: torch.Tensor, keys):
+        self._out, self._keys, self._vals = out, keys, None
+
+    def _get(self):
+        if self._vals is None:
+            host = self._out.detach().cpu().tolist()
+            self._vals = {k: float(host[i]) for i, k in enumerate(_DICT_KEYS) if k in self._keys}
+        return self._vals
+
+    def __getitem__(self, k):
+        return self._get()[k]
+
+    def __iter__(self):
+        return iter(self._get())
+
+    def __len__(self):
+        return len(self._get())
+
+    def get(self, k, default=None):
+        return self._get().get(k, default)
+
+
+class _DistillLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cfg, student, teacher, target):
+        lib = L.lib()
+        B, _, H, W = student.shape
+        dev = student.device
+        ws = torch.empty(int(lib.hiseg_distill_ws(B, H, W)), dtype=torch.float32, device=dev)
+        out = torch.empty(L.DISTILL_NOUT, dtype=torch.float32, device=dev)
+        L.check(lib.hiseg_distill_loss_fwd(ctypes.byref(cfg), B, H, W, student.data_ptr(), teacher.data_ptr(),
+                                           target.data_ptr() if target is not None else None, ws.data_ptr(),
+                                           out.data_ptr(), L.stream_ptr()), "distill_loss_fwd")
+        ctx.cfg = cfg
+        ctx.save_for_backward(student, teacher, target, ws)
+        ctx.mark_non_differentiable(out)
+        return out[0].clone(), out
+
+    @staticmethod
+    def backward(ctx, g_total, _g_out):
+        student, teacher, target, ws = ctx.saved_tensors
+        B, _, H, W = student.shape
+        ds = torch.empty_like(student)
+        g = g_total.contiguous().float()
+        L.check(L.lib().hiseg_distill_loss_bwd(ctypes.byref(ctx.cfg), B, H, W, student.data_ptr(), teacher.data_ptr(),
+                                               target.data_ptr() if target is not None else None, ws.data_ptr(),
+                                               g.data_ptr(), ds.data_ptr(), L.stream_ptr()), "distill_loss_bwd")
+        return None, ds, None, None
+
+
+class UNetDistillationLoss(nn.Module):
+    """unet_decoder_distillation.py:338-663 (constructor arguments and state as the reference)."""
+
+    def __init__(self, temperature: float = 3.0, alpha: float = 0.5, task_weight: float = 0.3,
+                 use_feature_matching: bool = False, fg_ratio: float = 0.162, use_dice_loss: bool = True,
+                 adaptive_distillation: bool = True):
+        super().__init__()
+        if use_feature_matching:
+            raise NotImplementedError("feature matching is not used by the distillation configs (SURVEY §8a D2)")
+        self.temperature = temperature
+        self.initial_temperature = temperature
+        self.alpha = alpha
+        self.initial_alpha = alpha
+        self.task_weight = task_weight
+        self.initial_task_weight = task_weight
+        self.use_feature_matching = use_feature_matching
+        self.use_dice_loss = use_dice_loss
+        self.adaptive_distillation = adaptive_distillation
+        self.performance_ratio = 1.0
+        self.distillation_eliminated = False
+        self.pos_weight_value = float(np.sqrt((1.0 - fg_ratio) / fg_ratio))
+
+    # -- schedules (host state, once per epoch: :366-469)
+    def update_temperature(self, current_epoch: int, total_epochs: int, final_temperature: float = 1.0,
+                           schedule_type: str = "linear") -> float:
+        if total_epochs <= 1:
+            self.temperature = final_temperature
+            return self.temperature
+        progress = current_epoch / (total_epochs - 1)
+        if schedule_type == "linear":
+            self.temperature = self.initial_temperature + (final_temperature - self.initial_temperature) * progress
+        elif schedule_type == "cosine":
+            f = 0.5 * (1 + math.cos(math.pi * progress))
+            self.temperature = final_temperature + (self.initial_temperature - final_temperature) * f
+        elif schedule_type == "exponential":
+            rate = math.log(final_temperature / self.initial_temperature)
+            self.temperature = self.initial_temperature * math.exp(rate * progress)
+        return self.temperature
+
+    def get_temperature(self) -> float:
+        return self.temperature
+
+    def update_distillation_weight(self, student_iou: float, teacher_iou: float, min_alpha: float = 0.0,
+                                   amplification_factor: float = 20.0,
+                                   zero_distillation_threshold: float = 0.03) -> float:
+        if not self.adaptive_distillation:
+            return self.alpha
+        if self.distillation_eliminated:
+            self.alpha, self.task_weight = 0.0, 1.0
+            return self.alpha
+        self.performance_ratio = student_iou / (teacher_iou + 1e-6)
+        if self.performance_ratio > 1.0 + zero_distillation_threshold:
+            self.alpha, self.task_weight = 0.0, 1.0
+            self.distillation_eliminated = True
+        elif self.performance_ratio > 1.0:
+            diff = (self.performance_ratio - 1.0) * amplification_factor
+            self.alpha = max(0.0, self.initial_alpha * np.exp(-diff))
+            target = 1.0 - np.exp(-diff * 2)
+            self.task_weight = min(1.0, self.initial_task_weight + (1.0 - self.initial_task_weight) * target)
+        else:
+            self.alpha, self.task_weight = self.initial_alpha, self.initial_task_weight
+        return self.alpha
+
+    # -- the reference's control flow (:510-663) reduced to the kernel configuration
+    def _cfg(self, has_target: bool) -> L.DistillCfg:
+        c = L.DistillCfg()
+        disabled = ((self.adaptive_distillation and self.alpha == 0.0) or self.task_weight >= 0.99
+                    or self.distillation_eliminated)
+        in_total = not ((self.adaptive_distillation and self.alpha == 0.0) or self.task_weight >= 0.99)
+        if self.adaptive_distillation and self.performance_ratio > 1.0:
+            eff_alpha = self.alpha * max(0.1, 2.0 - self.performance_ratio)
+        else:
+            eff_alpha = self.alpha
+        c.temperature = float(self.temperature)
+        c.kl_weight = float(min(eff_alpha, 0.1))
+        c.task_weight = float(self.task_weight)
+        c.pos_weight = self.pos_weight_value
+        c.distill_terms = int(not disabled)
+        c.distill_in_total = int(in_total)
+        c.use_dice = int(self.use_dice_loss)
+        c.has_target = int(has_target)
+        return c
+
+    def forward(self, student_output: torch.Tensor, teacher_output: torch.Tensor,
+                target_masks: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Dict[str, float]]:
+        if not student_output.is_cuda:
+            raise RuntimeError("hiseg UNetDistillationLoss runs on the GPU (libhiseg); got a CPU tensor")
+        s = student_output.float().contiguous()
+        t = teacher_output.detach().float().contiguous()
+        y = target_masks.float().contiguous() if target_masks is not None else None
+        if s.dim() != 4 or s.shape[1] != 1 or t.shape != s.shape or (y is not None and y.numel() != s.numel()):
+            raise ValueError(f"distillation loss: student {tuple(s.shape)} teacher {tuple(t.shape)} "
+                             f"target {None if y is None else tuple(y.shape)} (expect [B,1,H,W])")
+        total, out = _DistillLossFn.apply(self._cfg(y is not None), s, t, y)
+        return total, _LazyDict(out, _DICT_KEYS)
+
+    def dice_loss(self, pred: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+        """:471-508 (standalone helper; the forward computes it inside the fused kernels)."""
+        c = self._cfg(True)
+        c.distill_terms, c.distill_in_total, c.use_dice, c.task_weight = 0, 0, 1, 1.0
+        s = pred.float().contiguous()
+        _, out = _DistillLossFn.apply(c, s, torch.zeros_like(s), target.float().contiguous())
+        return out[4]
