@@ -587,6 +587,41 @@ __global__ void __launch_bounds__(256) resize_bwd_kernel(const float* dy, int NC
   }
 }
 
+// dx (+)= 2x2 sum of dy (nearest-x2 upsample backward), one 16-B chunk per thread
+template <typename T>
+__global__ void __launch_bounds__(256) up2_bwd_kernel(long long N, int h, int w, int C, hiseg_ew_view dy,
+                                                      hiseg_ew_view dx, int accumulate) {
+  constexpr int V = Chunk<T>::N;
+  const int nch = C / V;
+  const long long n_el = N * h * w * nch;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n_el; i += (long long)gridDim.x * 256) {
+    const int ch = (int)(i % nch);
+    const long long q = i / nch;            // low-res pixel
+    const int x = (int)(q % w);
+    const long long r = q / w;
+    const int y = (int)(r % h);
+    const long long n = r / h;
+    float acc[V], v[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) acc[k] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long long fp = (n * 2 * h + 2 * y + (j >> 1)) * (2 * w) + 2 * x + (j & 1);
+      Chunk<T>::unpack(*reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(dy.p) + fp * dy.cstride + dy.coff +
+                                                       ch * V), v);
+#pragma unroll
+      for (int k = 0; k < V; ++k) acc[k] += v[k];
+    }
+    T* dst = reinterpret_cast<T*>(dx.p) + q * dx.cstride + dx.coff + ch * V;
+    if (accumulate) {
+      Chunk<T>::unpack(*reinterpret_cast<const uint4*>(dst), v);
+#pragma unroll
+      for (int k = 0; k < V; ++k) acc[k] += v[k];
+    }
+    *reinterpret_cast<uint4*>(dst) = Chunk<T>::pack(acc);
+  }
+}
+
 inline unsigned ew_blocks(long long n) {
   long long b = (n + 255) / 256;
   return (unsigned)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
@@ -754,6 +789,17 @@ extern "C" int hiseg_maxpool2x2_bwd(int dtype, const void* x, int N, int H, int 
   DISPATCH_T(dtype, hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(ew_blocks((long long)N * H * W * C / 4)), dim3(256),
                                        0, (hipStream_t)stream, x, N, H, W, C, dy, dx, accumulate));
   return hiseg_check_launch("maxpool2x2_bwd");
+}
+
+extern "C" int hiseg_upsample2x_bwd(int dtype, long long N, int h, int w, int C, hiseg_ew_view dy, hiseg_ew_view dx,
+                                    int accumulate, hiseg_stream_t stream) {
+  HISEG_REQUIRE(dy.p && dx.p && N > 0 && h > 0 && w > 0 && C > 0, HISEG_ERR_BAD_ARG, "upsample2x_bwd: bad arguments");
+  HISEG_REQUIRE(vec_ok(dtype, C, dy.p, dy.cstride, dy.coff) && vec_ok(dtype, C, dx.p, dx.cstride, dx.coff),
+                HISEG_ERR_BAD_SHAPE, "upsample2x_bwd: channels/strides must be whole 16-B chunks");
+  const long long n = N * h * w * (C / (dtype == HISEG_BF16 ? 8 : 4));
+  DISPATCH_T(dtype, hipLaunchKernelGGL(up2_bwd_kernel<T>, dim3(ew_blocks(n)), dim3(256), 0, (hipStream_t)stream, N, h, w,
+                                       C, dy, dx, accumulate));
+  return hiseg_check_launch("upsample2x_bwd");
 }
 
 extern "C" int hiseg_resize_bilinear_bwd(const float* dy, int NC, int h, int w, int H, int W, float* dx,

@@ -16,7 +16,8 @@ from .model import (  # noqa: F401
 
 from .losses import RefinedHierarchicalLoss  # noqa: F401,E402
 from .optim import FusedAdamW, cosine_lr  # noqa: F401,E402
-from .distill import UNetDistillationLoss  # noqa: F401,E402
+from .distill import (  # noqa: F401,E402
+    DistillationUNetWrapper, UNetDecoderOnly, UNetDistillationLoss, create_unet_distillation_model)
 
 __version__ = "0.2.0"
 

@@ -181,6 +181,7 @@ def _declare(lib):
         "hiseg_act_bwd_cvt": ([c_int, c_ll, c_int, EwView, EwView, c_int, EwView, c_int, P], c_int),
         "hiseg_maxpool2x2_bwd": ([c_int, P, c_int, c_int, c_int, c_int, P, P, c_int, P], c_int),
         "hiseg_resize_bilinear_bwd": ([P, c_int, c_int, c_int, c_int, c_int, P, P], c_int),
+        "hiseg_upsample2x_bwd": ([c_int, c_ll, c_int, c_int, c_int, EwView, EwView, c_int, P], c_int),
         "hiseg_attn_spatial_train_fwd": ([c_int, P, c_int, c_int, c_int, c_int, P, c_int, P, P, P, P, P, P], c_int),
         "hiseg_attn_spatial_ws": ([c_int, c_int, c_int, c_int], c_int),
         "hiseg_attn_spatial_bwd": ([c_int, P, c_int, c_int, c_int, c_int, P, c_int, P, P, P, P, P, P, P, P, P], c_int),

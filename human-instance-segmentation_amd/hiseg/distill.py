@@ -181,3 +181,161 @@ class UNetDistillationLoss(nn.Module):
         s = pred.float().contiguous()
         _, out = _DistillLossFn.apply(c, s, torch.zeros_like(s), target.float().contiguous())
         return out[4]
+
+
+# ======================================================================================= models
+def _safe_state_dict(path: str) -> Dict[str, torch.Tensor]:
+    """Checkpoint tensors through the non-executing loader (weights_only=True) and the reference's key
+    handling (:173-195): 'state_dict' / 'model_state_dict' wrappers, 'model.' / 'unet.' prefixes."""
+    ck = torch.load(path, map_location="cpu", weights_only=True)
+    sd = ck.get("state_dict", ck.get("model_state_dict", ck)) if isinstance(ck, dict) else ck
+    out = {}
+    for k, v in sd.items():
+        nk = k.replace("model.", "") if k.startswith("model.") else k
+        nk = nk.replace("unet.", "") if nk.startswith("unet.") else nk
+        if any(part in nk for part in ("encoder", "decoder", "segmentation_head")):
+            out[nk] = v
+    return out
+
+
+class UNetDecoderOnly(nn.Module):
+    """advanced/unet_decoder_distillation.py:17-82: the smp-UNet student (``self.unet``), encoder frozen on
+    request.  Train mode runs the HIP training path (hiseg.effunet_train); eval runs the inference kernels."""
+
+    def __init__(self, encoder_name: str = "timm-efficientnet-b0", encoder_weights: Optional[str] = None,
+                 freeze_encoder: bool = True, freeze_decoder: bool = False):
+        super().__init__()
+        from .effunet import EfficientNetUnet
+        if encoder_weights is not None:
+            # the reference downloads ImageNet weights here (encoder_weights="imagenet"); no network on this
+            # path -- load a checkpoint through student_pretrained_path / load_state_dict instead
+            encoder_weights = None
+        self.unet = EfficientNetUnet(encoder_name=encoder_name, classes=1, encoder_weights=encoder_weights)
+        if freeze_encoder:
+            for p in self.unet.encoder.parameters():
+                p.requires_grad = False
+        if freeze_decoder:
+            for p in self.unet.decoder.parameters():
+                p.requires_grad = False
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        from . import engine as EG
+        if self.training:
+            from .effunet_train import student_train_forward
+            return student_train_forward(self, self.unet, x)
+        with torch.no_grad():
+            E = EG.Ctx(self.unet, EG._root_dtype(self), x.device)
+            from .ops import Act
+            return EG.effunet_forward(E, self.unet, Act.from_nchw(x.contiguous().float(), E.dtype))
+
+    def get_decoder_parameters(self):
+        return self.unet.decoder.parameters()
+
+    @property
+    def encoder(self):
+        return self.unet.encoder
+
+
+class _FrozenUnet(nn.Module):
+    """Teacher smp.Unet in eval mode on the inference kernels (no gradients)."""
+
+    def __init__(self, encoder_name: str):
+        super().__init__()
+        from .effunet import EfficientNetUnet
+        self.unet = EfficientNetUnet(encoder_name=encoder_name, classes=1)
+
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        from . import engine as EG
+        from .ops import Act
+        E = EG.Ctx(self.unet, EG._root_dtype(self), x.device)
+        return EG.effunet_forward(E, self.unet, Act.from_nchw(x.contiguous().float(), E.dtype))
+
+
+class DistillationUNetWrapper(nn.Module):
+    """advanced/unet_decoder_distillation.py:85-330: student + frozen teacher, progressive unfreezing."""
+
+    def __init__(self, student_encoder: str = "timm-efficientnet-b0", teacher_encoder: str = "timm-efficientnet-b3",
+                 teacher_checkpoint_path: Optional[str] = "ext_extractor/2020-09-23a.pth", freeze_teacher: bool = True,
+                 progressive_unfreeze: bool = False, student_pretrained_path: Optional[str] = None):
+        super().__init__()
+        import os
+        self.progressive_unfreeze = progressive_unfreeze
+        self.student_encoder_name = student_encoder
+        self.student = UNetDecoderOnly(encoder_name=student_encoder, freeze_encoder=progressive_unfreeze,
+                                       freeze_decoder=False)
+        if student_pretrained_path and os.path.exists(student_pretrained_path):
+            ck = torch.load(student_pretrained_path, map_location="cpu", weights_only=True)
+            sd = ck.get("model_state_dict", ck.get("state_dict", ck)) if isinstance(ck, dict) else ck
+            self.student.load_state_dict(sd, strict=False)
+        if teacher_checkpoint_path is not None and teacher_checkpoint_path != "":
+            self.teacher = _FrozenUnet(teacher_encoder)
+            if os.path.exists(teacher_checkpoint_path):
+                self.teacher.unet.load_state_dict(_safe_state_dict(teacher_checkpoint_path), strict=False)
+            if freeze_teacher:
+                for p in self.teacher.parameters():
+                    p.requires_grad = False
+            self.teacher.eval()
+        else:
+            self.teacher = None
+        if self.progressive_unfreeze:
+            self._setup_encoder_blocks()
+
+    def _setup_encoder_blocks(self):
+        self.encoder_blocks = [(f"block_{i}", b) for i, b in enumerate(self.student.encoder.blocks)]
+
+    def unfreeze_encoder_blocks(self, num_blocks: int, learning_rate_scale: float = 0.1):
+        """:233-274 -- the deepest ``num_blocks`` encoder stages become trainable; returns their parameters."""
+        if not self.progressive_unfreeze:
+            return []
+        for p in self.student.encoder.parameters():
+            p.requires_grad = False
+        params = []
+        start = max(0, len(self.encoder_blocks) - num_blocks)
+        for i in range(start, len(self.encoder_blocks)):
+            for p in self.encoder_blocks[i][1].parameters():
+                p.requires_grad = True
+                params.append(p)
+        return params
+
+    def get_progressive_unfreeze_schedule(self, total_epochs: int, unfreeze_start_epoch: int = 10,
+                                          unfreeze_rate: int = 5):
+        """:276-302"""
+        max_blocks = len(self.encoder_blocks) if hasattr(self, "encoder_blocks") else 7
+        return {e: 0 if e < unfreeze_start_epoch else min(1 + (e - unfreeze_start_epoch) // unfreeze_rate, max_blocks)
+                for e in range(total_epochs)}
+
+    def train(self, mode: bool = True):
+        super().train(mode)
+        if self.teacher is not None:
+            self.teacher.eval()   # the teacher always runs in eval mode (train_distillation_staged.py:270-271)
+        return self
+
+    def forward(self, x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        s = self.student(x)
+        if self.teacher is not None:
+            t = self.teacher(x)
+        else:
+            t = torch.zeros_like(s)
+        return s, t
+
+
+def create_unet_distillation_model(student_encoder: str = "timm-efficientnet-b0",
+                                   teacher_encoder: str = "timm-efficientnet-b3",
+                                   teacher_checkpoint: Optional[str] = "ext_extractor/2020-09-23a.pth",
+                                   device: str = "cuda", progressive_unfreeze: bool = False,
+                                   adaptive_distillation: bool = True, amplification_factor: float = 20.0,
+                                   min_alpha: float = 0.001, student_pretrained_path: Optional[str] = None
+                                   ) -> Tuple[nn.Module, nn.Module]:
+    """:665-720 -- (wrapper, loss) with the reference's loss settings for distillation / pure fine-tuning."""
+    model = DistillationUNetWrapper(student_encoder=student_encoder, teacher_encoder=teacher_encoder,
+                                    teacher_checkpoint_path=teacher_checkpoint, freeze_teacher=True,
+                                    progressive_unfreeze=progressive_unfreeze,
+                                    student_pretrained_path=student_pretrained_path).to(device)
+    if teacher_checkpoint is None or teacher_checkpoint == "":
+        loss = UNetDistillationLoss(temperature=1.0, alpha=0.0, task_weight=1.0, use_dice_loss=True,
+                                    adaptive_distillation=False)
+    else:
+        loss = UNetDistillationLoss(temperature=1.0, alpha=0.05, task_weight=0.7, use_dice_loss=True,
+                                    adaptive_distillation=adaptive_distillation)
+    return model, loss

@@ -1,0 +1,182 @@
+"""Train-mode execution of the smp-UNet student of the distillation path on libhiseg.
+
+The reference trains ``smp.Unet('timm-efficientnet-b0')`` in train mode (train_distillation_staged.py
+:256-366 with ``model.student.train()``): every BatchNorm of the student -- the frozen encoder's
+included -- normalises with batch statistics and updates its running buffers, while only the decoder
+(``unet.decoder``) and, after progressive unfreezing, the deepest encoder stages receive gradients.
+
+Here the encoder runs as a forward-only chain of raw convolutions (the inference kernels with no BN
+folded: stem conv, 1x1 expand/project convs, depthwise convs, SE gate fused into the projection
+loader) each followed by the train-mode BatchNorm kernels of hiseg.train_engine (batch statistics,
+running-stat update, SiLU / residual in the apply pass).  The decoder blocks (nearest-x2 upsample
+fused into conv1's loader, skip concatenation as the conv's second source, conv-BN-ReLU x 2) and the
+segmentation head record a tape exactly like the ROI path (hiseg.train_engine) and run the
+hand-written backward: BN backward, transposed-read MFMA weight gradients, and the data gradient
+through the upsample (dgrad conv at full resolution + 2x2 sum, hiseg_upsample2x_bwd).  The whole
+student is one autograd node; its parameter gradients land in the flat gradient buffer.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+
+from . import _lib as L
+from . import engine as EG
+from . import ops
+from . import train_engine as TE
+from .effunet import DepthwiseSeparableConv, InvertedResidual
+from .ops import Act, hdtype, round_up
+
+ACT_NONE, ACT_RELU, ACT_SILU = L.ACT_NONE, L.ACT_RELU, L.ACT_SILU
+
+
+# ======================================================================================= frozen encoder
+def _bn(T: TE.Tape, bn: nn.BatchNorm2d, z: Act, act: int, residual: Optional[Act] = None) -> Act:
+    y, _ = TE.bn_forward(T, bn, z, act=act, residual=residual)
+    return y
+
+
+def _mbconv(E: EG.Ctx, T: TE.Tape, blk: nn.Module, x: Act) -> Act:
+    """timm DepthwiseSeparableConv / InvertedResidual in train mode (forward only: frozen stage)."""
+    res = x if blk.has_skip else None
+    if isinstance(blk, DepthwiseSeparableConv):
+        h = _bn(T, blk.bn1, EG._dw(E, blk.conv_dw, None, x, ACT_NONE), ACT_SILU)
+        g = EG._se(E, blk.se, h)
+        return _bn(T, blk.bn2, ops.conv2d(E.conv(blk.conv_pw), h, in_scale=g), ACT_NONE, res)
+    if isinstance(blk, InvertedResidual):
+        h = _bn(T, blk.bn1, ops.conv2d(E.conv(blk.conv_pw), x), ACT_SILU)
+        h = _bn(T, blk.bn2, EG._dw(E, blk.conv_dw, None, h, ACT_NONE), ACT_SILU)
+        g = EG._se(E, blk.se, h)
+        return _bn(T, blk.bn3, ops.conv2d(E.conv(blk.conv_pwl), h, in_scale=g), ACT_NONE, res)
+    raise TypeError(type(blk))
+
+
+def encoder_features(E: EG.Ctx, T: TE.Tape, enc: nn.Module, x: Act) -> List[Act]:
+    """smp encoder taps (stride 2, 4, 8, 16, 32) of a frozen EfficientNet encoder in train mode."""
+    if any(p.requires_grad for p in enc.parameters()):
+        raise NotImplementedError("hiseg distillation: encoder stages with trainable parameters (progressive "
+                                  "unfreezing past the decoder-only phase) are not on the HIP training path yet")
+    x = _bn(T, enc.bn1, ops.conv2d(E.conv(enc.conv_stem), x), ACT_SILU)
+    feats = [x]
+    for si, stage in enumerate(enc.blocks):
+        for blk in stage:
+            x = _mbconv(E, T, blk, x)
+        if si + 1 in (2, 3, 5, 7):
+            feats.append(x)
+    return feats
+
+
+# ======================================================================================= trainable decoder
+def up_conv_bn_relu(T: TE.Tape, conv: nn.Conv2d, bn: nn.BatchNorm2d, x_low: Act, skip: Optional[Act],
+                    need_dx: bool) -> Act:
+    """DecoderBlock.conv1: Conv2dReLU over cat(upsample2x(x_low), skip) with the upsample fused into the
+    conv loader (a_up = 2); backward: BN bwd, wgrad, and (need_dx) dgrad + 2x2 sum into x_low's gradient."""
+    S, lib = T.S, L.lib()
+    split = (x_low.C, skip.C) if skip is not None else None
+    p = S.conv(conv, split=split)
+    H, W = 2 * x_low.H, 2 * x_low.W
+    dev = x_low.t.device
+    z = Act.new(x_low.N, H, W, p.cout, x_low.dtype, dev)
+    d = TE._desc(S, p, x_low, skip, z)
+    d.H, d.W, d.Ho, d.Wo, d.a_up = H, W, H, W, 2
+    TE._chk(lib.hiseg_conv2d_fwd(ctypes.byref(d), TE._stream()), "conv2d(decoder)")
+    y, st = TE.bn_forward(T, bn, z, act=ACT_RELU)
+    T.keep.extend([x_low, skip])   # the weight gradient re-reads both sources through d's raw pointers
+
+    def back():
+        dz = Act.new(z.N, z.H, z.W, z.C, z.dtype, dev, cpad=z.cstride, zero=z.cstride != z.C)
+        TE.bn_backward(T, bn, z, y, st, dz, act=ACT_RELU)
+        if TE._needs_wgrad(p):
+            TE.conv_wgrad(T, p, d, dz, bias_from_gemm=False)
+        if not need_dx:
+            return
+        dg = L.Conv2dDesc()
+        dg.dtype = dg.out_dtype = hdtype(dz.dtype)
+        dg.N, dg.H, dg.W, dg.Ho, dg.Wo = dz.N, H, W, H, W
+        dg.KH, dg.KW, dg.stride, dg.pad = p.kh, p.kw, 1, p.kh - 1 - p.pad
+        dg.srcA, dg.a_cstride, dg.a_coff, dg.Ca, dg.a_up = dz.ptr(), dz.cstride, dz.coff, p.cop, 1
+        # rows 0..ca-1 of the packed dgrad weights are the upsampled source's input channels
+        dg.weight, dg.Cout, dg.Cout_pad, dg.K_pad = p.w_dgrad.data_ptr(), p.ca, round_up(p.ca, 16), p.dg_k_pad
+        ones = torch.ones(round_up(p.ca, 16), dtype=torch.float32, device=dev)
+        zeros = torch.zeros_like(ones)
+        dg.scale, dg.shift, dg.act = ones.data_ptr(), zeros.data_ptr(), ACT_NONE
+        full = Act.new(z.N, H, W, p.ca, dz.dtype, dev, cpad=p.ca, zero=False)
+        dg.out, dg.o_cstride, dg.o_coff = full.ptr(), full.cstride, 0
+        TE._chk(TE._dgrad_launch(dg), "conv2d(decoder dgrad)")
+        gx, acc = T.grad(x_low)
+        TE._chk(lib.hiseg_upsample2x_bwd(hdtype(dz.dtype), x_low.N, x_low.H, x_low.W, p.ca, TE.ew(full), TE.ew(gx),
+                                         int(acc), TE._stream()), "upsample2x_bwd")
+        T.mark(x_low)
+        T.keep.extend([ones, zeros])
+    T.push(back)
+    return y
+
+
+def decoder_head(T: TE.Tape, net: nn.Module, feats: List[Act]) -> Act:
+    """UnetDecoder (5 DecoderBlocks) + SegmentationHead conv; returns the f32 logit Act [B,H,W,1]."""
+    skips = feats[-2::-1]
+    x = feats[-1]
+    for i, blk in enumerate(net.decoder.blocks):
+        skip = skips[i] if i < len(skips) else None
+        x = up_conv_bn_relu(T, blk.conv1[0], blk.conv1[1], x, skip, need_dx=i > 0)
+        x = TE.conv_bn_act(T, blk.conv2[0], blk.conv2[1], ACT_RELU, x)
+    u = Act.new(x.N, x.H, x.W, 1, torch.float32, x.t.device, cpad=1, zero=False)
+    TE.conv_plain(T, net.segmentation_head[0], ACT_NONE, x, out=u)
+    return u
+
+
+# ======================================================================================= autograd boundary
+class _StudentFunction(torch.autograd.Function):
+    """The student forward (frozen encoder + decoder + head) as one autograd node; parameter gradients are
+    written into the FlatParams buffer by the backward kernels (the node returns None for them)."""
+
+    @staticmethod
+    def forward(ctx, handle, x, *params):
+        net, S, E = handle["net"], handle["state"], handle["enc_ctx"]
+        T = TE.Tape(S)
+        S.pack()
+        xa = Act.from_nchw(x, S.dtype)
+        feats = encoder_features(E, T, net.encoder, xa)
+        u = decoder_head(T, net, feats)
+        ctx.tape, ctx.state, ctx.u = T, S, u
+        return u.t.view(u.N, 1, u.H, u.W)
+
+    @staticmethod
+    def backward(ctx, g):
+        T, S, u = ctx.tape, ctx.state, ctx.u
+        S.flat.prepare_backward()
+        gt = g.contiguous().float()
+        T.grads[id(u)] = Act(gt.view(-1), u.N, u.H, u.W, 1, 1, 0)
+        T.mark(u)
+        T.keep.append(gt)
+        T.run_backward()
+        return (None, None) + tuple(None for _ in range(len(ctx.needs_input_grad) - 2))
+
+
+def _trainable_key(module: nn.Module):
+    return tuple(id(p) for p in module.parameters() if p.requires_grad)
+
+
+def student_train_forward(owner: nn.Module, net: nn.Module, x: torch.Tensor) -> torch.Tensor:
+    """Train-mode forward of an EfficientNetUnet ``net`` owned by ``owner`` (UNetDecoderOnly): logits
+    [B,1,H,W] f32, differentiable w.r.t. the trainable parameters through the HIP backward."""
+    if not x.is_cuda:
+        raise RuntimeError("hiseg student training runs on the GPU (libhiseg); got a CPU tensor")
+    B, C, H, W = x.shape
+    if C != 3 or H % 32 or W % 32:
+        raise ValueError(f"student input must be [B,3,H,W] with H, W multiples of 32, got {tuple(x.shape)}")
+    dtype = EG._root_dtype(owner)
+    key = _trainable_key(owner)
+    S = owner.__dict__.get("_hiseg_train")
+    if S is None or S.dtype != dtype or S.device != x.device or owner.__dict__.get("_hiseg_train_key") != key:
+        S = TE.TrainState(owner, dtype, x.device)
+        owner.__dict__["_hiseg_train"] = S
+        owner.__dict__["_hiseg_train_key"] = key
+    S.sync = owner.__dict__.get("_hiseg_grad_sync")
+    E = EG.Ctx(net.encoder, dtype, x.device)
+    handle = {"net": net, "state": S, "enc_ctx": E}
+    params = [p for _, p in S.flat.named]
+    return _StudentFunction.apply(handle, x.contiguous().float(), *params)

@@ -302,11 +302,16 @@ def mbconv(E: Ctx, blk: nn.Module, x: Act) -> Act:
 
 def unet_logit(E: Ctx, pre: nn.Module, images: torch.Tensor) -> torch.Tensor:
     """PreTrainedPeopleSegmentationUNet.forward (unet.py:1901-1916): normalise, smp.Unet -> u [B,1,H,W] f32."""
-    net = pre.model
     B, _, H, W = images.shape
     if H % 32 or W % 32:
         raise NotImplementedError(f"image size {H}x{W} must be a multiple of 32 for the EfficientNet-UNet")
     x = ops.input_norm(images, E.f32(pre.norm_mean, (3,)), E.f32(pre.norm_std, (3,)), E.dtype)
+    return effunet_forward(E, pre.model, x)
+
+
+def effunet_forward(E: Ctx, net: nn.Module, x: Act) -> torch.Tensor:
+    """smp.Unet('timm-efficientnet-bX') forward (eval) on an NHWC input -> logits [B,1,H,W] f32."""
+    B, H, W = x.N, x.H, x.W
     enc = net.encoder
     x = ops.conv2d(E.conv(enc.conv_stem, enc.bn1, ACT_SILU), x)
     feats = [x]

@@ -28,8 +28,12 @@ class FusedAdamW:
     """AdamW + optional global-norm clipping over a model's FlatParams (param_groups: one, as the reference)."""
 
     def __init__(self, model: torch.nn.Module, lr: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.01, max_grad_norm: Optional[float] = 1.0):
+                 weight_decay: float = 0.01, max_grad_norm: Optional[float] = 1.0, params=None):
+        """``params`` (optional) restricts the step -- and the clipping norm -- to a subset of the trainable
+        parameters that is contiguous in the flat layout, e.g. ``unet.decoder.parameters()`` of the
+        distillation student (train_distillation_staged.py:1298-1305 optimises and clips the decoder only)."""
         self.model = model
+        self._subset = None if params is None else [p for p in params]
         self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
         self.max_grad_norm = max_grad_norm
         self.step_count = 0
@@ -43,8 +47,17 @@ class FusedAdamW:
         if self._flat is None:
             self._flat = flat_params_of(self.model)
             f = self._flat
-            self.exp_avg = torch.zeros_like(f.data)
-            self.exp_avg_sq = torch.zeros_like(f.data)
+            self._range = (0, f.numel)
+            if self._subset is not None:
+                spans = sorted(f.offsets[id(p)] for p in self._subset)
+                b, e = spans[0][0], spans[-1][0] + spans[-1][1]
+                covered = sum(k for _, k in spans)
+                if covered != e - b:
+                    raise ValueError("FusedAdamW(params=...): the parameters are not contiguous in the flat layout")
+                self._range = (b, e)
+            n = self._range[1] - self._range[0]
+            self.exp_avg = torch.zeros(n, dtype=torch.float32, device=f.data.device)
+            self.exp_avg_sq = torch.zeros_like(self.exp_avg)
             self.partial = torch.empty(L.lib().hiseg_optim_blocks(), dtype=torch.float32, device=f.data.device)
             self.last_norm = torch.zeros(1, dtype=torch.float32, device=f.data.device)
 
@@ -66,9 +79,11 @@ class FusedAdamW:
         bc1, bc2 = 1.0 - b1 ** self.step_count, 1.0 - b2 ** self.step_count
         s = L.stream_ptr()
         clip = self.max_grad_norm is not None and self.max_grad_norm > 0
-        L.check(lib.hiseg_grad_norm_partials(f.grad.data_ptr(), f.numel, self.partial.data_ptr(), s), "grad_norm")
-        L.check(lib.hiseg_adamw_step(f.data.data_ptr(), f.grad.data_ptr(), self.exp_avg.data_ptr(),
-                                     self.exp_avg_sq.data_ptr(), f.numel, float(lr), float(b1), float(b2),
+        b, e = self._range
+        gp, dp = f.grad.data_ptr() + 4 * b, f.data.data_ptr() + 4 * b
+        L.check(lib.hiseg_grad_norm_partials(gp, e - b, self.partial.data_ptr(), s), "grad_norm")
+        L.check(lib.hiseg_adamw_step(dp, gp, self.exp_avg.data_ptr(),
+                                     self.exp_avg_sq.data_ptr(), e - b, float(lr), float(b1), float(b2),
                                      float(self.eps), float(self.weight_decay), float(bc1), float(bc2),
                                      self.partial.data_ptr(), float(self.max_grad_norm) if clip else 0.0,
                                      self.last_norm.data_ptr(), s), "adamw_step")

@@ -338,10 +338,13 @@ def conv_fwd(S: TrainState, p: TConv, xa: Act, xb: Optional[Act] = None, *, act=
     return out, d
 
 
-def conv_bwd(T: Tape, p: TConv, d: L.Conv2dDesc, xa: Act, xb: Optional[Act], dz: Act, *, need_dx: bool = True,
-             bias_from_gemm: bool = True):
-    """Weight/bias gradient (MFMA wgrad + split reduce into the flat gradient) and the data gradient
-    (forward implicit-GEMM kernel with the packed dgrad weights), accumulated into the inputs' grads."""
+def _needs_wgrad(p: TConv) -> bool:
+    return p.conv.weight.requires_grad
+
+
+def conv_wgrad(T: Tape, p: TConv, d: L.Conv2dDesc, dz: Act, bias_from_gemm: bool = True):
+    """Weight (and GEMM-column bias) gradient of the conv described by d: MFMA wgrad + split reduce
+    accumulated into the flat gradient."""
     S, lib = T.S, L.lib()
     want_bias = int(p.has_bias and bias_from_gemm)
     wd = L.Conv2dDesc.from_buffer_copy(d)
@@ -362,6 +365,15 @@ def conv_bwd(T: Tape, p: TConv, d: L.Conv2dDesc, xa: Act, xb: Optional[Act], dz:
     gb = S.grad(p.conv.bias) if want_bias else None
     _chk(lib.hiseg_conv2d_wgrad_reduce(ws.data_ptr(), sp.value, ctypes.byref(m), gw.data_ptr(), _ptr(gb), 1,
                                        _stream()), "wgrad_reduce")
+
+
+def conv_bwd(T: Tape, p: TConv, d: L.Conv2dDesc, xa: Act, xb: Optional[Act], dz: Act, *, need_dx: bool = True,
+             bias_from_gemm: bool = True):
+    """Weight/bias gradient (MFMA wgrad + split reduce into the flat gradient) and the data gradient
+    (forward implicit-GEMM kernel with the packed dgrad weights), accumulated into the inputs' grads."""
+    S, lib = T.S, L.lib()
+    if _needs_wgrad(p):
+        conv_wgrad(T, p, d, dz, bias_from_gemm)
     if not need_dx:
         return
     # data gradient: conv over dz with the dgrad weights

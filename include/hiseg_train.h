@@ -139,6 +139,12 @@ int hiseg_maxpool2x2_bwd(int dtype, const void* x, int N, int H, int W, int C, c
  * (refinement.py:775-800): NCHW f32 planes, dx = adjoint of resize (h,w) -> (H,W). */
 int hiseg_resize_bilinear_bwd(const float* dy, int NC, int h, int w, int H, int W, float* dx, hiseg_stream_t stream);
 
+/* Backward of the nearest x2 upsample the UNet decoder fuses into its conv1 loader (smp DecoderBlock,
+ * F.interpolate(scale_factor=2, mode="nearest")): dx[n][y][x][c] (+)= sum of the 2x2 children
+ * dy[n][2y+i][2x+j][c].  dy is the full-resolution gradient view (N x 2h x 2w), dx the (h x w) one. */
+int hiseg_upsample2x_bwd(int dtype, long long N, int h, int w, int C, hiseg_ew_view dy, hiseg_ew_view dx,
+                         int accumulate, hiseg_stream_t stream);
+
 /* ----------------------------------------------------------------------------------------
  * Optimiser step over a flat f32 parameter space (all trainable parameters of the model are
  * views into one buffer, their gradients into another): torch.nn.utils.clip_grad_norm_ +

@@ -48,3 +48,96 @@ def test_distill_schedule_methods_match_reference_state():
     assert (fn.alpha, fn.task_weight, fn.performance_ratio) == pytest.approx((st[1], st[2], st[5]))
     fn.update_distillation_weight(0.90, 0.80, amplification_factor=30.0)
     assert fn.distillation_eliminated and fn.alpha == 0.0 and fn.task_weight == 1.0
+
+
+# ------------------------------------------------------------------------------------------ student training step
+def _distill_model(dt):
+    import filler
+    import hiseg
+    model, loss_fn = hiseg.create_unet_distillation_model("timm-efficientnet-b0", "timm-efficientnet-b7",
+                                                          teacher_checkpoint="absent.pth", device="cpu",
+                                                          progressive_unfreeze=True)
+    filler.fill_module(model.student, seed=11)
+    filler.fill_module(model.teacher, seed=12)
+    hiseg.set_compute_dtype(model, dt)
+    return model, loss_fn
+
+
+def test_distill_student_step_f32_matches_oracle():
+    """Decoder-only phase of train_distillation_staged.py (progressive unfreezing, epochs < start): student
+    B0 smp-UNet in train mode (batch-statistics BN everywhere, frozen encoder), teacher B7 in eval, the
+    distillation loss with targets, backward into the decoder + head.  Against oracle/ (torch autograd on
+    the CPU, f32): teacher logits 1e-4; student logits, loss 1e-3 (train-mode BN over a 2-image batch with
+    2x3-pixel deepest maps amplifies rounding, as in test_gpu_train); parameter gradients by cosine > 0.99
+    per tensor and total norm within 3 %."""
+    import filler
+    from oracle import distill as OD
+    from oracle import rgb_model as O
+    from oracle import train as OT
+    model, loss_fn = _distill_model(torch.float32)
+    sd_s, sd_t = OT.params_of(model.student), OT.params_of(model.teacher)
+    x = torch.from_numpy(filler.normal(21, (2, 3, 64, 96)))
+    _, _, m = OD.np_inputs(22, 2, 64, 96)
+    model = model.to(DEV).train()
+    loss_fn.temperature = 4.0
+    s, t = model(x.to(DEV))
+    loss, d = loss_fn(s, t, m.to(DEV))
+    loss.backward()
+    with OT.train_mode():
+        rs = O.effunet_logits(sd_s, "unet", x, "b0")
+    with torch.no_grad():
+        rt = O.effunet_logits(sd_t, "unet", x, "b7")
+    rl, rd = OD.distill_loss(rs, rt, m, temperature=4.0, alpha=0.05, task_weight=0.7)
+    rl.backward()
+
+    def rel(a, b):
+        a, b = a.detach().double().cpu(), b.detach().double().cpu()
+        return ((a - b).abs().max() / b.abs().max()).item()
+    assert rel(t, rt) < 1e-4
+    assert rel(s, rs) < 1e-3
+    assert loss.item() == pytest.approx(rl.item(), rel=1e-3)
+    for k in ("kl_loss", "mse_loss", "bce_loss", "dice_loss"):
+        assert d[k] == pytest.approx(rd[k], rel=2e-3, abs=1e-6), k
+    tot_m = tot_r = 0.0
+    bad = []
+    for n, p in model.student.named_parameters():
+        if not p.requires_grad:
+            assert n.startswith("unet.encoder."), n
+            continue
+        mg, rg = p.grad.detach().double().cpu().reshape(-1), sd_s[n].grad.double().reshape(-1)
+        tot_m += float((mg ** 2).sum())
+        tot_r += float((rg ** 2).sum())
+        if rg.norm() < 1e-6 * (1 + rg.numel()) ** 0.5:
+            continue
+        cos = float((mg * rg).sum() / (mg.norm() * rg.norm()))
+        if cos <= 0.99:
+            bad.append((n, round(cos, 4), float(mg.norm()), float(rg.norm())))
+    assert not bad, bad
+    assert abs(tot_m / tot_r - 1) < 3e-2
+
+
+def test_distill_bf16_training_lowers_loss():
+    """bf16 decoder-only distillation: decoder AdamW (clip 1.0 on the decoder, train_distillation_staged.py
+    :298-314) over a fixed batch lowers the loss; the segmentation head is not in the optimiser (the
+    reference optimises unet.decoder.parameters() only) and keeps its weights."""
+    import filler
+    import hiseg
+    model, loss_fn = _distill_model(torch.bfloat16)
+    model = model.to(DEV).train()
+    x = torch.from_numpy(filler.normal(31, (2, 3, 128, 128))).to(DEV)
+    _, _, m = __import__("oracle.distill", fromlist=["np_inputs"]).np_inputs(32, 2, 128, 128)
+    m = m.to(DEV)
+    head_w = model.student.unet.segmentation_head[0].weight.detach().clone()
+    opt, losses = None, []
+    for step in range(6):
+        s, t = model(x)
+        loss, d = loss_fn(s, t, m)
+        if opt is None:
+            opt = hiseg.FusedAdamW(model.student, lr=1e-3, weight_decay=1e-4, max_grad_norm=1.0,
+                                   params=model.student.get_decoder_parameters())
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert all(np.isfinite(losses)) and losses[-1] < losses[0], losses
+    assert torch.equal(model.student.unet.segmentation_head[0].weight.detach(), head_w)

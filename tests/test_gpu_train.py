@@ -495,3 +495,40 @@ def test_train_loop_bf16_decreases_loss():
     assert all(np.isfinite(losses)), losses
     assert losses[-1] < losses[0], losses
     assert set(d.keys()) >= {"bg_fg_loss", "final_loss", "dice_loss", "contour", "distance_transform"}
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cskip", [0, 24, 128])
+def test_up_conv_backward_matches_autograd(dt, cskip):
+    """smp DecoderBlock.conv1 (hiseg.effunet_train.up_conv_bn_relu): conv3x3 over cat(nearest-x2(x), skip)
+    -> BN(train) -> ReLU; weight gradient through the upsampled + concatenated loader, data gradient through
+    the 2x2 upsample sum, against float64 autograd on the kernels' ReLU pattern."""
+    from hiseg import effunet_train as ET
+    from hiseg.ops import Act
+    cin = 64 if cskip != 128 else 128
+    conv = nn.Conv2d(cin + cskip, 32, 3, padding=1, bias=False)
+    bn = nn.BatchNorm2d(32)
+    filler.fill_module(_Holder(c=conv, b=bn), seed=13)
+    TE, S, T = engine(_Holder(c=conv, b=bn), dt)
+    x = torch.from_numpy(filler.normal(14, (2, cin, 4, 6))).to(DEV)
+    sk = torch.from_numpy(filler.normal(15, (2, max(cskip, 1), 8, 12))).to(DEV)[:, :cskip]
+    xa = Act.from_nchw(x, dt)
+    ska = Act.from_nchw(sk, dt) if cskip else None
+    y = ET.up_conv_bn_relu(T, conv, bn, xa, ska, need_dx=True)
+    g = torch.from_numpy(filler.normal(16, (2, 32, 8, 12))).to(DEV)
+    inject(T, y, g, dt)
+    S.flat.prepare_backward()
+    T.run_backward()
+    xr = x.double().requires_grad_(True)
+    wr = conv.weight.detach().double().requires_grad_(True)
+    inp = F.interpolate(xr, scale_factor=2, mode="nearest")
+    if cskip:
+        inp = torch.cat([inp, sk.double()], 1)
+    zn = F.batch_norm(F.conv2d(inp, wr, None, padding=1), None, None, bn.weight.detach().double(),
+                      bn.bias.detach().double(), True, 0.1, 1e-5)
+    live = y.to_nchw() > 0
+    yr = torch.where(live, zn, torch.zeros_like(zn))
+    (yr * g.double()).sum().backward()
+    t = tol(dt)
+    assert err(dt)(conv.weight.grad, wr.grad) < 2 * t
+    assert err(dt)(grad_nchw(T, xa), xr.grad) < 2 * t
