@@ -18,7 +18,9 @@ boundary/contour/distance terms, the hand-written backward, FusedAdamW (clip 1.0
 averaged over the ranks by hiseg.distributed (bucketed RCCL all-reduce overlapped with the backward) when
 N > 1.
 
-Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--no-train]
+Third, under "distill": the C5 B7 -> B0 distillation step (decoder-only phase) of 4 640x640 images per GPU.
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--no-train] [--no-distill]
 """
 import argparse
 import json
@@ -136,6 +138,69 @@ def train_bench(device, dtype, rank, world, dist, steps, warmup):
                        "parallelism": f"dp{world} (DDP, bucketed RCCL grad all-reduce)" if world > 1 else "dp1"}}
 
 
+def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=640):
+    """C5 (BASELINE.json configs[4]): B7 -> B0 staged distillation step, decoder-only phase of the progressive
+    unfreezing schedule -- B7 teacher forward (eval), B0 student forward (train-mode BN) + decoder/head
+    backward, UNetDistillationLoss (T = 4, targets), decoder-subset FusedAdamW with clip 1.0 -- 4 images
+    640x640 per GPU (train_distillation_staged config batch_size 4), gradients averaged over ranks."""
+    import filler
+    import hiseg
+    from hiseg import distributed as HD
+    model, loss_fn = hiseg.create_unet_distillation_model("timm-efficientnet-b0", "timm-efficientnet-b7",
+                                                          teacher_checkpoint="absent.pth", device="cpu",
+                                                          progressive_unfreeze=True)
+    filler.fill_module(model.student, seed=11)
+    filler.fill_module(model.teacher, seed=12)
+    hiseg.set_compute_dtype(model, dtype)
+    model = model.to(device).train()
+    loss_fn.temperature = 4.0
+    g = torch.Generator().manual_seed(100 + rank)
+    x = torch.randn(batch, 3, hw, hw, generator=g).to(device)
+    yy, xx = torch.meshgrid(torch.linspace(-1, 1, hw), torch.linspace(-1, 1, hw), indexing="ij")
+    m = ((yy / 0.7) ** 2 + (xx / 0.45) ** 2 < 1).float()[None, None].expand(batch, 1, hw, hw).contiguous().to(device)
+    if world > 1:
+        HD.enable_grad_sync(model.student)
+    state = {"opt": None}
+
+    def step():
+        s, t = model(x)
+        loss, _ = loss_fn(s, t, m)
+        if state["opt"] is None:
+            state["opt"] = hiseg.FusedAdamW(model.student, lr=1e-4, weight_decay=1e-4, max_grad_norm=1.0,
+                                            params=model.student.get_decoder_parameters())
+        state["opt"].zero_grad()
+        loss.backward()
+        state["opt"].step()
+        return loss
+
+    for _ in range(warmup):
+        loss = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = tt.item()
+    sps = steps / elapsed
+    return {"metric": "distillation step/s", "value": round(sps, 3), "unit": "steps/s",
+            "ms_per_step": round(1e3 / sps, 2), "steps": steps, "warmup": warmup,
+            "images_per_s": round(sps * batch * world, 1), "loss_last": round(float(loss.detach()), 4),
+            "config": {"workload": f"C5: B7 teacher (eval) -> B0 student (train-mode BN, decoder-only phase), "
+                                   f"{batch} img {hw}x{hw}/GPU, UNetDistillationLoss T=4 + BCE/Dice targets, "
+                                   f"decoder FusedAdamW clip 1.0", "global_batch": batch * world,
+                       "parallelism": f"dp{world} (bucketed RCCL grad all-reduce)" if world > 1 else "dp1"}}
+
+
 def cpu_baseline(seconds_budget=30.0):
     """The oracle (float32 CPU restatement of the reference path) on a bounded sample of the same
     workload: 1 image 480x640 with 8 ROIs through UNet + ROI head (exported contract)."""
@@ -186,6 +251,7 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-train", action="store_true")
     ap.add_argument("--train-only", action="store_true")
+    ap.add_argument("--no-distill", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -206,6 +272,9 @@ def main():
     if not args.no_train:
         torch.cuda.empty_cache()
         out["train"] = train_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), max(2, args.warmup))
+    if not args.no_distill and not args.train_only:
+        torch.cuda.empty_cache()
+        out["distill"] = distill_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2)
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline and not args.train_only:
             out["cpu_baseline"] = cpu_baseline()
