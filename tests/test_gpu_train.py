@@ -532,3 +532,46 @@ def test_up_conv_backward_matches_autograd(dt, cskip):
     t = tol(dt)
     assert err(dt)(conv.weight.grad, wr.grad) < 2 * t
     assert err(dt)(grad_nchw(T, xa), xr.grad) < 2 * t
+
+
+def test_grad_sync_nccl_world1_matches_local():
+    """hiseg.distributed over RCCL (world size 1 on the one-GPU box): the bucketed all-reduce on the
+    communication stream, first-step schedule recording and the overlapped launches of the second step
+    leave the gradients of two B0 train steps bit-identical to the unsynchronised run."""
+    import os
+    import torch.distributed as dist
+    import hiseg
+    from hiseg import distributed as HD
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device(DEV, 0))
+    try:
+        grads = []
+        for sync in (False, True):
+            m = _model(torch.bfloat16).to(DEV).train()
+            for mm in (m.roi_align_mask, m.roi_align_rgb):
+                mm.spatial_scale_h, mm.spatial_scale_w = 96, 128
+            if sync:
+                s = HD.enable_grad_sync(m, bucket_mb=1.0)
+            images = torch.from_numpy(filler.uniform(41, (2, 3, 96, 128))).to(DEV)
+            rois = torch.from_numpy(filler.box_rois(42, 2, 2)).to(DEV)
+            tgt = torch.from_numpy(filler.ellipse_targets(43, 4, 128, 96)).to(DEV)
+            loss_fn = hiseg.RefinedHierarchicalLoss(use_contour_detection=True, use_distance_transform=True)
+            out = []
+            for step in range(2):
+                logits, aux = m(images, rois)
+                loss, _ = loss_fn(logits, tgt, aux)
+                for p in m.parameters():
+                    p.grad = None
+                loss.backward()
+                torch.cuda.synchronize()
+                out.append(m.__dict__["_hiseg_train"].flat.grad.clone())
+            if sync:
+                assert len(s.buckets) > 3 and any(k >= 0 for k in s.launch_after)
+                assert sorted(s.launched) == list(range(len(s.buckets)))
+            grads.append(out)
+        for a, b in zip(*grads):
+            assert torch.equal(a, b)
+    finally:
+        dist.destroy_process_group()
