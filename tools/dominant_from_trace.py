@@ -1,0 +1,27 @@
+"""Average duration of bench.py's dominant launch class from a rocprofv3 kernel trace (developer tool).
+
+The dominant class is the 256->256 3x3 conv at the 64x48 ROI grid over 256 ROIs: conv_fast_kernel
+<128,128,...> with 6144 pixel tiles x 2 Cout tiles = 12288 workgroups (grid 3 145 728 threads).  The
+kernel-stats summary averages every conv_fast launch (all layer shapes); this filters the trace to the
+class bench.py's HIP-event probe times, so the two averages can be compared.  The same grid also runs the
+256->256 1x1 (K = 256) and 128->256 3x3 (K = 1152) layers; the trace carries no shape, so the K = 2304
+class is taken as the launches longer than 0.75 x the median of the upper half (the three K values are
+9x / 2x apart, the clusters do not overlap).
+Usage: python tools/dominant_from_trace.py gpurun_out/prof_v3/trace_kernel_trace.csv > profiles/...json
+"""
+import csv
+import json
+import sys
+
+GRID = 12288 * 256
+rows = [r for r in csv.DictReader(open(sys.argv[1]))
+        if r["Kernel_Name"].startswith("void hiseg::conv_fast_kernel<128, 128") and int(r["Grid_Size_X"]) == GRID]
+d_all = sorted((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows)
+upper = d_all[len(d_all) // 2:]
+cut = 0.75 * upper[len(upper) // 2]
+d = [v for v in d_all if v > cut]
+print(json.dumps({"kernel": "conv_fast_kernel<128,128,2,2,2> grid 12288 x 256 (256->256 3x3 @64x48 x256 ROIs)",
+                  "launches": len(d), "same_grid_launches": len(d_all), "cluster_cut_ms": round(cut, 4), "avg_ms": round(sum(d) / len(d), 4), "median_ms": round(d[len(d) // 2], 4),
+                  "min_ms": round(d[0], 4), "max_ms": round(d[-1], 4),
+                  "flop_per_launch": 927712935936.0,
+                  "tflops_at_avg": round(927712935936.0 / (sum(d) / len(d) * 1e-3) / 1e12, 1)}, indent=1))
