@@ -248,7 +248,8 @@ __device__ __forceinline__ float act_d(float pre, int act) {
 
 // per image: gap, hidden pre-activation, gate
 __global__ void __launch_bounds__(256) ca_mlp_kernel(const float* part, int HW, int C, int Cr, const float* w1,
-                                                     const float* w2, int act, float* gap, float* hpre, float* gate) {
+                                                     const float* w2, int act, float* gap, float* hpre, float* gate,
+                                                     const float* b1 = nullptr, const float* b2 = nullptr) {
   extern __shared__ float sm[];
   float* g = sm;
   float* h = sm + C;
@@ -261,14 +262,14 @@ __global__ void __launch_bounds__(256) ca_mlp_kernel(const float* part, int HW, 
   }
   __syncthreads();
   for (int r = threadIdx.x; r < Cr; r += 256) {
-    float s = 0.f;
+    float s = b1 ? b1[r] : 0.f;
     for (int c = 0; c < C; ++c) s += w1[(long long)r * C + c] * g[c];
     hpre[(long long)n * Cr + r] = s;
     h[r] = act_f(s, act);
   }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += 256) {
-    float s = 0.f;
+    float s = b2 ? b2[c] : 0.f;
     for (int r = 0; r < Cr; ++r) s += w2[(long long)c * Cr + r] * h[r];
     gate[(long long)n * C + c] = sigmoidf_(s);
   }
@@ -296,7 +297,8 @@ __global__ void __launch_bounds__(256) ca_apply_kernel(const void* x, int N, int
 // per image: ds = dgate * g (1-g); dh; dgap; per-image weight-gradient rows
 __global__ void __launch_bounds__(256) ca_mlp_bwd_kernel(const float* part, int C, int Cr, const float* w1,
                                                          const float* w2, int act, const float* gap, const float* hpre,
-                                                         const float* gate, float* dgap, float* wpart) {
+                                                         const float* gate, float* dgap, float* wpart,
+                                                         float* bpart = nullptr) {
   extern __shared__ float sm[];
   float* ds = sm;
   float* dh = sm + C;
@@ -306,12 +308,14 @@ __global__ void __launch_bounds__(256) ca_mlp_bwd_kernel(const float* part, int 
     for (int k = 0; k < kGapSplits; ++k) s += part[((long long)n * kGapSplits + k) * C + c];
     const float g = gate[(long long)n * C + c];
     ds[c] = s * g * (1.f - g);
+    if (bpart) bpart[(long long)n * (Cr + C) + Cr + c] = ds[c];
   }
   __syncthreads();
   for (int r = threadIdx.x; r < Cr; r += 256) {
     float s = 0.f;
     for (int c = 0; c < C; ++c) s += w2[(long long)c * Cr + r] * ds[c];
     dh[r] = s * act_d(hpre[(long long)n * Cr + r], act);
+    if (bpart) bpart[(long long)n * (Cr + C) + r] = dh[r];
   }
   __syncthreads();
   float* wp = wpart + (long long)n * 2 * C * Cr;  // [dW1 (Cr x C)][dW2 (C x Cr)]
@@ -722,6 +726,54 @@ extern "C" int hiseg_attn_channel_bwd(int dtype, const void* x, int N, int HW, i
   DISPATCH_T(dtype, hipLaunchKernelGGL(ca_dx_kernel<T>, dim3(nb((long long)N * HW * (C / chunk_of(dtype)), 256)),
                                        dim3(256), 0, s, dout, N, HW, C, gate, chan_mul, dgap, dx));
   return hiseg_check_launch("attn_channel_bwd");
+}
+
+// timm SqueezeExcite (EfficientNet MBConv: GAP -> conv_reduce + bias -> SiLU -> conv_expand + bias -> sigmoid)
+// in train mode: the channel-attention kernels with biases.  fwd writes gap / hpre / gate and out = x * gate
+// (the projection conv's input, materialised so its weight gradient sees it); bwd from d(out).
+extern "C" long long hiseg_se_train_ws(int N, int C, int Cr) {
+  return (long long)N * kGapSplits * C + (long long)N * C + (long long)N * 2 * C * Cr + (long long)N * (Cr + C);
+}
+
+extern "C" int hiseg_se_train_fwd(int dtype, const void* x, int N, int HW, int C, const float* w1, const float* b1,
+                                  int Cr, const float* w2, const float* b2, int act, float* ws, float* gap,
+                                  float* hpre, float* gate, void* out, hiseg_stream_t stream) {
+  HISEG_REQUIRE(x && w1 && b1 && w2 && b2 && ws && gap && hpre && gate && out && N > 0 && HW > 0 && Cr > 0,
+                HISEG_ERR_BAD_ARG, "se_train_fwd: bad args");
+  HISEG_REQUIRE(C > 0 && C % chunk_of(dtype) == 0, HISEG_ERR_BAD_SHAPE, "se_train_fwd: C alignment");
+  hipStream_t s = (hipStream_t)stream;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_gap_kernel<T>, dim3(N, kGapSplits), dim3(256), 0, s, x, nullptr, nullptr, HW,
+                                       C, ws));
+  hipLaunchKernelGGL(ca_mlp_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, ws, HW, C, Cr, w1, w2, act,
+                     gap, hpre, gate, b1, b2);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_apply_kernel<T>, dim3(nb((long long)N * HW * (C / chunk_of(dtype)), 256)),
+                                       dim3(256), 0, s, x, N, HW, C, gate, nullptr, out));
+  return hiseg_check_launch("se_train_fwd");
+}
+
+extern "C" int hiseg_se_train_bwd(int dtype, const void* x, int N, int HW, int C, const float* w1, int Cr,
+                                  const float* w2, int act, const float* gap, const float* hpre, const float* gate,
+                                  const void* dout, void* dx, float* ws, float* dw1, float* db1, float* dw2, float* db2,
+                                  hiseg_stream_t stream) {
+  HISEG_REQUIRE(x && w1 && w2 && gap && hpre && gate && dout && dx && ws && dw1 && db1 && dw2 && db2,
+                HISEG_ERR_BAD_ARG, "se_train_bwd: null");
+  HISEG_REQUIRE(C > 0 && C % chunk_of(dtype) == 0, HISEG_ERR_BAD_SHAPE, "se_train_bwd: C alignment");
+  hipStream_t s = (hipStream_t)stream;
+  float* part = ws;
+  float* dgap = ws + (long long)N * kGapSplits * C;
+  float* wpart = dgap + (long long)N * C;
+  float* bpart = wpart + (long long)N * 2 * C * Cr;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_gap_kernel<T>, dim3(N, kGapSplits), dim3(256), 0, s, x, dout, nullptr, HW, C,
+                                       part));
+  hipLaunchKernelGGL(ca_mlp_bwd_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, part, C, Cr, w1, w2, act,
+                     gap, hpre, gate, dgap, wpart, bpart);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(nb(C * Cr, 128)), dim3(128), 0, s, wpart, N, 2 * C * Cr, C * Cr, dw1, 1);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(nb(C * Cr, 128)), dim3(128), 0, s, wpart + C * Cr, N, 2 * C * Cr, C * Cr, dw2, 1);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(nb(Cr, 128)), dim3(128), 0, s, bpart, N, Cr + C, Cr, db1, 1);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(nb(C, 128)), dim3(128), 0, s, bpart + Cr, N, Cr + C, C, db2, 1);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_dx_kernel<T>, dim3(nb((long long)N * HW * (C / chunk_of(dtype)), 256)),
+                                       dim3(256), 0, s, dout, N, HW, C, gate, nullptr, dgap, dx));
+  return hiseg_check_launch("se_train_bwd");
 }
 
 static UbfArgs ubf_args(const hiseg_ubf_desc* d) {

@@ -85,11 +85,18 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(hiseg_bn_apply_desc d) {
 }
 
 // ---------------------------------------------------------------------------------------- backward
+__device__ __forceinline__ float silu_grad_pre(const hiseg_bn_bwd_desc& d, float z, int c) {
+  const float v = (z - d.mean[c]) * d.invstd[c] * (d.gamma ? d.gamma[c] : 1.f) + (d.beta ? d.beta[c] : 0.f);
+  const float s = 1.f / (1.f + expf(-v));
+  return s * (1.f + v * (1.f - s));
+}
+
 template <typename T>
 __device__ __forceinline__ float bn_g(const hiseg_bn_bwd_desc& d, long long p, int c) {
   float g = ld<T>(d.dy, p * d.dy_cstride + d.dy_coff + c);
   if (d.chan_mul) g *= d.chan_mul[(p / d.HW) * d.C + c];
-  if (d.act != HISEG_ACT_NONE) g *= act_grad(ld<T>(d.y, p * d.y_cstride + d.y_coff + c), d.act);
+  if (d.act == HISEG_ACT_SILU) g *= silu_grad_pre(d, ld<T>(d.z, p * d.z_cstride + d.z_coff + c), c);
+  else if (d.act != HISEG_ACT_NONE) g *= act_grad(ld<T>(d.y, p * d.y_cstride + d.y_coff + c), d.act);
   return g;
 }
 
@@ -300,7 +307,12 @@ __device__ __forceinline__ void bn_gv(const hiseg_bn_bwd_desc& d, long long p, i
 #pragma unroll
     for (int k = 0; k < V; ++k) g[k] *= cm[k];
   }
-  if (d.act != HISEG_ACT_NONE) {
+  if (d.act == HISEG_ACT_SILU) {   // SiLU'(v) needs the pre-activation: v = xhat * gamma + beta from z
+    float z[V];
+    ldv<T>(d.z, p * d.z_cstride + d.z_coff + c, z);
+#pragma unroll
+    for (int k = 0; k < V; ++k) g[k] *= silu_grad_pre(d, z[k], c + k);
+  } else if (d.act != HISEG_ACT_NONE) {
     float y[V];
     ldv<T>(d.y, p * d.y_cstride + d.y_coff + c, y);
 #pragma unroll
@@ -706,7 +718,10 @@ extern "C" int hiseg_bn_apply(const hiseg_bn_apply_desc* d, hiseg_stream_t strea
 extern "C" int hiseg_bn_bwd(const hiseg_bn_bwd_desc* d, hiseg_stream_t stream) {
   HISEG_REQUIRE(d && d->dy && d->z && d->dz && d->mean && d->invstd && d->partial && d->P > 0 && d->C > 0 && d->HW > 0,
                 HISEG_ERR_BAD_ARG, "bn_bwd: bad arguments");
-  HISEG_REQUIRE(d->act == HISEG_ACT_NONE || d->y, HISEG_ERR_BAD_ARG, "bn_bwd: activation needs y");
+  HISEG_REQUIRE(d->act == HISEG_ACT_NONE || d->act == HISEG_ACT_SILU || d->y, HISEG_ERR_BAD_ARG,
+                "bn_bwd: activation needs y");
+  HISEG_REQUIRE(d->act != HISEG_ACT_SILU || !d->dres, HISEG_ERR_BAD_ARG,
+                "bn_bwd: SiLU after a residual add is not supported (no pre-activation)");
   HISEG_REQUIRE(d->P < (1ll << 31), HISEG_ERR_BAD_SHAPE, "bn_bwd: too many pixels");
   hipStream_t s = (hipStream_t)stream;
   const int S = kBnSplits;

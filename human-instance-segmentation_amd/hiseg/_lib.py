@@ -91,7 +91,8 @@ class BnBwdDesc(ctypes.Structure):
                 ("partial", c_void_p),
                 ("dgamma", c_void_p), ("dbeta", c_void_p), ("dconv_bias", c_void_p), ("accumulate_params", c_int),
                 ("dz", c_void_p), ("dz_cstride", c_int), ("dz_coff", c_int),
-                ("dres", c_void_p), ("dres_cstride", c_int), ("dres_coff", c_int), ("dres_accumulate", c_int)]
+                ("dres", c_void_p), ("dres_cstride", c_int), ("dres_coff", c_int), ("dres_accumulate", c_int),
+                ("beta", c_void_p)]
 
 
 class EwView(ctypes.Structure):
@@ -182,6 +183,16 @@ def _declare(lib):
         "hiseg_maxpool2x2_bwd": ([c_int, P, c_int, c_int, c_int, c_int, P, P, c_int, P], c_int),
         "hiseg_resize_bilinear_bwd": ([P, c_int, c_int, c_int, c_int, c_int, P, P], c_int),
         "hiseg_upsample2x_bwd": ([c_int, c_ll, c_int, c_int, c_int, EwView, EwView, c_int, P], c_int),
+        "hiseg_dw_train_fwd": ([c_int, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P, c_int, c_int, P], c_int),
+        "hiseg_dw_bwd_data": ([c_int, P, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P, c_int, P],
+                              c_int),
+        "hiseg_dw_bwd_weight_ws": ([c_int, c_int], c_ll),
+        "hiseg_dw_bwd_weight": ([c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P],
+                                c_int),
+        "hiseg_se_train_ws": ([c_int, c_int, c_int], c_ll),
+        "hiseg_se_train_fwd": ([c_int, P, c_int, c_int, c_int, P, P, c_int, P, P, c_int, P, P, P, P, P, P], c_int),
+        "hiseg_se_train_bwd": ([c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, P, P, P, P, P, P, P, P, P, P],
+                               c_int),
         "hiseg_attn_spatial_train_fwd": ([c_int, P, c_int, c_int, c_int, c_int, P, c_int, P, P, P, P, P, P], c_int),
         "hiseg_attn_spatial_ws": ([c_int, c_int, c_int, c_int], c_int),
         "hiseg_attn_spatial_bwd": ([c_int, P, c_int, c_int, c_int, c_int, P, c_int, P, P, P, P, P, P, P, P, P], c_int),

@@ -473,7 +473,7 @@ def bn_backward(T: Tape, bn: nn.BatchNorm2d, z: Act, y: Act, st: BNState, dz: Ac
     d.y, d.y_cstride, d.y_coff = y.ptr(), y.cstride, y.coff
     d.z, d.z_cstride, d.z_coff = z.ptr(), z.cstride, z.coff
     d.chan_mul, d.act = _ptr(drop), act
-    d.mean, d.invstd, d.gamma = st.mean.data_ptr(), st.invstd.data_ptr(), _ptr(bn.weight)
+    d.mean, d.invstd, d.gamma, d.beta = st.mean.data_ptr(), st.invstd.data_ptr(), _ptr(bn.weight), _ptr(bn.bias)
     d.partial = part.data_ptr()
     d.dgamma = _ptr(S.grad(bn.weight)) if bn.weight is not None and bn.weight.requires_grad else None
     d.dbeta = _ptr(S.grad(bn.bias)) if bn.bias is not None and bn.bias.requires_grad else None

@@ -83,7 +83,8 @@ typedef struct hiseg_bn_apply_desc {
 } hiseg_bn_apply_desc;
 int hiseg_bn_apply(const hiseg_bn_apply_desc* d, hiseg_stream_t stream);
 
-/* Backward.  g = dy * chan_mul * act'(y) (ReLU: y > 0; none: 1), xhat = (z - mean)*invstd:
+/* Backward.  g = dy * chan_mul * act'(y) (ReLU: y > 0; sigmoid: y(1-y); SiLU: from the pre-activation
+ * xhat*gamma + beta; none: 1), xhat = (z - mean)*invstd:
  *   reduce : dgamma[c] (+)= sum g*xhat, dbeta[c] (+)= sum g ; partial [splits][2][C]
  *   apply  : dz = gamma*invstd*(g - sum(g)/P - xhat*sum(g*xhat)/P)     (to dz, dtype)
  *            dres (+)= g  (the residual input's gradient, if dres != null; accumulate flag)
@@ -100,6 +101,7 @@ typedef struct hiseg_bn_bwd_desc {
   float* dgamma; float* dbeta; float* dconv_bias; int accumulate_params;
   void* dz; int dz_cstride, dz_coff;
   void* dres; int dres_cstride, dres_coff; int dres_accumulate;
+  const float* beta;              /* BN shift; needed for act = SiLU (pre-activation = xhat*gamma + beta) */
 } hiseg_bn_bwd_desc;
 int hiseg_bn_bwd(const hiseg_bn_bwd_desc* d, hiseg_stream_t stream);
 
@@ -138,6 +140,29 @@ int hiseg_maxpool2x2_bwd(int dtype, const void* x, int N, int H, int W, int C, c
 /* F.interpolate(bilinear, align_corners=False) backward for the aux heads' up-sampling
  * (refinement.py:775-800): NCHW f32 planes, dx = adjoint of resize (h,w) -> (H,W). */
 int hiseg_resize_bilinear_bwd(const float* dy, int NC, int h, int w, int H, int W, float* dx, hiseg_stream_t stream);
+
+/* EfficientNet MBConv training (timm InvertedResidual / DepthwiseSeparableConv, smp encoder stages unfrozen by
+ * train_distillation_staged.py's progressive schedule).  Depthwise conv: NHWC with cstride == C, weights in
+ * the parameter layout [C][K*K] f32; fwd writes the raw conv (train-mode BN follows); bwd_data writes or
+ * accumulates dx; bwd_weight ACCUMULATES into dw (f32 [C][K*K]) through ws (hiseg_dw_bwd_weight_ws floats). */
+int hiseg_dw_train_fwd(int dtype, const void* x, int N, int H, int W, int C, int K, int stride, const float* w,
+                       void* out, int Ho, int Wo, hiseg_stream_t stream);
+int hiseg_dw_bwd_data(int dtype, const void* dy, int N, int H, int W, int C, int K, int stride, const float* w,
+                      int Ho, int Wo, void* dx, int accumulate, hiseg_stream_t stream);
+long long hiseg_dw_bwd_weight_ws(int C, int K);
+int hiseg_dw_bwd_weight(int dtype, const void* x, const void* dy, int N, int H, int W, int C, int K, int stride,
+                        int Ho, int Wo, float* ws, float* dw, hiseg_stream_t stream);
+
+/* timm SqueezeExcite in training: gate = sigmoid(W2 act(W1 gap(x) + b1) + b2), out = x * gate (materialised:
+ * the projection conv's input).  fwd keeps gap [N][C], hpre [N][Cr], gate [N][C]; bwd from d(out) writes dx
+ * and ACCUMULATES dW1 [Cr][C], db1, dW2 [C][Cr], db2.  ws: hiseg_se_train_ws floats. */
+long long hiseg_se_train_ws(int N, int C, int Cr);
+int hiseg_se_train_fwd(int dtype, const void* x, int N, int HW, int C, const float* w1, const float* b1, int Cr,
+                       const float* w2, const float* b2, int act, float* ws, float* gap, float* hpre, float* gate,
+                       void* out, hiseg_stream_t stream);
+int hiseg_se_train_bwd(int dtype, const void* x, int N, int HW, int C, const float* w1, int Cr, const float* w2,
+                       int act, const float* gap, const float* hpre, const float* gate, const void* dout, void* dx,
+                       float* ws, float* dw1, float* db1, float* dw2, float* db2, hiseg_stream_t stream);
 
 /* Backward of the nearest x2 upsample the UNet decoder fuses into its conv1 loader (smp DecoderBlock,
  * F.interpolate(scale_factor=2, mode="nearest")): dx[n][y][x][c] (+)= sum of the 2x2 children

@@ -141,3 +141,85 @@ def test_distill_bf16_training_lowers_loss():
         losses.append(loss.item())
     assert all(np.isfinite(losses)) and losses[-1] < losses[0], losses
     assert torch.equal(model.student.unet.segmentation_head[0].weight.detach(), head_w)
+
+
+@pytest.mark.parametrize("blocks", [1, 3, 7])
+def test_distill_progressive_unfreeze_f32_matches_oracle(blocks):
+    """After unfreeze_encoder_blocks(k) (unet_decoder_distillation.py:233-274): the deepest k encoder stages
+    train too -- MBConv backward (1x1 convs, depthwise k3/k5 stride 1/2, SqueezeExcite, BN-SiLU) and the
+    decoder's gradients into their skip features.  Against the oracle as the decoder-only test."""
+    import filler
+    from oracle import distill as OD
+    from oracle import rgb_model as O
+    from oracle import train as OT
+    model, loss_fn = _distill_model(torch.float32)
+    unfrozen = model.unfreeze_encoder_blocks(blocks)
+    assert len(unfrozen) > 0
+    sd_s, sd_t = OT.params_of(model.student), OT.params_of(model.teacher)
+    x = torch.from_numpy(filler.normal(23, (2, 3, 64, 96)))
+    _, _, m = OD.np_inputs(24, 2, 64, 96)
+    model = model.to(DEV).train()
+    s, t = model(x.to(DEV))
+    loss, d = loss_fn(s, t, m.to(DEV))
+    loss.backward()
+    with OT.train_mode():
+        rs = O.effunet_logits(sd_s, "unet", x, "b0")
+    with torch.no_grad():
+        rt = O.effunet_logits(sd_t, "unet", x, "b7")
+    rl, rd = OD.distill_loss(rs, rt, m, temperature=1.0, alpha=0.05, task_weight=0.7)
+    rl.backward()
+    assert loss.item() == pytest.approx(rl.item(), rel=1e-3)
+    bad, tot_m, tot_r, n_enc = [], 0.0, 0.0, 0
+    for n, p in model.student.named_parameters():
+        if not p.requires_grad:
+            continue
+        n_enc += n.startswith("unet.encoder.")
+        mg, rg = p.grad.detach().double().cpu().reshape(-1), sd_s[n].grad.double().reshape(-1)
+        tot_m += float((mg ** 2).sum())
+        tot_r += float((rg ** 2).sum())
+        if rg.norm() < 1e-6 * (1 + rg.numel()) ** 0.5:
+            continue
+        cos = float((mg * rg).sum() / (mg.norm() * rg.norm()))
+        if cos <= 0.99:
+            bad.append((n, round(cos, 4)))
+    assert n_enc == len(unfrozen)
+    assert not bad, bad
+    assert abs(tot_m / tot_r - 1) < 3e-2
+
+
+def test_distill_bf16_progressive_schedule_runs():
+    """bf16, the reference's schedule in miniature: decoder-only steps, then unfreeze_encoder_blocks(2) with
+    the reference's two parameter groups (decoder: lr, clip 1.0; encoder: lr * encoder_lr_scale, unclipped,
+    train_distillation_staged.py:1516-1545) -- the new trainable set re-lays the flat parameters, the loss
+    keeps decreasing and stays finite."""
+    import filler
+    import hiseg
+    from oracle import distill as OD
+    model, loss_fn = _distill_model(torch.bfloat16)
+    model = model.to(DEV).train()
+    x = torch.from_numpy(filler.normal(33, (2, 3, 96, 128))).to(DEV)
+    _, _, m = OD.np_inputs(34, 2, 96, 128)
+    m = m.to(DEV)
+    losses = []
+    opts = None
+    for step in range(8):
+        if step == 4:
+            enc = model.unfreeze_encoder_blocks(2, learning_rate_scale=0.3)
+            assert enc
+            opts = None
+        s, t = model(x)
+        loss, _ = loss_fn(s, t, m)
+        if opts is None:
+            opts = [hiseg.FusedAdamW(model.student, lr=1e-3, weight_decay=1e-4, max_grad_norm=1.0,
+                                     params=model.student.get_decoder_parameters())]
+            if step >= 4:
+                opts.append(hiseg.FusedAdamW(model.student, lr=3e-4, weight_decay=1e-4, max_grad_norm=None,
+                                             params=enc))
+        for o in opts:
+            o.zero_grad()
+        loss.backward()
+        for o in opts:
+            o.step()
+        losses.append(loss.item())
+    assert all(np.isfinite(losses)), losses
+    assert losses[3] < losses[0] and losses[-1] < losses[4], losses
