@@ -150,24 +150,38 @@ __global__ void __launch_bounds__(256) gap_partial_kernel(const void* x, int HW,
   }
 }
 
-__global__ void __launch_bounds__(256) se_gate_kernel(const float* partial, int splits, int HW, int C, const float* w1,
+// sums[n][c] = sum over the splits of partial[n][split][c]: grid (N, ceil(C/64)), 64 channels x 4 split groups
+__global__ void __launch_bounds__(256) gap_reduce_kernel(const float* partial, int splits, int C, float* sums) {
+  __shared__ float red[256];
+  const int n = blockIdx.x, t = threadIdx.x;
+  const int c = blockIdx.y * 64 + (t & 63), sg = t >> 6;
+  float a = 0.f;
+  if (c < C)
+    for (int sp = sg; sp < splits; sp += 4) a += partial[((long long)n * splits + sp) * C + c];
+  red[t] = a;
+  __syncthreads();
+  if (sg == 0 && c < C) sums[(long long)n * C + c] = red[t] + red[t + 64] + red[t + 128] + red[t + 192];
+}
+
+// SE MLP per image from the pooled sums: hidden = act(W1 mean + b1) with one wavefront per hidden unit
+// (lanes stride the C inputs, coalesced rows of W1, DPP/shuffle reduction), gate = sigmoid(W2 hidden + b2).
+__global__ void __launch_bounds__(256) se_gate_kernel(const float* sums, int HW, int C, const float* w1,
                                                       const float* b1, int Cr, const float* w2, const float* b2, int act,
                                                       float* gate) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* mean = sm;
   float* hid = sm + C;
   const int n = blockIdx.x;
-  const int t = threadIdx.x;
-  for (int c = t; c < C; c += 256) {
-    float s = 0.f;
-    for (int sp = 0; sp < splits; ++sp) s += partial[((long long)n * splits + sp) * C + c];
-    mean[c] = s / (float)HW;
-  }
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const float inv = 1.f / (float)HW;
+  for (int c = t; c < C; c += 256) mean[c] = sums[(long long)n * C + c] * inv;
   __syncthreads();
-  for (int r = t; r < Cr; r += 256) {
-    float s = b1 ? b1[r] : 0.f;
-    for (int c = 0; c < C; ++c) s += w1[(long long)r * C + c] * mean[c];
-    hid[r] = apply_act(s, act);
+  for (int r = wave; r < Cr; r += 4) {
+    float s = 0.f;
+    for (int c = lane; c < C; c += 64) s += w1[(long long)r * C + c] * mean[c];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) hid[r] = apply_act(s + (b1 ? b1[r] : 0.f), act);
   }
   __syncthreads();
   for (int c = t; c < C; c += 256) {
@@ -196,40 +210,105 @@ __global__ void __launch_bounds__(256) channel_scale_kernel(const void* x, int N
 }
 
 // ------------------------------------------------------------------ depthwise conv + BN + act
-template <typename T>
-__global__ void __launch_bounds__(256) dwconv_kernel(const void* in, int N, int H, int W, int C, int Kk, int stride,
-                                                     const float* w, const float* scale, const float* shift, int act,
-                                                     void* out, int Ho, int Wo) {
-  constexpr int K = Chunk<T>::N;
-  const int nch = C / K;
-  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
-  const long long total = (long long)N * Ho * Wo * nch;
-  if (gid >= total) return;
-  const int ch = (int)(gid % nch);
-  long long p = gid / nch;
-  const int x = (int)(p % Wo); p /= Wo;
-  const int y = (int)(p % Ho);
-  const int n = (int)(p / Ho);
-  const int pad = Kk / 2;
-  float acc[K], v[K];
+// Block = CT channel-chunk lanes x R strip rows (CT = min(C/V, 256); blockIdx.z = chunk group), one image
+// (blockIdx.y) and a contiguous range of output strips (blockIdx.x).  A strip is XS consecutive output
+// pixels of one row: the (XS-1)*stride + K input columns of each filter row are loaded once and reused by
+// the XS outputs, the K weights of a filter row once per strip (cached in L1).  32-bit indices only.
+// With gap != nullptr every block also writes the per-channel sum of its outputs (after BN + act) to
+// gap[(n * tiles + tile) * C + c] -- the SqueezeExcite global average pool fused into the producer.
+constexpr int kDwXS = 4;
+
+template <typename T, int KS, int ST>
+__global__ void __launch_bounds__(256) dwconv_kernel(const void* in, int H, int W, int C, const float* w,
+                                                     const float* scale, const float* shift, int act, void* out,
+                                                     int Ho, int Wo, float* gap) {
+  constexpr int V = Chunk<T>::N;
+  constexpr int NIN = (kDwXS - 1) * ST + KS;
+  __shared__ float red[256 * V];
+  const int nch = C / V;
+  const int g0 = blockIdx.z * 256;
+  const int CT = (nch - g0) < 256 ? (nch - g0) : 256;
+  const int R = 256 / CT;
+  const int t = threadIdx.x;
+  const int cl = t % CT, r = t / CT;
+  const int ch = g0 + cl;
+  const bool live = r < R;
+  const int n = blockIdx.y, tiles = gridDim.x, tile = blockIdx.x;
+  const int sx = (Wo + kDwXS - 1) / kDwXS;
+  const int strips = Ho * sx;
+  const int s0 = (int)((long long)strips * tile / tiles), s1 = (int)((long long)strips * (tile + 1) / tiles);
+  const int c = ch * V;
+  const int pad = KS / 2;
+  float sc[V], sh[V], gs[V];
 #pragma unroll
-  for (int e = 0; e < K; ++e) acc[e] = 0.f;
-  const uint4* src = reinterpret_cast<const uint4*>(in);
-  for (int ky = 0; ky < Kk; ++ky) {
-    const int yy = y * stride - pad + ky;
-    if (yy < 0 || yy >= H) continue;
-    for (int kx = 0; kx < Kk; ++kx) {
-      const int xx = x * stride - pad + kx;
-      if (xx < 0 || xx >= W) continue;
-      Chunk<T>::unpack(src[(((long long)n * H + yy) * W + xx) * nch + ch], v);
-      const float* wp = w + (long long)(ky * Kk + kx) * C + ch * K;
+  for (int e = 0; e < V; ++e) { sc[e] = scale[c + e]; sh[e] = shift[c + e]; gs[e] = 0.f; }
+  const uint4* src = reinterpret_cast<const uint4*>(in) + (long long)n * H * W * nch;
+  uint4* dst = reinterpret_cast<uint4*>(out) + (long long)n * Ho * Wo * nch;
+  if (live) {
+    for (int st = s0 + r; st < s1; st += R) {
+      const int oy = st / sx;
+      const int ox0 = (st - oy * sx) * kDwXS;
+      float acc[kDwXS][V];
 #pragma unroll
-      for (int e = 0; e < K; ++e) acc[e] += wp[e] * v[e];
+      for (int xo = 0; xo < kDwXS; ++xo)
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[xo][e] = 0.f;
+#pragma unroll
+      for (int ky = 0; ky < KS; ++ky) {
+        const int iy = oy * ST - pad + ky;
+        if ((unsigned)iy >= (unsigned)H) continue;
+        float wk[KS][V];
+#pragma unroll
+        for (int kx = 0; kx < KS; ++kx) {
+          const float4* wp = reinterpret_cast<const float4*>(w + (ky * KS + kx) * C + c);
+#pragma unroll
+          for (int q = 0; q < V / 4; ++q) {
+            const float4 f = wp[q];
+            wk[kx][4 * q] = f.x; wk[kx][4 * q + 1] = f.y; wk[kx][4 * q + 2] = f.z; wk[kx][4 * q + 3] = f.w;
+          }
+        }
+        const uint4* row = src + (long long)iy * W * nch + ch;
+        const int ix0 = ox0 * ST - pad;
+#pragma unroll
+        for (int j = 0; j < NIN; ++j) {
+          const int ix = ix0 + j;
+          if ((unsigned)ix >= (unsigned)W) continue;
+          float v[V];
+          Chunk<T>::unpack(row[(long long)ix * nch], v);
+#pragma unroll
+          for (int xo = 0; xo < kDwXS; ++xo) {
+            const int kx = j - xo * ST;
+            if (kx < 0 || kx >= KS) continue;
+#pragma unroll
+            for (int e = 0; e < V; ++e) acc[xo][e] += wk[kx][e] * v[e];
+          }
+        }
+      }
+#pragma unroll
+      for (int xo = 0; xo < kDwXS; ++xo) {
+        if (ox0 + xo >= Wo) break;
+        float o[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          o[e] = apply_act(acc[xo][e] * sc[e] + sh[e], act);
+          gs[e] += o[e];
+        }
+        dst[((long long)oy * Wo + ox0 + xo) * nch + ch] = Chunk<T>::pack(o);
+      }
     }
   }
+  if (gap == nullptr) return;
 #pragma unroll
-  for (int e = 0; e < K; ++e) acc[e] = apply_act(acc[e] * scale[ch * K + e] + shift[ch * K + e], act);
-  reinterpret_cast<uint4*>(out)[gid] = Chunk<T>::pack(acc);
+  for (int e = 0; e < V; ++e) red[t * V + e] = gs[e];
+  __syncthreads();
+  if (r == 0) {
+    for (int rr = 1; rr < R; ++rr)
+#pragma unroll
+      for (int e = 0; e < V; ++e) gs[e] += red[(rr * CT + cl) * V + e];
+    float* gp = gap + ((long long)n * tiles + tile) * C + c;
+#pragma unroll
+    for (int e = 0; e < V; ++e) gp[e] = gs[e];
+  }
 }
 
 // ------------------------------------------------------------------ input prologue
@@ -494,8 +573,11 @@ extern "C" int hiseg_se_gate_fwd(int dtype, const void* x, int N, int HW, int C,
   const size_t lds = nch >= 256 ? 0 : (size_t)(256 / nch) * C * sizeof(float);
   hipStream_t s = (hipStream_t)stream;
   DISPATCH_T(dtype, gap_partial_kernel, dim3(N, splits), dim3(256), lds, s, x, HW, C, splits, partial);
-  hipLaunchKernelGGL(se_gate_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, partial, splits, HW, C, w1, b1,
-                     Cr, w2, b2, act, gate);
+  // the pooled sums go through the gate buffer: each se_gate block reads its image's row into LDS before
+  // it overwrites that row with the gate
+  hipLaunchKernelGGL(gap_reduce_kernel, dim3(N, (C + 63) / 64), dim3(256), 0, s, partial, splits, C, gate);
+  hipLaunchKernelGGL(se_gate_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, gate, HW, C, w1, b1, Cr,
+                     w2, b2, act, gate);
   return hiseg_check_launch("se_gate");
 }
 
@@ -508,17 +590,69 @@ extern "C" int hiseg_channel_scale_fwd(int dtype, const void* x, int N, int HW, 
   return hiseg_check_launch("channel_scale");
 }
 
+extern "C" int hiseg_dw_gap_tiles(int N, int Ho, int Wo) {
+  const int strips = Ho * ((Wo + kDwXS - 1) / kDwXS);
+  int t = 2048 / (N > 0 ? N : 1);
+  if (t < 1) t = 1;
+  return t < strips ? t : strips;
+}
+
+static int dwconv_launch(int dtype, const void* in, int N, int H, int W, int C, int K, int stride, const float* w,
+                         const float* scale, const float* shift, int act, void* out, int Ho, int Wo, float* gap,
+                         hipStream_t s) {
+  HISEG_REQUIRE(in && w && scale && shift && out && N > 0 && H > 0 && W > 0, HISEG_ERR_BAD_ARG, "dwconv: bad args");
+  HISEG_REQUIRE(C % chunk_of(dtype) == 0, HISEG_ERR_BAD_SHAPE, "dwconv: C must be chunk aligned");
+  HISEG_REQUIRE((K == 3 || K == 5) && (stride == 1 || stride == 2), HISEG_ERR_BAD_SHAPE, "dwconv: K %d stride %d", K,
+                stride);
+  HISEG_REQUIRE(Ho == (H + 2 * (K / 2) - K) / stride + 1 && Wo == (W + 2 * (K / 2) - K) / stride + 1, HISEG_ERR_BAD_SHAPE,
+                "dwconv: output grid mismatch");
+  HISEG_REQUIRE((reinterpret_cast<uintptr_t>(w) & 15) == 0 && (long long)H * W * C < (1ll << 31), HISEG_ERR_BAD_SHAPE,
+                "dwconv: weights must be 16-B aligned, image < 2^31 elements");
+  const int nch = C / chunk_of(dtype);
+  dim3 grid(hiseg_dw_gap_tiles(N, Ho, Wo), N, (nch + 255) / 256);
+#define DW_L(KS, ST)                                                                                          \
+  do {                                                                                                        \
+    if (dtype == HISEG_BF16)                                                                                  \
+      hipLaunchKernelGGL((dwconv_kernel<bf16_t, KS, ST>), grid, dim3(256), 0, s, in, H, W, C, w, scale, shift, \
+                         act, out, Ho, Wo, gap);                                                              \
+    else                                                                                                      \
+      hipLaunchKernelGGL((dwconv_kernel<float, KS, ST>), grid, dim3(256), 0, s, in, H, W, C, w, scale, shift,  \
+                         act, out, Ho, Wo, gap);                                                              \
+  } while (0)
+  if (K == 3 && stride == 1) DW_L(3, 1);
+  else if (K == 3) DW_L(3, 2);
+  else if (stride == 1) DW_L(5, 1);
+  else DW_L(5, 2);
+#undef DW_L
+  return hiseg_check_launch("dwconv");
+}
+
 extern "C" int hiseg_dwconv_fwd(int dtype, const void* in, int N, int H, int W, int C, int K, int stride, const float* w,
                                 const float* scale, const float* shift, int act, void* out, int Ho, int Wo,
                                 hiseg_stream_t stream) {
-  HISEG_REQUIRE(in && w && scale && shift && out && N > 0 && C % chunk_of(dtype) == 0 && (K & 1) && stride >= 1,
-                HISEG_ERR_BAD_ARG, "dwconv: bad args");
-  HISEG_REQUIRE(Ho == (H + 2 * (K / 2) - K) / stride + 1 && Wo == (W + 2 * (K / 2) - K) / stride + 1, HISEG_ERR_BAD_SHAPE,
-                "dwconv: output grid mismatch");
-  const long long total = (long long)N * Ho * Wo * (C / chunk_of(dtype));
-  DISPATCH_T(dtype, dwconv_kernel, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, in, N, H, W, C, K, stride, w,
-             scale, shift, act, out, Ho, Wo);
-  return hiseg_check_launch("dwconv");
+  return dwconv_launch(dtype, in, N, H, W, C, K, stride, w, scale, shift, act, out, Ho, Wo, nullptr,
+                       (hipStream_t)stream);
+}
+
+extern "C" int hiseg_dwconv_gap_fwd(int dtype, const void* in, int N, int H, int W, int C, int K, int stride,
+                                    const float* w, const float* scale, const float* shift, int act, void* out, int Ho,
+                                    int Wo, float* gap_partial, hiseg_stream_t stream) {
+  HISEG_REQUIRE(gap_partial, HISEG_ERR_BAD_ARG, "dwconv_gap: null partial buffer");
+  return dwconv_launch(dtype, in, N, H, W, C, K, stride, w, scale, shift, act, out, Ho, Wo, gap_partial,
+                       (hipStream_t)stream);
+}
+
+extern "C" int hiseg_se_gate_partials_fwd(const float* partial, int splits, int N, int HW, int C, const float* w1,
+                                          const float* b1, int Cr, const float* w2, const float* b2, int act, float* gate,
+                                          hiseg_stream_t stream) {
+  HISEG_REQUIRE(partial && w1 && w2 && gate && splits > 0 && N > 0 && HW > 0 && C > 0 && Cr > 0, HISEG_ERR_BAD_ARG,
+                "se_gate_partials: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  // pooled sums through the gate buffer (read into LDS per image before the gate overwrites them)
+  hipLaunchKernelGGL(gap_reduce_kernel, dim3(N, (C + 63) / 64), dim3(256), 0, s, partial, splits, C, gate);
+  hipLaunchKernelGGL(se_gate_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, gate, HW, C, w1, b1, Cr,
+                     w2, b2, act, gate);
+  return hiseg_check_launch("se_gate_partials");
 }
 
 extern "C" int hiseg_image_max_fwd(const float* x, long long n, float* maxbuf, hiseg_stream_t stream) {

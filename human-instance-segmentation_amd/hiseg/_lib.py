@@ -152,6 +152,10 @@ def _declare(lib):
         "hiseg_channel_scale_fwd": ([c_int, P, c_int, c_int, c_int, P, P, P], c_int),
         "hiseg_dwconv_fwd": ([c_int, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, c_int, P,
                               c_int, c_int, P], c_int),
+        "hiseg_dw_gap_tiles": ([c_int, c_int, c_int], c_int),
+        "hiseg_dwconv_gap_fwd": ([c_int, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, c_int, P,
+                                  c_int, c_int, P, P], c_int),
+        "hiseg_se_gate_partials_fwd": ([P, c_int, c_int, c_int, c_int, P, P, c_int, P, P, c_int, P, P], c_int),
         "hiseg_image_max_fwd": ([P, c_ll, P, P], c_int),
         "hiseg_input_norm_fwd": ([c_int, P, c_int, c_int, c_int, c_int, P, P, P, P, c_int, P], c_int),
         "hiseg_hier_combine_fwd": ([c_int, P, c_int, c_int, c_int, P, c_int, P, P, P, c_int, P, P, P, P,

@@ -285,17 +285,24 @@ def _dw(E: Ctx, conv: nn.Conv2d, bn, x: Act, act: int) -> Act:
     return ops.dwconv(x, w, s, h, k, stride, act)
 
 
+def _dw_se(E: Ctx, conv: nn.Conv2d, bn, se: nn.Module, x: Act) -> Tuple[Act, torch.Tensor]:
+    """conv_dw + BN + SiLU with the SE global pool fused into it, then the SE MLP -> gate [N, C]."""
+    w, s, h, k, stride = E.dw(conv, bn)
+    rd, c = se.conv_reduce.out_channels, se.conv_reduce.in_channels
+    return ops.dwconv_se_gate(x, w, s, h, k, stride, ACT_SILU, E.f32(se.conv_reduce.weight, (rd, c)),
+                              E.f32(se.conv_reduce.bias), E.f32(se.conv_expand.weight, (c, rd)),
+                              E.f32(se.conv_expand.bias), ACT_SILU)
+
+
 def mbconv(E: Ctx, blk: nn.Module, x: Act) -> Act:
-    """timm DepthwiseSeparableConv / InvertedResidual (eval): the SE gate is applied inside the
-    projection conv's loader (in_scale), the skip add in its epilogue."""
+    """timm DepthwiseSeparableConv / InvertedResidual (eval): the SE pool is fused into the depthwise conv,
+    the SE gate is applied inside the projection conv's loader (in_scale), the skip add in its epilogue."""
     if isinstance(blk, DepthwiseSeparableConv):
-        h = _dw(E, blk.conv_dw, blk.bn1, x, ACT_SILU)
-        g = _se(E, blk.se, h)
+        h, g = _dw_se(E, blk.conv_dw, blk.bn1, blk.se, x)
         return ops.conv2d(E.conv(blk.conv_pw, blk.bn2), h, in_scale=g, residual=x if blk.has_skip else None)
     if isinstance(blk, InvertedResidual):
         h = ops.conv2d(E.conv(blk.conv_pw, blk.bn1, ACT_SILU), x)
-        h = _dw(E, blk.conv_dw, blk.bn2, h, ACT_SILU)
-        g = _se(E, blk.se, h)
+        h, g = _dw_se(E, blk.conv_dw, blk.bn2, blk.se, h)
         return ops.conv2d(E.conv(blk.conv_pwl, blk.bn3), h, in_scale=g, residual=x if blk.has_skip else None)
     raise TypeError(type(blk))
 

@@ -391,6 +391,27 @@ def dwconv(x: Act, w: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor, k:
     return out
 
 
+def dwconv_se_gate(x: Act, w: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor, k: int, stride: int, act: int,
+                   w1, b1, w2, b2, se_act: int):
+    """Depthwise conv + folded BN + act with the SqueezeExcite pool fused into it; returns (h, gate [N, C])."""
+    assert x.coff == 0 and x.cstride == x.C
+    pad = k // 2
+    Ho = (x.H + 2 * pad - k) // stride + 1
+    Wo = (x.W + 2 * pad - k) // stride + 1
+    lib = L.lib()
+    out = Act.new(x.N, Ho, Wo, x.C, x.dtype, x.t.device, zero=False)
+    tiles = lib.hiseg_dw_gap_tiles(x.N, Ho, Wo)
+    partial = torch.empty(x.N * tiles * x.C, dtype=torch.float32, device=x.t.device)
+    L.check(lib.hiseg_dwconv_gap_fwd(hdtype(x.dtype), x.ptr(), x.N, x.H, x.W, x.C, k, stride, w.data_ptr(),
+                                     scale.data_ptr(), shift.data_ptr(), act, out.ptr(), Ho, Wo, partial.data_ptr(),
+                                     L.stream_ptr()), "dwconv_gap")
+    gate = torch.empty(x.N, x.C, dtype=torch.float32, device=x.t.device)
+    L.check(lib.hiseg_se_gate_partials_fwd(partial.data_ptr(), tiles, x.N, Ho * Wo, x.C, w1.data_ptr(), _ptr(b1),
+                                           w1.shape[0], w2.data_ptr(), _ptr(b2), se_act, gate.data_ptr(),
+                                           L.stream_ptr()), "se_gate_partials")
+    return out, gate
+
+
 def input_norm(images: torch.Tensor, mean: torch.Tensor, std: torch.Tensor, dtype: torch.dtype) -> Act:
     """normalize_input (hierarchical_segmentation_unet.py:1885-1890) with a device-side max flag."""
     _require_gpu(images)

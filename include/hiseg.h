@@ -151,6 +151,17 @@ int hiseg_channel_scale_fwd(int dtype, const void* x, int N, int HW, int C, cons
 int hiseg_dwconv_fwd(int dtype, const void* in, int N, int H, int W, int C, int K, int stride,
                      const float* w, const float* scale, const float* shift, int act, void* out,
                      int Ho, int Wo, hiseg_stream_t stream);
+/* The same depthwise conv fused with the SqueezeExcite global average pool that consumes its output
+ * (timm MBConv: conv_dw -> bn -> act -> se): gap_partial [N][tiles][C] f32 receives per-tile channel
+ * sums of the output (tiles = hiseg_dw_gap_tiles(N, Ho, Wo)); hiseg_se_gate_partials_fwd turns them
+ * into the gate [N][C] without re-reading the activation. */
+int hiseg_dw_gap_tiles(int N, int Ho, int Wo);
+int hiseg_dwconv_gap_fwd(int dtype, const void* in, int N, int H, int W, int C, int K, int stride,
+                         const float* w, const float* scale, const float* shift, int act, void* out,
+                         int Ho, int Wo, float* gap_partial, hiseg_stream_t stream);
+int hiseg_se_gate_partials_fwd(const float* partial, int splits, int N, int HW, int C, const float* w1,
+                               const float* b1, int Cr, const float* w2, const float* b2, int act,
+                               float* gate, hiseg_stream_t stream);
 
 /* Image prologue of PreTrainedPeopleSegmentationUNet.normalize_input
  * (hierarchical_segmentation_unet.py:1885-1890) fused with NCHW f32 -> NHWC(dtype, C padded
