@@ -12,7 +12,8 @@ from .layers import (  # noqa: F401
 from .effunet import EfficientNetUnet  # noqa: F401
 from .model import (  # noqa: F401
     DynamicRoIAlign, HierarchicalRGBSegmentationModelWithFullImagePretrainedUNet, PreTrainedPeopleSegmentationUNet,
-    PreTrainedPeopleSegmentationUNetWrapper, RGBHierarchicalExportWrapper, create_rgb_hierarchical_model)
+    PreTrainedPeopleSegmentationUNetWrapper, RGBHierarchicalExportWrapper, StreamPipelinedExport,
+    create_rgb_hierarchical_model)
 
 from .losses import RefinedHierarchicalLoss  # noqa: F401,E402
 from .optim import FusedAdamW, cosine_lr  # noqa: F401,E402

@@ -431,6 +431,21 @@ def export_forward(model: nn.Module, images: torch.Tensor, rois: torch.Tensor, d
     return inst, binary
 
 
+def export_unet_phase(model: nn.Module, images: torch.Tensor):
+    """First half of the exported contract: full-image UNet logit u and binary_masks."""
+    _check_input(images, "RGBHierarchicalExportWrapper")
+    E = Ctx(model, _root_dtype(model), images.device)
+    u = unet_logit(E, model.pretrained_unet.model, images.contiguous().float())
+    oc = model.pretrained_unet.output_conv
+    return u, ops.binary_masks(u, E.f32(oc.weight, (2,)), E.f32(oc.bias))
+
+
+def export_head_phase(model: nn.Module, images: torch.Tensor, rois: torch.Tensor, u: torch.Tensor, dilation: int = 0):
+    """Second half: RoIAlign + ROI head from u -> instance_masks."""
+    logits, _ = rgb_model_forward(model, images, rois, aux="none", unet_logit_override=u)
+    return ops.instance_masks(logits, dilation)
+
+
 # ------------------------------------------------------------------------------------ sub-module forwards (NCHW f32)
 def _root_for(m: nn.Module):
     return m

@@ -206,6 +206,50 @@ class RGBHierarchicalExportWrapper(nn.Module):
         return engine.export_forward(self.model, images, rois, self.dilation_pixels)
 
 
+class StreamPipelinedExport:
+    """Serving schedule of the exported contract on two HIP streams: the full-image UNet of batch k+1 (HBM /
+    latency-bound depthwise, SE and narrow decoder kernels) runs on one stream while the ROI head of batch k
+    (MFMA-bound 256-channel convs) runs on the other, so the two kernel classes share the CUs instead of
+    alternating.  Every batch still runs the complete contract; results are identical to
+    ``RGBHierarchicalExportWrapper(model)(images, rois)`` per batch (same kernels, same inputs).
+
+    ``run(batches)`` takes an iterable of (images, rois) and returns [(instance_masks, binary_masks), ...],
+    ready on the caller's current stream when it returns (the caller synchronises as usual).
+    """
+
+    def __init__(self, wrapper: "RGBHierarchicalExportWrapper"):
+        self.wrapper = wrapper
+        self.s_unet = torch.cuda.Stream()
+        self.s_head = torch.cuda.Stream()
+
+    def run(self, batches):
+        w = self.wrapper
+        caller = torch.cuda.current_stream()
+        self.s_unet.wait_stream(caller)
+        self.s_head.wait_stream(caller)
+        outs = []
+        for images, rois in batches:
+            H, W = images.shape[-2:] if w.image_size is None else w.image_size
+            for m in (w.model.roi_align_mask, w.model.roi_align_rgb):
+                m.spatial_scale = (H, W)
+                m.spatial_scale_h, m.spatial_scale_w = H, W
+            with torch.cuda.stream(self.s_unet):
+                u, binary = engine.export_unet_phase(w.model, images)
+                ready = torch.cuda.Event()
+                ready.record(self.s_unet)
+            with torch.cuda.stream(self.s_head):
+                self.s_head.wait_event(ready)
+                u.record_stream(self.s_head)
+                inst = engine.export_head_phase(w.model, images, rois, u, w.dilation_pixels)
+            outs.append((inst, binary))
+        caller.wait_stream(self.s_unet)
+        caller.wait_stream(self.s_head)
+        for inst, binary in outs:
+            inst.record_stream(caller)
+            binary.record_stream(caller)
+        return outs
+
+
 def create_rgb_hierarchical_model(roi_size=28, mask_size=56, multi_scale: bool = False,
                                   activation_function: str = "relu", activation_beta: float = 1.0,
                                   normalization_type: str = "layernorm2d", normalization_groups: int = 8,

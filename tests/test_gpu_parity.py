@@ -418,3 +418,25 @@ def test_bf16_pipeline_instance_mask_agreement():
     agree = (inst.cpu() == O.instance_masks(ref_logits)).float().mean().item()
     assert agree > 0.97, agree
     assert max_abs(binary.cpu(), O.binary_masks(sd, ref_u)) < 0.05
+
+
+def test_stream_pipelined_export_matches_serial():
+    """hiseg.StreamPipelinedExport (UNet of batch k+1 on a second stream beside the head of batch k) returns
+    exactly the per-batch outputs of the serial RGBHierarchicalExportWrapper."""
+    import filler
+    import hiseg
+    from helpers import b0_kwargs, hiseg_kwargs
+    m = filler.fill_module(hiseg.create_rgb_hierarchical_model(**hiseg_kwargs(b0_kwargs()))).eval().to("cuda")
+    hiseg.set_compute_dtype(m, torch.bfloat16)
+    w = hiseg.RGBHierarchicalExportWrapper(m)
+    batches = []
+    for k in range(3):
+        images = torch.from_numpy(filler.uniform(200 + k, (2, 3, 96, 128))).cuda()
+        rois = torch.from_numpy(filler.box_rois(300 + k, 2, 3)).cuda()
+        batches.append((images, rois))
+    with torch.no_grad():
+        serial = [w(i, r) for i, r in batches]
+        piped = hiseg.StreamPipelinedExport(w).run(batches)
+    torch.cuda.synchronize()
+    for (a, b), (c, d) in zip(serial, piped):
+        assert torch.equal(a, c) and torch.equal(b, d)
