@@ -42,6 +42,7 @@ METRIC = "ROI-masks/sec (fwd) + train step/s, B0 640×480×8-ROI, 1/2/4/8 MI355X
 B, R, H, W = 32, 8, 480, 640
 ROI_HW, MASK_HW = (64, 48), (128, 96)
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
+PEAK_HBM_GBS = 8000.0     # MI355X HBM3E (MI355X_MICROARCH.md)
 # Algorithmic work per ROI mask: head 53.1 GFLOP (inference graph) + B0 UNet 27.7/8
 GFLOP_PER_ROI_MASK = 53.1 + 27.7 / 8
 # Algorithmic work per training sample: B0-std head fwd+bwd 173.5 GFLOP + UNet fwd per ROI
@@ -205,6 +206,36 @@ def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=6
                        "parallelism": f"dp{world} (bucketed RCCL grad all-reduce)" if world > 1 else "dp1"}}
 
 
+def eval_bench(device, steps=20, n_roi=2048, mh=128, mw=96):
+    """(f)-row 3, GPU validation metrics: hiseg_seg_confusion (argmax + per-sample histogram, the whole
+    metric state of train_utils.evaluate_model) over 2048 ROI masks of C2's output size -- logits f32
+    [N,3,128,96] + int64 targets, 20 B per pixel read once (algorithmic bytes).  HIP events on the launch
+    stream."""
+    from hiseg.metrics import seg_confusion
+    g = torch.Generator(device=device).manual_seed(7)
+    logits = torch.randn(n_roi, 3, mh, mw, device=device, generator=g)
+    masks = torch.randint(0, 3, (n_roi, mh, mw), device=device, generator=g)
+    out = torch.zeros(n_roi, 5, 4, dtype=torch.int64, device=device)
+    for _ in range(3):
+        seg_confusion(logits, masks, 3, out=out)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        seg_confusion(logits, masks, 3, out=out)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    nbytes = n_roi * mh * mw * (3 * 4 + 8)
+    gbs = nbytes / ms / 1e6
+    return {"metric": "validation ROI-masks/s (metrics kernel)", "value": round(n_roi / ms * 1e3, 1),
+            "unit": "ROI-masks/s", "avg_launch_ms": round(ms, 4),
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(gbs / PEAK_HBM_GBS, 4)},
+            "config": {"workload": f"{n_roi} ROI masks 3x{mh}x{mw} f32 logits + int64 targets per launch "
+                                   f"(argmax + per-sample 5x4 histogram; every evaluate_model metric derives from it)"}}
+
+
 def cpu_baseline(seconds_budget=30.0):
     """The oracle (float32 CPU restatement of the reference path) on a bounded sample of the same
     workload: 1 image 480x640 with 8 ROIs through UNet + ROI head (exported contract)."""
@@ -280,6 +311,9 @@ def main():
     if not args.no_distill and not args.train_only:
         torch.cuda.empty_cache()
         out["distill"] = distill_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2)
+    if not args.train_only and world == 1:
+        torch.cuda.empty_cache()
+        out["eval"] = eval_bench(device)
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline and not args.train_only:
             out["cpu_baseline"] = cpu_baseline()

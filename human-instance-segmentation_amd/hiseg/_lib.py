@@ -220,6 +220,7 @@ def _declare(lib):
         "hiseg_distill_ws": ([c_int, c_int, c_int], c_ll),
         "hiseg_distill_loss_fwd": ([ctypes.POINTER(DistillCfg), c_int, c_int, c_int, P, P, P, P, P, P], c_int),
         "hiseg_distill_loss_bwd": ([ctypes.POINTER(DistillCfg), c_int, c_int, c_int, P, P, P, P, P, P, P], c_int),
+        "hiseg_seg_confusion": ([P, c_int, P, P, c_int, c_int, c_ll, P, P], c_int),
         "hiseg_optim_blocks": ([], c_int),
         "hiseg_grad_norm_partials": ([P, c_ll, P, P], c_int),
         "hiseg_adamw_step": ([P, P, P, P, c_ll, c_float, c_float, c_float, c_float, c_float, c_float, c_float, P,

@@ -31,9 +31,12 @@ class LazyLossDict(Mapping):
         self._out, self._keys, self._extra = out, keys, extra
         self._vals: Optional[Dict[str, float]] = None
 
-    def _materialise(self) -> Dict[str, float]:
+    def _materialise(self, host=None) -> Dict[str, float]:
+        """``host``: the device values already copied (hiseg.metrics.evaluate_model copies every batch's
+        values in one transfer at the end of the loop)."""
         if self._vals is None:
-            host = self._out.detach().cpu().tolist()
+            if host is None:
+                host = self._out.detach().cpu().tolist()
             v = {"bg_fg_loss": host[1], "target_nontarget_loss": host[2], "final_loss": host[3],
                  "consistency_loss": host[4], "total_loss": host[0], "ce_loss": host[3], "dice_loss": host[5],
                  "aux_fg_bg_loss": host[1], "aux_fg_accuracy": host[9], "aux_fg_iou": host[10],

@@ -5,17 +5,27 @@ import re
 from conftest import ROOT
 
 
-def header_functions():
-    src = open(os.path.join(ROOT, "include", "hiseg.h")).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(hiseg_\w+)\s*\(", src, flags=re.M)))
+def header_functions(names=None):
+    """Entry points declared in include/*.h (every header by default)."""
+    inc = os.path.join(ROOT, "include")
+    names = names or sorted(f for f in os.listdir(inc) if f.endswith(".h"))
+    out = set()
+    for n in names:
+        src = open(os.path.join(inc, n)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        out |= set(re.findall(r"^\s*(?:int|long long|const char\*)\s+(hiseg_\w+)\s*\(", src, flags=re.M))
+    return sorted(out)
 
 
 def test_header_declares_the_hot_path():
-    fns = header_functions()
+    fns = header_functions(["hiseg.h"])
     for must in ("hiseg_roi_align_fwd", "hiseg_conv2d_fwd", "hiseg_hier_combine_fwd", "hiseg_dwconv_fwd",
                  "hiseg_se_gate_fwd", "hiseg_attn_spatial_fwd", "hiseg_instance_masks_fwd"):
         assert must in fns
+    every = header_functions()
+    for must in ("hiseg_conv2d_wgrad", "hiseg_loss_fwd", "hiseg_distill_loss_fwd", "hiseg_adamw_step",
+                 "hiseg_seg_confusion"):
+        assert must in every
 
 
 def test_library_exports_every_declared_symbol():
