@@ -354,6 +354,8 @@ int conv_8ph_try(const ConvArgs& a, hipStream_t s, int variant) {
   const long long span_b = d.Cb ? (long long)d.N * d.H * d.W * d.b_cstride * 2 : 0;
   const long long span_w = (long long)d.Cout_pad * d.K_pad * 2;
   if (span_a >= 0x7fffffffll || span_b >= 0x7fffffffll || span_w >= 0x7fffffffll) return 0;
+  // the STAMP diagnostic writes 4 u64 per workgroup through desc.out2: refuse it without that buffer
+  HISEG_REQUIRE(variant != 41 || d.out2 != nullptr, HISEG_ERR_BAD_ARG, "conv_8ph: stamp variant needs desc.out2");
   int r;
   switch (variant) {
     case 0: case 40: r = launch_8ph<true, true, false>(a, s); break;

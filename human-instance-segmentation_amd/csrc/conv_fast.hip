@@ -241,6 +241,8 @@ int conv_fast_try(const ConvArgs& a, hipStream_t s, int variant) {
   const long long span_b = d.Cb ? (long long)d.N * d.H * d.W * d.b_cstride * 2 : 0;
   const long long span_w = (long long)d.Cout_pad * d.K_pad * 2;
   if (span_a >= 0x7fffffffll || span_b >= 0x7fffffffll || span_w >= 0x7fffffffll) return 0;
+  // the STAMP diagnostic writes 4 u64 per workgroup through desc.out2: refuse it without that buffer
+  HISEG_REQUIRE(variant != 18 || d.out2 != nullptr, HISEG_ERR_BAD_ARG, "conv_fast: stamp variant needs desc.out2");
   int r;
   if (variant == 0) variant = (d.Cout_pad % 128 == 0) ? 1 : (d.Cout_pad % 64 == 0 ? 3 : -1);
   switch (variant) {

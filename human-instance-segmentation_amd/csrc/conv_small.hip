@@ -321,6 +321,7 @@ int conv_small_try(const ConvArgs& a, hipStream_t s, int variant) {
   if ((size_t)d.Cout_pad * WS * 16 > 96 * 1024) return 0;
   int th = 0;
   const bool stamp = variant == 59;   // diagnostic: TH 8 with stamps (see conv_small_kernel)
+  HISEG_REQUIRE(!stamp || a.d.out2 != nullptr, HISEG_ERR_BAD_ARG, "conv_small: stamp variant needs desc.out2");
   if (stamp) th = 8;
   if (variant >= 51 && variant <= 58) th = variant - 50;
   if (th != 0 && th != 1 && th != 2 && th != 4 && th != 8) return 0;

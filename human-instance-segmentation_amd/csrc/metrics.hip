@@ -58,33 +58,47 @@ __global__ void __launch_bounds__(256) seg_confusion_kernel(const void* logits, 
   const T* lg = LABELS ? nullptr : reinterpret_cast<const T*>(logits) + (long long)n * C * HW;
 
   if (vec) {   // HW % 4 == 0 and 16-B (f32) / 8-B (bf16) aligned planes
-    for (long long i = beg + 4 * t; i < end; i += 4 * 256) {
-      const longlong2 t01 = *reinterpret_cast<const longlong2*>(tg + i);
-      const longlong2 t23 = *reinterpret_cast<const longlong2*>(tg + i + 2);
-      const long long tv[4] = {t01.x, t01.y, t23.x, t23.y};
-      int col[4];
-      if constexpr (LABELS) {
-        const longlong2 l01 = *reinterpret_cast<const longlong2*>(lb + i);
-        const longlong2 l23 = *reinterpret_cast<const longlong2*>(lb + i + 2);
-        col[0] = col_of<C>(l01.x); col[1] = col_of<C>(l01.y); col[2] = col_of<C>(l23.x); col[3] = col_of<C>(l23.y);
-      } else {
-        float v[4][C];
+    // two 4-pixel groups per thread and iteration, every load of both issued before the counting
+    for (long long i0 = beg + 4 * t; i0 < end; i0 += 8 * 256) {
+      long long tv[2][4];
+      float v[2][4][C];
+      long long lv[2][4];
 #pragma unroll
-        for (int c = 0; c < C; ++c) {
-          if constexpr (sizeof(T) == 4) {
-            const float4 q = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(lg) + (long long)c * HW + i);
-            v[0][c] = q.x; v[1][c] = q.y; v[2][c] = q.z; v[3][c] = q.w;
-          } else {
-            const uint2 q = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(lg) + (long long)c * HW + i);
-            v[0][c] = __uint_as_float(q.x << 16); v[1][c] = __uint_as_float(q.x & 0xffff0000u);
-            v[2][c] = __uint_as_float(q.y << 16); v[3][c] = __uint_as_float(q.y & 0xffff0000u);
+      for (int g = 0; g < 2; ++g) {
+        const long long i = i0 + g * 1024;
+        if (g == 1 && i >= end) break;
+        const longlong2 t01 = *reinterpret_cast<const longlong2*>(tg + i);
+        const longlong2 t23 = *reinterpret_cast<const longlong2*>(tg + i + 2);
+        tv[g][0] = t01.x; tv[g][1] = t01.y; tv[g][2] = t23.x; tv[g][3] = t23.y;
+        if constexpr (LABELS) {
+          const longlong2 l01 = *reinterpret_cast<const longlong2*>(lb + i);
+          const longlong2 l23 = *reinterpret_cast<const longlong2*>(lb + i + 2);
+          lv[g][0] = l01.x; lv[g][1] = l01.y; lv[g][2] = l23.x; lv[g][3] = l23.y;
+        } else {
+#pragma unroll
+          for (int c = 0; c < C; ++c) {
+            if constexpr (sizeof(T) == 4) {
+              const float4 q = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(lg) + (long long)c * HW + i);
+              v[g][0][c] = q.x; v[g][1][c] = q.y; v[g][2][c] = q.z; v[g][3][c] = q.w;
+            } else {
+              const uint2 q = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(lg) + (long long)c * HW + i);
+              v[g][0][c] = __uint_as_float(q.x << 16); v[g][1][c] = __uint_as_float(q.x & 0xffff0000u);
+              v[g][2][c] = __uint_as_float(q.y << 16); v[g][3][c] = __uint_as_float(q.y & 0xffff0000u);
+            }
           }
         }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) col[e] = argmax_c<C>(v[e]);
       }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) count<K>(cnt, row_of<C>(tv[e]) * (C + 1) + col[e]);
+      for (int g = 0; g < 2; ++g) {
+        if (g == 1 && i0 + 1024 >= end) break;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          int col;
+          if constexpr (LABELS) col = col_of<C>(lv[g][e]);
+          else col = argmax_c<C>(v[g][e]);
+          count<K>(cnt, row_of<C>(tv[g][e]) * (C + 1) + col);
+        }
+      }
     }
   } else {
     for (long long i = beg + t; i < end; i += 256) {

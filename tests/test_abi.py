@@ -55,3 +55,24 @@ def test_product_path_refuses_cpu_tensors():
     from hiseg import DynamicRoIAlign
     with pytest.raises(RuntimeError, match="GPU only"):
         DynamicRoIAlign(640, aligned=True)(torch.zeros(1, 1, 4, 4), torch.zeros(1, 5), 2, 2)
+
+
+def test_stamp_diagnostic_variants_refuse_a_missing_stamp_buffer():
+    """The s_memtime diagnostic variants (18 conv_fast, 41 conv_8ph; 59 conv_small likewise) write their stamps
+    through desc.out2; without that buffer they must refuse before any launch (a null-pointer stamp write
+    is an illegal address on the GPU)."""
+    import ctypes
+    from hiseg import _lib as L
+    d = L.Conv2dDesc()
+    d.dtype = d.out_dtype = 1  # bf16
+    d.N, d.H, d.W, d.Ho, d.Wo = 1, 16, 16, 16, 16
+    d.KH, d.KW, d.stride, d.pad = 3, 3, 1, 1
+    fake = 1 << 20
+    d.srcA, d.a_cstride, d.a_coff, d.Ca, d.a_up = fake, 256, 0, 256, 1
+    d.weight, d.Cout, d.Cout_pad, d.K_pad = fake, 256, 256, 9 * 256
+    d.scale, d.shift, d.act = fake, fake, 0
+    d.out, d.o_cstride, d.o_coff = fake, 256, 0
+    for v in (18, 41):
+        st = L.lib().hiseg_conv2d_fwd_variant(ctypes.byref(d), v, None)
+        assert st != 0, v
+        assert b"stamp variant needs desc.out2" in L.lib().hiseg_last_error_string(), v
