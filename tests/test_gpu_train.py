@@ -575,3 +575,53 @@ def test_grad_sync_nccl_world1_matches_local():
             assert torch.equal(a, b)
     finally:
         dist.destroy_process_group()
+
+
+def test_checkpoint_resume_continues_training_identically(tmp_path):
+    """Two bf16 train steps, save_checkpoint (reference format, AdamW-layout optimizer state, torch cosine
+    scheduler), resume into a fresh model + optimizer, one more step on both: identical parameters."""
+    import hiseg
+    images = torch.from_numpy(filler.uniform(191, (2, 3, 160, 192))).to(DEV)
+    rois = torch.from_numpy(filler.box_rois(192, 2, 1)).to(DEV)
+    tgt = torch.from_numpy(filler.ellipse_targets(193, 2, 128, 96)).to(DEV)
+
+    def setup():
+        m = _model(torch.bfloat16).to(DEV).train()
+        for mm in (m.roi_align_mask, m.roi_align_rgb):
+            mm.spatial_scale_h, mm.spatial_scale_w = 160, 192
+        return m, hiseg.RefinedHierarchicalLoss(use_contour_detection=True, use_distance_transform=True)
+
+    def step(m, loss_fn, state):
+        if state.get("opt") is None:
+            if state.get("resume"):
+                m(images, rois)   # lays the parameters out flat (the optimiser's moments index into it)
+            state["opt"] = hiseg.FusedAdamW(m, lr=5e-4)
+            state["sched"] = torch.optim.lr_scheduler.CosineAnnealingLR(state["opt"], T_max=5, eta_min=1e-6)
+            if state.get("resume"):
+                hiseg.resume_from_checkpoint(state["resume"], m, state["opt"], state["sched"], map_location=DEV)
+        logits, aux = m(images, rois)
+        loss, _ = loss_fn(logits, tgt, aux)
+        state["opt"].zero_grad()
+        loss.backward()
+        state["opt"].step()
+        state["sched"].step()
+
+    a, la = setup()
+    sa = {}
+    step(a, la, sa)
+    step(a, la, sa)
+    path = str(tmp_path / "ck.pth")
+    hiseg.save_checkpoint(path, a, sa["opt"], epoch=1, best_miou=0.5, scheduler=sa["sched"])
+    from hiseg.checkpoint import _reseed_output_conv
+    _reseed_output_conv(a)   # what the resume does (train_advanced.py:1230-1241)
+    b, lb = setup()
+    sb = {"resume": path}
+    # the loss EMA state is not part of the reference checkpoint: carry it over as the reference process would
+    lb._state = la._state.clone()
+    step(a, la, sa)
+    step(b, lb, sb)
+    torch.cuda.synchronize()
+    assert sb["opt"].step_count == sa["opt"].step_count == 3
+    assert sb["opt"].param_groups[0]["lr"] == sa["opt"].param_groups[0]["lr"]
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        assert torch.equal(pa, pb), n
