@@ -128,6 +128,12 @@ class DistillCfg(ctypes.Structure):
 DISTILL_NOUT = 5  # include/hiseg_distill.h HISEG_DISTILL_NOUT
 
 
+class RoiTargetDesc(ctypes.Structure):
+    """include/hiseg_data.h hiseg_roi_target_desc"""
+    _fields_ = [("mask_offset", c_ll)] + [(n, c_int) for n in ("n_inst", "target", "h0", "w0", "x1", "y1", "x2",
+                                                                 "y2", "img_w", "img_h")]
+
+
 class HisegError(RuntimeError):
     """Raised when a libhiseg entry point returns a non-zero status."""
 
@@ -221,6 +227,10 @@ def _declare(lib):
         "hiseg_distill_loss_fwd": ([ctypes.POINTER(DistillCfg), c_int, c_int, c_int, P, P, P, P, P, P], c_int),
         "hiseg_distill_loss_bwd": ([ctypes.POINTER(DistillCfg), c_int, c_int, c_int, P, P, P, P, P, P, P], c_int),
         "hiseg_seg_confusion": ([P, c_int, P, P, c_int, c_int, c_ll, P, P], c_int),
+        "hiseg_pil_bilinear_table": ([c_int, c_int, P, P, P], c_int),
+        "hiseg_pil_resample_h": ([P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, P], c_int),
+        "hiseg_pil_resample_v": ([P, c_int, c_int, c_int, c_int, c_int, c_int, P, P, c_int, P, P], c_int),
+        "hiseg_roi_targets": ([P, P, c_int, c_int, c_int, P, P], c_int),
         "hiseg_optim_blocks": ([], c_int),
         "hiseg_grad_norm_partials": ([P, c_ll, P, P], c_int),
         "hiseg_adamw_step": ([P, P, P, P, c_ll, c_float, c_float, c_float, c_float, c_float, c_float, c_float, P,
