@@ -236,6 +236,56 @@ def eval_bench(device, steps=20, n_roi=2048, mh=128, mw=96):
                                    f"(argmax + per-sample 5x4 histogram; every evaluate_model metric derives from it)"}}
 
 
+def data_bench(device, steps=10, batch=32, src_hw=(480, 640), image_size=(640, 640), mask_hw=(128, 96)):
+    """(f)-row 2, on-device data path: a C3-shaped batch (32 decoded 480x640 RGB images, 3 instance masks
+    each) -> PIL-exact 640x640 f32 CHW images + 3-class 128x96 ROI targets (resize_bilinear_pil +
+    roi_targets, the two passes hiseg.GpuRoiBatchBuilder launches).  Inputs resident in HBM.  Beside it
+    the reference's own host path for one image: PIL Image.resize (the library dataset.py:98 calls)."""
+    import numpy as np
+    from PIL import Image
+    from hiseg.data import resize_bilinear_pil, roi_targets
+    g = torch.Generator(device=device).manual_seed(3)
+    H0, W0 = src_hw
+    imgs = torch.randint(0, 256, (batch, H0, W0, 3), dtype=torch.uint8, device=device, generator=g)
+    masks = (torch.rand(batch * 3, H0, W0, device=device, generator=g) > 0.5).to(torch.uint8).reshape(-1)
+    descs = [(i * 3 * H0 * W0, 3, i % 3, H0, W0, 100, 120, 420, 600) for i in range(batch)]
+
+    def step():
+        resize_bilinear_pil(imgs, image_size)
+        roi_targets(masks, descs, mask_hw, image_size)
+
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    # algorithmic bytes: source image read once, the resized row strip written + read once (8-bit), the
+    # f32 output written; targets: (1 + instances) bytes gathered + 8 written per mask pixel
+    rows = H0   # vertical support of a 480 -> 640 upscale spans every source row
+    nbytes = batch * (H0 * W0 * 3 + 2 * rows * image_size[0] * 3 + 3 * image_size[0] * image_size[1] * 4
+                      + mask_hw[0] * mask_hw[1] * (3 + 8))
+    host = np.asarray(imgs[0].cpu())
+    pil = Image.fromarray(host)
+    pil.resize(image_size, Image.BILINEAR)
+    t1 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t1 < 2.0:
+        np.asarray(pil.resize(image_size, Image.BILINEAR), dtype=np.float32) / 255.0
+        n += 1
+    cpu_ips = n / (time.perf_counter() - t1)
+    return {"metric": "training batches built on the GPU (images/s)", "value": round(batch / dt, 1),
+            "unit": "images/s", "ms_per_batch": round(dt * 1e3, 3),
+            "roofline": {"bound": "hbm", "achieved": round(nbytes / dt / 1e9, 1), "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": round(nbytes / dt / 1e9 / PEAK_HBM_GBS, 4)},
+            "cpu_reference": {"value": round(cpu_ips, 1), "unit": "images/s", "cores": 1, "kind": "reference",
+                              "sample": "PIL Image.resize(640x640, BILINEAR) + /255 of one 480x640 image, 2 s loop"},
+            "config": {"workload": f"{batch} x {H0}x{W0} RGB -> {image_size[0]}x{image_size[1]} f32 CHW + "
+                                   f"{mask_hw[0]}x{mask_hw[1]} ROI targets from 3 instance masks per image"}}
+
+
 def cpu_baseline(seconds_budget=30.0):
     """The oracle (float32 CPU restatement of the reference path) on a bounded sample of the same
     workload: 1 image 480x640 with 8 ROIs through UNet + ROI head (exported contract)."""
@@ -314,6 +364,7 @@ def main():
     if not args.train_only and world == 1:
         torch.cuda.empty_cache()
         out["eval"] = eval_bench(device)
+        out["datapath"] = data_bench(device)
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline and not args.train_only:
             out["cpu_baseline"] = cpu_baseline()
