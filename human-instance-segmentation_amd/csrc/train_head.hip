@@ -190,6 +190,36 @@ __global__ void __launch_bounds__(128) sum_rows_kernel(const float* part, int ro
   out[c] = acc ? (float)(out[c] + s) : (float)s;
 }
 
+// First level of sum_rows for tall inputs: split s (rows [s*R, s*R+R)) of a 64-column tile, 4 row lanes per
+// column; the split's sum overwrites its first row (read only by this block), so the second level sums
+// ceil(rows/R) rows of stride R*ld.  part is scratch: its contents are consumed.
+__global__ void __launch_bounds__(256) sum_rows_split_kernel(float* part, int rows, int ld, int cols, int R) {
+  __shared__ double red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), lane = threadIdx.x >> 6;
+  const long long r0 = (long long)blockIdx.y * R;
+  const long long r1 = r0 + R < rows ? r0 + R : rows;
+  double s = 0;
+  if (c < cols)
+    for (long long r = r0 + lane; r < r1; r += 4) s += part[r * ld + c];
+  red[lane][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (lane == 0 && c < cols)
+    part[r0 * ld + c] = (float)(red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]);
+}
+
+// out[c] (+)= sum_r part[r*ld + c]; consumes part (scratch) when rows > 64
+static void sum_rows(float* part, int rows, int ld, int cols, float* out, int acc, hipStream_t s) {
+  if (rows <= 64) {
+    hipLaunchKernelGGL(sum_rows_kernel, dim3((cols + 127) / 128), dim3(128), 0, s, part, rows, ld, cols, out, acc);
+    return;
+  }
+  int R = (rows + 63) / 64;
+  R = R < 64 ? 64 : R;
+  const int S = (rows + R - 1) / R;
+  hipLaunchKernelGGL(sum_rows_split_kernel, dim3((cols + 63) / 64, S), dim3(256), 0, s, part, rows, ld, cols, R);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3((cols + 127) / 128), dim3(128), 0, s, part, S, R * ld, cols, out, acc);
+}
+
 // dx = dout*mul*att + dstats0 / C + [c == argmax] * dstats1
 template <typename T>
 __global__ void __launch_bounds__(256) sa_bwd3_kernel(const void* dout, long long P, int HW, int C, const float* att,
@@ -234,6 +264,56 @@ __global__ void __launch_bounds__(256) ca_gap_kernel(const void* x, const void* 
     }
     part[((long long)n * kGapSplits + s) * C + c] = acc;
   }
+}
+
+// Same partials, 16-B loads: 256 threads = (256 / nch) pixel lanes x nch channel chunks (nch = C / chunk
+// divides 256), lanes reduced in LDS.
+template <typename T>
+__global__ void __launch_bounds__(256) ca_gap_vec_kernel(const void* x, const void* dout, const float* mul, int HW,
+                                                         int C, float* part) {
+  constexpr int K = Chunk<T>::N;
+  extern __shared__ float red[];   // [R][C]
+  const int n = blockIdx.x, sp = blockIdx.y;
+  const int nch = C / K, R = 256 / nch;
+  const int ch = threadIdx.x % nch, lane = threadIdx.x / nch;
+  const int p0 = (int)((long long)HW * sp / kGapSplits), p1 = (int)((long long)HW * (sp + 1) / kGapSplits);
+  float acc[K], v[K], g[K];
+#pragma unroll
+  for (int e = 0; e < K; ++e) acc[e] = 0.f;
+  const uint4* xs = reinterpret_cast<const uint4*>(x) + (long long)n * HW * nch + ch;
+  const uint4* ds = dout ? reinterpret_cast<const uint4*>(dout) + (long long)n * HW * nch + ch : nullptr;
+  for (int p = p0 + lane; p < p1; p += R) {
+    Chunk<T>::unpack(xs[(long long)p * nch], v);
+    if (ds) {
+      Chunk<T>::unpack(ds[(long long)p * nch], g);
+#pragma unroll
+      for (int e = 0; e < K; ++e) v[e] *= g[e];
+    }
+#pragma unroll
+    for (int e = 0; e < K; ++e) acc[e] += v[e];
+  }
+  if (ds && mul) {
+#pragma unroll
+    for (int e = 0; e < K; ++e) acc[e] *= mul[(long long)n * C + ch * K + e];
+  }
+#pragma unroll
+  for (int e = 0; e < K; ++e) red[lane * C + ch * K + e] = acc[e];
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float s = 0.f;
+    for (int l = 0; l < R; ++l) s += red[l * C + c];
+    part[((long long)n * kGapSplits + sp) * C + c] = s;
+  }
+}
+
+template <typename T>
+static void ca_gap(const void* x, const void* dout, const float* mul, int N, int HW, int C, float* part, hipStream_t s) {
+  const int nch = C / Chunk<T>::N;
+  if (nch <= 256 && 256 % nch == 0)
+    hipLaunchKernelGGL(ca_gap_vec_kernel<T>, dim3(N, kGapSplits), dim3(256), (size_t)256 * Chunk<T>::N * sizeof(float),
+                       s, x, dout, mul, HW, C, part);
+  else
+    hipLaunchKernelGGL(ca_gap_kernel<T>, dim3(N, kGapSplits), dim3(256), 0, s, x, dout, mul, HW, C, part);
 }
 
 __device__ __forceinline__ float act_f(float v, int act) { return apply_act(v, act); }
@@ -281,10 +361,11 @@ __global__ void __launch_bounds__(256) ca_apply_kernel(const void* x, int N, int
                                                        const float* mul, void* out) {
   constexpr int K = Chunk<T>::N;
   const int nch = C / K;
-  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (gid >= (long long)N * HW * nch) return;
-  const int ch = (int)(gid % nch);
-  const long long n = gid / nch / HW;
+  const int li = blockIdx.x * 256 + threadIdx.x;   // chunk within image blockIdx.y
+  if (li >= HW * nch) return;
+  const int ch = li % nch;
+  const long long n = blockIdx.y;
+  const long long gid = n * HW * nch + li;
   float v[K];
   Chunk<T>::unpack(reinterpret_cast<const uint4*>(x)[gid], v);
   const float* g = gate + n * C + ch * K;
@@ -338,10 +419,11 @@ __global__ void __launch_bounds__(256) ca_dx_kernel(const void* dout, int N, int
                                                     const float* mul, const float* dgap, void* dx) {
   constexpr int K = Chunk<T>::N;
   const int nch = C / K;
-  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (gid >= (long long)N * HW * nch) return;
-  const int ch = (int)(gid % nch);
-  const long long n = gid / nch / HW;
+  const int li = blockIdx.x * 256 + threadIdx.x;   // chunk within image blockIdx.y
+  if (li >= HW * nch) return;
+  const int ch = li % nch;
+  const long long n = blockIdx.y;
+  const long long gid = n * HW * nch + li;
   float v[K];
   Chunk<T>::unpack(reinterpret_cast<const uint4*>(dout)[gid], v);
   const float inv = 1.f / (float)HW;
@@ -680,7 +762,7 @@ extern "C" int hiseg_attn_spatial_bwd(int dtype, const void* x, int N, int H, in
                                        att, chan_mul, dpre));
   hipLaunchKernelGGL(sa_bwd2_kernel, dim3(nb(P, 256)), dim3(256), 0, s, dpre, N, H, W, w7, k, dstats);
   hipLaunchKernelGGL(sa_dw_kernel, dim3(N * H), dim3(256), 0, s, dpre, stats, N, H, W, k, part);
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(nb(2 * k * k, 128)), dim3(128), 0, s, part, N * H, 2 * k * k, 2 * k * k, dw7, 1);
+  sum_rows(part, N * H, 2 * k * k, 2 * k * k, dw7, 1, s);
   DISPATCH_T(dtype, hipLaunchKernelGGL(sa_bwd3_kernel<T>, dim3(nb(P * (C / chunk_of(dtype)), 256)), dim3(256), 0, s,
                                        dout, P, H * W, C, att, chan_mul, dstats, argmax, dx));
   return hiseg_check_launch("attn_spatial_bwd");
@@ -697,11 +779,10 @@ extern "C" int hiseg_attn_channel_train_fwd(int dtype, const void* x, int N, int
                 "attn_channel_train_fwd: bad args");
   HISEG_REQUIRE(C > 0 && C % chunk_of(dtype) == 0, HISEG_ERR_BAD_SHAPE, "attn_channel_train_fwd: C alignment");
   hipStream_t s = (hipStream_t)stream;
-  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_gap_kernel<T>, dim3(N, kGapSplits), dim3(256), 0, s, x, nullptr, nullptr, HW,
-                                       C, ws));
+  DISPATCH_T(dtype, ca_gap<T>(x, nullptr, nullptr, N, HW, C, ws, s));
   hipLaunchKernelGGL(ca_mlp_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, ws, HW, C, Cr, w1, w2, act,
                      gap, hpre, gate);
-  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_apply_kernel<T>, dim3(nb((long long)N * HW * (C / chunk_of(dtype)), 256)),
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_apply_kernel<T>, dim3(nb((long long)HW * (C / chunk_of(dtype)), 256), N),
                                        dim3(256), 0, s, x, N, HW, C, gate, chan_mul, out));
   return hiseg_check_launch("attn_channel_train_fwd");
 }
@@ -717,13 +798,12 @@ extern "C" int hiseg_attn_channel_bwd(int dtype, const void* x, int N, int HW, i
   float* part = ws;
   float* dgap = ws + (long long)N * kGapSplits * C;
   float* wpart = dgap + (long long)N * C;
-  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_gap_kernel<T>, dim3(N, kGapSplits), dim3(256), 0, s, x, dout, chan_mul, HW, C,
-                                       part));
+  DISPATCH_T(dtype, ca_gap<T>(x, dout, chan_mul, N, HW, C, part, s));
   hipLaunchKernelGGL(ca_mlp_bwd_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, part, C, Cr, w1, w2, act,
                      gap, hpre, gate, dgap, wpart);
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(nb(C * Cr, 128)), dim3(128), 0, s, wpart, N, 2 * C * Cr, C * Cr, dw1, 1);
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(nb(C * Cr, 128)), dim3(128), 0, s, wpart + C * Cr, N, 2 * C * Cr, C * Cr, dw2, 1);
-  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_dx_kernel<T>, dim3(nb((long long)N * HW * (C / chunk_of(dtype)), 256)),
+  sum_rows(wpart, N, 2 * C * Cr, C * Cr, dw1, 1, s);
+  sum_rows(wpart + C * Cr, N, 2 * C * Cr, C * Cr, dw2, 1, s);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_dx_kernel<T>, dim3(nb((long long)HW * (C / chunk_of(dtype)), 256), N),
                                        dim3(256), 0, s, dout, N, HW, C, gate, chan_mul, dgap, dx));
   return hiseg_check_launch("attn_channel_bwd");
 }
@@ -742,11 +822,10 @@ extern "C" int hiseg_se_train_fwd(int dtype, const void* x, int N, int HW, int C
                 HISEG_ERR_BAD_ARG, "se_train_fwd: bad args");
   HISEG_REQUIRE(C > 0 && C % chunk_of(dtype) == 0, HISEG_ERR_BAD_SHAPE, "se_train_fwd: C alignment");
   hipStream_t s = (hipStream_t)stream;
-  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_gap_kernel<T>, dim3(N, kGapSplits), dim3(256), 0, s, x, nullptr, nullptr, HW,
-                                       C, ws));
+  DISPATCH_T(dtype, ca_gap<T>(x, nullptr, nullptr, N, HW, C, ws, s));
   hipLaunchKernelGGL(ca_mlp_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, ws, HW, C, Cr, w1, w2, act,
                      gap, hpre, gate, b1, b2);
-  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_apply_kernel<T>, dim3(nb((long long)N * HW * (C / chunk_of(dtype)), 256)),
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_apply_kernel<T>, dim3(nb((long long)HW * (C / chunk_of(dtype)), 256), N),
                                        dim3(256), 0, s, x, N, HW, C, gate, nullptr, out));
   return hiseg_check_launch("se_train_fwd");
 }
@@ -763,15 +842,14 @@ extern "C" int hiseg_se_train_bwd(int dtype, const void* x, int N, int HW, int C
   float* dgap = ws + (long long)N * kGapSplits * C;
   float* wpart = dgap + (long long)N * C;
   float* bpart = wpart + (long long)N * 2 * C * Cr;
-  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_gap_kernel<T>, dim3(N, kGapSplits), dim3(256), 0, s, x, dout, nullptr, HW, C,
-                                       part));
+  DISPATCH_T(dtype, ca_gap<T>(x, dout, nullptr, N, HW, C, part, s));
   hipLaunchKernelGGL(ca_mlp_bwd_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, part, C, Cr, w1, w2, act,
                      gap, hpre, gate, dgap, wpart, bpart);
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(nb(C * Cr, 128)), dim3(128), 0, s, wpart, N, 2 * C * Cr, C * Cr, dw1, 1);
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(nb(C * Cr, 128)), dim3(128), 0, s, wpart + C * Cr, N, 2 * C * Cr, C * Cr, dw2, 1);
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(nb(Cr, 128)), dim3(128), 0, s, bpart, N, Cr + C, Cr, db1, 1);
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(nb(C, 128)), dim3(128), 0, s, bpart + Cr, N, Cr + C, C, db2, 1);
-  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_dx_kernel<T>, dim3(nb((long long)N * HW * (C / chunk_of(dtype)), 256)),
+  sum_rows(wpart, N, 2 * C * Cr, C * Cr, dw1, 1, s);
+  sum_rows(wpart + C * Cr, N, 2 * C * Cr, C * Cr, dw2, 1, s);
+  sum_rows(bpart, N, Cr + C, Cr, db1, 1, s);
+  sum_rows(bpart + Cr, N, Cr + C, C, db2, 1, s);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_dx_kernel<T>, dim3(nb((long long)HW * (C / chunk_of(dtype)), 256), N),
                                        dim3(256), 0, s, dout, N, HW, C, gate, nullptr, dgap, dx));
   return hiseg_check_launch("se_train_bwd");
 }
@@ -826,7 +904,7 @@ extern "C" int hiseg_ubf_train_bwd(const hiseg_ubf_desc* d, const float* dlogits
                      g->du1_w, g->du1_b, g->dut_b);
   hipLaunchKernelGGL(ubf_bwd2_kernel, dim3(kUbfBlocks), dim3(256), 0, s, u, db_buf, coef, dlow, part);
   // dWt [ci][c][q] in the ConvTranspose2d layout [2][32][2][2] == (ci*32 + c)*4 + q
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(2), dim3(128), 0, s, part, kUbfBlocks, 256, 256, g->dut_w, 1);
+  sum_rows(part, kUbfBlocks, 256, 256, g->dut_w, 1, s);
   (void)PL;
   return hiseg_check_launch("ubf_train_bwd");
 }
@@ -843,7 +921,7 @@ extern "C" int hiseg_pw2_bwd(int dtype, const void* tfeat, long long P, int Ct, 
   const int R = 256 / nch;
   const size_t lds = (size_t)R * (2 * Ct + 2) * sizeof(float);
   DISPATCH_T(dtype, hipLaunchKernelGGL(pw2_bwd_kernel<T>, dim3(kPw2Blocks), dim3(256), lds, s, tfeat, P, Ct, dtn, w, dt, ws));
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(nb(2 * Ct, 128)), dim3(128), 0, s, ws, kPw2Blocks, 2 * Ct + 2, 2 * Ct, dw, 1);
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(128), 0, s, ws + 2 * Ct, kPw2Blocks, 2 * Ct + 2, 2, db, 1);
+  sum_rows(ws, kPw2Blocks, 2 * Ct + 2, 2 * Ct, dw, 1, s);
+  sum_rows(ws + 2 * Ct, kPw2Blocks, 2 * Ct + 2, 2, db, 1, s);
   return hiseg_check_launch("pw2_bwd");
 }
