@@ -337,6 +337,7 @@ def main():
     ap.add_argument("--no-train", action="store_true")
     ap.add_argument("--train-only", action="store_true")
     ap.add_argument("--no-distill", action="store_true")
+    ap.add_argument("--distill-only", action="store_true", help="only the C5 distillation line (profiling)")
     ap.add_argument("--serial", action="store_true", help="one stream (no UNet/head overlap across steps)")
     args = ap.parse_args()
 
@@ -353,6 +354,9 @@ def main():
 
     import hiseg  # noqa: F401
     out = {}
+    if args.distill_only:
+        args.train_only, args.no_train = True, True
+        out["distill"] = distill_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2)
     if not args.train_only:
         out = infer_bench(args, device, dtype, rank, world, dist)
     if not args.no_train:

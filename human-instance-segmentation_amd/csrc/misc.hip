@@ -163,32 +163,42 @@ __global__ void __launch_bounds__(256) gap_reduce_kernel(const float* partial, i
   if (sg == 0 && c < C) sums[(long long)n * C + c] = red[t] + red[t + 64] + red[t + 128] + red[t + 192];
 }
 
-// SE MLP per image from the pooled sums: hidden = act(W1 mean + b1) with one wavefront per hidden unit
-// (lanes stride the C inputs, coalesced rows of W1, DPP/shuffle reduction), gate = sigmoid(W2 hidden + b2).
-__global__ void __launch_bounds__(256) se_gate_kernel(const float* sums, int HW, int C, const float* w1,
-                                                      const float* b1, int Cr, const float* w2, const float* b2, int act,
-                                                      float* gate) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* mean = sm;
-  float* hid = sm + C;
-  const int n = blockIdx.x;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+// SqueezeExcite MLP from the pooled sums, spread over the chip (one block per image would leave most CUs
+// idle at the distillation batch of 4): hidden = act(W1 mean + b1), one wave per hidden unit, grid
+// (N, ceil(Cr / 4)); gate = sigmoid(W2 hidden + b2), one wave per channel, grid (N, ceil(C / 4)).  Lanes
+// stride the reduction axis (coalesced weight rows), xor-shuffle reduction.
+__global__ void __launch_bounds__(256) se_hidden_kernel(const float* sums, int HW, int C, const float* w1,
+                                                        const float* b1, int Cr, int act, float* hid) {
+  const int n = blockIdx.x, lane = threadIdx.x & 63;
+  const int r = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (r >= Cr) return;
   const float inv = 1.f / (float)HW;
-  for (int c = t; c < C; c += 256) mean[c] = sums[(long long)n * C + c] * inv;
-  __syncthreads();
-  for (int r = wave; r < Cr; r += 4) {
-    float s = 0.f;
-    for (int c = lane; c < C; c += 64) s += w1[(long long)r * C + c] * mean[c];
+  const float* m = sums + (long long)n * C;
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) s += w1[(long long)r * C + c] * (m[c] * inv);
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    if (lane == 0) hid[r] = apply_act(s + (b1 ? b1[r] : 0.f), act);
-  }
-  __syncthreads();
-  for (int c = t; c < C; c += 256) {
-    float s = b2 ? b2[c] : 0.f;
-    for (int r = 0; r < Cr; ++r) s += w2[(long long)c * Cr + r] * hid[r];
-    gate[(long long)n * C + c] = sigmoidf_(s);
-  }
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) hid[(long long)n * Cr + r] = apply_act(s + (b1 ? b1[r] : 0.f), act);
+}
+
+__global__ void __launch_bounds__(256) se_out_kernel(const float* hid, int C, int Cr, const float* w2, const float* b2,
+                                                     float* gate) {
+  const int n = blockIdx.x, lane = threadIdx.x & 63;
+  const int c = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (c >= C) return;
+  const float* h = hid + (long long)n * Cr;
+  float s = 0.f;
+  for (int r = lane; r < Cr; r += 64) s += w2[(long long)c * Cr + r] * h[r];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) gate[(long long)n * C + c] = sigmoidf_(s + (b2 ? b2[c] : 0.f));
+}
+
+// gate holds the pooled sums on entry and the gate on exit; scratch (>= N * Cr floats) takes the hidden units
+static void se_mlp(const float* w1, const float* b1, int Cr, const float* w2, const float* b2, int act, int N, int HW,
+                   int C, float* scratch, float* gate, hipStream_t s) {
+  hipLaunchKernelGGL(se_hidden_kernel, dim3(N, (Cr + 3) / 4), dim3(256), 0, s, gate, HW, C, w1, b1, Cr, act, scratch);
+  hipLaunchKernelGGL(se_out_kernel, dim3(N, (C + 3) / 4), dim3(256), 0, s, scratch, C, Cr, w2, b2, gate);
 }
 
 template <typename T>
@@ -570,14 +580,14 @@ extern "C" int hiseg_se_gate_fwd(int dtype, const void* x, int N, int HW, int C,
   HISEG_REQUIRE(C % K == 0, HISEG_ERR_BAD_SHAPE, "se_gate: C must be chunk aligned");
   const int nch = C / K;
   const int splits = hiseg_gap_splits(HW);
+  HISEG_REQUIRE((long long)splits * C >= Cr, HISEG_ERR_BAD_SHAPE, "se_gate: partial buffer below N * Cr");
   const size_t lds = nch >= 256 ? 0 : (size_t)(256 / nch) * C * sizeof(float);
   hipStream_t s = (hipStream_t)stream;
   DISPATCH_T(dtype, gap_partial_kernel, dim3(N, splits), dim3(256), lds, s, x, HW, C, splits, partial);
   // the pooled sums go through the gate buffer: each se_gate block reads its image's row into LDS before
   // it overwrites that row with the gate
   hipLaunchKernelGGL(gap_reduce_kernel, dim3(N, (C + 63) / 64), dim3(256), 0, s, partial, splits, C, gate);
-  hipLaunchKernelGGL(se_gate_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, gate, HW, C, w1, b1, Cr,
-                     w2, b2, act, gate);
+  se_mlp(w1, b1, Cr, w2, b2, act, N, HW, C, partial, gate, s);   // partial (consumed) holds the hidden units
   return hiseg_check_launch("se_gate");
 }
 
@@ -642,16 +652,16 @@ extern "C" int hiseg_dwconv_gap_fwd(int dtype, const void* in, int N, int H, int
                        (hipStream_t)stream);
 }
 
-extern "C" int hiseg_se_gate_partials_fwd(const float* partial, int splits, int N, int HW, int C, const float* w1,
+extern "C" int hiseg_se_gate_partials_fwd(float* partial, int splits, int N, int HW, int C, const float* w1,
                                           const float* b1, int Cr, const float* w2, const float* b2, int act, float* gate,
                                           hiseg_stream_t stream) {
   HISEG_REQUIRE(partial && w1 && w2 && gate && splits > 0 && N > 0 && HW > 0 && C > 0 && Cr > 0, HISEG_ERR_BAD_ARG,
                 "se_gate_partials: bad args");
   hipStream_t s = (hipStream_t)stream;
   // pooled sums through the gate buffer (read into LDS per image before the gate overwrites them)
+  HISEG_REQUIRE((long long)splits * C >= Cr, HISEG_ERR_BAD_SHAPE, "se_gate_partials: partial buffer below N * Cr");
   hipLaunchKernelGGL(gap_reduce_kernel, dim3(N, (C + 63) / 64), dim3(256), 0, s, partial, splits, C, gate);
-  hipLaunchKernelGGL(se_gate_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, gate, HW, C, w1, b1, Cr,
-                     w2, b2, act, gate);
+  se_mlp(w1, b1, Cr, w2, b2, act, N, HW, C, partial, gate, s);   // partial (consumed) holds the hidden units
   return hiseg_check_launch("se_gate_partials");
 }
 

@@ -159,7 +159,8 @@ int hiseg_dw_gap_tiles(int N, int Ho, int Wo);
 int hiseg_dwconv_gap_fwd(int dtype, const void* in, int N, int H, int W, int C, int K, int stride,
                          const float* w, const float* scale, const float* shift, int act, void* out,
                          int Ho, int Wo, float* gap_partial, hiseg_stream_t stream);
-int hiseg_se_gate_partials_fwd(const float* partial, int splits, int N, int HW, int C, const float* w1,
+/* partial is consumed: after the pooled sums are read, its first N * Cr floats hold the hidden units. */
+int hiseg_se_gate_partials_fwd(float* partial, int splits, int N, int HW, int C, const float* w1,
                                const float* b1, int Cr, const float* w2, const float* b2, int act,
                                float* gate, hiseg_stream_t stream);
 
