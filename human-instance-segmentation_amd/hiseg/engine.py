@@ -59,31 +59,42 @@ def _bn(m: Optional[nn.Module]):
     raise NotImplementedError(f"normalisation {type(m).__name__}")
 
 
-def _signature(model: nn.Module):
-    return tuple((t.data_ptr(), t._version) for t in model.parameters()) + \
-        tuple((t.data_ptr(), t._version) for t in model.buffers())
+def _signature(tensors):
+    return tuple((t.data_ptr(), t._version) for t in tensors if t is not None)
+
+
+def _bn_tensors(bn):
+    if bn is None:
+        return ()
+    return (getattr(bn, "weight", None), getattr(bn, "bias", None), getattr(bn, "running_mean", None),
+            getattr(bn, "running_var", None))
 
 
 class Ctx:
-    """Per-forward context: compute dtype, device and the model's plan cache."""
+    """Per-forward context: compute dtype, device and the model's plan cache.
+
+    Every plan records the (storage, version) of the tensors it was packed from and is rebuilt only when one
+    of them changed -- so a training step that updates some parameters (or train-mode BN running statistics)
+    re-packs just those layers, not the whole model (the frozen encoder of the distillation student, the
+    teacher)."""
 
     def __init__(self, root: nn.Module, dtype: torch.dtype, device: torch.device):
         if dtype not in (torch.float32, torch.bfloat16):
             raise TypeError(f"hiseg compute dtype must be float32 or bfloat16, got {dtype}")
         self.dtype, self.device = dtype, device
-        sig = _signature(root)
         cache = root.__dict__.get("_hiseg_plans")
-        if cache is None or cache["dtype"] != dtype or cache["device"] != device or cache["sig"] != sig:
-            cache = {"dtype": dtype, "device": device, "sig": sig, "plans": {}}
+        if cache is None or cache["dtype"] != dtype or cache["device"] != device:
+            cache = {"dtype": dtype, "device": device, "plans": {}}
             root.__dict__["_hiseg_plans"] = cache
         self.plans: Dict = cache["plans"]
 
-    def _get(self, key, build):
-        p = self.plans.get(key)
-        if p is None:
-            p = build()
-            self.plans[key] = p
-        return p
+    def _get(self, key, build, deps=()):
+        sig = _signature(deps)
+        ent = self.plans.get(key)
+        if ent is None or ent[0] != sig:
+            ent = (sig, build())
+            self.plans[key] = ent
+        return ent[1]
 
     def conv(self, conv: nn.Conv2d, bn=None, act: int = ACT_NONE, split=None) -> ops.ConvPlan:
         def build():
@@ -91,25 +102,25 @@ class Ctx:
             assert conv.kernel_size[0] == conv.kernel_size[1] and conv.stride[0] == conv.stride[1]
             return ops.pack_conv(conv.weight, conv.bias, _bn(bn), act, self.dtype, self.device,
                                  stride=conv.stride[0], pad=conv.padding[0], split=split)
-        return self._get(("conv", id(conv), act, split), build)
+        return self._get(("conv", id(conv), act, split), build, (conv.weight, conv.bias) + _bn_tensors(bn))
 
     def convT(self, conv: nn.ConvTranspose2d, bn=None, act: int = ACT_NONE) -> ops.ConvPlan:
         def build():
             assert conv.kernel_size == (2, 2) and conv.stride == (2, 2) and conv.padding == (0, 0)
             return ops.pack_convT2x2(conv.weight, conv.bias, _bn(bn), act, self.dtype, self.device)
-        return self._get(("convT", id(conv), act), build)
+        return self._get(("convT", id(conv), act), build, (conv.weight, conv.bias) + _bn_tensors(bn))
 
     def f32(self, t: torch.Tensor, shape=None) -> torch.Tensor:
         def build():
             v = t.detach().to(device=self.device, dtype=torch.float32).contiguous()
             return v.view(shape) if shape is not None else v
-        return self._get(("f32", id(t), shape), build)
+        return self._get(("f32", id(t), shape), build, (t,))
 
     def affine(self, key, cout, bias, bn):
         def build():
             s, h = ops.fold_affine(cout, bias, _bn(bn), self.device)
             return s.contiguous(), h.contiguous()
-        return self._get(("aff", key), build)
+        return self._get(("aff", key), build, (bias,) + _bn_tensors(bn))
 
     def dw(self, conv: nn.Conv2d, bn):
         def build():
@@ -117,7 +128,7 @@ class Ctx:
             w = conv.weight.detach().float().to(self.device).view(c, k * k).t().contiguous()
             s, h = ops.fold_affine(c, conv.bias, _bn(bn), self.device)
             return w, s.contiguous(), h.contiguous(), k, conv.stride[0]
-        return self._get(("dw", id(conv)), build)
+        return self._get(("dw", id(conv)), build, (conv.weight, conv.bias) + _bn_tensors(bn))
 
 
 def _check_input(x: torch.Tensor, what: str):

@@ -53,6 +53,7 @@ class FusedAdamW(torch.optim.Optimizer):
         self.partial = None
         self.last_norm: Optional[torch.Tensor] = None
         self._pending_state = None
+        self._bump = None
 
     @property
     def lr(self) -> float:
@@ -109,6 +110,11 @@ class FusedAdamW(torch.optim.Optimizer):
                                      float(eps), float(wd), float(bc1), float(bc2),
                                      self.partial.data_ptr(), float(self.max_grad_norm) if clip else 0.0,
                                      self.last_norm.data_ptr(), s), "adamw_step")
+        # the kernel wrote the parameters in place: bump their versions so plans packed from them (eval
+        # forward, frozen-layer caches keyed by tensor version) are rebuilt
+        if self._bump is None:
+            self._bump = [p for _, p, _ in self._slots()]
+        torch.autograd.graph.increment_version(self._bump)
         return self.last_norm
 
     # ---------------------------------------------------------------- torch.optim.AdamW state layout

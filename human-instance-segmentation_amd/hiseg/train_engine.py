@@ -446,6 +446,8 @@ def bn_forward(T: Tape, bn: nn.BatchNorm2d, z: Act, *, act: int, residual: Optio
                                _ptr(bn.running_mean) if track else None, _ptr(bn.running_var) if track else None,
                                st.mean.data_ptr(), st.invstd.data_ptr(), st.scale.data_ptr(), st.shift.data_ptr(),
                                _stream()), "bn_finalize")
+    if track:   # the kernel updated the running statistics in place: invalidate eval plans folded from them
+        torch.autograd.graph.increment_version([bn.running_mean, bn.running_var])
     y = out if out is not None else Act.new(z.N, z.H, z.W, C, z.dtype, z.t.device, cpad=z.cstride)
     d = L.BnApplyDesc()
     d.dtype, d.P, d.HW, d.C = hdtype(z.dtype), P, z.H * z.W, C
@@ -824,6 +826,7 @@ def hier_head_train(T: Tape, head: nn.Module, feat: Act):
     _chk(lib.hiseg_ubf_train_fwd(ctypes.byref(ud), float(ubn.eps), float(ubn.momentum or 0.1),
                                  ubn.running_mean.data_ptr(), ubn.running_var.data_ptr(), ws.data_ptr(), _stream()),
          "ubf_train_fwd")
+    torch.autograd.graph.increment_version([ubn.running_mean, ubn.running_var])
     T.keep.extend([bst, ws])
     aux = {"bg_fg_logits": bgfg, "target_nontarget_logits": tn}
 

@@ -625,3 +625,38 @@ def test_checkpoint_resume_continues_training_identically(tmp_path):
     assert sb["opt"].param_groups[0]["lr"] == sa["opt"].param_groups[0]["lr"]
     for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
         assert torch.equal(pa, pb), n
+
+
+def test_eval_after_training_sees_the_updated_weights():
+    """Eval plans are cached per layer and keyed by the versions of the tensors they were packed from;
+    FusedAdamW and the train-mode BN kernels write parameters / running statistics in place and must
+    invalidate them: an eval forward after a train step equals a fresh model loaded with the new state."""
+    import hiseg
+    images = torch.from_numpy(filler.uniform(291, (2, 3, 160, 192))).to(DEV)
+    rois = torch.from_numpy(filler.box_rois(292, 2, 1)).to(DEV)
+    tgt = torch.from_numpy(filler.ellipse_targets(293, 2, 128, 96)).to(DEV)
+
+    def prep(m):
+        for mm in (m.roi_align_mask, m.roi_align_rgb):
+            mm.spatial_scale_h, mm.spatial_scale_w = 160, 192
+        return m
+
+    m = prep(_model(torch.float32).to(DEV))
+    with torch.no_grad():
+        before, _ = m.eval()(images, rois)
+    m.train()
+    logits, aux = m(images, rois)
+    loss, _ = hiseg.RefinedHierarchicalLoss()(logits, tgt, aux)
+    opt = hiseg.FusedAdamW(m, lr=1e-3)
+    opt.zero_grad()
+    loss.backward()
+    opt.step()
+    with torch.no_grad():
+        after, _ = m.eval()(images, rois)
+    fresh = _model(torch.float32)
+    fresh.load_state_dict({k: v.detach().cpu() for k, v in m.state_dict().items()})
+    fresh = prep(fresh.to(DEV))
+    with torch.no_grad():
+        ref, _ = fresh.eval()(images, rois)
+    assert not torch.equal(before, after)
+    assert torch.equal(after, ref)
