@@ -40,7 +40,11 @@ __device__ __forceinline__ unsigned long long stamp_now() {
   return t;
 }
 
-template <int BCO, int BPX, int WCO, int WPX, int STAGES, bool NOLOAD = false, bool STAMP = false>
+// PRIO: s_setprio 1 around each MFMA cluster (cdna_hip_programming.md T2).  LATE: the next stage's DMA is
+// issued after the first K-substep's fragment reads and MFMAs instead of right after the barrier, so the
+// DMA issue of one wave overlaps the MFMAs of the other waves on its SIMD.  Same addresses either way.
+template <int BCO, int BPX, int WCO, int WPX, int STAGES, bool NOLOAD = false, bool STAMP = false, bool PRIO = false,
+          bool LATE = false>
 __global__ void __launch_bounds__(64 * WCO * WPX) conv_fast_kernel(ConvArgs a) {
   unsigned long long st0 = 0, st1 = 0, st2 = 0;
   if constexpr (STAMP) st0 = stamp_now();
@@ -169,7 +173,7 @@ __global__ void __launch_bounds__(64 * WCO * WPX) conv_fast_kernel(ConvArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (!NOLOAD && kb + STAGES - 1 < nK) issue(kb + STAGES - 1, (kb + STAGES - 1) % STAGES);
+    if (!LATE && !NOLOAD && kb + STAGES - 1 < nK) issue(kb + STAGES - 1, (kb + STAGES - 1) % STAGES);
 
     const uint4* sW = smem + (kb % STAGES) * STAGE;
     const uint4* sX = sW + BCO * 8;
@@ -181,12 +185,17 @@ __global__ void __launch_bounds__(64 * WCO * WPX) conv_fast_kernel(ConvArgs a) {
       for (int i = 0; i < TM; ++i) af[i] = sW[swz(wco * TM * 16 + i * 16 + (lane & 15), ch)];
 #pragma unroll
       for (int j = 0; j < TN; ++j) bfr[j] = sX[swz(wpx * TN * 16 + j * 16 + (lane & 15), ch)];
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[i]),
                                                               __builtin_bit_cast(bf16x8_t, bfr[j]), acc[i][j], 0, 0, 0);
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+      if constexpr (LATE) {
+        if (s == 0 && !NOLOAD && kb + STAGES - 1 < nK) issue(kb + STAGES - 1, (kb + STAGES - 1) % STAGES);
+      }
     }
   }
 
@@ -212,12 +221,13 @@ __global__ void __launch_bounds__(64 * WCO * WPX) conv_fast_kernel(ConvArgs a) {
   }
 }
 
-template <int BCO, int BPX, int WCO, int WPX, int STAGES, bool NOLOAD = false, bool STAMP = false>
+template <int BCO, int BPX, int WCO, int WPX, int STAGES, bool NOLOAD = false, bool STAMP = false, bool PRIO = false,
+          bool LATE = false>
 static int launch_fast(const ConvArgs& a, hipStream_t s) {
   const int npx = (a.M + BPX - 1) / BPX;
   const int nco = a.d.Cout_pad / BCO;
   const size_t lds = (size_t)STAGES * (BCO + BPX) * 8 * 16;
-  auto kern = conv_fast_kernel<BCO, BPX, WCO, WPX, STAGES, NOLOAD, STAMP>;
+  auto kern = conv_fast_kernel<BCO, BPX, WCO, WPX, STAGES, NOLOAD, STAMP, PRIO, LATE>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -258,6 +268,13 @@ int conv_fast_try(const ConvArgs& a, hipStream_t s, int variant) {
     case 9: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 2, 2, 2, true>(a, s); break;
     case 19: if (d.Cout_pad % 256) return 0; r = launch_fast<256, 256, 2, 4, 2, true>(a, s); break;
     case 18: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 2, 2, 2, false, true>(a, s); break;
+    // schedule variants of the production 128x128 configuration (variant 4)
+    case 60: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 2, 2, 2, false, false, true, false>(a, s); break;
+    case 61: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 2, 2, 2, false, false, false, true>(a, s); break;
+    case 62: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 2, 2, 2, false, false, true, true>(a, s); break;
+    case 63: if (d.Cout_pad % 64) return 0; r = launch_fast<64, 128, 1, 4, 2, false, false, false, true>(a, s); break;
+    case 64: if (d.Cout_pad % 64) return 0; r = launch_fast<64, 128, 1, 4, 2, false, false, true, false>(a, s); break;
+    case 65: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 2, 2, 3, false, false, true, false>(a, s); break;
     default: return 0;
   }
   return r < 0 ? r : 1;

@@ -292,7 +292,10 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
   // Automatic choice (variant 0) = the fastest measured configuration per layer class
   // (tools/conv_bench.py): LDS-DMA ring kernel, 128x128 tiles for Cout >= 128, 64x128 for 64.
   // Experimental kernels (halo / halo2 / halo3) run only when forced by variant.
-  if (variant >= 50) {
+  if (variant >= 60 && variant < 70) {
+    const int r = conv_fast_try(a, s, variant);
+    if (r != 0) return r < 0 ? r : HISEG_OK;
+  } else if (variant >= 50) {
     const int r = conv_small_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
   } else if (variant >= 40) {
@@ -309,7 +312,7 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
     if (r != 0) return r < 0 ? r : HISEG_OK;
   } else if (variant >= 0) {
     int v = variant;
-    if (v == 0) v = (d->Cout_pad % 128 == 0) ? 4 : 8;
+    if (v == 0) v = (d->Cout_pad % 128 == 0) ? 60 : 8;   // 60 = 4 with s_setprio around the MFMA clusters (+1..5 %)
     const int r = conv_fast_try(a, s, v);
     if (r != 0) return r < 0 ? r : HISEG_OK;
     if (variant == 0) {   // narrow / ragged layers: halo-tiled direct kernel

@@ -20,7 +20,7 @@ d_all = sorted((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r
 upper = d_all[len(d_all) // 2:]
 cut = 0.75 * upper[len(upper) // 2]
 d = [v for v in d_all if v > cut]
-print(json.dumps({"kernel": "conv_fast_kernel<128,128,2,2,2> grid 12288 x 256 (256->256 3x3 @64x48 x256 ROIs)",
+print(json.dumps({"kernel": "conv_fast_kernel<128,128,2,2,2,prio> grid 12288 x 256 (256->256 3x3 @64x48 x256 ROIs)",
                   "launches": len(d), "same_grid_launches": len(d_all), "cluster_cut_ms": round(cut, 4), "avg_ms": round(sum(d) / len(d), 4), "median_ms": round(d[len(d) // 2], 4),
                   "min_ms": round(d[0], 4), "max_ms": round(d[-1], 4),
                   "flop_per_launch": 927712935936.0,
