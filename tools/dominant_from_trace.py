@@ -7,19 +7,30 @@ class bench.py's HIP-event probe times, so the two averages can be compared.  Th
 256->256 1x1 (K = 256) and 128->256 3x3 (K = 1152) layers; the trace carries no shape, so the K = 2304
 class is taken as the launches longer than 0.75 x the median of the upper half (the three K values are
 9x / 2x apart, the clusters do not overlap).
-Usage: python tools/dominant_from_trace.py gpurun_out/prof_v3/trace_kernel_trace.csv > profiles/...json
+The bench's probe times the inference launches only; the trace of a full bench run also holds the same
+class from the train step (uncontended: no UNet overlapping it), so launches from the first training kernel
+on (bn_stats: train-mode BatchNorm) are dropped, and with --last N only the N latest inference launches
+(the timed steps: 9 per step) are kept.
+Usage: python tools/dominant_from_trace.py gpurun_out/prof_v5/trace_kernel_trace.csv [--last N] > profiles/...json
 """
 import csv
 import json
 import sys
 
 GRID = 12288 * 256
-rows = [r for r in csv.DictReader(open(sys.argv[1]))
-        if r["Kernel_Name"].startswith("void hiseg::conv_fast_kernel<128, 128") and int(r["Grid_Size_X"]) == GRID]
-d_all = sorted((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows)
+allrows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
+cut_t = next((int(r["Start_Timestamp"]) for r in allrows if "bn_stats" in r["Kernel_Name"]), None)
+rows = [r for r in allrows
+        if r["Kernel_Name"].startswith("void hiseg::conv_fast_kernel<128, 128") and int(r["Grid_Size_X"]) == GRID
+        and (cut_t is None or int(r["Start_Timestamp"]) < cut_t)]
+d_seq = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows]
+d_all = sorted(d_seq)
 upper = d_all[len(d_all) // 2:]
 cut = 0.75 * upper[len(upper) // 2]
-d = [v for v in d_all if v > cut]
+d = [v for v in d_seq if v > cut]
+if "--last" in sys.argv:
+    d = d[-int(sys.argv[sys.argv.index("--last") + 1]):]
+d = sorted(d)
 print(json.dumps({"kernel": "conv_fast_kernel<128,128,2,2,2,prio> grid 12288 x 256 (256->256 3x3 @64x48 x256 ROIs)",
                   "launches": len(d), "same_grid_launches": len(d_all), "cluster_cut_ms": round(cut, 4), "avg_ms": round(sum(d) / len(d), 4), "median_ms": round(d[len(d) // 2], 4),
                   "min_ms": round(d[0], 4), "max_ms": round(d[-1], 4),
