@@ -43,8 +43,13 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 // PRIO: s_setprio 1 around each MFMA cluster (cdna_hip_programming.md T2).  LATE: the next stage's DMA is
 // issued after the first K-substep's fragment reads and MFMAs instead of right after the barrier, so the
 // DMA issue of one wave overlaps the MFMAs of the other waves on its SIMD.  Same addresses either way.
+// EPI: the epilogue goes through LDS -- each lane writes its scaled / shifted / residual-added / activated
+// f32 fragments into a [BPX][BCO] tile (16-B chunks XOR-swizzled by row, conflict-free both ways), then the
+// workgroup stores whole output rows: consecutive lanes write consecutive channels of one pixel (for a
+// ConvTranspose tile: of one scattered output pixel), so every store instruction covers full lines instead
+// of 16 pixels x 32 B.  Same arithmetic and rounding as TileEpi::store.
 template <int BCO, int BPX, int WCO, int WPX, int STAGES, bool NOLOAD = false, bool STAMP = false, bool PRIO = false,
-          bool LATE = false>
+          bool LATE = false, bool EPI = false>
 __global__ void __launch_bounds__(64 * WCO * WPX) conv_fast_kernel(ConvArgs a) {
   unsigned long long st0 = 0, st1 = 0, st2 = 0;
   if constexpr (STAMP) st0 = stamp_now();
@@ -200,6 +205,52 @@ __global__ void __launch_bounds__(64 * WCO * WPX) conv_fast_kernel(ConvArgs a) {
   }
 
   if constexpr (STAMP) st2 = stamp_now();
+  if constexpr (EPI && !STAMP) {
+    static_assert(STAGES * (BCO + BPX) * 128 >= BCO * BPX * 4, "LDS epilogue tile exceeds the ring");
+    constexpr int NCH = BCO / 4;                          // 16-B chunks per tile row
+    if (fast_ep) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __syncthreads();                                      // every wave is done with the ring (no DMA in flight)
+      float* st = reinterpret_cast<float*>(smem);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int rl = wpx * TN * 16 + j * 16 + (lane & 15);
+          const int cl = wco * TM * 16 + i * 16 + (lane >> 4) * 4;
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * ep.sc[i][e] + ep.sh[i][e];
+          if (d.residual) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += Quad<bf16_t>::get(ep.res[i][j], e);
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], d.act);
+          *reinterpret_cast<float4*>(st + rl * BCO + (((cl >> 2) ^ (rl & (NCH - 1))) << 2)) =
+              make_float4(v[0], v[1], v[2], v[3]);
+        }
+      __syncthreads();
+      for (int idx = t; idx < BPX * NCH; idx += 64 * NW) {
+        const int rl = idx / NCH, k = idx - (idx / NCH) * NCH;
+        const int px = px0 + rl, co = co0 + 4 * k;
+        if (px >= a.M || co >= d.Cout) continue;
+        const float4 q = *reinterpret_cast<const float4*>(st + rl * BCO + ((k ^ (rl & (NCH - 1))) << 2));
+        float v[4] = {q.x, q.y, q.z, q.w};
+        long long op;
+        int oc;
+        out_site(d, px, co, op, oc);
+        if (d.mul) {
+          const typename Quad<bf16_t>::V m = Quad<bf16_t>::load(d.mul, op * d.m_cstride + d.m_coff + oc);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] *= Quad<bf16_t>::get(m, e);
+        }
+        Quad<bf16_t>::store(d.out, op * d.o_cstride + d.o_coff + oc, v);
+        if (d.out2) Quad<bf16_t>::store(d.out2, op * d.o2_cstride + d.o2_coff + oc, v);
+      }
+      return;
+    }
+  }
   if (fast_ep) {
     ep.store(d, a.M, epx, eco, acc, !STAMP);
   } else {
@@ -222,12 +273,12 @@ __global__ void __launch_bounds__(64 * WCO * WPX) conv_fast_kernel(ConvArgs a) {
 }
 
 template <int BCO, int BPX, int WCO, int WPX, int STAGES, bool NOLOAD = false, bool STAMP = false, bool PRIO = false,
-          bool LATE = false>
+          bool LATE = false, bool EPI = false>
 static int launch_fast(const ConvArgs& a, hipStream_t s) {
   const int npx = (a.M + BPX - 1) / BPX;
   const int nco = a.d.Cout_pad / BCO;
   const size_t lds = (size_t)STAGES * (BCO + BPX) * 8 * 16;
-  auto kern = conv_fast_kernel<BCO, BPX, WCO, WPX, STAGES, NOLOAD, STAMP, PRIO, LATE>;
+  auto kern = conv_fast_kernel<BCO, BPX, WCO, WPX, STAGES, NOLOAD, STAMP, PRIO, LATE, EPI>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -275,6 +326,8 @@ int conv_fast_try(const ConvArgs& a, hipStream_t s, int variant) {
     case 63: if (d.Cout_pad % 64) return 0; r = launch_fast<64, 128, 1, 4, 2, false, false, false, true>(a, s); break;
     case 64: if (d.Cout_pad % 64) return 0; r = launch_fast<64, 128, 1, 4, 2, false, false, true, false>(a, s); break;
     case 65: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 2, 2, 3, false, false, true, false>(a, s); break;
+    case 66: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 2, 2, 2, false, false, true, false, true>(a, s); break;
+    case 67: if (d.Cout_pad % 64) return 0; r = launch_fast<64, 128, 1, 4, 2, false, false, false, false, true>(a, s); break;
     default: return 0;
   }
   return r < 0 ? r : 1;

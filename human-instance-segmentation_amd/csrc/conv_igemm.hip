@@ -312,7 +312,9 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
     if (r != 0) return r < 0 ? r : HISEG_OK;
   } else if (variant >= 0) {
     int v = variant;
-    if (v == 0) v = (d->Cout_pad % 128 == 0) ? 60 : 8;   // 60 = 4 with s_setprio around the MFMA clusters (+1..5 %)
+    // 66 = 128x128 ring with s_setprio MFMA clusters and the LDS full-row epilogue, 67 = 64x128 with the LDS
+    // epilogue (tools/conv_bench.py: +4..17 % over the register epilogue, bit-identical)
+    if (v == 0) v = (d->Cout_pad % 128 == 0) ? 66 : 67;
     const int r = conv_fast_try(a, s, v);
     if (r != 0) return r < 0 ? r : HISEG_OK;
     if (variant == 0) {   // narrow / ragged layers: halo-tiled direct kernel

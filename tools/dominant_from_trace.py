@@ -31,7 +31,7 @@ d = [v for v in d_seq if v > cut]
 if "--last" in sys.argv:
     d = d[-int(sys.argv[sys.argv.index("--last") + 1]):]
 d = sorted(d)
-print(json.dumps({"kernel": "conv_fast_kernel<128,128,2,2,2,prio> grid 12288 x 256 (256->256 3x3 @64x48 x256 ROIs)",
+print(json.dumps({"kernel": "conv_fast_kernel<128,128,2,2,2,prio,lds-epilogue> grid 12288 x 256 (256->256 3x3 @64x48 x256 ROIs)",
                   "launches": len(d), "same_grid_launches": len(d_all), "cluster_cut_ms": round(cut, 4), "avg_ms": round(sum(d) / len(d), 4), "median_ms": round(d[len(d) // 2], 4),
                   "min_ms": round(d[0], 4), "max_ms": round(d[-1], 4),
                   "flop_per_launch": 927712935936.0,

@@ -11,7 +11,7 @@ import json
 import statistics
 import sys
 
-KERNEL = "conv_fast_kernel<128, 128, 2, 2, 2, false, false, true, false>"
+KERNEL = "conv_fast_kernel<128, 128, 2, 2, 2, false, false, true, false, true>"
 GRID = 12288 * 256
 ALG_BYTES = 2 * 786432 * 256 * 2 + 256 * 2304 * 2  # in + out activations (bf16) + weights
 
