@@ -355,24 +355,50 @@ __global__ void __launch_bounds__(256) ca_mlp_kernel(const float* part, int HW, 
   }
 }
 
-// out = x * gate[n][c] * mul[n][c]   (NHWC, C channels contiguous)
+// out = x * gate[n][c] * mul[n][c]   (NHWC, C channels contiguous).  Block = (256 / nch) pixel lanes x nch
+// channel chunks over a pixel range of image blockIdx.y (blockIdx.x = range): the chunk's gate factors stay
+// in registers across the thread's pixels.  Falls back to one chunk per thread when nch does not divide 256.
+static unsigned ca_ranges(int N, int HW) {   // pixel ranges per image: ~8k blocks, >= 64 pixels per range
+  long long r = (8192 + N - 1) / N;
+  const long long cap = HW / 64 > 0 ? HW / 64 : 1;
+  if (r > cap) r = cap;
+  return (unsigned)(r < 1 ? 1 : (r > 65535 ? 65535 : r));
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) ca_apply_kernel(const void* x, int N, int HW, int C, const float* gate,
                                                        const float* mul, void* out) {
   constexpr int K = Chunk<T>::N;
   const int nch = C / K;
-  const int li = blockIdx.x * 256 + threadIdx.x;   // chunk within image blockIdx.y
-  if (li >= HW * nch) return;
-  const int ch = li % nch;
   const long long n = blockIdx.y;
-  const long long gid = n * HW * nch + li;
-  float v[K];
-  Chunk<T>::unpack(reinterpret_cast<const uint4*>(x)[gid], v);
-  const float* g = gate + n * C + ch * K;
-  const float* m = mul ? mul + n * C + ch * K : nullptr;
+  if (nch <= 256 && 256 % nch == 0) {
+    const int R = 256 / nch, ch = threadIdx.x % nch, lane = threadIdx.x / nch;
+    float g[K];
 #pragma unroll
-  for (int e = 0; e < K; ++e) v[e] *= g[e] * (m ? m[e] : 1.f);
-  reinterpret_cast<uint4*>(out)[gid] = Chunk<T>::pack(v);
+    for (int e = 0; e < K; ++e) g[e] = gate[n * C + ch * K + e] * (mul ? mul[n * C + ch * K + e] : 1.f);
+    const int p0 = (int)((long long)HW * blockIdx.x / gridDim.x), p1 = (int)((long long)HW * (blockIdx.x + 1) / gridDim.x);
+    const uint4* xs = reinterpret_cast<const uint4*>(x) + n * HW * nch + ch;
+    uint4* os = reinterpret_cast<uint4*>(out) + n * HW * nch + ch;
+    for (int p = p0 + lane; p < p1; p += R) {
+      float v[K];
+      Chunk<T>::unpack(xs[(long long)p * nch], v);
+#pragma unroll
+      for (int e = 0; e < K; ++e) v[e] *= g[e];
+      os[(long long)p * nch] = Chunk<T>::pack(v);
+    }
+    return;
+  }
+  for (int li = blockIdx.x * 256 + threadIdx.x; li < HW * nch; li += gridDim.x * 256) {
+    const int ch = li % nch;
+    const long long gid = n * HW * nch + li;
+    float v[K];
+    Chunk<T>::unpack(reinterpret_cast<const uint4*>(x)[gid], v);
+    const float* gg = gate + n * C + ch * K;
+    const float* m = mul ? mul + n * C + ch * K : nullptr;
+#pragma unroll
+    for (int e = 0; e < K; ++e) v[e] *= gg[e] * (m ? m[e] : 1.f);
+    reinterpret_cast<uint4*>(out)[gid] = Chunk<T>::pack(v);
+  }
 }
 
 // per image: ds = dgate * g (1-g); dh; dgap; per-image weight-gradient rows
@@ -413,26 +439,47 @@ __global__ void __launch_bounds__(256) ca_mlp_bwd_kernel(const float* part, int 
   }
 }
 
-// dx = dout*mul*gate + dgap/HW
+// dx = dout*mul*gate + dgap/HW, same block layout as ca_apply_kernel
 template <typename T>
 __global__ void __launch_bounds__(256) ca_dx_kernel(const void* dout, int N, int HW, int C, const float* gate,
                                                     const float* mul, const float* dgap, void* dx) {
   constexpr int K = Chunk<T>::N;
   const int nch = C / K;
-  const int li = blockIdx.x * 256 + threadIdx.x;   // chunk within image blockIdx.y
-  if (li >= HW * nch) return;
-  const int ch = li % nch;
   const long long n = blockIdx.y;
-  const long long gid = n * HW * nch + li;
-  float v[K];
-  Chunk<T>::unpack(reinterpret_cast<const uint4*>(dout)[gid], v);
   const float inv = 1.f / (float)HW;
+  if (nch <= 256 && 256 % nch == 0) {
+    const int R = 256 / nch, ch = threadIdx.x % nch, lane = threadIdx.x / nch;
+    float g[K], d[K];
 #pragma unroll
-  for (int e = 0; e < K; ++e) {
-    const long long i = n * C + ch * K + e;
-    v[e] = v[e] * gate[i] * (mul ? mul[i] : 1.f) + dgap[i] * inv;
+    for (int e = 0; e < K; ++e) {
+      const long long i = n * C + ch * K + e;
+      g[e] = gate[i] * (mul ? mul[i] : 1.f);
+      d[e] = dgap[i] * inv;
+    }
+    const int p0 = (int)((long long)HW * blockIdx.x / gridDim.x), p1 = (int)((long long)HW * (blockIdx.x + 1) / gridDim.x);
+    const uint4* ds = reinterpret_cast<const uint4*>(dout) + n * HW * nch + ch;
+    uint4* os = reinterpret_cast<uint4*>(dx) + n * HW * nch + ch;
+    for (int p = p0 + lane; p < p1; p += R) {
+      float v[K];
+      Chunk<T>::unpack(ds[(long long)p * nch], v);
+#pragma unroll
+      for (int e = 0; e < K; ++e) v[e] = v[e] * g[e] + d[e];
+      os[(long long)p * nch] = Chunk<T>::pack(v);
+    }
+    return;
   }
-  reinterpret_cast<uint4*>(dx)[gid] = Chunk<T>::pack(v);
+  for (int li = blockIdx.x * 256 + threadIdx.x; li < HW * nch; li += gridDim.x * 256) {
+    const int ch = li % nch;
+    const long long gid = n * HW * nch + li;
+    float v[K];
+    Chunk<T>::unpack(reinterpret_cast<const uint4*>(dout)[gid], v);
+#pragma unroll
+    for (int e = 0; e < K; ++e) {
+      const long long i = n * C + ch * K + e;
+      v[e] = v[e] * gate[i] * (mul ? mul[i] : 1.f) + dgap[i] * inv;
+    }
+    reinterpret_cast<uint4*>(dx)[gid] = Chunk<T>::pack(v);
+  }
 }
 
 // ======================================================================================= upsample_bg_fg + combine
@@ -782,7 +829,7 @@ extern "C" int hiseg_attn_channel_train_fwd(int dtype, const void* x, int N, int
   DISPATCH_T(dtype, ca_gap<T>(x, nullptr, nullptr, N, HW, C, ws, s));
   hipLaunchKernelGGL(ca_mlp_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, ws, HW, C, Cr, w1, w2, act,
                      gap, hpre, gate);
-  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_apply_kernel<T>, dim3(nb((long long)HW * (C / chunk_of(dtype)), 256), N),
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_apply_kernel<T>, dim3(ca_ranges(N, HW), N),
                                        dim3(256), 0, s, x, N, HW, C, gate, chan_mul, out));
   return hiseg_check_launch("attn_channel_train_fwd");
 }
@@ -803,7 +850,7 @@ extern "C" int hiseg_attn_channel_bwd(int dtype, const void* x, int N, int HW, i
                      gap, hpre, gate, dgap, wpart);
   sum_rows(wpart, N, 2 * C * Cr, C * Cr, dw1, 1, s);
   sum_rows(wpart + C * Cr, N, 2 * C * Cr, C * Cr, dw2, 1, s);
-  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_dx_kernel<T>, dim3(nb((long long)HW * (C / chunk_of(dtype)), 256), N),
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_dx_kernel<T>, dim3(ca_ranges(N, HW), N),
                                        dim3(256), 0, s, dout, N, HW, C, gate, chan_mul, dgap, dx));
   return hiseg_check_launch("attn_channel_bwd");
 }
@@ -825,7 +872,7 @@ extern "C" int hiseg_se_train_fwd(int dtype, const void* x, int N, int HW, int C
   DISPATCH_T(dtype, ca_gap<T>(x, nullptr, nullptr, N, HW, C, ws, s));
   hipLaunchKernelGGL(ca_mlp_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, ws, HW, C, Cr, w1, w2, act,
                      gap, hpre, gate, b1, b2);
-  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_apply_kernel<T>, dim3(nb((long long)HW * (C / chunk_of(dtype)), 256), N),
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_apply_kernel<T>, dim3(ca_ranges(N, HW), N),
                                        dim3(256), 0, s, x, N, HW, C, gate, nullptr, out));
   return hiseg_check_launch("se_train_fwd");
 }
@@ -849,7 +896,7 @@ extern "C" int hiseg_se_train_bwd(int dtype, const void* x, int N, int HW, int C
   sum_rows(wpart + C * Cr, N, 2 * C * Cr, C * Cr, dw2, 1, s);
   sum_rows(bpart, N, Cr + C, Cr, db1, 1, s);
   sum_rows(bpart + Cr, N, Cr + C, C, db2, 1, s);
-  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_dx_kernel<T>, dim3(nb((long long)HW * (C / chunk_of(dtype)), 256), N),
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ca_dx_kernel<T>, dim3(ca_ranges(N, HW), N),
                                        dim3(256), 0, s, dout, N, HW, C, gate, nullptr, dgap, dx));
   return hiseg_check_launch("se_train_bwd");
 }
