@@ -511,6 +511,40 @@ __global__ void __launch_bounds__(256) gate_bwd_kernel(long long P, int C, hiseg
   }
 }
 
+// Vector form of gate_bwd_kernel: 16-B chunks, (channel chunk, pixel lane) threads as bn_apply_vec_kernel.
+template <typename T>
+__global__ void __launch_bounds__(256) gate_bwd_vec_kernel(int P, int C, hiseg_ew_view dy, hiseg_ew_view a,
+                                                           hiseg_ew_view g, hiseg_ew_view da, int acc,
+                                                           hiseg_ew_view dzg) {
+  constexpr int V = Chunk<T>::N;
+  const int NCH = C / V;
+  const int CT = NCH < 256 ? NCH : 256;
+  const int R = 256 / CT;
+  const int cl = threadIdx.x % CT, r = threadIdx.x / CT;
+  const int ch = blockIdx.y * 256 + cl;
+  if (r >= R || ch >= NCH) return;
+  const int c = ch * V;
+  for (int p = blockIdx.x * R + r; p < P; p += gridDim.x * R) {
+    float gy[V], gv[V], o[V];
+    ldv<T>(dy.p, (long long)p * dy.cstride + dy.coff + c, gy);
+    ldv<T>(g.p, (long long)p * g.cstride + g.coff + c, gv);
+    if (da.p) {
+      const long long off = (long long)p * da.cstride + da.coff + c;
+      if (acc) ldv<T>(da.p, off, o);
+#pragma unroll
+      for (int k = 0; k < V; ++k) o[k] = acc ? o[k] + gy[k] * gv[k] : gy[k] * gv[k];
+      stv<T>(da.p, off, o);
+    }
+    if (dzg.p) {
+      float av[V];
+      ldv<T>(a.p, (long long)p * a.cstride + a.coff + c, av);
+#pragma unroll
+      for (int k = 0; k < V; ++k) o[k] = gy[k] * av[k] * gv[k] * (1.f - gv[k]);
+      stv<T>(dzg.p, (long long)p * dzg.cstride + dzg.coff + c, o);
+    }
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) act_bwd_cvt_kernel(long long P, int C, hiseg_ew_view dy, hiseg_ew_view y, int act,
                                                           hiseg_ew_view dz, int acc) {
@@ -775,6 +809,13 @@ extern "C" int hiseg_gate_fwd(int dtype, long long P, int C, hiseg_ew_view a, hi
 extern "C" int hiseg_gate_bwd(int dtype, long long P, int C, hiseg_ew_view dy, hiseg_ew_view a, hiseg_ew_view g,
                               hiseg_ew_view da, int da_accumulate, hiseg_ew_view dzg, hiseg_stream_t stream) {
   HISEG_REQUIRE(dy.p && a.p && g.p && P > 0 && C > 0, HISEG_ERR_BAD_ARG, "gate_bwd: bad arguments");
+  if (P < (1ll << 31) && vec_ok(dtype, C, dy.p, dy.cstride, dy.coff) && vec_ok(dtype, C, a.p, a.cstride, a.coff) &&
+      vec_ok(dtype, C, g.p, g.cstride, g.coff) && vec_ok(dtype, C, da.p, da.cstride, da.coff) &&
+      vec_ok(dtype, C, dzg.p, dzg.cstride, dzg.coff)) {
+    DISPATCH_T(dtype, hipLaunchKernelGGL(gate_bwd_vec_kernel<T>, vec_grid(P, C, dtype), dim3(256), 0,
+                                         (hipStream_t)stream, (int)P, C, dy, a, g, da, da_accumulate, dzg));
+    return hiseg_check_launch("gate_bwd");
+  }
   DISPATCH_T(dtype, hipLaunchKernelGGL(gate_bwd_kernel<T>, dim3(ew_blocks(P * C)), dim3(256), 0, (hipStream_t)stream,
                                        P, C, dy, a, g, da, da_accumulate, dzg));
   return hiseg_check_launch("gate_bwd");
