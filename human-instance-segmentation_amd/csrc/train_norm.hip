@@ -298,8 +298,9 @@ __global__ void __launch_bounds__(256) bn_apply_vec_kernel(hiseg_bn_apply_desc d
   }
 }
 
+// g = dy (* chan_mul) * act'(.) for one 16-B chunk; z = the chunk's pre-BN values (already loaded)
 template <typename T>
-__device__ __forceinline__ void bn_gv(const hiseg_bn_bwd_desc& d, long long p, int c, float* g) {
+__device__ __forceinline__ void bn_gv(const hiseg_bn_bwd_desc& d, long long p, int c, float* g, const float* z) {
   constexpr int V = Chunk<T>::N;
   ldv<T>(d.dy, p * d.dy_cstride + d.dy_coff + c, g);
   if (d.chan_mul) {
@@ -308,10 +309,11 @@ __device__ __forceinline__ void bn_gv(const hiseg_bn_bwd_desc& d, long long p, i
     for (int k = 0; k < V; ++k) g[k] *= cm[k];
   }
   if (d.act == HISEG_ACT_SILU) {   // SiLU'(v) needs the pre-activation: v = xhat * gamma + beta from z
-    float z[V];
-    ldv<T>(d.z, p * d.z_cstride + d.z_coff + c, z);
 #pragma unroll
     for (int k = 0; k < V; ++k) g[k] *= silu_grad_pre(d, z[k], c + k);
+  } else if (d.act == HISEG_ACT_RELU && d.fwd_scale && !d.dres) {   // the forward's mask, from z
+#pragma unroll
+    for (int k = 0; k < V; ++k) g[k] = (z[k] * d.fwd_scale[c + k] + d.fwd_shift[c + k] > 0.f) ? g[k] : 0.f;
   } else if (d.act != HISEG_ACT_NONE) {
     float y[V];
     ldv<T>(d.y, p * d.y_cstride + d.y_coff + c, y);
@@ -343,8 +345,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_vec_kernel(hiseg_bn_bwd_des
     for (int k = 0; k < V; ++k) { mu[k] = d.mean[c + k]; inv[k] = d.invstd[c + k]; }
     for (long long p = b + r; p < e; p += R) {
       float g[V], z[V];
-      bn_gv<T>(d, p, c, g);
       ldv<T>(d.z, p * d.z_cstride + d.z_coff + c, z);
+      bn_gv<T>(d, p, c, g, z);
 #pragma unroll
       for (int k = 0; k < V; ++k) {
         const float xh = (z[k] - mu[k]) * inv[k];
@@ -421,8 +423,8 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_vec_kernel(hiseg_bn_bwd_desc
   const int P = (int)d.P;
   for (int p = blockIdx.x * R + r; p < P; p += gridDim.x * R) {
     float g[V], z[V], o[V];
-    bn_gv<T>(d, p, c, g);
     ldv<T>(d.z, (long long)p * d.z_cstride + d.z_coff + c, z);
+    bn_gv<T>(d, p, c, g, z);
 #pragma unroll
     for (int k = 0; k < V; ++k) o[k] = k0[k] * (g[k] - k1[k] - (z[k] - mu[k]) * inv[k] * k2[k]);
     stv<T>(d.dz, (long long)p * d.dz_cstride + d.dz_coff + c, o);

@@ -92,7 +92,7 @@ class BnBwdDesc(ctypes.Structure):
                 ("dgamma", c_void_p), ("dbeta", c_void_p), ("dconv_bias", c_void_p), ("accumulate_params", c_int),
                 ("dz", c_void_p), ("dz_cstride", c_int), ("dz_coff", c_int),
                 ("dres", c_void_p), ("dres_cstride", c_int), ("dres_coff", c_int), ("dres_accumulate", c_int),
-                ("beta", c_void_p)]
+                ("beta", c_void_p), ("fwd_scale", c_void_p), ("fwd_shift", c_void_p)]
 
 
 class EwView(ctypes.Structure):

@@ -485,6 +485,8 @@ def bn_backward(T: Tape, bn: nn.BatchNorm2d, z: Act, y: Act, st: BNState, dz: Ac
     if residual is not None:
         gr, acc = T.grad(residual)
         d.dres, d.dres_cstride, d.dres_coff, d.dres_accumulate = gr.ptr(), gr.cstride, gr.coff, int(acc)
+    elif act == ACT_RELU:   # ReLU mask recomputed from z with the forward's folded affine: y is not re-read
+        d.fwd_scale, d.fwd_shift = st.scale.data_ptr(), st.shift.data_ptr()
     _chk(lib.hiseg_bn_bwd(ctypes.byref(d), _stream()), "bn_bwd")
     if residual is not None:
         T.mark(residual)

@@ -102,6 +102,10 @@ typedef struct hiseg_bn_bwd_desc {
   void* dz; int dz_cstride, dz_coff;
   void* dres; int dres_cstride, dres_coff; int dres_accumulate;
   const float* beta;              /* BN shift; needed for act = SiLU (pre-activation = xhat*gamma + beta) */
+  /* optional, act = ReLU without dres: the forward's folded affine (hiseg_bn_finalize scale / shift); the
+   * ReLU mask is then recomputed from z as z*scale + shift > 0 -- exactly the forward's expression -- and
+   * y is not read (one activation stream less in each pass) */
+  const float* fwd_scale; const float* fwd_shift;
 } hiseg_bn_bwd_desc;
 int hiseg_bn_bwd(const hiseg_bn_bwd_desc* d, hiseg_stream_t stream);
 
