@@ -114,7 +114,7 @@ __global__ void __launch_bounds__(64 * WCO * WPX) conv_fast_kernel(ConvArgs a) {
   const unsigned OOB = 0x80000000u;  // >= num_records: the DMA returns zeros
 
   const int Cin = a.Cin;
-  const int bpt = Cin >> 6;  // K blocks per tap
+  const int bpt = (Cin + 63) >> 6;  // K blocks per tap (a 1x1 layer's src-B tail block is partial)
   const int nK = a.nK;
   const unsigned lds_base = (unsigned)(uintptr_t)(lds_void*)smem;
 
@@ -130,7 +130,8 @@ __global__ void __launch_bounds__(64 * WCO * WPX) conv_fast_kernel(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int iy = piy[i] + ky, ix = pix[i] + kx;
-      const bool ok = (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+      const bool ok = (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W &&
+                      (fromA || ci0 - d.Ca + pch[i] * 8 < d.Cb);
       const unsigned off = ok ? ((unsigned)((pidx[i] + dpix) * cs + cbase) + (unsigned)pch[i] * 8u) * 2u : OOB;
       const unsigned dst = sbase + (unsigned)(BCO * 8 + 8 * 8 * (w + NW * i)) * 16u;
       dma16(fromA ? rA : rB, dst, off);
@@ -294,8 +295,12 @@ int conv_fast_try(const ConvArgs& a, hipStream_t s, int variant) {
   const hiseg_conv2d_desc& d = a.d;
   if (d.dtype != HISEG_BF16 || d.out_dtype != HISEG_BF16) return 0;
   if (d.a_up != 1 || d.in_scale != nullptr) return 0;
-  if (d.Ca % 64 != 0 || d.Cb % 64 != 0) return 0;
-  if (d.K_pad != d.KH * d.KW * a.Cin) return 0;
+  // K blocks must not straddle a tap or a source: Ca, Cb multiples of 64, or (1x1 only) a src-B tail of
+  // 8k channels in one last partial block whose missing chunks the DMA zero-fills (feature_combiner's
+  // 256 RGB + 2 logit channels, rgb.py:695)
+  const bool tail = d.KH == 1 && d.KW == 1 && d.Cb % 64 != 0 && d.Cb < 64 && d.Cb % 8 == 0;
+  if (d.Ca % 64 != 0 || (d.Cb % 64 != 0 && !tail)) return 0;
+  if (d.K_pad != d.KH * d.KW * ((a.Cin + 63) / 64) * 64) return 0;
   if (((d.a_cstride | d.a_coff) & 7) || (d.Cb && ((d.b_cstride | d.b_coff) & 7))) return 0;
   // 32-bit byte offsets
   const long long span_a = (long long)d.N * d.H * d.W * d.a_cstride * 2;
@@ -321,8 +326,11 @@ int conv_fast_try(const ConvArgs& a, hipStream_t s, int variant) {
     case 18: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 2, 2, 2, false, true>(a, s); break;
     // schedule variants of the production 128x128 configuration (variant 4)
     case 60: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 2, 2, 2, false, false, true, false>(a, s); break;
-    case 61: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 2, 2, 2, false, false, false, true>(a, s); break;
-    case 62: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 2, 2, 2, false, false, true, true>(a, s); break;
+    // 8-wave tiles (4 Cout x 2 pixel waves): 128x128 without s_setprio / 3-stage ring, 64x128, 128x128 (69)
+    case 61: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 4, 2, 2, false, false, false, false, true>(a, s); break;
+    case 62: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 4, 2, 3, false, false, true, false, true>(a, s); break;
+    case 68: if (d.Cout_pad % 64) return 0; r = launch_fast<64, 128, 4, 2, 2, false, false, true, false, true>(a, s); break;
+    case 69: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 4, 2, 2, false, false, true, false, true>(a, s); break;
     case 63: if (d.Cout_pad % 64) return 0; r = launch_fast<64, 128, 1, 4, 2, false, false, false, true>(a, s); break;
     case 64: if (d.Cout_pad % 64) return 0; r = launch_fast<64, 128, 1, 4, 2, false, false, true, false>(a, s); break;
     case 65: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 2, 2, 3, false, false, true, false>(a, s); break;

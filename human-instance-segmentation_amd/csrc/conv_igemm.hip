@@ -18,6 +18,7 @@
 // groups of the fragment reads (MI355X_MICROARCH.md §LDS) and for the row-wise stores.
 // Two LDS stages; the next K block is gathered into registers while the current one feeds
 // the MFMAs (register-staged double buffering, one barrier per K block).
+#include <cstdlib>
 #include "conv_common.h"
 
 namespace hiseg {
@@ -312,9 +313,12 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
     if (r != 0) return r < 0 ? r : HISEG_OK;
   } else if (variant >= 0) {
     int v = variant;
-    // 66 = 128x128 ring with s_setprio MFMA clusters and the LDS full-row epilogue, 67 = 64x128 with the LDS
-    // epilogue (tools/conv_bench.py: +4..17 % over the register epilogue, bit-identical)
-    if (v == 0) v = (d->Cout_pad % 128 == 0) ? 66 : 67;
+    // 61 = 128x128 ring, 8 waves as 4 (Cout) x 2 (pixel) with 32x64 wave tiles, LDS full-row epilogue;
+    // 68 = the same wave grid on 64x128 tiles (tools/conv_bench.py: +1..4 % / +7..9 % over the 4-wave
+    // 66 / 67, which had beaten the register epilogue by 4..17 %; all bit-identical)
+    // HISEG_CONV_WAVES=4 restores the 4-wave tiles (A/B timing only)
+    static const bool four_waves = [] { const char* e = getenv("HISEG_CONV_WAVES"); return e && atoi(e) == 4; }();
+    if (v == 0) v = four_waves ? ((d->Cout_pad % 128 == 0) ? 66 : 67) : ((d->Cout_pad % 128 == 0) ? 61 : 68);
     const int r = conv_fast_try(a, s, v);
     if (r != 0) return r < 0 ? r : HISEG_OK;
     if (variant == 0) {   // narrow / ragged layers: halo-tiled direct kernel

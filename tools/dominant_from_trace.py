@@ -1,7 +1,7 @@
 """Average duration of bench.py's dominant launch class from a rocprofv3 kernel trace (developer tool).
 
 The dominant class is the 256->256 3x3 conv at the 64x48 ROI grid over 256 ROIs: conv_fast_kernel
-<128,128,...> with 6144 pixel tiles x 2 Cout tiles = 12288 workgroups (grid 3 145 728 threads).  The
+<128,128,...> with 6144 pixel tiles x 2 Cout tiles = 12288 workgroups (grid 6 291 456 threads: 512-thread workgroups).  The
 kernel-stats summary averages every conv_fast launch (all layer shapes); this filters the trace to the
 class bench.py's HIP-event probe times, so the two averages can be compared.  The same grid also runs the
 256->256 1x1 (K = 256) and 128->256 3x3 (K = 1152) layers; the trace carries no shape, so the K = 2304
@@ -17,7 +17,7 @@ import csv
 import json
 import sys
 
-GRID = 12288 * 256
+GRID = 12288 * 512
 allrows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 cut_t = next((int(r["Start_Timestamp"]) for r in allrows if "bn_stats" in r["Kernel_Name"]), None)
 rows = [r for r in allrows
@@ -31,7 +31,7 @@ d = [v for v in d_seq if v > cut]
 if "--last" in sys.argv:
     d = d[-int(sys.argv[sys.argv.index("--last") + 1]):]
 d = sorted(d)
-print(json.dumps({"kernel": "conv_fast_kernel<128,128,2,2,2,prio,lds-epilogue> grid 12288 x 256 (256->256 3x3 @64x48 x256 ROIs)",
+print(json.dumps({"kernel": "conv_fast_kernel<128,128,4,2,2,lds-epilogue> grid 12288 x 512 (256->256 3x3 @64x48 x256 ROIs)",
                   "launches": len(d), "same_grid_launches": len(d_all), "cluster_cut_ms": round(cut, 4), "avg_ms": round(sum(d) / len(d), 4), "median_ms": round(d[len(d) // 2], 4),
                   "min_ms": round(d[0], 4), "max_ms": round(d[-1], 4),
                   "flop_per_launch": 927712935936.0,
