@@ -326,14 +326,15 @@ int conv_fast_try(const ConvArgs& a, hipStream_t s, int variant) {
     case 18: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 2, 2, 2, false, true>(a, s); break;
     // schedule variants of the production 128x128 configuration (variant 4)
     case 60: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 2, 2, 2, false, false, true, false>(a, s); break;
-    // 8-wave tiles (4 Cout x 2 pixel waves): 128x128 without s_setprio / 3-stage ring, 64x128, 128x128 (69)
+    // 4 Cout x N pixel wave grids with 32x64 wave tiles: 128x128 (61, 8 waves), 128x64 (62), 128x256 (63, 16 waves),
+    // 256x128 (64, 8x2), 64x64 (65), 64x128 (68), 128x128 with s_setprio (69)
     case 61: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 4, 2, 2, false, false, false, false, true>(a, s); break;
-    case 62: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 4, 2, 3, false, false, true, false, true>(a, s); break;
+    case 62: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 64, 4, 1, 2, false, false, false, false, true>(a, s); break;
     case 68: if (d.Cout_pad % 64) return 0; r = launch_fast<64, 128, 4, 2, 2, false, false, true, false, true>(a, s); break;
     case 69: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 4, 2, 2, false, false, true, false, true>(a, s); break;
-    case 63: if (d.Cout_pad % 64) return 0; r = launch_fast<64, 128, 1, 4, 2, false, false, false, true>(a, s); break;
-    case 64: if (d.Cout_pad % 64) return 0; r = launch_fast<64, 128, 1, 4, 2, false, false, true, false>(a, s); break;
-    case 65: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 2, 2, 3, false, false, true, false>(a, s); break;
+    case 63: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 256, 4, 4, 2, false, false, false, false, false>(a, s); break;
+    case 64: if (d.Cout_pad % 256) return 0; r = launch_fast<256, 128, 8, 2, 2, false, false, false, false, false>(a, s); break;
+    case 65: if (d.Cout_pad % 64) return 0; r = launch_fast<64, 64, 4, 1, 2, false, false, false, false, true>(a, s); break;
     case 66: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 2, 2, 2, false, false, true, false, true>(a, s); break;
     case 67: if (d.Cout_pad % 64) return 0; r = launch_fast<64, 128, 1, 4, 2, false, false, false, false, true>(a, s); break;
     default: return 0;

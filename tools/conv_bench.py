@@ -31,13 +31,18 @@ SHAPES = {
     "dec16_3x3_480x640": (32, 16, 0, 16, 480, 640, 3, False),
     "dec32_3x3_240x320": (32, 32, 0, 32, 240, 320, 3, False),
     "c16to96_1x1_240x320": (32, 16, 0, 96, 240, 320, 1, False),
+    # smp decoder blocks 3/4 (nearest-x2 upsampled src A + skip), B0 at 480x640
+    "dec3_up64+32to32_3x3_240x320": (32, 64, 32, 32, 240, 320, 3, False, 2),
+    "dec4_up32to16_3x3_480x640": (32, 32, 0, 16, 480, 640, 3, False, 2),
 }
 
 
 def make(shape, dt):
-    N, Ca, Cb, Cout, H, W, k, res = shape
+    N, Ca, Cb, Cout, H, W, k, res = shape[:8]
+    up = shape[8] if len(shape) > 8 else 1
     g = torch.Generator(device=DEV).manual_seed(0)
-    xa = ops.Act.new(N, H, W, Ca, dt, DEV, zero=False)
+    xa = ops.Act.new(N, H // up, W // up, Ca, dt, DEV, zero=False)
+    xa.up = up
     xa.t.copy_(torch.randn(xa.t.numel(), device=DEV, generator=g))
     xb = None
     if Cb:
@@ -57,9 +62,10 @@ def make(shape, dt):
 def desc(p, xa, xb, r, out):
     d = L.Conv2dDesc()
     d.dtype = d.out_dtype = ops.hdtype(xa.dtype)
-    d.N, d.H, d.W, d.Ho, d.Wo = xa.N, xa.H, xa.W, xa.H, xa.W
+    up = getattr(xa, "up", 1)
+    d.N, d.H, d.W, d.Ho, d.Wo = xa.N, xa.H * up, xa.W * up, xa.H * up, xa.W * up
     d.KH, d.KW, d.stride, d.pad = p.kh, p.kw, 1, p.pad
-    d.srcA, d.a_cstride, d.a_coff, d.Ca, d.a_up = xa.ptr(), xa.cstride, 0, p.ca, 1
+    d.srcA, d.a_cstride, d.a_coff, d.Ca, d.a_up = xa.ptr(), xa.cstride, 0, p.ca, up
     if xb is not None:
         d.srcB, d.b_cstride, d.b_coff, d.Cb = xb.ptr(), xb.cstride, 0, p.cb
     d.weight, d.Cout, d.Cout_pad, d.K_pad = p.weight.data_ptr(), p.gemm_cols, p.cout_pad, p.k_pad
@@ -87,7 +93,7 @@ def main():
     results = {}
     for name in args.shapes.split(","):
         shape = SHAPES[name]
-        N, Ca, Cb, Cout, H, W, k, res = shape
+        N, Ca, Cb, Cout, H, W, k, res = shape[:8]
         flops = 2.0 * N * H * W * Cout * k * k * (Ca + Cb)
         p, xa, xb, r, out = make(shape, torch.bfloat16)
         d = desc(p, xa, xb, r, out)
