@@ -24,11 +24,23 @@ N > 1.
 
 Third, under "distill": the C5 B7 -> B0 distillation step (decoder-only phase) of 4 640x640 images per GPU.
 
+Fourth/fifth, under "train_c3" / "train_c4": the BASELINE C3 (B1-enhanced, 80x60 ROI / 160x120 mask) and C4
+(B7-ultra, 128x96 ROI / 256x192 mask, depth-4 head) training steps in the reference's training semantics
+(640x640 images, one ROI per image; 32 / 8 images per GPU).
+
+Multi-GPU launch: under torch.distributed.run (WORLD_SIZE set) every rank runs this file; `python bench.py
+--gpus N` without a launcher spawns the N rank processes itself (this parent never touches the GPU) and
+exits non-zero if any rank fails.  Every rank checks that the process group has exactly N ranks.
+
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--no-train] [--no-distill]
+                        [--no-presets] [--backend nccl|gloo] [--dry-run]
 """
 import argparse
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
@@ -83,21 +95,51 @@ def dominant_select(d):
     return None
 
 
-def train_bench(device, dtype, rank, world, dist, steps, warmup):
-    """Train steps/s of the B0-std ROI model on the C2-shaped batch (module docstring)."""
+def preset_kwargs(name):
+    """create_rgb_hierarchical_model kwargs of a reference preset (the reference's ConfigManager dump,
+    tests/golden/configs.json: b0 = B0-std, b1 = B1-enhanced, b7 = B7-ultra)."""
+    with open(os.path.join(ROOT, "tests", "golden", "configs.json")) as f:
+        kw = dict(json.load(f)[name]["model_kwargs"])
+    kw["roi_size"], kw["mask_size"] = tuple(kw["roi_size"]), tuple(kw["mask_size"])
+    return kw
+
+
+# Algorithmic GFLOP per training sample (one 640x640 image + its ROI, SURVEY §8d): head fwd+bwd + UNet fwd
+GFLOP_PER_TRAIN_SAMPLE = {"b1": 279.0 + 40.0, "b7": 835.3 + 120.3}
+
+
+def train_bench(device, dtype, rank, world, dist, steps, warmup, preset=None, batch=B, rois_per_img=R,
+                hw=(H, W), local_first=False):
+    """Train steps/s of an ROI model (module docstring).  preset None: the B0-std model on the C2-shaped batch
+    (32 images 640x480 x 8 ROIs, RoIAlign scale (H, W)); preset "b1"/"b7": the C3/C4 preset on `batch` 640x640
+    images with one ROI each (the reference's training semantics: dataset.py:74-80, RoIAlign scale 640).
+    local_first (world > 1): also time the same step with the gradient exchange off (each rank alone) first, so
+    the line carries the DDP step's cost over a rank's local step."""
     import filler
     import hiseg
     from hiseg import distributed as HD
-    model = build_model(device, dtype).train()
-    for m in (model.roi_align_mask, model.roi_align_rgb):
-        m.spatial_scale_h, m.spatial_scale_w = H, W
-    images, rois = synthetic_batch(device, rank)
-    tgt = torch.from_numpy(filler.ellipse_targets(7 + rank, B * R, *MASK_HW)).to(device)
+    if preset is None:
+        model = build_model(device, dtype).train()
+        for m in (model.roi_align_mask, model.roi_align_rgb):
+            m.spatial_scale_h, m.spatial_scale_w = H, W
+        images, rois = synthetic_batch(device, rank)
+        mask_hw = MASK_HW
+    else:
+        kw = preset_kwargs(preset)
+        model = hiseg.create_rgb_hierarchical_model(**kw)
+        filler.fill_module(model).eval()
+        model = model.to(device)
+        hiseg.set_compute_dtype(model, dtype)
+        model.train()
+        g = torch.Generator().manual_seed(rank)
+        images = torch.rand(batch, 3, hw[0], hw[1], generator=g).to(device)
+        rois = torch.from_numpy(filler.box_rois(1 + 1000 * rank, batch, rois_per_img)).to(device)
+        mask_hw = kw["mask_size"]
+    n_samples = int(rois.shape[0])
+    tgt = torch.from_numpy(filler.ellipse_targets(7 + rank, n_samples, *mask_hw)).to(device)
     loss_fn = hiseg.RefinedHierarchicalLoss(use_boundary_aware_loss=True, use_contour_detection=True,
                                             use_distance_transform=True, boundary_aware_weight=0.1,
                                             contour_loss_weight=0.1, distance_loss_weight=0.1)
-    if world > 1:
-        HD.enable_grad_sync(model)
     state = {"opt": None}
 
     def step():
@@ -110,37 +152,61 @@ def train_bench(device, dtype, rank, world, dist, steps, warmup):
         state["opt"].step()
         return loss
 
-    for _ in range(warmup):
-        loss = step()
-    torch.cuda.synchronize()
-    first = float(loss.detach())
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        loss = step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-    last = float(loss.detach())
-    if not (first == first and last == last):
-        raise RuntimeError("train bench: non-finite loss")
+    def timed():
+        for _ in range(warmup):
+            loss = step()
+        torch.cuda.synchronize()
+        first = float(loss.detach())
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            loss = step()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        if dist:
+            t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = t.item()
+        last = float(loss.detach())
+        if not (first == first and last == last):
+            raise RuntimeError("train bench: non-finite loss")
+        return elapsed, first, last
+
+    local = None
+    if world > 1 and local_first:
+        el, _, _ = timed()
+        local = steps / el
+    if world > 1:
+        HD.enable_grad_sync(model)
+    elapsed, first, last = timed()
     sps = steps / elapsed
-    return {"metric": "train step/s", "value": round(sps, 3), "unit": "steps/s", "ms_per_step": round(1e3 / sps, 2),
-            "steps": steps, "warmup": warmup, "samples_per_s": round(sps * B * R * world, 1),
-            "pipeline_tflops": round(sps * B * R * world * GFLOP_PER_TRAIN_ROI / 1e3, 1),
-            "loss_first_last": [round(first, 4), round(last, 4)],
-            "config": {"workload": "B0-std train step: 32 img 640x480 x 8 ROIs/GPU (256 ROI samples), ROI 64x48, "
-                                   "mask 128x96, frozen UNet fwd + ROI path fwd/bwd + RefinedHierarchicalLoss + "
-                                   "FusedAdamW", "global_batch": B * world, "roi_samples_per_step": B * R * world,
-                       "parallelism": f"dp{world} (DDP, bucketed RCCL grad all-reduce)" if world > 1 else "dp1"}}
+    gflop = GFLOP_PER_TRAIN_ROI if preset is None else GFLOP_PER_TRAIN_SAMPLE[preset]
+    if preset is None:
+        workload = ("B0-std train step: 32 img 640x480 x 8 ROIs/GPU (256 ROI samples), ROI 64x48, mask 128x96, "
+                    "frozen UNet fwd + ROI path fwd/bwd + RefinedHierarchicalLoss + FusedAdamW")
+    else:
+        kw = preset_kwargs(preset)
+        workload = (f"{'C3 B1-enhanced' if preset == 'b1' else 'C4 B7-ultra'} train step: {batch} img "
+                    f"{hw[0]}x{hw[1]} x {rois_per_img} ROI/GPU, ROI {kw['roi_size'][0]}x{kw['roi_size'][1]}, mask "
+                    f"{kw['mask_size'][0]}x{kw['mask_size'][1]}, head depth {kw['hierarchical_depth']}, frozen "
+                    f"{kw['encoder_name'][-2:].upper()} UNet fwd + ROI path fwd/bwd + RefinedHierarchicalLoss + FusedAdamW")
+    out = {"metric": "train step/s", "value": round(sps, 3), "unit": "steps/s", "ms_per_step": round(1e3 / sps, 2),
+           "steps": steps, "warmup": warmup, "samples_per_s": round(sps * n_samples * world, 1),
+           "pipeline_tflops": round(sps * n_samples * world * gflop / 1e3, 1),
+           "loss_first_last": [round(first, 4), round(last, 4)],
+           "config": {"workload": workload, "global_batch": int(images.shape[0]) * world,
+                      "roi_samples_per_step": n_samples * world,
+                      "parallelism": f"dp{world} (DDP, bucketed RCCL grad all-reduce)" if world > 1 else "dp1"}}
+    if local is not None:
+        out["local_step_per_s"] = round(local, 3)
+        out["ddp_over_local"] = round(sps / local, 4)   # 1.0 = the gradient exchange is fully hidden
+    del model
+    return out
 
 
 def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=640):
@@ -286,33 +352,92 @@ def data_bench(device, steps=10, batch=32, src_hw=(480, 640), image_size=(640, 6
                                    f"{mask_hw[0]}x{mask_hw[1]} ROI targets from 3 instance masks per image"}}
 
 
+def cpu_threads():
+    """Host threads the CPU baselines use: the CPUs this process may run on, capped by OMP_NUM_THREADS when the
+    environment sets it (the GPU box sets 16 = its CPU share; os.cpu_count() there reports the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(cap))) if cap and cap.isdigit() else max(1, n)
+
+
+def _median_runs(fn, warmup=2, runs=5, budget_s=30.0):
+    for _ in range(warmup):
+        fn()
+    times = []
+    t_all = time.perf_counter()
+    while len(times) < runs or (time.perf_counter() - t_all < 2.0 and len(times) < 2 * runs):
+        t0 = time.perf_counter()
+        fn()
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_all > budget_s and len(times) >= 3:
+            break
+    return statistics.median(times), len(times)
+
+
 def cpu_baseline(seconds_budget=30.0):
     """The oracle (float32 CPU restatement of the reference path) on a bounded sample of the same
-    workload: 1 image 480x640 with 8 ROIs through UNet + ROI head (exported contract)."""
+    workload: 1 image 480x640 with 8 ROIs through UNet + ROI head (exported contract).  BASELINE.md §3 /
+    SURVEY §8d: 2 warm-up runs, then the median of >= 5."""
     import filler
     from oracle import rgb_model as O
     import hiseg
-    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    torch.set_num_threads(cpu_threads())
     model = hiseg.create_rgb_hierarchical_model(**B0_KWARGS)
     filler.fill_module(model).eval()
     sd = O.np_state(model)
     cfg = O.cfg_from_kwargs(B0_KWARGS)
     images = torch.rand(1, 3, H, W, generator=torch.Generator().manual_seed(0))
     rois = torch.from_numpy(filler.box_rois(1, 1, R))
-    times = []
-    with torch.no_grad():
-        for i in range(3):
-            t0 = time.perf_counter()
+
+    def run():
+        with torch.no_grad():
             logits, _, u = O.rgb_model(sd, images, rois, cfg, (H, W), "b0")
             O.instance_masks(logits)
             O.binary_masks(sd, u)
-            times.append(time.perf_counter() - t0)
-            if sum(times) > seconds_budget:
-                break
-    t = min(times[1:]) if len(times) > 1 else times[0]
+
+    t, n = _median_runs(run, budget_s=seconds_budget)
     return {"value": round(R / t, 3), "unit": "ROI-masks/s", "cores": torch.get_num_threads(), "kind": "port",
             "sample": f"oracle/rgb_model.py fp32 CPU, 1 image 480x640 x {R} ROIs (UNet B0 + head + export masks), "
-                      f"best of {len(times) - 1 if len(times) > 1 else 1} after 1 warm-up, {t:.2f} s/iter"}
+                      f"median of {n} after 2 warm-ups, {t:.2f} s/iter"}
+
+
+def cpu_train_baseline(seconds_budget=30.0):
+    """The oracle's B0-std training step on the host cores (baseline beside `train`): 1 image 480x640 x 8 ROIs,
+    fp32 -- frozen UNet forward, train-mode ROI path (oracle/train.py, torch autograd), RefinedHierarchicalLoss,
+    backward, clip + AdamW.  2 warm-ups, median of >= 5."""
+    import filler
+    from oracle import rgb_model as O
+    from oracle import train as OT
+    import hiseg
+    torch.set_num_threads(cpu_threads())
+    model = hiseg.create_rgb_hierarchical_model(**B0_KWARGS)
+    filler.fill_module(model)
+    for m in model.modules():
+        if isinstance(m, (torch.nn.Dropout, torch.nn.Dropout2d)):
+            m.p = 0.0
+    sd = OT.params_of(model)
+    cfg = O.cfg_from_kwargs(B0_KWARGS)
+    images = torch.rand(1, 3, H, W, generator=torch.Generator().manual_seed(0))
+    rois = torch.from_numpy(filler.box_rois(1, 1, R))
+    tgt = torch.from_numpy(filler.ellipse_targets(7, R, *MASK_HW))
+    params = [v for v in sd.values() if v.requires_grad]
+    state = {}
+    loss_fn = OT.RefinedHierarchicalLoss()
+
+    def run():
+        with torch.no_grad():
+            u = O.pretrained_unet_logits(sd, images, "b0")
+        logits, aux = OT.forward_train(sd, images, rois, u, cfg, (H, W))
+        loss, _ = loss_fn(logits, tgt, aux)
+        for p in params:
+            p.grad = None
+        loss.backward()
+        OT.adamw_step(params, [p.grad if p.grad is not None else torch.zeros_like(p) for p in params], state)
+
+    t, n = _median_runs(run, budget_s=seconds_budget)
+    return {"value": round(1.0 / t, 4), "unit": "steps/s", "samples_per_s": round(R / t, 3), "cores": torch.get_num_threads(),
+            "kind": "port", "sample": f"oracle/train.py fp32 CPU B0-std train step, 1 image 480x640 x {R} ROI samples, "
+                                      f"median of {n} after 2 warm-ups, {t:.2f} s/step"}
 
 
 def load_traffic():
@@ -327,9 +452,43 @@ def load_traffic():
         return None
 
 
+def _free_port():
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`--gpus N` without a torch.distributed launcher: start N rank processes of this script (this process never
+    touches the GPU), RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1.  Rank output passes through;
+    the first rank that fails ends the others and sets the exit status."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    if rc:
+        print(f"bench.py: a rank failed (exit {rc})", file=sys.stderr)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (default: WORLD_SIZE of a launcher, else 1)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -337,18 +496,47 @@ def main():
     ap.add_argument("--no-train", action="store_true")
     ap.add_argument("--train-only", action="store_true")
     ap.add_argument("--no-distill", action="store_true")
+    ap.add_argument("--no-presets", action="store_true", help="skip the C3 (B1) / C4 (B7) train lines")
     ap.add_argument("--distill-only", action="store_true", help="only the C5 distillation line (profiling)")
     ap.add_argument("--serial", action="store_true", help="one stream (no UNet/head overlap across steps)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher + rendezvous check only (no GPU work): CPU tests of the multi-rank path")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus is not None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = int(env_world or "1")
+    if args.gpus is not None and args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    if args.dry_run and os.environ.get("HISEG_BENCH_FAIL_RANK") == str(rank):
+        sys.exit(5)   # test hook (tests/test_bench_launcher.py): a rank that dies before the rendezvous
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            probe = torch.ones(1, device=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+            probe = torch.ones(1)
+        dist.all_reduce(probe)   # the communicator formed over every rank
+        if dist.get_world_size() != world or int(probe.item()) != world:
+            print(f"bench.py: rank {rank}: process group has {dist.get_world_size()} ranks, expected {world}",
+                  file=sys.stderr)
+            sys.exit(3)
+    if args.dry_run:
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": world, "backend": args.backend}))
+        if dist:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     device = torch.device("cuda", local)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
 
@@ -361,7 +549,15 @@ def main():
         out = infer_bench(args, device, dtype, rank, world, dist)
     if not args.no_train:
         torch.cuda.empty_cache()
-        out["train"] = train_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), max(2, args.warmup))
+        out["train"] = train_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), max(2, args.warmup),
+                                   local_first=True)
+        if not args.no_presets:
+            torch.cuda.empty_cache()
+            out["train_c3"] = train_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2, preset="b1",
+                                          batch=32, rois_per_img=1, hw=(640, 640))
+            torch.cuda.empty_cache()
+            out["train_c4"] = train_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2, preset="b7",
+                                          batch=8, rois_per_img=1, hw=(640, 640))
     if not args.no_distill and not args.train_only:
         torch.cuda.empty_cache()
         out["distill"] = distill_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2)
@@ -372,6 +568,8 @@ def main():
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline and not args.train_only:
             out["cpu_baseline"] = cpu_baseline()
+            if not args.no_train:
+                out["cpu_baseline_train"] = cpu_train_baseline()
         print(json.dumps(out))
     if dist:
         dist.destroy_process_group()

@@ -240,6 +240,7 @@ int conv_halo_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_halo2_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_halo3_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_8ph_try(const ConvArgs& a, hipStream_t s, int variant);
+int conv_wide_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_small_try(const ConvArgs& a, hipStream_t s, int variant);
 }
 
@@ -293,7 +294,10 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
   // Automatic choice (variant 0) = the fastest measured configuration per layer class
   // (tools/conv_bench.py): LDS-DMA ring kernel, 128x128 tiles for Cout >= 128, 64x128 for 64.
   // Experimental kernels (halo / halo2 / halo3) run only when forced by variant.
-  if (variant >= 60 && variant < 70) {
+  if (variant >= 70 && variant < 80) {
+    const int r = conv_wide_try(a, s, variant);
+    if (r != 0) return r < 0 ? r : HISEG_OK;
+  } else if (variant >= 60 && variant < 70) {
     const int r = conv_fast_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
   } else if (variant >= 50) {
@@ -318,6 +322,13 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
     // 66 / 67, which had beaten the register epilogue by 4..17 %; all bit-identical)
     // HISEG_CONV_WAVES=4 restores the 4-wave tiles (A/B timing only)
     static const bool four_waves = [] { const char* e = getenv("HISEG_CONV_WAVES"); return e && atoi(e) == 4; }();
+    // 256-output-channel 3x3 layers: the wide-tile kernel (conv_wide.hip: 256x256 workgroup tile, 128x128 wave
+    // tiles, LDS epilogue; tools/conv_bench.py: 0.99 vs 1.23 ms on the 256->256 3x3 @64x48 x256 ROI class,
+    // 0.58 vs 0.66 ms on 128->256, bit-identical).  It declines what it does not cover.
+    if (v == 0 && d->Cout % 256 == 0 && d->KH * d->KW > 1 && !four_waves) {
+      const int r = conv_wide_try(a, s, 70);
+      if (r != 0) return r < 0 ? r : HISEG_OK;
+    }
     if (v == 0) v = four_waves ? ((d->Cout_pad % 128 == 0) ? 66 : 67) : ((d->Cout_pad % 128 == 0) ? 61 : 68);
     const int r = conv_fast_try(a, s, v);
     if (r != 0) return r < 0 ? r : HISEG_OK;

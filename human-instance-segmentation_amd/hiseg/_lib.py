@@ -235,6 +235,8 @@ def _declare(lib):
         "hiseg_grad_norm_partials": ([P, c_ll, P, P], c_int),
         "hiseg_adamw_step": ([P, P, P, P, c_ll, c_float, c_float, c_float, c_float, c_float, c_float, c_float, P,
                               c_float, P, P], c_int),
+        "hiseg_adamw_step_guarded": ([P, P, P, P, c_ll, c_float, c_float, c_float, c_float, c_float, P, c_float, P,
+                                      P, c_int, P, P], c_int),
     }
     for name, (argtypes, restype) in sigs.items():
         fn = getattr(lib, name)

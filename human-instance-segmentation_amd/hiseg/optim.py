@@ -10,6 +10,7 @@ square root) and clip_grad_norm_ (coef = min(1, max_norm / (norm + 1e-6)), gradi
 from __future__ import annotations
 
 import math
+from collections.abc import MutableMapping
 from typing import Optional
 
 import torch
@@ -24,6 +25,79 @@ def flat_params_of(model: torch.nn.Module):
     return S.flat
 
 
+class _LiveState(MutableMapping):
+    """``optimizer.state`` of a FusedAdamW: a live view of its flat moment buffers keyed by parameter, in
+    torch.optim.AdamW's per-parameter form (``step`` CPU tensor, ``exp_avg`` / ``exp_avg_sq`` views).  Assigning
+    ``new_opt.state[p] = old_opt.state[p]`` copies the moments in -- the reference's optimizer-state transfer
+    when progressive unfreezing builds a new optimizer (train_distillation_staged.py:1537-1550) works unchanged
+    between two FusedAdamW instances."""
+
+    def __init__(self, opt: "FusedAdamW"):
+        self._opt = opt
+        self._pending = {}
+
+    def _off(self, p):
+        o = self._opt
+        o._ensure(required=False)
+        if o._flat is None:
+            return None
+        for _, q, off in o._slots():
+            if q is p:
+                return off
+        return None
+
+    def __getitem__(self, p):
+        o = self._opt
+        off = self._off(p)
+        if off is None or o.step_count == 0:
+            raise KeyError(p)
+        k = p.numel()
+        return {"step": torch.tensor(float(o.step_count)), "exp_avg": o.exp_avg[off:off + k].view(p.shape),
+                "exp_avg_sq": o.exp_avg_sq[off:off + k].view(p.shape)}
+
+    def __setitem__(self, p, ent):
+        o = self._opt
+        if o._flat is None:
+            o._ensure(required=False)
+        if o._flat is None:      # no training forward yet: applied once the flat layout exists
+            self._pending[p] = ent
+            return
+        off = self._off(p)
+        if off is None:
+            raise KeyError("FusedAdamW.state: parameter is not optimised by this optimizer")
+        k = p.numel()
+        with torch.no_grad():
+            o.exp_avg[off:off + k].copy_(ent["exp_avg"].reshape(-1))
+            o.exp_avg_sq[off:off + k].copy_(ent["exp_avg_sq"].reshape(-1))
+        o.step_count = max(o.step_count, int(float(ent["step"])))
+
+    def __delitem__(self, p):
+        off = self._off(p)
+        if off is None:
+            raise KeyError(p)
+        k = p.numel()
+        self._opt.exp_avg[off:off + k].zero_()
+        self._opt.exp_avg_sq[off:off + k].zero_()
+
+    def __iter__(self):
+        o = self._opt
+        o._ensure(required=False)
+        if o._flat is None or o.step_count == 0:
+            return iter(())
+        return iter([q for _, q, _ in o._slots()])
+
+    def __len__(self):
+        return sum(1 for _ in self)
+
+    def __bool__(self):
+        return len(self) > 0
+
+    def apply_pending(self):
+        pend, self._pending = self._pending, {}
+        for p, ent in pend.items():
+            self[p] = ent
+
+
 class FusedAdamW(torch.optim.Optimizer):
     """AdamW + optional global-norm clipping over a model's FlatParams (param_groups: one, as the reference).
 
@@ -32,7 +106,19 @@ class FusedAdamW(torch.optim.Optimizer):
     (CosineAnnealingLR, :1126-1131) drive its ``param_groups[0]['lr']`` and ``state_dict()`` /
     ``load_state_dict()`` use torch.optim.AdamW's layout (per-parameter ``step`` / ``exp_avg`` /
     ``exp_avg_sq`` keyed by the index in that list): optimizer states of reference checkpoints load here and
-    vice versa (train_advanced.py:1226, 1592-1599).  The moments themselves live in two flat device buffers."""
+    vice versa (train_advanced.py:1226, 1592-1599).  The moments themselves live in two flat device buffers;
+    ``optimizer.state`` is a live per-parameter view of them (_LiveState).
+
+    Non-finite steps are skipped on the device, as the reference never applies them (GradScaler.step on the AMP
+    path, train_advanced.py:751-762; the NaN loss / NaN gradient checks of the fp32 path, :814-832): when the
+    gradient norm is NaN or Inf the parameters, gradients and moments stay untouched, the step count (kept on the
+    device, so no host sync per step) does not advance and ``skipped_steps`` counts the skip.  Under
+    hiseg.distributed the gradients are averaged over the ranks before the step, so a non-finite gradient on any
+    rank makes every rank skip the same step.
+
+    When the model's flat layout is rebuilt (a new trainable set after ``unfreeze_encoder_blocks``, a dtype
+    change), the next ``zero_grad`` / ``step`` re-binds to the new buffers and carries every kept parameter's
+    moments over."""
 
     def __init__(self, model: torch.nn.Module, lr: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.01, max_grad_norm: Optional[float] = 1.0, params=None):
@@ -45,13 +131,17 @@ class FusedAdamW(torch.optim.Optimizer):
         super().__init__(plist, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False,
                                      maximize=False, foreach=None, capturable=False, differentiable=False,
                                      fused=None, decoupled_weight_decay=True))
+        self.state = _LiveState(self)
         self.betas, self.eps, self.weight_decay = betas, eps, weight_decay
         self.max_grad_norm = max_grad_norm
-        self.step_count = 0
         self._flat = None
         self.exp_avg = self.exp_avg_sq = None
         self.partial = None
         self.last_norm: Optional[torch.Tensor] = None
+        self._steps: Optional[torch.Tensor] = None     # device step count, two slots (see hiseg_adamw_step_guarded)
+        self._parity = 0
+        self._host_steps = 0
+        self._skipped: Optional[torch.Tensor] = None
         self._pending_state = None
         self._bump = None
 
@@ -59,57 +149,116 @@ class FusedAdamW(torch.optim.Optimizer):
     def lr(self) -> float:
         return self.param_groups[0]["lr"]
 
-    def _init(self):
+    @property
+    def step_count(self) -> int:
+        """Applied (not skipped) steps; reads the device counter (a host sync) once the buffers exist."""
+        if self._steps is None:
+            return self._host_steps
+        return int(self._steps[self._parity].item())
+
+    @step_count.setter
+    def step_count(self, v: int):
+        if self._steps is None:
+            self._host_steps = int(v)
+        else:
+            self._steps[self._parity] = int(v)
+
+    @property
+    def skipped_steps(self) -> int:
+        """Steps skipped because the gradient norm was not finite (host sync)."""
+        return 0 if self._skipped is None else int(self._skipped.item())
+
+    # ------------------------------------------------------------------------------------- flat layout
+    def _ensure(self, required: bool = True):
+        S = self.model.__dict__.get("_hiseg_train")
+        if S is None:
+            if self._flat is None and required:
+                flat_params_of(self.model)   # raises with the message
+            return
+        f = S.flat
         if self._flat is None:
-            self._flat = flat_params_of(self.model)
-            f = self._flat
-            self._range = (0, f.numel)
-            if self._subset is not None:
-                spans = sorted(f.offsets[id(p)] for p in self._subset)
-                b, e = spans[0][0], spans[-1][0] + spans[-1][1]
-                covered = sum(k for _, k in spans)
-                if covered != e - b:
-                    raise ValueError("FusedAdamW(params=...): the parameters are not contiguous in the flat layout")
-                self._range = (b, e)
-            n = self._range[1] - self._range[0]
-            self.exp_avg = torch.zeros(n, dtype=torch.float32, device=f.data.device)
-            self.exp_avg_sq = torch.zeros_like(self.exp_avg)
-            self.partial = torch.empty(L.lib().hiseg_optim_blocks(), dtype=torch.float32, device=f.data.device)
-            self.last_norm = torch.zeros(1, dtype=torch.float32, device=f.data.device)
-            if self._pending_state is not None:
-                sd, self._pending_state = self._pending_state, None
-                self._load_moments(sd)
+            self._bind(f, carried=None)
+        elif f is not self._flat:
+            self._rebind(f)
+
+    def _range_of(self, f):
+        if self._subset is None:
+            return (0, f.numel)
+        spans = sorted(f.offsets[id(p)] for p in self._subset if id(p) in f.offsets)
+        if not spans:
+            raise ValueError("FusedAdamW(params=...): none of the parameters is trainable in the flat layout")
+        b, e = spans[0][0], spans[-1][0] + spans[-1][1]
+        covered = sum(k for _, k in spans)
+        if covered != e - b:
+            raise ValueError("FusedAdamW(params=...): the parameters are not contiguous in the flat layout")
+        return (b, e)
+
+    def _bind(self, f, carried):
+        steps = self.step_count if self._steps is not None else self._host_steps
+        self._flat = f
+        self._range = self._range_of(f)
+        n = self._range[1] - self._range[0]
+        dev = f.data.device
+        self.exp_avg = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros_like(self.exp_avg)
+        self.partial = torch.empty(L.lib().hiseg_optim_blocks(), dtype=torch.float32, device=dev)
+        self.last_norm = torch.zeros(1, dtype=torch.float32, device=dev)
+        skipped = 0 if self._skipped is None else int(self._skipped.item())
+        self._steps = torch.zeros(2, dtype=torch.int32, device=dev)
+        self._parity = 0
+        self._steps[0] = steps
+        self._skipped = torch.full((1,), skipped, dtype=torch.int32, device=dev)
+        self._bump = None
+        if carried:
+            for _, p, off in self._slots():
+                ent = carried.get(id(p))
+                if ent is not None:
+                    k = p.numel()
+                    self.exp_avg[off:off + k].copy_(ent[0])
+                    self.exp_avg_sq[off:off + k].copy_(ent[1])
+        if self._pending_state is not None:
+            sd, self._pending_state = self._pending_state, None
+            self._load_moments(sd)
+        self.state.apply_pending()
+
+    def _rebind(self, f):
+        """The model re-laid its trainable parameters (new FlatParams): keep every parameter's moments."""
+        carried = {}
+        for _, p, off in self._slots():
+            k = p.numel()
+            carried[id(p)] = (self.exp_avg[off:off + k].clone(), self.exp_avg_sq[off:off + k].clone())
+        self._bind(f, carried)
 
     def zero_grad(self, set_to_none: bool = False):
-        self._init()
+        self._ensure()
         self._flat.grad.zero_()
         self._flat.attach_grads()
 
     @torch.no_grad()
     def step(self, closure=None):
-        """Returns the pre-clip total gradient norm as a device tensor (like clip_grad_norm_)."""
+        """Returns the pre-clip total gradient norm as a device tensor (like clip_grad_norm_); a non-finite norm
+        means the step was skipped (class docstring)."""
         if closure is not None:
             raise NotImplementedError("FusedAdamW.step: closures are not supported (the reference passes none)")
-        self._init()
+        self._ensure()
         f = self._flat
         f.prepare_backward()  # adopt any .grad tensors replaced since the backward
         lib = L.lib()
-        self.step_count += 1
         g0 = self.param_groups[0]
         lr = g0["lr"]
         b1, b2 = g0["betas"]
         eps, wd = g0["eps"], g0["weight_decay"]
-        bc1, bc2 = 1.0 - b1 ** self.step_count, 1.0 - b2 ** self.step_count
         s = L.stream_ptr()
         clip = self.max_grad_norm is not None and self.max_grad_norm > 0
         b, e = self._range
         gp, dp = f.grad.data_ptr() + 4 * b, f.data.data_ptr() + 4 * b
         L.check(lib.hiseg_grad_norm_partials(gp, e - b, self.partial.data_ptr(), s), "grad_norm")
-        L.check(lib.hiseg_adamw_step(dp, gp, self.exp_avg.data_ptr(),
-                                     self.exp_avg_sq.data_ptr(), e - b, float(lr), float(b1), float(b2),
-                                     float(eps), float(wd), float(bc1), float(bc2),
-                                     self.partial.data_ptr(), float(self.max_grad_norm) if clip else 0.0,
-                                     self.last_norm.data_ptr(), s), "adamw_step")
+        L.check(lib.hiseg_adamw_step_guarded(dp, gp, self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), e - b,
+                                             float(lr), float(b1), float(b2), float(eps), float(wd),
+                                             self.partial.data_ptr(), float(self.max_grad_norm) if clip else 0.0,
+                                             self.last_norm.data_ptr(), self._steps.data_ptr(), self._parity,
+                                             self._skipped.data_ptr(), s), "adamw_step")
+        self._parity ^= 1
         # the kernel wrote the parameters in place: bump their versions so plans packed from them (eval
         # forward, frozen-layer caches keyed by tensor version) are rebuilt
         if self._bump is None:
@@ -132,12 +281,13 @@ class FusedAdamW(torch.optim.Optimizer):
         return out
 
     def state_dict(self):
-        self._init()
+        self._ensure()
         state = {}
-        if self.step_count > 0:
+        steps = self.step_count
+        if steps > 0:
             for i, p, off in self._slots():
                 k = p.numel()
-                state[i] = {"step": torch.tensor(float(self.step_count)),
+                state[i] = {"step": torch.tensor(float(steps)),
                             "exp_avg": self.exp_avg[off:off + k].view(p.shape).clone(),
                             "exp_avg_sq": self.exp_avg_sq[off:off + k].view(p.shape).clone()}
         groups = []
@@ -157,8 +307,7 @@ class FusedAdamW(torch.optim.Optimizer):
         for k, v in g.items():
             if k != "params":
                 self.param_groups[0][k] = v
-        if self._flat is None and self.model.__dict__.get("_hiseg_train") is not None:
-            self._init()
+        self._ensure(required=False)
         if self._flat is None:   # no training forward yet: applied when the flat layout exists
             self._pending_state = sd
         else:

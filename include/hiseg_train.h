@@ -188,6 +188,17 @@ int hiseg_grad_norm_partials(const float* g, long long n, float* partial, hiseg_
 int hiseg_adamw_step(float* p, float* g, float* m, float* v, long long n, float lr, float beta1, float beta2, float eps,
                      float weight_decay, float bc1, float bc2, const float* partial, float max_norm, float* norm_out,
                      hiseg_stream_t stream);
+/* The same step with the non-finite guard and the step count on the device (no host sync):
+ *   the reference never applies a step whose gradients are not finite -- GradScaler.step skips it on the
+ *   AMP path (train_advanced.py:751-762), the fp32 path skips a NaN loss / NaN gradients (:814-832).  If
+ *   total = sqrt(sum partial) is NaN or Inf, p, g, m, v are left untouched, the step count is not
+ *   advanced and *skipped is incremented; otherwise t = steps[parity] + 1 drives the bias corrections
+ *   (computed in double as torch.optim.AdamW does) and steps[parity ^ 1] receives the new count
+ *   (steps[parity] otherwise).  The caller flips `parity` every call (two slots: every block reads slot
+ *   `parity` while block 0 writes the other).  norm_out (optional) receives total. */
+int hiseg_adamw_step_guarded(float* p, float* g, float* m, float* v, long long n, float lr, float beta1, float beta2,
+                             float eps, float weight_decay, const float* partial, float max_norm, float* norm_out,
+                             int* steps, int parity, int* skipped, hiseg_stream_t stream);
 
 #ifdef __cplusplus
 }

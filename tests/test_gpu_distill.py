@@ -190,8 +190,9 @@ def test_distill_progressive_unfreeze_f32_matches_oracle(blocks):
 def test_distill_bf16_progressive_schedule_runs():
     """bf16, the reference's schedule in miniature: decoder-only steps, then unfreeze_encoder_blocks(2) with
     the reference's two parameter groups (decoder: lr, clip 1.0; encoder: lr * encoder_lr_scale, unclipped,
-    train_distillation_staged.py:1516-1545) -- the new trainable set re-lays the flat parameters, the loss
-    keeps decreasing and stays finite."""
+    train_distillation_staged.py:1516-1545) and its optimizer-state transfer for the decoder parameters
+    (:1537-1550, new_optimizer.state[p] = optimizer.state[p]) -- the new trainable set re-lays the flat
+    parameters, the decoder keeps its AdamW moments, the loss keeps decreasing and stays finite."""
     import filler
     import hiseg
     from oracle import distill as OD
@@ -201,20 +202,31 @@ def test_distill_bf16_progressive_schedule_runs():
     _, _, m = OD.np_inputs(34, 2, 96, 128)
     m = m.to(DEV)
     losses = []
-    opts = None
+    opts, enc = None, None
     for step in range(8):
         if step == 4:
             enc = model.unfreeze_encoder_blocks(2, learning_rate_scale=0.3)
             assert enc
-            opts = None
         s, t = model(x)
         loss, _ = loss_fn(s, t, m)
         if opts is None:
             opts = [hiseg.FusedAdamW(model.student, lr=1e-3, weight_decay=1e-4, max_grad_norm=1.0,
                                      params=model.student.get_decoder_parameters())]
-            if step >= 4:
-                opts.append(hiseg.FusedAdamW(model.student, lr=3e-4, weight_decay=1e-4, max_grad_norm=None,
-                                             params=enc))
+        elif step == 4:
+            old = opts[0]
+            new = hiseg.FusedAdamW(model.student, lr=1e-3, weight_decay=1e-4, max_grad_norm=1.0,
+                                   params=model.student.get_decoder_parameters())
+            moved = 0
+            if hasattr(old, "state") and old.state:
+                for new_p in new.param_groups[0]["params"]:
+                    for old_p in old.param_groups[0]["params"]:
+                        if new_p is old_p and old_p in old.state:
+                            new.state[new_p] = old.state[old_p]
+                            moved += 1
+                            break
+            assert moved == len(new.param_groups[0]["params"]) and new.step_count == 4
+            opts = [new, hiseg.FusedAdamW(model.student, lr=3e-4, weight_decay=1e-4, max_grad_norm=None,
+                                          params=enc)]
         for o in opts:
             o.zero_grad()
         loss.backward()

@@ -164,6 +164,11 @@ VARIANT_CASES = {
     "3x3_40_to_240_overhang": (2, 40, 0, 240, 6, 7, 3, False, False, True, True),
     "1x1_256+8_combiner_tail": (2, 256, 8, 256, 9, 7, 1, False, True, False, True),
     "1x1_128+40_tail_cout64": (2, 128, 40, 64, 5, 13, 1, False, False, True, False),
+    # the wide-tile kernel's classes (variants 70 / 72): ragged pixel tiles, two sources, Cout 128 / 256
+    "3x3_256_res_ragged": (3, 256, 0, 256, 13, 11, 3, False, True, False, False),
+    "3x3_128+128_to_256": (2, 128, 128, 256, 9, 7, 3, False, False, False, False),
+    "1x1_256_to_128_res": (2, 256, 0, 128, 10, 9, 1, False, True, False, False),
+    "3x3_256_smp_decoder0_30x40": (2, 256, 0, 256, 30, 40, 3, False, False, False, False),
 }
 
 
@@ -188,7 +193,7 @@ def test_conv_kernel_variants_bit_identical(name):
     R = ops.Act.from_nchw(torch.randn(N, Cout, oH, oW, device=DEV, generator=g), dt) if res else None
     M = ops.Act.from_nchw(torch.rand(N, Cout, oH, oW, device=DEV, generator=g), dt) if mul else None
     outs = {}
-    for v in (-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 40, 42, 43, 61, 62, 66, 67, 68, 69):
+    for v in (-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 40, 42, 43, 61, 62, 66, 67, 68, 69, 70, 72):
         o2a = ops.Act.new(N, oH, oW, Cout, dt, DEV) if o2 else None
         y = ops.conv2d(p, xa, xb, residual=R, mul=M, out2=o2a, variant=v)
         torch.cuda.synchronize()
