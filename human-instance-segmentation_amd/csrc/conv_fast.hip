@@ -320,10 +320,12 @@ int conv_fast_try(const ConvArgs& a, hipStream_t s, int variant) {
     case 6: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 256, 2, 4, 2>(a, s); break;
     case 7: if (d.Cout_pad % 256) return 0; r = launch_fast<256, 128, 4, 2, 2>(a, s); break;
     case 8: if (d.Cout_pad % 64) return 0; r = launch_fast<64, 128, 1, 4, 2>(a, s); break;
-    // timing-only ceilings (K-loop without global loads: wrong outputs)
+#ifdef HISEG_DIAG
+    // timing-only ceilings (K-loop without global loads: wrong outputs) and the s_memtime stamp variant
     case 9: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 2, 2, 2, true>(a, s); break;
     case 19: if (d.Cout_pad % 256) return 0; r = launch_fast<256, 256, 2, 4, 2, true>(a, s); break;
     case 18: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 2, 2, 2, false, true>(a, s); break;
+#endif
     // schedule variants of the production 128x128 configuration (variant 4)
     case 60: if (d.Cout_pad % 128) return 0; r = launch_fast<128, 128, 2, 2, 2, false, false, true, false>(a, s); break;
     // 4 Cout x N pixel wave grids with 32x64 wave tiles: 128x128 (61, 8 waves), 128x64 (62), 128x256 (63, 16 waves),

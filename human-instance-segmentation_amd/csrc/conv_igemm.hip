@@ -236,10 +236,12 @@ static int launch_typed(const ConvArgs& a, hipStream_t s) {
 
 namespace hiseg {
 int conv_fast_try(const ConvArgs& a, hipStream_t s, int variant);
+#ifdef HISEG_DIAG
 int conv_halo_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_halo2_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_halo3_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_8ph_try(const ConvArgs& a, hipStream_t s, int variant);
+#endif
 int conv_wide_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_small_try(const ConvArgs& a, hipStream_t s, int variant);
 }
@@ -253,7 +255,19 @@ extern "C" int hiseg_conv2d_fwd(const hiseg_conv2d_desc* d, hiseg_stream_t strea
   return conv2d_impl(d, stream, 0);
 }
 
+// The variants a release library accepts: the automatic choice, the generic kernel and every configuration
+// tests/test_gpu_parity.py checks bit for bit.  Timing-only, stamp and experimental kernels exist only in a
+// -DHISEG_DIAG build (Makefile DIAG=1).
+static bool release_variant(int v) {
+  return v == -1 || v == 0 || (v >= 1 && v <= 8) || v == 50 || v == 51 || v == 52 || v == 54 || v == 58 ||
+         (v >= 60 && v <= 69) || v == 70 || v == 71 || v == 72;
+}
+
 extern "C" int hiseg_conv2d_fwd_variant(const hiseg_conv2d_desc* d, int variant, hiseg_stream_t stream) {
+#ifndef HISEG_DIAG
+  HISEG_REQUIRE(release_variant(variant), HISEG_ERR_BAD_ARG,
+                "conv2d: variant %d is not a release variant (diagnostic kernels need a DIAG=1 build)", variant);
+#endif
   return conv2d_impl(d, stream, variant);
 }
 
@@ -303,6 +317,7 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
   } else if (variant >= 50) {
     const int r = conv_small_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
+#ifdef HISEG_DIAG
   } else if (variant >= 40) {
     const int r = conv_8ph_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
@@ -315,6 +330,7 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
   } else if (variant >= 10 && variant != 18 && variant != 19) {
     const int r = conv_halo_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
+#endif
   } else if (variant >= 0) {
     int v = variant;
     // 61 = 128x128 ring, 8 waves as 4 (Cout) x 2 (pixel) with 32x64 wave tiles, LDS full-row epilogue;

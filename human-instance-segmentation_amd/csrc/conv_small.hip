@@ -291,10 +291,14 @@ static int pick_th(const ConvArgs& a, hipStream_t s, int WS, int PS, int force_t
   }
   if (lds_for(th) > 160 * 1024) return 0;
   int r;
+#ifdef HISEG_DIAG
   if (stamp) {
     r = th == 8 ? launch_small<KS, 8, TO, true>(a, s, WS, PS, lds_for(8)) : HISEG_ERR_BAD_ARG;
     return r < 0 ? r : 1;
   }
+#else
+  if (stamp) return HISEG_ERR_BAD_ARG;   // the stamp variant exists only in a DIAG=1 build
+#endif
   switch (th) {
     case 8: r = launch_small<KS, 8, TO>(a, s, WS, PS, lds_for(8)); break;
     case 4: r = launch_small<KS, 4, TO>(a, s, WS, PS, lds_for(4)); break;

@@ -28,6 +28,12 @@
 
 namespace hiseg {
 
+#ifdef HISEG_DIAG
+constexpr bool HISEG_DIAG_ON = true;
+#else
+constexpr bool HISEG_DIAG_ON = false;
+#endif
+
 typedef __attribute__((address_space(3))) void lds_void_w;
 
 __device__ __forceinline__ void dma16w(__amdgpu_buffer_rsrc_t rsrc, unsigned lds_addr, unsigned voff) {
@@ -466,7 +472,7 @@ static int launch_wide(const ConvArgs& a, hipStream_t s) {
 int conv_wide_try(const ConvArgs& a, hipStream_t s, int variant) {
   const hiseg_conv2d_desc& d = a.d;
   if (d.dtype != HISEG_BF16 || d.out_dtype != HISEG_BF16) return 0;
-  if (d.a_up != 1 || d.in_scale != nullptr || d.convT || d.mul != nullptr || (d.out2 != nullptr && variant != 79)) return 0;
+  if (d.a_up != 1 || d.in_scale != nullptr || d.convT || d.mul != nullptr || (d.out2 != nullptr && !(HISEG_DIAG_ON && variant == 79))) return 0;
   if (d.act != HISEG_ACT_NONE && d.act != HISEG_ACT_RELU) return 0;
   if (d.Ca % 64 != 0 || d.Cb % 64 != 0) return 0;
   if (d.K_pad != d.KH * d.KW * a.Cin || d.K_pad < 128) return 0;   // >= 4 K stages (the pipeline's depth)
@@ -486,18 +492,21 @@ int conv_wide_try(const ConvArgs& a, hipStream_t s, int variant) {
   switch (variant) {
     case 70: if (d.Cout % 256) return 0; r = launch_wide<256>(a, s); break;
     case 72: r = launch_wide<128>(a, s); break;
-    // timing-only diagnostics (wrong outputs): 77 no K-loop DMA, 75 no activation DMA, 76 no weight DMA
+#ifdef HISEG_DIAG
+    // timing-only diagnostics (wrong outputs): 77 no K-loop DMA, 75 no activation DMA, 76 no weight DMA, 73 every
+    // activation read an L2 hit; 79 per-workgroup s_memtime stamps into desc.out2
     case 77: if (d.Cout % 256) return 0; r = launch_wide<256, false, 1>(a, s); break;
     case 75: if (d.Cout % 256) return 0; r = launch_wide<256, false, 2>(a, s); break;
     case 76: if (d.Cout % 256) return 0; r = launch_wide<256, false, 3>(a, s); break;
-    case 74: if (d.Cout % 256) return 0; r = launch_wide<256, false, 0, true>(a, s); break;   // channel-major K
-    case 71: if (d.Cout % 256) return 0; r = launch_wide<256, false, 0, false, 5>(a, s); break;   // 5-deep ring
-    case 73: if (d.Cout % 256) return 0; r = launch_wide<256, false, 4>(a, s); break;         // diagnostic
-    case 79:   // diagnostic: per-workgroup s_memtime stamps into desc.out2
+    case 73: if (d.Cout % 256) return 0; r = launch_wide<256, false, 4>(a, s); break;
+    case 79:
       HISEG_REQUIRE(d.out2 != nullptr, HISEG_ERR_BAD_ARG, "conv_wide: stamp variant needs desc.out2");
       if (d.Cout % 256) return 0;
       r = launch_wide<256, true>(a, s);
       break;
+    case 74: if (d.Cout % 256) return 0; r = launch_wide<256, false, 0, true>(a, s); break;   // channel-major K
+#endif
+    case 71: if (d.Cout % 256) return 0; r = launch_wide<256, false, 0, false, 5>(a, s); break;   // 5-deep ring
     default: return 0;
   }
   return r < 0 ? r : 1;

@@ -57,10 +57,10 @@ def test_product_path_refuses_cpu_tensors():
         DynamicRoIAlign(640, aligned=True)(torch.zeros(1, 1, 4, 4), torch.zeros(1, 5), 2, 2)
 
 
-def test_stamp_diagnostic_variants_refuse_a_missing_stamp_buffer():
-    """The s_memtime diagnostic variants (18 conv_fast, 41 conv_8ph; 59 conv_small likewise) write their stamps
-    through desc.out2; without that buffer they must refuse before any launch (a null-pointer stamp write
-    is an illegal address on the GPU)."""
+def test_release_library_refuses_diagnostic_conv_variants():
+    """Timing-only (9, 19, 73, 75-77), s_memtime-stamp (18, 41, 59, 79) and experimental (10-45) conv variants
+    exist only in a DIAG=1 build (Makefile): the release libhiseg.so refuses them before any launch, with
+    HISEG_ERR_BAD_ARG (a stamp variant without its buffer once wrote to an illegal address)."""
     import ctypes
     from hiseg import _lib as L
     d = L.Conv2dDesc()
@@ -72,7 +72,7 @@ def test_stamp_diagnostic_variants_refuse_a_missing_stamp_buffer():
     d.weight, d.Cout, d.Cout_pad, d.K_pad = fake, 256, 256, 9 * 256
     d.scale, d.shift, d.act = fake, fake, 0
     d.out, d.o_cstride, d.o_coff = fake, 256, 0
-    for v in (18, 41):
+    for v in (9, 10, 18, 19, 20, 30, 40, 41, 44, 59, 73, 75, 76, 77, 79, 99, -5):
         st = L.lib().hiseg_conv2d_fwd_variant(ctypes.byref(d), v, None)
-        assert st != 0, v
-        assert b"stamp variant needs desc.out2" in L.lib().hiseg_last_error_string(), v
+        assert st == -1, v   # HISEG_ERR_BAD_ARG
+        assert b"not a release variant" in L.lib().hiseg_last_error_string(), v

@@ -193,7 +193,7 @@ def test_conv_kernel_variants_bit_identical(name):
     R = ops.Act.from_nchw(torch.randn(N, Cout, oH, oW, device=DEV, generator=g), dt) if res else None
     M = ops.Act.from_nchw(torch.rand(N, Cout, oH, oW, device=DEV, generator=g), dt) if mul else None
     outs = {}
-    for v in (-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 40, 42, 43, 61, 62, 66, 67, 68, 69, 70, 72):
+    for v in (-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 61, 62, 66, 67, 68, 69, 70, 71, 72):
         o2a = ops.Act.new(N, oH, oW, Cout, dt, DEV) if o2 else None
         y = ops.conv2d(p, xa, xb, residual=R, mul=M, out2=o2a, variant=v)
         torch.cuda.synchronize()

@@ -3,6 +3,9 @@
 For every shape: checks each variant against the generic kernel (variant -1), then times all
 variants in interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24).
 Usage: python tools/conv_bench.py [--variants -1,0,1,2] [--reps 20] [--rounds 3]
+
+Diagnostic variants (timing-only, stamps, experimental kernels) need the DIAG=1 library:
+`make -C human-instance-segmentation_amd DIAG=1` and HISEG_LIB=human-instance-segmentation_amd/hiseg/libhiseg_diag.so.
 """
 import argparse
 import ctypes

@@ -3,6 +3,9 @@ rocprofv3 --pmc / --kernel-trace passes over a single launch class.
 
 Usage: python tools/conv_one.py --shape res256_3x3_64x48 --variants 61,40 [--reps 20]
 Shapes are tools/conv_bench.SHAPES.
+
+Diagnostic variants (timing-only, stamps, experimental kernels) need the DIAG=1 library:
+`make -C human-instance-segmentation_amd DIAG=1` and HISEG_LIB=human-instance-segmentation_amd/hiseg/libhiseg_diag.so.
 """
 import argparse
 import os

@@ -1,4 +1,5 @@
-"""Per-workgroup s_memtime breakdown (prologue / K loop / epilogue) of a conv variant (diagnostic)."""
+"""(DIAG=1 library: make -C human-instance-segmentation_amd DIAG=1; HISEG_LIB=.../libhiseg_diag.so)
+Per-workgroup s_memtime breakdown (prologue / K loop / epilogue) of a conv variant (diagnostic)."""
 import ctypes, os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "human-instance-segmentation_amd"))
