@@ -442,7 +442,7 @@ def cpu_train_baseline(seconds_budget=30.0):
 
 def load_traffic():
     """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3 PMC summary, if any."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    path = os.path.join(ROOT, "profiles", "r2_pmc_traffic.json")
     if not os.path.exists(path):
         return None
     try:
@@ -624,7 +624,7 @@ def infer_bench(args, device, dtype, rank, world, dist):
         achieved = summ["flops"] / (summ["avg_ms"] * 1e-3) / 1e12
         roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": load_traffic(),
-                    "kernel": "conv_fast_kernel<128,128,4,2,2,lds-epilogue> (LDS-DMA ring, 8 waves as 4 Cout x 2 pixel, LDS full-row epilogue) 256->256 3x3 @64x48 x256 ROIs",
+                    "kernel": "conv_wide_kernel<256,4> (256x256 workgroup tile, 4-stage LDS-DMA ring, 128x128 wave tiles in AGPRs, LDS-staged epilogue) 256->256 3x3 @64x48 x256 ROIs",
                     "launches_timed": summ["launches"], "avg_launch_ms": round(summ["avg_ms"], 4),
                     "flop_per_launch": summ["flops"]}
     pipeline_tflops = value * GFLOP_PER_ROI_MASK / 1e3

@@ -41,13 +41,37 @@ template <> struct Elem<bf16_t> {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
-__device__ __forceinline__ float apply_act(float v, int act) {
+// nn.GELU() (approximate='none'): x * Phi(x) with the exact erf
+__device__ __forceinline__ float gelu_(float v) { return 0.5f * v * (1.f + erff(v * 0.70710678118654752f)); }
+
+// Activation of the pre-activation v (advanced/activation_utils.py:71-101); beta is Swish's.
+__device__ __forceinline__ float apply_act(float v, int act, float beta = 1.f) {
   switch (act) {
     case HISEG_ACT_RELU: return v > 0.f ? v : 0.f;
     case HISEG_ACT_SIGMOID: return sigmoidf_(v);
     case HISEG_ACT_SILU: return v * sigmoidf_(v);
+    case HISEG_ACT_GELU: return gelu_(v);
+    case HISEG_ACT_SWISH: return v * sigmoidf_(beta * v);
     default: return v;
   }
+}
+
+// d act / d v at the pre-activation v.
+__device__ __forceinline__ float act_grad_pre(float v, int act, float beta = 1.f) {
+  switch (act) {
+    case HISEG_ACT_RELU: return v > 0.f ? 1.f : 0.f;
+    case HISEG_ACT_SIGMOID: { const float s = sigmoidf_(v); return s * (1.f - s); }
+    case HISEG_ACT_SILU: { const float s = sigmoidf_(v); return s * (1.f + v * (1.f - s)); }
+    case HISEG_ACT_SWISH: { const float s = sigmoidf_(beta * v); return s * (1.f + beta * v * (1.f - s)); }
+    case HISEG_ACT_GELU:
+      return 0.5f * (1.f + erff(v * 0.70710678118654752f)) + v * 0.39894228040143268f * __expf(-0.5f * v * v);
+    default: return 1.f;
+  }
+}
+
+// Activations whose derivative needs the pre-activation (not recoverable from the output).
+__host__ __device__ __forceinline__ bool act_smooth(int act) {
+  return act == HISEG_ACT_SILU || act == HISEG_ACT_GELU || act == HISEG_ACT_SWISH;
 }
 
 // Unpack a 16-B chunk into f32 values / pack back.

@@ -287,7 +287,7 @@ __global__ void __launch_bounds__(512) conv_8ph_kernel(ConvArgs a) {
             v[2] += __uint_as_float(qv.y << 16); v[3] += __uint_as_float(qv.y & 0xffff0000u);
           }
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], d.act);
+          for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], d.act, d.act_beta);
           if (has_mul) {
             const uint2 qv = em[i][j];
             v[0] *= __uint_as_float(qv.x << 16); v[1] *= __uint_as_float(qv.x & 0xffff0000u);

@@ -95,7 +95,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, int px, int co,
     for (int e = 0; e < 4; ++e) v[e] += r[e];
   }
 #pragma unroll
-  for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], d.act);
+  for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], d.act, d.act_beta);
   if (d.mul) {
     float m[4];
     const bool vec = (nv == 4) && ((d.m_cstride | d.m_coff | oc) & 3) == 0;
@@ -204,7 +204,7 @@ struct TileEpi {
           for (int e = 0; e < 4; ++e) v[e] += Quad<T>::get(res[i][j], e);
         }
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], d.act);
+        for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], d.act, d.act_beta);
         if (d.mul) {
           const typename Quad<T>::V m = Quad<T>::load(d.mul, op * d.m_cstride + d.m_coff + oc);
 #pragma unroll

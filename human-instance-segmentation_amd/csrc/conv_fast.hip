@@ -227,7 +227,7 @@ __global__ void __launch_bounds__(64 * WCO * WPX) conv_fast_kernel(ConvArgs a) {
             for (int e = 0; e < 4; ++e) v[e] += Quad<bf16_t>::get(ep.res[i][j], e);
           }
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], d.act);
+          for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], d.act, d.act_beta);
           *reinterpret_cast<float4*>(st + rl * BCO + (((cl >> 2) ^ (rl & (NCH - 1))) << 2)) =
               make_float4(v[0], v[1], v[2], v[3]);
         }

@@ -223,7 +223,7 @@ __global__ void __launch_bounds__(256) conv_small_kernel(ConvArgs a, int WS, int
               v[2] += __uint_as_float(eres[q][j].y << 16); v[3] += __uint_as_float(eres[q][j].y & 0xffff0000u);
             }
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], d.act);
+            for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], d.act, d.act_beta);
             if (d.mul) {   // (vec only: lite without vec excludes mul)
               const uint2 m = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(d.mul) + (long long)px * d.m_cstride + d.m_coff + co);
               v[0] *= __uint_as_float(m.x << 16); v[1] *= __uint_as_float(m.x & 0xffff0000u);

@@ -168,7 +168,7 @@ __global__ void __launch_bounds__(256) gap_reduce_kernel(const float* partial, i
 // (N, ceil(Cr / 4)); gate = sigmoid(W2 hidden + b2), one wave per channel, grid (N, ceil(C / 4)).  Lanes
 // stride the reduction axis (coalesced weight rows), xor-shuffle reduction.
 __global__ void __launch_bounds__(256) se_hidden_kernel(const float* sums, int HW, int C, const float* w1,
-                                                        const float* b1, int Cr, int act, float* hid) {
+                                                        const float* b1, int Cr, int act, float beta, float* hid) {
   const int n = blockIdx.x, lane = threadIdx.x & 63;
   const int r = blockIdx.y * 4 + (threadIdx.x >> 6);
   if (r >= Cr) return;
@@ -178,7 +178,7 @@ __global__ void __launch_bounds__(256) se_hidden_kernel(const float* sums, int H
   for (int c = lane; c < C; c += 64) s += w1[(long long)r * C + c] * (m[c] * inv);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  if (lane == 0) hid[(long long)n * Cr + r] = apply_act(s + (b1 ? b1[r] : 0.f), act);
+  if (lane == 0) hid[(long long)n * Cr + r] = apply_act(s + (b1 ? b1[r] : 0.f), act, beta);
 }
 
 __global__ void __launch_bounds__(256) se_out_kernel(const float* hid, int C, int Cr, const float* w2, const float* b2,
@@ -195,9 +195,9 @@ __global__ void __launch_bounds__(256) se_out_kernel(const float* hid, int C, in
 }
 
 // gate holds the pooled sums on entry and the gate on exit; scratch (>= N * Cr floats) takes the hidden units
-static void se_mlp(const float* w1, const float* b1, int Cr, const float* w2, const float* b2, int act, int N, int HW,
-                   int C, float* scratch, float* gate, hipStream_t s) {
-  hipLaunchKernelGGL(se_hidden_kernel, dim3(N, (Cr + 3) / 4), dim3(256), 0, s, gate, HW, C, w1, b1, Cr, act, scratch);
+static void se_mlp(const float* w1, const float* b1, int Cr, const float* w2, const float* b2, int act, float beta, int N,
+                   int HW, int C, float* scratch, float* gate, hipStream_t s) {
+  hipLaunchKernelGGL(se_hidden_kernel, dim3(N, (Cr + 3) / 4), dim3(256), 0, s, gate, HW, C, w1, b1, Cr, act, beta, scratch);
   hipLaunchKernelGGL(se_out_kernel, dim3(N, (C + 3) / 4), dim3(256), 0, s, scratch, C, Cr, w2, b2, gate);
 }
 
@@ -363,13 +363,13 @@ __global__ void __launch_bounds__(256) input_norm_kernel(const float* x, int B, 
 template <typename T>
 __global__ void __launch_bounds__(256) hier_combine_kernel(const float* low, int N, int h, int w, const void* tfeat, int Ct,
                                                            const float* ut_w, const float* ut_scale, const float* ut_shift,
-                                                           int ut_act, const float* u1_w, const float* u1_b,
-                                                           const float* t_w, const float* t_b, float* logits, float* bgfg,
-                                                           float* tn) {
+                                                           int ut_act, float ut_beta, int ut_ns, const float* u1_w,
+                                                           const float* u1_b, const float* t_w, const float* t_b,
+                                                           float* logits, float* bgfg, float* tn) {
   __shared__ float s_ut[2 * 32 * 4], s_us[32], s_ush[32], s_u1[64], s_tw[2 * 512];
   const int t = threadIdx.x;
   for (int i = t; i < 256; i += 256) s_ut[i] = ut_w[i];
-  if (t < 32) { s_us[t] = ut_scale[t]; s_ush[t] = ut_shift[t]; }
+  if (t < 32 && !ut_ns) { s_us[t] = ut_scale[t]; s_ush[t] = ut_shift[t]; }
   if (t < 64) s_u1[t] = u1_w[t];
   for (int i = t; i < 2 * Ct; i += 256) s_tw[i] = t_w[i];
   __syncthreads();
@@ -385,10 +385,13 @@ __global__ void __launch_bounds__(256) hier_combine_kernel(const float* low, int
   const float* lo = low + (((long long)n * h + (Y >> 1)) * w + (X >> 1)) * 2;
   const float l0 = lo[0], l1 = lo[1];
   float b0 = u1_b[0], b1 = u1_b[1];
+  // per-sample tables (LayerNorm2d: ut_ns == 32) are read from global memory, the shared fold otherwise
+  const float* usc = ut_ns ? ut_scale + (long long)n * ut_ns : s_us;
+  const float* ush = ut_ns ? ut_shift + (long long)n * ut_ns : s_ush;
   for (int co = 0; co < 32; ++co) {
     // ConvTranspose2d weight [ci][co][dy][dx]
     float hsum = l0 * s_ut[((0 * 32 + co) * 2 + dy) * 2 + dx] + l1 * s_ut[((1 * 32 + co) * 2 + dy) * 2 + dx];
-    hsum = apply_act(hsum * s_us[co] + s_ush[co], ut_act);
+    hsum = apply_act(hsum * usc[co] + ush[co], ut_act, ut_beta);
     b0 += s_u1[co] * hsum;
     b1 += s_u1[32 + co] * hsum;
   }
@@ -572,7 +575,7 @@ extern "C" int hiseg_gap_splits(int HW) {
 }
 
 extern "C" int hiseg_se_gate_fwd(int dtype, const void* x, int N, int HW, int C, const float* w1, const float* b1, int Cr,
-                                 const float* w2, const float* b2, int act, float* partial, float* gate,
+                                 const float* w2, const float* b2, int act, float act_beta, float* partial, float* gate,
                                  hiseg_stream_t stream) {
   HISEG_REQUIRE(x && w1 && w2 && partial && gate && N > 0 && HW > 0 && C > 0 && Cr > 0, HISEG_ERR_BAD_ARG,
                 "se_gate: bad args");
@@ -587,7 +590,7 @@ extern "C" int hiseg_se_gate_fwd(int dtype, const void* x, int N, int HW, int C,
   // the pooled sums go through the gate buffer: each se_gate block reads its image's row into LDS before
   // it overwrites that row with the gate
   hipLaunchKernelGGL(gap_reduce_kernel, dim3(N, (C + 63) / 64), dim3(256), 0, s, partial, splits, C, gate);
-  se_mlp(w1, b1, Cr, w2, b2, act, N, HW, C, partial, gate, s);   // partial (consumed) holds the hidden units
+  se_mlp(w1, b1, Cr, w2, b2, act, act_beta, N, HW, C, partial, gate, s);   // partial (consumed): hidden units
   return hiseg_check_launch("se_gate");
 }
 
@@ -611,6 +614,7 @@ static int dwconv_launch(int dtype, const void* in, int N, int H, int W, int C, 
                          const float* scale, const float* shift, int act, void* out, int Ho, int Wo, float* gap,
                          hipStream_t s) {
   HISEG_REQUIRE(in && w && scale && shift && out && N > 0 && H > 0 && W > 0, HISEG_ERR_BAD_ARG, "dwconv: bad args");
+  HISEG_REQUIRE(act != HISEG_ACT_SWISH, HISEG_ERR_BAD_ARG, "dwconv: Swish(beta) is not an EfficientNet activation");
   HISEG_REQUIRE(C % chunk_of(dtype) == 0, HISEG_ERR_BAD_SHAPE, "dwconv: C must be chunk aligned");
   HISEG_REQUIRE((K == 3 || K == 5) && (stride == 1 || stride == 2), HISEG_ERR_BAD_SHAPE, "dwconv: K %d stride %d", K,
                 stride);
@@ -661,7 +665,8 @@ extern "C" int hiseg_se_gate_partials_fwd(float* partial, int splits, int N, int
   // pooled sums through the gate buffer (read into LDS per image before the gate overwrites them)
   HISEG_REQUIRE((long long)splits * C >= Cr, HISEG_ERR_BAD_SHAPE, "se_gate_partials: partial buffer below N * Cr");
   hipLaunchKernelGGL(gap_reduce_kernel, dim3(N, (C + 63) / 64), dim3(256), 0, s, partial, splits, C, gate);
-  se_mlp(w1, b1, Cr, w2, b2, act, N, HW, C, partial, gate, s);   // partial (consumed) holds the hidden units
+  HISEG_REQUIRE(act != HISEG_ACT_SWISH, HISEG_ERR_BAD_ARG, "se_gate_partials: Swish(beta) is not an EfficientNet act");
+  se_mlp(w1, b1, Cr, w2, b2, act, 1.f, N, HW, C, partial, gate, s);   // partial (consumed) holds the hidden units
   return hiseg_check_launch("se_gate_partials");
 }
 
@@ -687,8 +692,9 @@ extern "C" int hiseg_input_norm_fwd(int dtype, const float* x, int B, int C, int
 
 extern "C" int hiseg_hier_combine_fwd(int dtype, const float* low, int N, int h, int w, const void* tfeat, int Ct,
                                       const float* ut_w, const float* ut_scale, const float* ut_shift, int ut_act,
-                                      const float* u1_w, const float* u1_b, const float* t_w, const float* t_b, float* logits,
-                                      float* bgfg, float* tn, hiseg_stream_t stream) {
+                                      float ut_beta, int ut_per_sample, const float* u1_w, const float* u1_b,
+                                      const float* t_w, const float* t_b, float* logits, float* bgfg, float* tn,
+                                      hiseg_stream_t stream) {
   HISEG_REQUIRE(low && tfeat && ut_w && ut_scale && ut_shift && u1_w && u1_b && t_w && t_b && logits, HISEG_ERR_BAD_ARG,
                 "hier_combine: null pointer");
   HISEG_REQUIRE(N >= 0 && h > 0 && w > 0 && Ct > 0 && Ct <= 512 && Ct % chunk_of(dtype) == 0, HISEG_ERR_BAD_SHAPE,
@@ -696,8 +702,70 @@ extern "C" int hiseg_hier_combine_fwd(int dtype, const float* low, int N, int h,
   if (N == 0) return HISEG_OK;
   const long long total = (long long)N * 4 * h * w;
   DISPATCH_T(dtype, hier_combine_kernel, dim3(nblocks(total, 256)), dim3(256), 0, (hipStream_t)stream, low, N, h, w, tfeat,
-             Ct, ut_w, ut_scale, ut_shift, ut_act, u1_w, u1_b, t_w, t_b, logits, bgfg, tn);
+             Ct, ut_w, ut_scale, ut_shift, ut_act, ut_beta, ut_per_sample ? 32 : 0, u1_w, u1_b, t_w, t_b, logits, bgfg,
+             tn);
   return hiseg_check_launch("hier_combine");
+}
+
+// LayerNorm2d over upsample_bg_fg's ConvTranspose2d(2, 32, 2, s2) output z (model.py:18-38 at
+// refinement.py:501-503): per sample n, mean / biased variance of z over (32, 2h, 2w) accumulated in double,
+// then the folded tables scale[n][c] = gamma_c * invstd_n, shift[n][c] = beta_c - mean_n * scale[n][c].
+// One block per sample: 32 channel lanes x 8 low-pixel rows, 4 children per low pixel.
+__global__ void __launch_bounds__(256) ubf_ln_tables_kernel(const float* low, int h, int w, const float* ut_w,
+                                                            const float* ut_b, const float* gamma, const float* beta,
+                                                            float eps, int fold_bias, float* mean, float* invstd,
+                                                            float* scale, float* shift) {
+  __shared__ double s1[256], s2[256];
+  __shared__ float s_mi[2];
+  const int n = blockIdx.x, t = threadIdx.x, c = t & 31, r = t >> 5;
+  float wa[4], wb[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) { wa[q] = ut_w[c * 4 + q]; wb[q] = ut_w[(32 + c) * 4 + q]; }
+  const float bc = ut_b ? ut_b[c] : 0.f;
+  double a1 = 0.0, a2 = 0.0;
+  const int PL = h * w;
+  const float* lo = low + (long long)n * PL * 2;
+  for (int p = r; p < PL; p += 8) {
+    const float l0 = lo[p * 2], l1 = lo[p * 2 + 1];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const double z = (double)(l0 * wa[q] + l1 * wb[q] + bc);
+      a1 += z; a2 += z * z;
+    }
+  }
+  s1[t] = a1; s2[t] = a2;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (t < st) { s1[t] += s1[t + st]; s2[t] += s2[t + st]; }
+    __syncthreads();
+  }
+  if (t == 0) {
+    const double M = 128.0 * PL;
+    const double m = s1[0] / M;
+    double var = s2[0] / M - m * m;
+    if (var < 0.0) var = 0.0;
+    const float inv = (float)(1.0 / sqrt(var + (double)eps));
+    s_mi[0] = (float)m; s_mi[1] = inv;
+    if (mean) mean[n] = (float)m;
+    if (invstd) invstd[n] = inv;
+  }
+  __syncthreads();
+  if (t < 32) {   // fold_bias: tables for the bias-free ConvTranspose sum of hier_combine_kernel
+    const float k = (gamma ? gamma[t] : 1.f) * s_mi[1];
+    const float m = fold_bias && ut_b ? s_mi[0] - ut_b[t] : s_mi[0];
+    scale[n * 32 + t] = k;
+    shift[n * 32 + t] = (beta ? beta[t] : 0.f) - m * k;
+  }
+}
+
+extern "C" int hiseg_ubf_ln_tables(const float* low, int N, int h, int w, const float* ut_w, const float* ut_b,
+                                   const float* gamma, const float* beta, float eps, int fold_bias, float* mean,
+                                   float* invstd, float* scale, float* shift, hiseg_stream_t stream) {
+  HISEG_REQUIRE(low && ut_w && scale && shift && N >= 0 && h > 0 && w > 0, HISEG_ERR_BAD_ARG, "ubf_ln_tables: bad args");
+  if (N == 0) return HISEG_OK;
+  hipLaunchKernelGGL(ubf_ln_tables_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, low, h, w, ut_w, ut_b, gamma,
+                     beta, eps, fold_bias, mean, invstd, scale, shift);
+  return hiseg_check_launch("ubf_ln_tables");
 }
 
 extern "C" int hiseg_nhwc_to_nchw_fwd(int dtype, const void* in, int N, int H, int W, int C, int cstride, int coff, float* out,

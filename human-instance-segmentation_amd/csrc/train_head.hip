@@ -316,20 +316,13 @@ static void ca_gap(const void* x, const void* dout, const float* mul, int N, int
     hipLaunchKernelGGL(ca_gap_kernel<T>, dim3(N, kGapSplits), dim3(256), 0, s, x, dout, mul, HW, C, part);
 }
 
-__device__ __forceinline__ float act_f(float v, int act) { return apply_act(v, act); }
-__device__ __forceinline__ float act_d(float pre, int act) {
-  switch (act) {
-    case HISEG_ACT_RELU: return pre > 0.f ? 1.f : 0.f;
-    case HISEG_ACT_SILU: { const float s = sigmoidf_(pre); return s * (1.f + pre * (1.f - s)); }
-    case HISEG_ACT_SIGMOID: { const float s = sigmoidf_(pre); return s * (1.f - s); }
-    default: return 1.f;
-  }
-}
+__device__ __forceinline__ float act_f(float v, int act, float beta) { return apply_act(v, act, beta); }
+__device__ __forceinline__ float act_d(float pre, int act, float beta) { return act_grad_pre(pre, act, beta); }
 
 // per image: gap, hidden pre-activation, gate
 __global__ void __launch_bounds__(256) ca_mlp_kernel(const float* part, int HW, int C, int Cr, const float* w1,
-                                                     const float* w2, int act, float* gap, float* hpre, float* gate,
-                                                     const float* b1 = nullptr, const float* b2 = nullptr) {
+                                                     const float* w2, int act, float beta, float* gap, float* hpre,
+                                                     float* gate, const float* b1 = nullptr, const float* b2 = nullptr) {
   extern __shared__ float sm[];
   float* g = sm;
   float* h = sm + C;
@@ -345,7 +338,7 @@ __global__ void __launch_bounds__(256) ca_mlp_kernel(const float* part, int HW, 
     float s = b1 ? b1[r] : 0.f;
     for (int c = 0; c < C; ++c) s += w1[(long long)r * C + c] * g[c];
     hpre[(long long)n * Cr + r] = s;
-    h[r] = act_f(s, act);
+    h[r] = act_f(s, act, beta);
   }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += 256) {
@@ -403,7 +396,8 @@ __global__ void __launch_bounds__(256) ca_apply_kernel(const void* x, int N, int
 
 // per image: ds = dgate * g (1-g); dh; dgap; per-image weight-gradient rows
 __global__ void __launch_bounds__(256) ca_mlp_bwd_kernel(const float* part, int C, int Cr, const float* w1,
-                                                         const float* w2, int act, const float* gap, const float* hpre,
+                                                         const float* w2, int act, float beta, const float* gap,
+                                                         const float* hpre,
                                                          const float* gate, float* dgap, float* wpart,
                                                          float* bpart = nullptr) {
   extern __shared__ float sm[];
@@ -421,7 +415,7 @@ __global__ void __launch_bounds__(256) ca_mlp_bwd_kernel(const float* part, int 
   for (int r = threadIdx.x; r < Cr; r += 256) {
     float s = 0.f;
     for (int c = 0; c < C; ++c) s += w2[(long long)c * Cr + r] * ds[c];
-    dh[r] = s * act_d(hpre[(long long)n * Cr + r], act);
+    dh[r] = s * act_d(hpre[(long long)n * Cr + r], act, beta);
     if (bpart) bpart[(long long)n * (Cr + C) + r] = dh[r];
   }
   __syncthreads();
@@ -435,7 +429,7 @@ __global__ void __launch_bounds__(256) ca_mlp_bwd_kernel(const float* part, int 
     const int r = i / C, c = i - r * C;
     wp[i] = dh[r] * gap[(long long)n * C + c];
     const int c2 = i / Cr, r2 = i - c2 * Cr;
-    wp[C * Cr + i] = ds[c2] * act_f(hpre[(long long)n * Cr + r2], act);
+    wp[C * Cr + i] = ds[c2] * act_f(hpre[(long long)n * Cr + r2], act, beta);
   }
 }
 
@@ -486,9 +480,10 @@ __global__ void __launch_bounds__(256) ca_dx_kernel(const void* dout, int N, int
 struct UbfArgs {
   const float* low; int N, h, w;
   const float* ut_w; const float* ut_b;     // ConvT [2][32][2][2], bias [32]
-  const float* scale; const float* shift;   // BN(train) fold: a = relu(z*scale + shift)
-  const float* mean; const float* invstd; const float* gamma;
+  const float* scale; const float* shift;   // norm fold: a = act(z*scale + shift); [32] (BN) or [N][32] (LN)
+  const float* mean; const float* invstd; const float* gamma;   // [32] (BN) or [N] (LN)
   const float* u1_w; const float* u1_b;     // [2][32], [2]
+  int act; float beta; int ln;
 };
 
 __device__ __forceinline__ float ubf_z(const UbfArgs& u, float l0, float l1, int c, int q) {
@@ -548,9 +543,10 @@ __global__ void __launch_bounds__(256) ubf_fwd_kernel(UbfArgs u, const void* tfe
   const float* lo = u.low + (((long long)n * u.h + (Y >> 1)) * u.w + (X >> 1)) * 2;
   const float l0 = lo[0], l1 = lo[1];
   float b0 = u.u1_b[0], b1 = u.u1_b[1];
+  const float* sc = u.scale + (u.ln ? n * 32 : 0);
+  const float* sh = u.shift + (u.ln ? n * 32 : 0);
   for (int c = 0; c < 32; ++c) {
-    float a = ubf_z(u, l0, l1, c, q) * u.scale[c] + u.shift[c];
-    a = a > 0.f ? a : 0.f;
+    const float a = apply_act(ubf_z(u, l0, l1, c, q) * sc[c] + sh[c], u.act, u.beta);
     b0 += u.u1_w[c] * a;
     b1 += u.u1_w[32 + c] * a;
   }
@@ -582,15 +578,29 @@ __global__ void __launch_bounds__(256) ubf_fwd_kernel(UbfArgs u, const void* tfe
 // pass 1 (8 pixel rows x 32 channels per block): combine backward -> db, dtn per pixel (written by c == 0);
 // per channel: sum g, sum g*xhat, sum xhat (BN bwd), dW1[k][c] = sum db_k * a_c; db1.
 // partial layout per block: [32 g][32 gx][32 x][64 dW1][2 db1]  (162)
+// LayerNorm (u.ln): sb blocks per sample, block j of sample n covers a slice of that sample only, so the
+// per-block channel sums add up to per-(sample, channel) sums.
 __global__ void __launch_bounds__(256) ubf_bwd1_kernel(UbfArgs u, const float* dlogits, const float* dbgfg_ext,
                                                        const float* dtn_ext, const float* bgfg, const float* tn,
-                                                       float* db_out, float* dtn_out, float* partial) {
+                                                       float* db_out, float* dtn_out, float* partial, int sb) {
   __shared__ float red[8][162];
   const int t = threadIdx.x, c = t & 31, r = t >> 5;
   const int H = 2 * u.h, W = 2 * u.w;
   const long long P = (long long)u.N * H * W, plane = (long long)H * W;
-  const long long b = P * blockIdx.x / gridDim.x, e = P * (blockIdx.x + 1) / gridDim.x;
-  const float mu = u.mean[c], inv = u.invstd[c], w0 = u.u1_w[c], w1 = u.u1_w[32 + c];
+  long long b, e;
+  int ns = 0;
+  if (u.ln) {
+    ns = blockIdx.x / sb;
+    const int j = blockIdx.x % sb;
+    b = ns * plane + plane * j / sb;
+    e = ns * plane + plane * (j + 1) / sb;
+  } else {
+    b = P * blockIdx.x / gridDim.x;
+    e = P * (blockIdx.x + 1) / gridDim.x;
+  }
+  const float mu = u.ln ? u.mean[ns] : u.mean[c], inv = u.ln ? u.invstd[ns] : u.invstd[c];
+  const float scc = u.ln ? u.scale[ns * 32 + c] : u.scale[c], shc = u.ln ? u.shift[ns * 32 + c] : u.shift[c];
+  const float w0 = u.u1_w[c], w1 = u.u1_w[32 + c];
   float sg = 0.f, sgx = 0.f, sx = 0.f, dw0 = 0.f, dw1 = 0.f, db0s = 0.f, db1s = 0.f;
   for (long long p = b + r; p < e; p += 8) {
     const int X = (int)(p % W);
@@ -620,9 +630,9 @@ __global__ void __launch_bounds__(256) ubf_bwd1_kernel(UbfArgs u, const float* d
     const int q = (Y & 1) * 2 + (X & 1);
     const float* lo = u.low + ((n * u.h + (Y >> 1)) * u.w + (X >> 1)) * 2;
     const float z = ubf_z(u, lo[0], lo[1], c, q);
-    float a = z * u.scale[c] + u.shift[c];
-    a = a > 0.f ? a : 0.f;
-    const float g = a > 0.f ? (w0 * db0 + w1 * db1) : 0.f;
+    const float pre = z * scc + shc;
+    const float a = apply_act(pre, u.act, u.beta);
+    const float g = (w0 * db0 + w1 * db1) * act_grad_pre(pre, u.act, u.beta);
     const float xh = (z - mu) * inv;
     sg += g; sgx += g * xh; sx += xh;
     dw0 += db0 * a; dw1 += db1 * a;
@@ -649,7 +659,7 @@ __global__ void ubf_fin1_kernel(UbfArgs u, const float* partial, int nblk, long 
   S[t] = s;
   __syncthreads();
   if (t < 32) {
-    const double k = (u.gamma ? u.gamma[t] : 1.0) * u.invstd[t];
+    const double k = u.ln ? 0.0 : (u.gamma ? u.gamma[t] : 1.0) * u.invstd[t];   // BN coefficients only
     coef[t] = (float)k;
     coef[32 + t] = (float)(S[t] / P);
     coef[64 + t] = (float)(S[32 + t] / P);
@@ -661,14 +671,37 @@ __global__ void ubf_fin1_kernel(UbfArgs u, const float* partial, int nblk, long 
   if (t >= 160) du1_b[t - 160] += (float)S[t];
 }
 
+// LayerNorm finalize (grid N, 32 lanes): the sample's sb block partials -> G, GX, X per channel,
+// coef_ln[n] = (a_n, b_n), dbias[n][c] = invstd_n (gamma_c G - HWm a_n - X b_n) (the ConvTranspose bias gradient)
+__global__ void ubf_ln_fin_kernel(UbfArgs u, const float* partial, int sb, float* coef_ln, float* dbias) {
+  __shared__ float sa[32], sbb[32];
+  const int n = blockIdx.x, c = threadIdx.x;
+  double G = 0, GX = 0, X = 0;
+  for (int j = 0; j < sb; ++j) {
+    const float* q = partial + ((long long)n * sb + j) * 162;
+    G += q[c]; GX += q[32 + c]; X += q[64 + c];
+  }
+  const float gam = u.gamma ? u.gamma[c] : 1.f;
+  sa[c] = (float)(gam * G); sbb[c] = (float)(gam * GX);
+  __syncthreads();
+  double A = 0, B = 0;
+  for (int i = 0; i < 32; ++i) { A += sa[i]; B += sbb[i]; }
+  const double HWm = 4.0 * u.h * u.w, M = 32.0 * HWm;
+  const double an = A / M, bn = B / M;
+  if (c == 0) { coef_ln[n * 2] = (float)an; coef_ln[n * 2 + 1] = (float)bn; }
+  dbias[n * 32 + c] = (float)(u.invstd[n] * (gam * G - HWm * an - X * bn));
+}
+
 // pass 2 (per low pixel, 8 rows x 32 channels): dz of the 4 children, dlow, dWt partial [ci][c][q] (256)
-__global__ void __launch_bounds__(256) ubf_bwd2_kernel(UbfArgs u, const float* db_in, const float* coef, float* dlow,
-                                                       float* partial) {
+// LayerNorm: coef_ln [N][2] = (a_n, b_n); dz = invstd_n * (gamma_c g - a_n - xhat b_n)
+__global__ void __launch_bounds__(256) ubf_bwd2_kernel(UbfArgs u, const float* db_in, const float* coef,
+                                                       const float* coef_ln, float* dlow, float* partial) {
   __shared__ float red[8][256];
   const int t = threadIdx.x, c = t & 31, r = t >> 5;
   const long long PL = (long long)u.N * u.h * u.w;
   const long long b = PL * blockIdx.x / gridDim.x, e = PL * (blockIdx.x + 1) / gridDim.x;
-  const float k = coef[c], m1 = coef[32 + c], m2 = coef[64 + c], mu = u.mean[c], inv = u.invstd[c];
+  const float k = u.ln ? 0.f : coef[c], m1 = u.ln ? 0.f : coef[32 + c], m2 = u.ln ? 0.f : coef[64 + c];
+  const float gam = u.gamma ? u.gamma[c] : 1.f;
   const float w0 = u.u1_w[c], w1 = u.u1_w[32 + c];
   const int W = 2 * u.w;
   float dw[8];
@@ -680,14 +713,17 @@ __global__ void __launch_bounds__(256) ubf_bwd2_kernel(UbfArgs u, const float* d
     const int y = (int)(tt % u.h);
     const long long n = tt / u.h;
     const float l0 = u.low[p * 2], l1 = u.low[p * 2 + 1];
+    const float mu = u.ln ? u.mean[n] : u.mean[c], inv = u.ln ? u.invstd[n] : u.invstd[c];
+    const float scc = u.ln ? u.scale[n * 32 + c] : u.scale[c], shc = u.ln ? u.shift[n * 32 + c] : u.shift[c];
     float dl0 = 0.f, dl1 = 0.f;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const long long P = (n * (2 * u.h) + 2 * y + (q >> 1)) * W + 2 * x + (q & 1);
       const float z = ubf_z(u, l0, l1, c, q);
-      const float a = z * u.scale[c] + u.shift[c];
-      const float g = a > 0.f ? (w0 * db_in[P * 2] + w1 * db_in[P * 2 + 1]) : 0.f;
-      const float dz = k * (g - m1 - (z - mu) * inv * m2);
+      const float pre = z * scc + shc;
+      const float g = (w0 * db_in[P * 2] + w1 * db_in[P * 2 + 1]) * act_grad_pre(pre, u.act, u.beta);
+      const float dz = u.ln ? inv * (gam * g - coef_ln[n * 2] - (z - mu) * inv * coef_ln[n * 2 + 1])
+                            : k * (g - m1 - (z - mu) * inv * m2);
       const float wa = u.ut_w[(c * 2 + (q >> 1)) * 2 + (q & 1)];
       const float wb = u.ut_w[((32 + c) * 2 + (q >> 1)) * 2 + (q & 1)];
       dl0 += wa * dz;
@@ -820,24 +856,24 @@ extern "C" int hiseg_attn_channel_ws(int N, int C, int Cr) {
 }
 
 extern "C" int hiseg_attn_channel_train_fwd(int dtype, const void* x, int N, int HW, int C, const float* w1, int Cr,
-                                            const float* w2, int act, const float* chan_mul, float* ws, float* gap,
-                                            float* hpre, float* gate, void* out, hiseg_stream_t stream) {
+                                            const float* w2, int act, float act_beta, const float* chan_mul, float* ws,
+                                            float* gap, float* hpre, float* gate, void* out, hiseg_stream_t stream) {
   HISEG_REQUIRE(x && w1 && w2 && ws && gap && hpre && gate && out && N > 0 && HW > 0 && Cr > 0, HISEG_ERR_BAD_ARG,
                 "attn_channel_train_fwd: bad args");
   HISEG_REQUIRE(C > 0 && C % chunk_of(dtype) == 0, HISEG_ERR_BAD_SHAPE, "attn_channel_train_fwd: C alignment");
   hipStream_t s = (hipStream_t)stream;
   DISPATCH_T(dtype, ca_gap<T>(x, nullptr, nullptr, N, HW, C, ws, s));
   hipLaunchKernelGGL(ca_mlp_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, ws, HW, C, Cr, w1, w2, act,
-                     gap, hpre, gate);
+                     act_beta, gap, hpre, gate);
   DISPATCH_T(dtype, hipLaunchKernelGGL(ca_apply_kernel<T>, dim3(ca_ranges(N, HW), N),
                                        dim3(256), 0, s, x, N, HW, C, gate, chan_mul, out));
   return hiseg_check_launch("attn_channel_train_fwd");
 }
 
 extern "C" int hiseg_attn_channel_bwd(int dtype, const void* x, int N, int HW, int C, const float* w1, int Cr,
-                                      const float* w2, int act, const float* chan_mul, const float* gap,
-                                      const float* hpre, const float* gate, const void* dout, void* dx, float* ws,
-                                      float* dw1, float* dw2, hiseg_stream_t stream) {
+                                      const float* w2, int act, float act_beta, const float* chan_mul,
+                                      const float* gap, const float* hpre, const float* gate, const void* dout, void* dx,
+                                      float* ws, float* dw1, float* dw2, hiseg_stream_t stream) {
   HISEG_REQUIRE(x && w1 && w2 && gap && hpre && gate && dout && dx && ws && dw1 && dw2, HISEG_ERR_BAD_ARG,
                 "attn_channel_bwd: null");
   HISEG_REQUIRE(C > 0 && C % chunk_of(dtype) == 0, HISEG_ERR_BAD_SHAPE, "attn_channel_bwd: C alignment");
@@ -847,7 +883,7 @@ extern "C" int hiseg_attn_channel_bwd(int dtype, const void* x, int N, int HW, i
   float* wpart = dgap + (long long)N * C;
   DISPATCH_T(dtype, ca_gap<T>(x, dout, chan_mul, N, HW, C, part, s));
   hipLaunchKernelGGL(ca_mlp_bwd_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, part, C, Cr, w1, w2, act,
-                     gap, hpre, gate, dgap, wpart);
+                     act_beta, gap, hpre, gate, dgap, wpart);
   sum_rows(wpart, N, 2 * C * Cr, C * Cr, dw1, 1, s);
   sum_rows(wpart + C * Cr, N, 2 * C * Cr, C * Cr, dw2, 1, s);
   DISPATCH_T(dtype, hipLaunchKernelGGL(ca_dx_kernel<T>, dim3(ca_ranges(N, HW), N),
@@ -871,7 +907,7 @@ extern "C" int hiseg_se_train_fwd(int dtype, const void* x, int N, int HW, int C
   hipStream_t s = (hipStream_t)stream;
   DISPATCH_T(dtype, ca_gap<T>(x, nullptr, nullptr, N, HW, C, ws, s));
   hipLaunchKernelGGL(ca_mlp_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, ws, HW, C, Cr, w1, w2, act,
-                     gap, hpre, gate, b1, b2);
+                     1.f, gap, hpre, gate, b1, b2);
   DISPATCH_T(dtype, hipLaunchKernelGGL(ca_apply_kernel<T>, dim3(ca_ranges(N, HW), N),
                                        dim3(256), 0, s, x, N, HW, C, gate, nullptr, out));
   return hiseg_check_launch("se_train_fwd");
@@ -891,7 +927,7 @@ extern "C" int hiseg_se_train_bwd(int dtype, const void* x, int N, int HW, int C
   float* bpart = wpart + (long long)N * 2 * C * Cr;
   DISPATCH_T(dtype, ca_gap<T>(x, dout, nullptr, N, HW, C, part, s));
   hipLaunchKernelGGL(ca_mlp_bwd_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, part, C, Cr, w1, w2, act,
-                     gap, hpre, gate, dgap, wpart, bpart);
+                     1.f, gap, hpre, gate, dgap, wpart, bpart);
   sum_rows(wpart, N, 2 * C * Cr, C * Cr, dw1, 1, s);
   sum_rows(wpart + C * Cr, N, 2 * C * Cr, C * Cr, dw2, 1, s);
   sum_rows(bpart, N, Cr + C, Cr, db1, 1, s);
@@ -907,12 +943,22 @@ static UbfArgs ubf_args(const hiseg_ubf_desc* d) {
   u.ut_w = d->ut_w; u.ut_b = d->ut_b;
   u.scale = d->scale; u.shift = d->shift; u.mean = d->mean; u.invstd = d->invstd; u.gamma = d->gamma;
   u.u1_w = d->u1_w; u.u1_b = d->u1_b;
+  u.act = d->act; u.beta = d->act_beta; u.ln = d->layernorm;
   return u;
 }
 
+// blocks of the pass-1 reduction: kUbfBlocks pixel ranges (BN), or sb ranges per sample (LN)
+static int ubf_sb(int N) { const int sb = 512 / (N > 0 ? N : 1); return sb < 1 ? 1 : sb; }
+
 static const int kUbfBlocks = 512;
 
-extern "C" int hiseg_ubf_ws(void) { return hiseg_bn_partials() * 96 + kUbfBlocks * 256 + 96; }
+extern "C" int hiseg_ubf_ws(int N) {
+  const long long nb1 = (long long)N * ubf_sb(N);
+  const long long part = nb1 * 162 > (long long)kUbfBlocks * 256 ? nb1 * 162 : (long long)kUbfBlocks * 256;
+  const long long bwd = part + 96 + (long long)N * 34;
+  const long long fwd = (long long)hiseg_bn_partials() * 96;
+  return (int)(bwd > fwd ? bwd : fwd);
+}
 
 extern "C" int hiseg_ubf_train_fwd(const hiseg_ubf_desc* d, float eps, float momentum, float* running_mean,
                                    float* running_var, float* ws, hiseg_stream_t stream) {
@@ -920,15 +966,23 @@ extern "C" int hiseg_ubf_train_fwd(const hiseg_ubf_desc* d, float eps, float mom
                     d->bgfg && d->tn && ws && d->scale && d->shift && d->mean && d->invstd,
                 HISEG_ERR_BAD_ARG, "ubf_train_fwd: null argument");
   HISEG_REQUIRE(d->Ct > 0 && d->Ct <= 512 && d->Ct % chunk_of(d->dtype) == 0, HISEG_ERR_BAD_SHAPE, "ubf: Ct");
+  HISEG_REQUIRE(d->act >= HISEG_ACT_NONE && d->act <= HISEG_ACT_SWISH, HISEG_ERR_BAD_ARG, "ubf: activation");
   hipStream_t s = (hipStream_t)stream;
   const UbfArgs u = ubf_args(d);
-  const int S = hiseg_bn_partials();
-  hipLaunchKernelGGL(ubf_stats_kernel, dim3(S), dim3(256), 0, s, u, ws);
   const long long Pm = (long long)d->N * 4 * d->h * d->w;
-  int r = hiseg_bn_finalize(ws, 32, Pm, d->gamma, d->beta, eps, momentum, running_mean, running_var,
-                            const_cast<float*>(d->mean), const_cast<float*>(d->invstd), const_cast<float*>(d->scale),
-                            const_cast<float*>(d->shift), stream);
-  if (r) return r;
+  if (d->layernorm) {   // per-sample statistics; no running statistics
+    int r = hiseg_ubf_ln_tables(d->low, d->N, d->h, d->w, d->ut_w, d->ut_b, d->gamma, d->beta, eps, 0,
+                                const_cast<float*>(d->mean), const_cast<float*>(d->invstd), const_cast<float*>(d->scale),
+                                const_cast<float*>(d->shift), stream);
+    if (r) return r;
+  } else {
+    const int S = hiseg_bn_partials();
+    hipLaunchKernelGGL(ubf_stats_kernel, dim3(S), dim3(256), 0, s, u, ws);
+    int r = hiseg_bn_finalize(ws, 32, Pm, d->gamma, d->beta, eps, momentum, running_mean, running_var,
+                              const_cast<float*>(d->mean), const_cast<float*>(d->invstd), const_cast<float*>(d->scale),
+                              const_cast<float*>(d->shift), stream);
+    if (r) return r;
+  }
   DISPATCH_T(d->dtype, hipLaunchKernelGGL(ubf_fwd_kernel<T>, dim3(nb(Pm, 256)), dim3(256), 0, s, u, d->tfeat, d->Ct,
                                           d->t_w, d->t_b, d->logits, d->bgfg, d->tn));
   return hiseg_check_launch("ubf_train_fwd");
@@ -943,13 +997,22 @@ extern "C" int hiseg_ubf_train_bwd(const hiseg_ubf_desc* d, const float* dlogits
   hipStream_t s = (hipStream_t)stream;
   const UbfArgs u = ubf_args(d);
   const long long Pm = (long long)d->N * 4 * d->h * d->w, PL = (long long)d->N * d->h * d->w;
-  float* part = ws;                          // [kUbfBlocks][256]
-  float* coef = ws + (long long)kUbfBlocks * 256;
-  hipLaunchKernelGGL(ubf_bwd1_kernel, dim3(kUbfBlocks), dim3(256), 0, s, u, dlogits, dbgfg_ext, dtn_ext, d->bgfg, d->tn,
-                     db_buf, dtn_out, part);
-  hipLaunchKernelGGL(ubf_fin1_kernel, dim3(1), dim3(192), 0, s, u, part, kUbfBlocks, Pm, coef, g->dgamma, g->dbeta,
-                     g->du1_w, g->du1_b, g->dut_b);
-  hipLaunchKernelGGL(ubf_bwd2_kernel, dim3(kUbfBlocks), dim3(256), 0, s, u, db_buf, coef, dlow, part);
+  const int sb = ubf_sb(d->N);
+  const int nb1 = d->layernorm ? d->N * sb : kUbfBlocks;
+  const long long part_len = (long long)nb1 * 162 > (long long)kUbfBlocks * 256 ? (long long)nb1 * 162
+                                                                                  : (long long)kUbfBlocks * 256;
+  float* part = ws;                          // [nb1][162] (pass 1), then [kUbfBlocks][256] (pass 2)
+  float* coef = ws + part_len;               // [96] (BN)
+  float* coef_ln = coef + 96;                // [N][2] (LN)
+  float* dbias = coef_ln + 2LL * d->N;       // [N][32] (LN)
+  hipLaunchKernelGGL(ubf_bwd1_kernel, dim3(nb1), dim3(256), 0, s, u, dlogits, dbgfg_ext, dtn_ext, d->bgfg, d->tn,
+                     db_buf, dtn_out, part, sb);
+  if (d->layernorm)
+    hipLaunchKernelGGL(ubf_ln_fin_kernel, dim3(d->N), dim3(32), 0, s, u, part, sb, coef_ln, dbias);
+  hipLaunchKernelGGL(ubf_fin1_kernel, dim3(1), dim3(192), 0, s, u, part, nb1, Pm, coef, g->dgamma, g->dbeta,
+                     g->du1_w, g->du1_b, d->layernorm ? nullptr : g->dut_b);
+  if (d->layernorm) sum_rows(dbias, d->N, 32, 32, g->dut_b, 1, s);
+  hipLaunchKernelGGL(ubf_bwd2_kernel, dim3(kUbfBlocks), dim3(256), 0, s, u, db_buf, coef, coef_ln, dlow, part);
   // dWt [ci][c][q] in the ConvTranspose2d layout [2][32][2][2] == (ci*32 + c)*4 + q
   sum_rows(part, kUbfBlocks, 256, 256, g->dut_w, 1, s);
   (void)PL;

@@ -76,9 +76,10 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(hiseg_bn_apply_desc d) {
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
     const long long p = i / d.C;
     const int c = (int)(i - p * d.C);
-    float v = ld<T>(d.z, p * d.z_cstride + d.z_coff + c) * d.scale[c] + d.shift[c];
+    const long long tc = d.per_sample ? (p / d.HW) * d.C + c : c;
+    float v = ld<T>(d.z, p * d.z_cstride + d.z_coff + c) * d.scale[tc] + d.shift[tc];
     if (d.residual) v += ld<T>(d.residual, p * d.r_cstride + d.r_coff + c);
-    v = apply_act(v, d.act);
+    v = apply_act(v, d.act, d.act_beta);
     if (d.chan_mul) v *= d.chan_mul[(p / d.HW) * d.C + c];
     st<T>(d.y, p * d.y_cstride + d.y_coff + c, v);
   }
@@ -91,11 +92,21 @@ __device__ __forceinline__ float silu_grad_pre(const hiseg_bn_bwd_desc& d, float
   return s * (1.f + v * (1.f - s));
 }
 
+// The derivative is taken at the forward's own pre-activation z*fwd_scale + fwd_shift (+ residual) when the
+// folded affine is given and the activation needs it (smooth ones; ReLU after a residual add with the residual).
+__device__ __forceinline__ bool bn_pre_path(const hiseg_bn_bwd_desc& d) {
+  return d.fwd_scale && (act_smooth(d.act) || (d.act == HISEG_ACT_RELU && (!d.dres || d.residual)));
+}
+
 template <typename T>
 __device__ __forceinline__ float bn_g(const hiseg_bn_bwd_desc& d, long long p, int c) {
   float g = ld<T>(d.dy, p * d.dy_cstride + d.dy_coff + c);
   if (d.chan_mul) g *= d.chan_mul[(p / d.HW) * d.C + c];
-  if (d.act == HISEG_ACT_SILU) g *= silu_grad_pre(d, ld<T>(d.z, p * d.z_cstride + d.z_coff + c), c);
+  if (bn_pre_path(d)) {
+    float v = ld<T>(d.z, p * d.z_cstride + d.z_coff + c) * d.fwd_scale[c] + d.fwd_shift[c];
+    if (d.residual) v += ld<T>(d.residual, p * d.r_cstride + d.r_coff + c);
+    g *= act_grad_pre(v, d.act, d.act_beta);
+  } else if (d.act == HISEG_ACT_SILU) g *= silu_grad_pre(d, ld<T>(d.z, p * d.z_cstride + d.z_coff + c), c);
   else if (d.act != HISEG_ACT_NONE) g *= act_grad(ld<T>(d.y, p * d.y_cstride + d.y_coff + c), d.act);
   return g;
 }
@@ -280,17 +291,22 @@ __global__ void __launch_bounds__(256) bn_apply_vec_kernel(hiseg_bn_apply_desc d
   const int P = (int)d.P;
   float sc[V], sf[V];
 #pragma unroll
-  for (int k = 0; k < V; ++k) { sc[k] = d.scale[c + k]; sf[k] = d.shift[c + k]; }
+  for (int k = 0; k < V; ++k) { sc[k] = d.per_sample ? 0.f : d.scale[c + k]; sf[k] = d.per_sample ? 0.f : d.shift[c + k]; }
   for (int p = blockIdx.x * R + r; p < P; p += gridDim.x * R) {
     float v[V], rr[V];
     ldv<T>(d.z, (long long)p * d.z_cstride + d.z_coff + c, v);
     if (d.residual) ldv<T>(d.residual, (long long)p * d.r_cstride + d.r_coff + c, rr);
     const float* cm = d.chan_mul ? d.chan_mul + (long long)(p / d.HW) * d.C + c : nullptr;
+    if (d.per_sample) {   // LayerNorm2d: the sample's folded tables
+      const long long tb = (long long)(p / d.HW) * d.C + c;
+#pragma unroll
+      for (int k = 0; k < V; ++k) { sc[k] = d.scale[tb + k]; sf[k] = d.shift[tb + k]; }
+    }
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       float x = v[k] * sc[k] + sf[k];
       if (d.residual) x += rr[k];
-      x = apply_act(x, d.act);
+      x = apply_act(x, d.act, d.act_beta);
       if (cm) x *= cm[k];
       v[k] = x;
     }
@@ -308,7 +324,16 @@ __device__ __forceinline__ void bn_gv(const hiseg_bn_bwd_desc& d, long long p, i
 #pragma unroll
     for (int k = 0; k < V; ++k) g[k] *= cm[k];
   }
-  if (d.act == HISEG_ACT_SILU) {   // SiLU'(v) needs the pre-activation: v = xhat * gamma + beta from z
+  if (bn_pre_path(d)) {   // at the forward's pre-activation (+ residual)
+    float rr[V];
+    if (d.residual) ldv<T>(d.residual, p * d.r_cstride + d.r_coff + c, rr);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      float v = z[k] * d.fwd_scale[c + k] + d.fwd_shift[c + k];
+      if (d.residual) v += rr[k];
+      g[k] *= act_grad_pre(v, d.act, d.act_beta);
+    }
+  } else if (d.act == HISEG_ACT_SILU) {   // SiLU'(v) needs the pre-activation: v = xhat * gamma + beta from z
 #pragma unroll
     for (int k = 0; k < V; ++k) g[k] *= silu_grad_pre(d, z[k], c + k);
   } else if (d.act == HISEG_ACT_RELU && d.fwd_scale && !d.dres) {   // the forward's mask, from z
@@ -675,6 +700,253 @@ inline unsigned ew_blocks(long long n) {
   return (unsigned)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
 }
 
+
+// ---------------------------------------------------------------------------------------- LayerNorm2d
+// model.py:18-38: per sample n, mean / biased variance over (C, H, W), eps; y = (z - mean) * invstd * w + b.
+// Statistics in double (per-thread sums of the sample's values), sample n's HW pixels split into Sp
+// contiguous slices, one block per (slice, sample): CT channel-chunk lanes x R pixel rows, V channels per
+// chunk (a 16-B chunk, or 1 on the scalar path).  The forward apply is hiseg_bn_apply with per-sample tables.
+template <typename T, int V>
+__device__ __forceinline__ void ldn(const void* p, long long i, float* v) {
+  if constexpr (V == 1) v[0] = ld<T>(p, i);
+  else ldv<T>(p, i, v);
+}
+template <typename T, int V>
+__device__ __forceinline__ void stn(void* p, long long i, const float* v) {
+  if constexpr (V == 1) st<T>(p, i, v[0]);
+  else stv<T>(p, i, v);
+}
+
+__device__ __forceinline__ void ln_layout(int C, int V, int& NCH, int& CT, int& R) {
+  NCH = C / V;
+  CT = NCH < 256 ? NCH : 256;
+  R = 256 / CT;
+}
+
+template <typename T, int V>
+__global__ void __launch_bounds__(256) ln_stats_kernel(const void* z, int HW, int C, int cs, int coff, double* part) {
+  __shared__ double s1[256], s2[256];
+  int NCH, CT, R;
+  ln_layout(C, V, NCH, CT, R);
+  const int t = threadIdx.x, cl = t % CT, r = t / CT;
+  const int n = blockIdx.y, Sp = gridDim.x;
+  const long long b = (long long)HW * blockIdx.x / Sp, e = (long long)HW * (blockIdx.x + 1) / Sp;
+  const long long p0 = (long long)n * HW;
+  double a1 = 0.0, a2 = 0.0;
+  if (r < R) {
+    for (long long p = b + r; p < e; p += R)
+      for (int ch = cl; ch < NCH; ch += CT) {
+        float v[V];
+        ldn<T, V>(z, (p0 + p) * cs + coff + ch * V, v);
+#pragma unroll
+        for (int k = 0; k < V; ++k) { a1 += v[k]; a2 += (double)v[k] * v[k]; }
+      }
+  }
+  s1[t] = a1; s2[t] = a2;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) { s1[t] += s1[t + w]; s2[t] += s2[t + w]; }
+    __syncthreads();
+  }
+  if (t == 0) {
+    double* o = part + ((long long)n * Sp + blockIdx.x) * 2;
+    o[0] = s1[0]; o[1] = s2[0];
+  }
+}
+
+__global__ void __launch_bounds__(256) ln_finalize_kernel(const double* part, int Sp, int C, int HW, const float* gamma,
+                                                          const float* beta, float eps, float* mean, float* invstd,
+                                                          float* scale, float* shift) {
+  __shared__ double s1[256], s2[256];
+  __shared__ float s_m, s_i;
+  const int n = blockIdx.x, t = threadIdx.x;
+  double a1 = 0.0, a2 = 0.0;
+  for (int s = t; s < Sp; s += 256) { a1 += part[((long long)n * Sp + s) * 2]; a2 += part[((long long)n * Sp + s) * 2 + 1]; }
+  s1[t] = a1; s2[t] = a2;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) { s1[t] += s1[t + w]; s2[t] += s2[t + w]; }
+    __syncthreads();
+  }
+  if (t == 0) {
+    const double M = (double)C * HW;
+    const double m = s1[0] / M;
+    double var = s2[0] / M - m * m;
+    if (var < 0.0) var = 0.0;
+    s_m = (float)m;
+    s_i = (float)(1.0 / sqrt(var + (double)eps));
+    mean[n] = s_m;
+    invstd[n] = s_i;
+  }
+  __syncthreads();
+  for (int c = t; c < C; c += 256) {
+    const float k = (gamma ? gamma[c] : 1.f) * s_i;
+    scale[(long long)n * C + c] = k;
+    shift[(long long)n * C + c] = (beta ? beta[c] : 0.f) - s_m * k;
+  }
+}
+
+// Backward.  g = dy * chan_mul * act'(pre), pre = z*scale[n][c] + shift[n][c] (+ residual), xhat = (z - mean_n)
+// * invstd_n; per block and channel: G = sum g, GX = sum g*xhat, X = sum xhat (blocks never straddle samples)
+//   per sample:  a_n = sum_c w_c G_nc / M,  b_n = sum_c w_c GX_nc / M   (M = C*HW)
+//   dz = invstd_n * (g*w_c - a_n - xhat*b_n),  dw_c = sum GX, db_c = sum G,
+//   dconv_bias_c = sum_n invstd_n * (w_c G_nc - HW a_n - X_nc b_n)
+template <typename T, int V>
+__device__ __forceinline__ void ln_g(const hiseg_ln_bwd_desc& d, long long p, int n, int c, const float* z, float* g) {
+  ldn<T, V>(d.dy, p * d.dy_cstride + d.dy_coff + c, g);
+  float rr[V];
+  if (d.residual) ldn<T, V>(d.residual, p * d.r_cstride + d.r_coff + c, rr);
+  const long long tb = (long long)n * d.C + c;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    if (d.chan_mul) g[k] *= d.chan_mul[tb + k];
+    if (d.act != HISEG_ACT_NONE) {
+      float v = z[k] * d.scale[tb + k] + d.shift[tb + k];
+      if (d.residual) v += rr[k];
+      g[k] *= act_grad_pre(v, d.act, d.act_beta);
+    }
+  }
+}
+
+template <typename T, int V>
+__global__ void __launch_bounds__(256) ln_bwd_reduce_kernel(hiseg_ln_bwd_desc d, float* part) {
+  int NCH, CT, R;
+  ln_layout(d.C, V, NCH, CT, R);
+  const int t = threadIdx.x, cl = t % CT, r = t / CT;
+  const int n = blockIdx.y, Sp = gridDim.x, C = d.C;
+  const long long b = (long long)d.HW * blockIdx.x / Sp, e = (long long)d.HW * (blockIdx.x + 1) / Sp;
+  const long long p0 = (long long)n * d.HW;
+  const float mu = d.mean[n], inv = d.invstd[n];
+  float* out = part + ((long long)n * Sp + blockIdx.x) * 3 * C;
+  __shared__ float sh[3][256][V];
+  for (int cg = 0; cg < NCH; cg += CT) {   // channel groups of CT chunks
+    const int ch = cg + cl;
+    float s1[V], s2[V], s3[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) s1[k] = s2[k] = s3[k] = 0.f;
+    if (r < R && ch < NCH) {
+      for (long long p = b + r; p < e; p += R) {
+        float z[V], g[V];
+        ldn<T, V>(d.z, (p0 + p) * d.z_cstride + d.z_coff + ch * V, z);
+        ln_g<T, V>(d, p0 + p, n, ch * V, z, g);
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+          const float xh = (z[k] - mu) * inv;
+          s1[k] += g[k]; s2[k] += g[k] * xh; s3[k] += xh;
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < V; ++k) { sh[0][t][k] = s1[k]; sh[1][t][k] = s2[k]; sh[2][t][k] = s3[k]; }
+    __syncthreads();
+    if (r == 0 && ch < NCH) {
+      for (int rr = 1; rr < R; ++rr) {
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+          s1[k] += sh[0][rr * CT + cl][k]; s2[k] += sh[1][rr * CT + cl][k]; s3[k] += sh[2][rr * CT + cl][k];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < V; ++k) { out[ch * V + k] = s1[k]; out[C + ch * V + k] = s2[k]; out[2 * C + ch * V + k] = s3[k]; }
+    }
+    __syncthreads();
+  }
+}
+
+// per sample: the Sp slices' sums -> nc [N][3][C] and coef [N][2] = (a_n, b_n)
+__global__ void __launch_bounds__(256) ln_bwd_sample_kernel(hiseg_ln_bwd_desc d, const float* part, int Sp, float* nc,
+                                                            float* coef) {
+  __shared__ double sa[256], sb[256];
+  const int n = blockIdx.x, t = threadIdx.x, C = d.C;
+  double a = 0.0, bb = 0.0;
+  for (int c = t; c < C; c += 256) {
+    double G = 0.0, GX = 0.0, X = 0.0;
+    for (int s = 0; s < Sp; ++s) {
+      const float* q = part + ((long long)n * Sp + s) * 3 * C;
+      G += q[c]; GX += q[C + c]; X += q[2 * C + c];
+    }
+    float* o = nc + (long long)n * 3 * C;
+    o[c] = (float)G; o[C + c] = (float)GX; o[2 * C + c] = (float)X;
+    const double w = d.gamma ? d.gamma[c] : 1.0;
+    a += w * G; bb += w * GX;
+  }
+  sa[t] = a; sb[t] = bb;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) { sa[t] += sa[t + w]; sb[t] += sb[t + w]; }
+    __syncthreads();
+  }
+  if (t == 0) {
+    const double M = (double)C * d.HW;
+    coef[n * 2] = (float)(sa[0] / M);
+    coef[n * 2 + 1] = (float)(sb[0] / M);
+  }
+}
+
+// per channel: dw, db, dconv_bias over the samples
+__global__ void __launch_bounds__(256) ln_bwd_channel_kernel(hiseg_ln_bwd_desc d, const float* nc, const float* coef) {
+  const int c = blockIdx.x * 256 + threadIdx.x, C = d.C;
+  if (c >= C) return;
+  const double w = d.gamma ? d.gamma[c] : 1.0;
+  double G = 0.0, GX = 0.0, DB = 0.0;
+  for (int n = 0; n < d.N; ++n) {
+    const float* o = nc + (long long)n * 3 * C;
+    G += o[c]; GX += o[C + c];
+    DB += (double)d.invstd[n] * (w * o[c] - (double)d.HW * coef[n * 2] - (double)o[2 * C + c] * coef[n * 2 + 1]);
+  }
+  if (d.dgamma) d.dgamma[c] = (float)(d.accumulate_params ? d.dgamma[c] + GX : GX);
+  if (d.dbeta) d.dbeta[c] = (float)(d.accumulate_params ? d.dbeta[c] + G : G);
+  if (d.dconv_bias) d.dconv_bias[c] = (float)(d.accumulate_params ? d.dconv_bias[c] + DB : DB);
+}
+
+template <typename T, int V>
+__global__ void __launch_bounds__(256) ln_bwd_apply_kernel(hiseg_ln_bwd_desc d, const float* coef) {
+  int NCH, CT, R;
+  ln_layout(d.C, V, NCH, CT, R);
+  const int t = threadIdx.x, cl = t % CT, r = t / CT;
+  if (r >= R) return;
+  const long long P = (long long)d.N * d.HW;
+  for (long long p = (long long)blockIdx.x * R + r; p < P; p += (long long)gridDim.x * R) {
+    const int n = (int)(p / d.HW);
+    const float mu = d.mean[n], inv = d.invstd[n], an = coef[n * 2], bn = coef[n * 2 + 1];
+    for (int ch = cl; ch < NCH; ch += CT) {
+      const int c = ch * V;
+      float z[V], g[V], o[V];
+      ldn<T, V>(d.z, p * d.z_cstride + d.z_coff + c, z);
+      ln_g<T, V>(d, p, n, c, z, g);
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        const float w = d.gamma ? d.gamma[c + k] : 1.f;
+        o[k] = inv * (g[k] * w - an - (z[k] - mu) * inv * bn);
+      }
+      stn<T, V>(d.dz, p * d.dz_cstride + d.dz_coff + c, o);
+      if (d.dres) {
+        const long long off = p * d.dres_cstride + d.dres_coff + c;
+        if (d.dres_accumulate) {
+          float q[V];
+          ldn<T, V>(d.dres, off, q);
+#pragma unroll
+          for (int k = 0; k < V; ++k) g[k] += q[k];
+        }
+        stn<T, V>(d.dres, off, g);
+      }
+    }
+  }
+}
+
+// dz (+)= dy * act'(z) for an activation applied without normalisation (the fg_gate convs with GELU / Swish /
+// SiLU: the conv writes the pre-activation, hiseg_bn_apply with unit tables the activation).
+template <typename T>
+__global__ void __launch_bounds__(256) act_bwd_pre_kernel(long long P, int C, hiseg_ew_view dy, hiseg_ew_view z, int act,
+                                                          float beta, hiseg_ew_view dz, int accumulate) {
+  EW_LOOP(P, C) {
+    const long long p = i / C;
+    const int c = (int)(i - p * C);
+    float g = ld<T>(dy.p, vi(dy, p, c)) * act_grad_pre(ld<T>(z.p, vi(z, p, c)), act, beta);
+    if (accumulate) g += ld<T>(dz.p, vi(dz, p, c));
+    st<T>(dz.p, vi(dz, p, c), g);
+  }
+}
 }  // namespace hiseg
 
 using namespace hiseg;
@@ -754,17 +1026,21 @@ extern "C" int hiseg_bn_apply(const hiseg_bn_apply_desc* d, hiseg_stream_t strea
 extern "C" int hiseg_bn_bwd(const hiseg_bn_bwd_desc* d, hiseg_stream_t stream) {
   HISEG_REQUIRE(d && d->dy && d->z && d->dz && d->mean && d->invstd && d->partial && d->P > 0 && d->C > 0 && d->HW > 0,
                 HISEG_ERR_BAD_ARG, "bn_bwd: bad arguments");
-  HISEG_REQUIRE(d->act == HISEG_ACT_NONE || d->act == HISEG_ACT_SILU || d->y, HISEG_ERR_BAD_ARG,
+  const bool pre = d->fwd_scale && d->fwd_shift &&
+                   (act_smooth(d->act) || (d->act == HISEG_ACT_RELU && (!d->dres || d->residual)));
+  HISEG_REQUIRE(pre || d->act == HISEG_ACT_NONE || d->act == HISEG_ACT_SILU || d->y, HISEG_ERR_BAD_ARG,
                 "bn_bwd: activation needs y");
-  HISEG_REQUIRE(d->act != HISEG_ACT_SILU || !d->dres, HISEG_ERR_BAD_ARG,
-                "bn_bwd: SiLU after a residual add is not supported (no pre-activation)");
+  HISEG_REQUIRE(pre || (d->act != HISEG_ACT_GELU && d->act != HISEG_ACT_SWISH), HISEG_ERR_BAD_ARG,
+                "bn_bwd: GELU / Swish need the forward's fwd_scale / fwd_shift");
+  HISEG_REQUIRE(!d->dres || !act_smooth(d->act) || (pre && d->residual), HISEG_ERR_BAD_ARG,
+                "bn_bwd: a smooth activation after a residual add needs the residual (pre-activation)");
   HISEG_REQUIRE(d->P < (1ll << 31), HISEG_ERR_BAD_SHAPE, "bn_bwd: too many pixels");
   hipStream_t s = (hipStream_t)stream;
   const int S = kBnSplits;
   const int dt = d->dtype, C = d->C;
   if (vec_ok(dt, C, d->dy, d->dy_cstride, d->dy_coff) && vec_ok(dt, C, d->y, d->y_cstride, d->y_coff) &&
       vec_ok(dt, C, d->z, d->z_cstride, d->z_coff) && vec_ok(dt, C, d->dz, d->dz_cstride, d->dz_coff) &&
-      vec_ok(dt, C, d->dres, d->dres_cstride, d->dres_coff)) {
+      vec_ok(dt, C, d->dres, d->dres_cstride, d->dres_coff) && vec_ok(dt, C, d->residual, d->r_cstride, d->r_coff)) {
     const int V = dt == HISEG_BF16 ? 8 : 4;
     DISPATCH_T(dt, hipLaunchKernelGGL(bn_bwd_reduce_vec_kernel<T>, dim3(S, (C / V + 255) / 256), dim3(256), 0, s, *d));
     hipLaunchKernelGGL(bn_bwd_finalize_par_kernel, dim3(C), dim3(256), 0, s, *d, S);
@@ -866,4 +1142,82 @@ extern "C" int hiseg_resize_bilinear_bwd(const float* dy, int NC, int h, int w, 
   hipLaunchKernelGGL(resize_bwd_kernel, dim3(ew_blocks((long long)NC * h * w)), dim3(256), 0, (hipStream_t)stream, dy,
                      NC, h, w, H, W, dx);
   return hiseg_check_launch("resize_bilinear_bwd");
+}
+
+// ---------------------------------------------------------------------------------------- LayerNorm2d host side
+static int ln_splits(int N, int HW) {
+  int sp = (2048 + N - 1) / N;
+  const int cap = HW / 16 > 0 ? HW / 16 : 1;
+  if (sp > cap) sp = cap;
+  if (sp > 256) sp = 256;
+  return sp < 1 ? 1 : sp;
+}
+
+extern "C" long long hiseg_ln_ws(int N, int HW, int C) {
+  const long long sp = ln_splits(N, HW);
+  const long long stats = (long long)N * sp * 4;                                  // doubles as float pairs
+  const long long bwd = (long long)N * sp * 3 * C + (long long)N * 3 * C + 2LL * N;
+  return stats > bwd ? stats : bwd;
+}
+
+extern "C" int hiseg_ln_fwd_stats(int dtype, const void* z, int N, int HW, int C, int cstride, int coff,
+                                  const float* gamma, const float* beta, float eps, float* ws, float* mean,
+                                  float* invstd, float* scale, float* shift, hiseg_stream_t stream) {
+  HISEG_REQUIRE(z && ws && mean && invstd && scale && shift && N > 0 && HW > 0 && C > 0 && cstride >= coff + C,
+                HISEG_ERR_BAD_ARG, "ln_fwd_stats: bad arguments");
+  HISEG_REQUIRE(dtype == HISEG_F32 || dtype == HISEG_BF16, HISEG_ERR_BAD_DTYPE, "ln_fwd_stats: dtype");
+  HISEG_REQUIRE(al16(ws), HISEG_ERR_BAD_ARG, "ln_fwd_stats: workspace must be 16-B aligned");
+  hipStream_t s = (hipStream_t)stream;
+  const int sp = ln_splits(N, HW);
+  double* part = reinterpret_cast<double*>(ws);
+  if (vec_ok(dtype, C, z, cstride, coff)) {
+    DISPATCH_T(dtype, hipLaunchKernelGGL((ln_stats_kernel<T, Chunk<T>::N>), dim3(sp, N), dim3(256), 0, s, z, HW, C,
+                                         cstride, coff, part));
+  } else {
+    DISPATCH_T(dtype, hipLaunchKernelGGL((ln_stats_kernel<T, 1>), dim3(sp, N), dim3(256), 0, s, z, HW, C, cstride, coff,
+                                         part));
+  }
+  hipLaunchKernelGGL(ln_finalize_kernel, dim3(N), dim3(256), 0, s, part, sp, C, HW, gamma, beta, eps, mean, invstd,
+                     scale, shift);
+  return hiseg_check_launch("ln_fwd_stats");
+}
+
+extern "C" int hiseg_ln_bwd(const hiseg_ln_bwd_desc* d, hiseg_stream_t stream) {
+  HISEG_REQUIRE(d && d->dy && d->z && d->dz && d->mean && d->invstd && d->scale && d->shift && d->ws && d->N > 0 &&
+                    d->HW > 0 && d->C > 0,
+                HISEG_ERR_BAD_ARG, "ln_bwd: bad arguments");
+  HISEG_REQUIRE(d->dtype == HISEG_F32 || d->dtype == HISEG_BF16, HISEG_ERR_BAD_DTYPE, "ln_bwd: dtype");
+  hipStream_t s = (hipStream_t)stream;
+  const int sp = ln_splits(d->N, d->HW), dt = d->dtype, C = d->C;
+  float* part = d->ws;
+  float* nc = part + (long long)d->N * sp * 3 * C;
+  float* coef = nc + (long long)d->N * 3 * C;
+  const bool vec = vec_ok(dt, C, d->dy, d->dy_cstride, d->dy_coff) && vec_ok(dt, C, d->z, d->z_cstride, d->z_coff) &&
+                   vec_ok(dt, C, d->dz, d->dz_cstride, d->dz_coff) &&
+                   vec_ok(dt, C, d->dres, d->dres_cstride, d->dres_coff) &&
+                   vec_ok(dt, C, d->residual, d->r_cstride, d->r_coff);
+  long long bx = ((long long)d->N * d->HW + 7) / 8;
+  if (bx > 4096) bx = 4096;
+  if (vec) {
+    DISPATCH_T(dt, hipLaunchKernelGGL((ln_bwd_reduce_kernel<T, Chunk<T>::N>), dim3(sp, d->N), dim3(256), 0, s, *d, part));
+  } else {
+    DISPATCH_T(dt, hipLaunchKernelGGL((ln_bwd_reduce_kernel<T, 1>), dim3(sp, d->N), dim3(256), 0, s, *d, part));
+  }
+  hipLaunchKernelGGL(ln_bwd_sample_kernel, dim3(d->N), dim3(256), 0, s, *d, part, sp, nc, coef);
+  hipLaunchKernelGGL(ln_bwd_channel_kernel, dim3((C + 255) / 256), dim3(256), 0, s, *d, nc, coef);
+  if (vec) {
+    DISPATCH_T(dt, hipLaunchKernelGGL((ln_bwd_apply_kernel<T, Chunk<T>::N>), dim3((unsigned)bx), dim3(256), 0, s, *d,
+                                      coef));
+  } else {
+    DISPATCH_T(dt, hipLaunchKernelGGL((ln_bwd_apply_kernel<T, 1>), dim3((unsigned)bx), dim3(256), 0, s, *d, coef));
+  }
+  return hiseg_check_launch("ln_bwd");
+}
+
+extern "C" int hiseg_act_bwd_pre(int dtype, long long P, int C, hiseg_ew_view dy, hiseg_ew_view z, int act,
+                                 float act_beta, hiseg_ew_view dz, int accumulate, hiseg_stream_t stream) {
+  HISEG_REQUIRE(dy.p && z.p && dz.p && P > 0 && C > 0, HISEG_ERR_BAD_ARG, "act_bwd_pre: bad arguments");
+  DISPATCH_T(dtype, hipLaunchKernelGGL(act_bwd_pre_kernel<T>, dim3(ew_blocks(P * C)), dim3(256), 0, (hipStream_t)stream,
+                                       P, C, dy, z, act, act_beta, dz, accumulate));
+  return hiseg_check_launch("act_bwd_pre");
 }

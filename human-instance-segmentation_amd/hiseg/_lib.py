@@ -17,7 +17,24 @@ LIB_PATH = os.environ.get("HISEG_LIB", os.path.join(_HERE, "libhiseg.so"))
 
 HISEG_F32 = 0
 HISEG_BF16 = 1
-ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_SILU = 0, 1, 2, 3
+ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_SILU, ACT_GELU, ACT_SWISH = 0, 1, 2, 3, 4, 5
+
+
+class ActCode(int):
+    """An activation code (include/hiseg.h hiseg_act) that carries Swish's beta (act_beta fields)."""
+
+    def __new__(cls, code: int, beta: float = 1.0):
+        o = int.__new__(cls, code)
+        o.beta = float(beta)
+        return o
+
+    def __repr__(self):
+        return f"ActCode({int(self)}, beta={self.beta})"
+
+
+def act_beta(act) -> float:
+    """Swish beta of an activation code (1.0 for plain int codes)."""
+    return float(getattr(act, "beta", 1.0))
 LOSS_NOUT = 15  # include/hiseg_loss.h HISEG_LOSS_NOUT
 
 c_int = ctypes.c_int
@@ -57,6 +74,7 @@ class Conv2dDesc(ctypes.Structure):
         ("out2", c_void_p), ("o2_cstride", c_int), ("o2_coff", c_int),
         ("convT", c_int),
         ("weight_frag", c_void_p),
+        ("act_beta", c_float),
     ]
 
 
@@ -78,7 +96,8 @@ class BnApplyDesc(ctypes.Structure):
                 ("scale", c_void_p), ("shift", c_void_p),
                 ("residual", c_void_p), ("r_cstride", c_int), ("r_coff", c_int),
                 ("act", c_int), ("chan_mul", c_void_p),
-                ("y", c_void_p), ("y_cstride", c_int), ("y_coff", c_int)]
+                ("y", c_void_p), ("y_cstride", c_int), ("y_coff", c_int),
+                ("act_beta", c_float), ("per_sample", c_int)]
 
 
 class BnBwdDesc(ctypes.Structure):
@@ -92,7 +111,22 @@ class BnBwdDesc(ctypes.Structure):
                 ("dgamma", c_void_p), ("dbeta", c_void_p), ("dconv_bias", c_void_p), ("accumulate_params", c_int),
                 ("dz", c_void_p), ("dz_cstride", c_int), ("dz_coff", c_int),
                 ("dres", c_void_p), ("dres_cstride", c_int), ("dres_coff", c_int), ("dres_accumulate", c_int),
-                ("beta", c_void_p), ("fwd_scale", c_void_p), ("fwd_shift", c_void_p)]
+                ("beta", c_void_p), ("fwd_scale", c_void_p), ("fwd_shift", c_void_p),
+                ("act_beta", c_float), ("residual", c_void_p), ("r_cstride", c_int), ("r_coff", c_int)]
+
+
+class LnBwdDesc(ctypes.Structure):
+    _fields_ = [("dtype", c_int), ("N", c_int), ("HW", c_int), ("C", c_int),
+                ("dy", c_void_p), ("dy_cstride", c_int), ("dy_coff", c_int),
+                ("z", c_void_p), ("z_cstride", c_int), ("z_coff", c_int),
+                ("residual", c_void_p), ("r_cstride", c_int), ("r_coff", c_int),
+                ("chan_mul", c_void_p), ("act", c_int), ("act_beta", c_float),
+                ("mean", c_void_p), ("invstd", c_void_p), ("scale", c_void_p), ("shift", c_void_p),
+                ("gamma", c_void_p),
+                ("dgamma", c_void_p), ("dbeta", c_void_p), ("dconv_bias", c_void_p), ("accumulate_params", c_int),
+                ("dz", c_void_p), ("dz_cstride", c_int), ("dz_coff", c_int),
+                ("dres", c_void_p), ("dres_cstride", c_int), ("dres_coff", c_int), ("dres_accumulate", c_int),
+                ("ws", c_void_p)]
 
 
 class EwView(ctypes.Structure):
@@ -105,7 +139,8 @@ class UbfDesc(ctypes.Structure):
                 ("mean", c_void_p), ("invstd", c_void_p), ("scale", c_void_p), ("shift", c_void_p),
                 ("u1_w", c_void_p), ("u1_b", c_void_p),
                 ("tfeat", c_void_p), ("Ct", c_int), ("t_w", c_void_p), ("t_b", c_void_p),
-                ("logits", c_void_p), ("bgfg", c_void_p), ("tn", c_void_p)]
+                ("logits", c_void_p), ("bgfg", c_void_p), ("tn", c_void_p),
+                ("act", c_int), ("act_beta", c_float), ("layernorm", c_int)]
 
 
 class UbfGrads(ctypes.Structure):
@@ -154,7 +189,7 @@ def _declare(lib):
         "hiseg_maxpool2x2_fwd": ([c_int, P, c_int, c_int, c_int, c_int, P, P], c_int),
         "hiseg_attn_spatial_fwd": ([c_int, P, c_int, c_int, c_int, c_int, P, c_int, P, P, P, P], c_int),
         "hiseg_gap_splits": ([c_int], c_int),
-        "hiseg_se_gate_fwd": ([c_int, P, c_int, c_int, c_int, P, P, c_int, P, P, c_int, P, P, P], c_int),
+        "hiseg_se_gate_fwd": ([c_int, P, c_int, c_int, c_int, P, P, c_int, P, P, c_int, c_float, P, P, P], c_int),
         "hiseg_channel_scale_fwd": ([c_int, P, c_int, c_int, c_int, P, P, P], c_int),
         "hiseg_dwconv_fwd": ([c_int, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, c_int, P,
                               c_int, c_int, P], c_int),
@@ -164,8 +199,9 @@ def _declare(lib):
         "hiseg_se_gate_partials_fwd": ([P, c_int, c_int, c_int, c_int, P, P, c_int, P, P, c_int, P, P], c_int),
         "hiseg_image_max_fwd": ([P, c_ll, P, P], c_int),
         "hiseg_input_norm_fwd": ([c_int, P, c_int, c_int, c_int, c_int, P, P, P, P, c_int, P], c_int),
-        "hiseg_hier_combine_fwd": ([c_int, P, c_int, c_int, c_int, P, c_int, P, P, P, c_int, P, P, P, P,
-                                    P, P, P, P], c_int),
+        "hiseg_hier_combine_fwd": ([c_int, P, c_int, c_int, c_int, P, c_int, P, P, P, c_int, c_float, c_int, P, P,
+                                    P, P, P, P, P, P], c_int),
+        "hiseg_ubf_ln_tables": ([P, c_int, c_int, c_int, P, P, P, P, c_float, c_int, P, P, P, P, P], c_int),
         "hiseg_nhwc_to_nchw_fwd": ([c_int, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P], c_int),
         "hiseg_nchw_to_nhwc_fwd": ([c_int, P, c_int, c_int, c_int, c_int, P, c_int, P], c_int),
         "hiseg_instance_masks_fwd": ([P, c_int, c_int, c_int, c_int, P, P], c_int),
@@ -190,6 +226,11 @@ def _declare(lib):
         "hiseg_gate_bwd": ([c_int, c_ll, c_int, EwView, EwView, EwView, EwView, c_int, EwView, P], c_int),
         "hiseg_add_inplace": ([c_int, c_ll, c_int, EwView, EwView, P], c_int),
         "hiseg_act_bwd_cvt": ([c_int, c_ll, c_int, EwView, EwView, c_int, EwView, c_int, P], c_int),
+        "hiseg_act_bwd_pre": ([c_int, c_ll, c_int, EwView, EwView, c_int, c_float, EwView, c_int, P], c_int),
+        "hiseg_ln_ws": ([c_int, c_int, c_int], c_ll),
+        "hiseg_ln_fwd_stats": ([c_int, P, c_int, c_int, c_int, c_int, c_int, P, P, c_float, P, P, P, P, P, P],
+                               c_int),
+        "hiseg_ln_bwd": ([ctypes.POINTER(LnBwdDesc), P], c_int),
         "hiseg_maxpool2x2_bwd": ([c_int, P, c_int, c_int, c_int, c_int, P, P, c_int, P], c_int),
         "hiseg_resize_bilinear_bwd": ([P, c_int, c_int, c_int, c_int, c_int, P, P], c_int),
         "hiseg_upsample2x_bwd": ([c_int, c_ll, c_int, c_int, c_int, EwView, EwView, c_int, P], c_int),
@@ -207,11 +248,11 @@ def _declare(lib):
         "hiseg_attn_spatial_ws": ([c_int, c_int, c_int, c_int], c_int),
         "hiseg_attn_spatial_bwd": ([c_int, P, c_int, c_int, c_int, c_int, P, c_int, P, P, P, P, P, P, P, P, P], c_int),
         "hiseg_attn_channel_ws": ([c_int, c_int, c_int], c_int),
-        "hiseg_attn_channel_train_fwd": ([c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, P, P, P, P, P, P],
-                                         c_int),
-        "hiseg_attn_channel_bwd": ([c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, P, P, P, P, P, P, P, P, P, P],
-                                   c_int),
-        "hiseg_ubf_ws": ([], c_int),
+        "hiseg_attn_channel_train_fwd": ([c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, c_float, P, P, P, P, P,
+                                          P, P], c_int),
+        "hiseg_attn_channel_bwd": ([c_int, P, c_int, c_int, c_int, P, c_int, P, c_int, c_float, P, P, P, P, P, P, P,
+                                    P, P, P], c_int),
+        "hiseg_ubf_ws": ([c_int], c_int),
         "hiseg_ubf_train_fwd": ([ctypes.POINTER(UbfDesc), c_float, c_float, P, P, P, P], c_int),
         "hiseg_ubf_train_bwd": ([ctypes.POINTER(UbfDesc), P, P, P, P, P, P, P, ctypes.POINTER(UbfGrads), P], c_int),
         "hiseg_pw2_ws": ([c_int], c_int),

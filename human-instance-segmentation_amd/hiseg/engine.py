@@ -30,21 +30,28 @@ from .layers import LayerNorm2d, Swish
 from .ops import Act
 
 ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_SILU = L.ACT_NONE, L.ACT_RELU, L.ACT_SIGMOID, L.ACT_SILU
+ACT_GELU, ACT_SWISH = L.ACT_GELU, L.ACT_SWISH
 
 
 # ------------------------------------------------------------------------------------ plans
 def act_code(m: nn.Module) -> int:
+    """The hiseg activation code of an activation module (advanced/activation_utils.py:71-101).
+    Swish(beta != 1) returns an L.ActCode carrying beta."""
     if isinstance(m, nn.ReLU):
         return ACT_RELU
     if isinstance(m, nn.SiLU):
         return ACT_SILU
-    if isinstance(m, Swish) and float(m.beta) == 1.0:
-        return ACT_SILU
+    if isinstance(m, Swish):
+        return ACT_SILU if float(m.beta) == 1.0 else L.ActCode(ACT_SWISH, float(m.beta))
+    if isinstance(m, nn.GELU):
+        if getattr(m, "approximate", "none") != "none":
+            raise NotImplementedError("tanh-approximate GELU is not in the reference's activation factory")
+        return ACT_GELU
     if isinstance(m, nn.Sigmoid):
         return ACT_SIGMOID
     if isinstance(m, nn.Identity):
         return ACT_NONE
-    raise NotImplementedError(f"activation {type(m).__name__} is not fused by the hiseg kernels yet")
+    raise NotImplementedError(f"activation {type(m).__name__} is not in the reference's activation factory")
 
 
 def _bn(m: Optional[nn.Module]):
@@ -55,7 +62,7 @@ def _bn(m: Optional[nn.Module]):
             raise NotImplementedError("batch-statistics BatchNorm (train mode) is not on the hiseg inference path")
         return m
     if isinstance(m, LayerNorm2d):
-        raise NotImplementedError("layernorm2d normalisation is not implemented on the hiseg path yet (batchnorm is)")
+        raise AssertionError("LayerNorm2d has per-sample statistics and cannot be folded into a conv plan (use cna)")
     raise NotImplementedError(f"normalisation {type(m).__name__}")
 
 
@@ -131,6 +138,21 @@ class Ctx:
         return self._get(("dw", id(conv)), build, (conv.weight, conv.bias) + _bn_tensors(bn))
 
 
+def cna(E: Ctx, conv: nn.Module, norm: Optional[nn.Module], act: int, x: Act, xb: Optional[Act] = None, *,
+        split=None, residual: Optional[Act] = None, out: Optional[Act] = None, convT: bool = False) -> Act:
+    """conv -> norm -> (+ residual) -> act.  Eval BatchNorm (or no norm) folds into the conv launch;
+    LayerNorm2d (model.py:18-38) needs the conv output's per-sample statistics first: raw conv (+ bias),
+    then ops.layernorm2d (statistics + one apply pass with residual and activation)."""
+    if isinstance(norm, LayerNorm2d):
+        plan = E.convT(conv, None, ACT_NONE) if convT else E.conv(conv, None, ACT_NONE, split=split)
+        z = ops.conv2d(plan, x, xb)
+        C = z.C
+        return ops.layernorm2d(z, E.f32(norm.weight, (C,)), E.f32(norm.bias, (C,)), norm.eps, act,
+                               residual=residual, out=out)
+    plan = E.convT(conv, norm, act) if convT else E.conv(conv, norm, act, split=split)
+    return ops.conv2d(plan, x, xb, residual=residual, out=out)
+
+
 def _check_input(x: torch.Tensor, what: str):
     if not x.is_cuda:
         raise RuntimeError(f"{what}: hiseg runs on the GPU only (got a CPU tensor); there is no CPU fallback")
@@ -141,19 +163,19 @@ def residual_block(E: Ctx, blk: nn.Module, x: Act, out: Optional[Act] = None) ->
     """ResidualBlock (refinement.py:31-55 / unet.py:35-58): two fused launches."""
     a1 = act_code(blk.activation1 if hasattr(blk, "activation1") else blk.activation)
     a2 = act_code(blk.activation2 if hasattr(blk, "activation2") else blk.activation)
-    h = ops.conv2d(E.conv(blk.conv1, blk.norm1, a1), x)
-    return ops.conv2d(E.conv(blk.conv2, blk.norm2, a2), h, residual=x, out=out)
+    h = cna(E, blk.conv1, blk.norm1, a1, x)
+    return cna(E, blk.conv2, blk.norm2, a2, h, residual=x, out=out)
 
 
 def rgb_feature_extractor(E: Ctx, seq: nn.Sequential, x: Act) -> Act:
     """hierarchical_segmentation_rgb.py:657-673."""
-    h = ops.conv2d(E.conv(seq[0], seq[1], act_code(seq[2])), x)
+    h = cna(E, seq[0], seq[1], act_code(seq[2]), x)
     h = residual_block(E, seq[3], h)
-    h = ops.conv2d(E.conv(seq[4], seq[5], act_code(seq[6])), h)
+    h = cna(E, seq[4], seq[5], act_code(seq[6]), h)
     h = residual_block(E, seq[7], h)
-    h = ops.conv2d(E.conv(seq[8], seq[9], act_code(seq[10])), h)
+    h = cna(E, seq[8], seq[9], act_code(seq[10]), h)
     h = residual_block(E, seq[11], h)
-    return ops.conv2d(E.conv(seq[12], seq[13], act_code(seq[14])), h)
+    return cna(E, seq[12], seq[13], act_code(seq[14]), h)
 
 
 def enhanced_unet(E: Ctx, u: nn.Module, x: Act) -> Tuple[Act, Act]:
@@ -171,31 +193,31 @@ def enhanced_unet(E: Ctx, u: nn.Module, x: Act) -> Tuple[Act, Act]:
     for i in range(d):
         enc = u.encoders[i]
         if i == 0:
-            x = ops.conv2d(E.conv(enc[0], enc[1], act_code(enc[2])), x)
+            x = cna(E, enc[0], enc[1], act_code(enc[2]), x)
             x = residual_block(E, enc[3], x)
             x = residual_block(E, enc[4], x)
         else:
             x = residual_block(E, enc[0], x)
             x = residual_block(E, enc[1], x)
-            x = ops.conv2d(E.conv(enc[2], enc[3], act_code(enc[4])), x)
+            x = cna(E, enc[2], enc[3], act_code(enc[4]), x)
         feats.append(x)
         if i < d - 1:
             x = ops.maxpool2x2(x)
     b = u.bottleneck
     a = residual_block(E, b[0], x)
     a = residual_block(E, b[1], a)
-    a = ops.conv2d(E.conv(b[2], b[3], act_code(b[4])), a)
+    a = cna(E, b[2], b[3], act_code(b[4]), a)
     att = ops.conv2d(E.conv(b[5], None, ACT_SIGMOID), a)
     x = ops.conv2d(E.conv(u.bottleneck_conv), x, mul=att)
     for i in range(d - 1):
         up = ops.conv2d(E.convT(u.upconvs[i]), x)
         skip = feats[d - 2 - i]
         dec = u.decoders[i]
-        x = ops.conv2d(E.conv(dec[0], dec[1], act_code(dec[2]), split=(up.C, skip.C)), up, skip)
+        x = cna(E, dec[0], dec[1], act_code(dec[2]), up, skip, split=(up.C, skip.C))
         x = residual_block(E, dec[3], x)
         x = residual_block(E, dec[4], x)
     f = u.final
-    h = ops.conv2d(E.conv(f[0], f[1], act_code(f[2])), x)
+    h = cna(E, f[0], f[1], act_code(f[2]), x)
     low = Act.new(h.N, h.H, h.W, 2, torch.float32, E.device, cpad=2, zero=False)
     low_t = Act.new(h.N, h.H, h.W, 2, E.dtype, E.device)
     ops.conv2d(E.conv(f[3]), h, out=low, out2=low_t)
@@ -207,19 +229,19 @@ def hier_head(E: Ctx, head: nn.Module, feat: Act, aux: str) -> Tuple[torch.Tenso
     ExtendedHierarchicalSegmentationHeadUNetV2.forward (:550-606)."""
     bh = head.base_head
     sf = bh.shared_features
-    s = ops.conv2d(E.conv(sf[0], sf[1], act_code(sf[2])), feat)
+    s = cna(E, sf[0], sf[1], act_code(sf[2]), feat)
     s = residual_block(E, sf[4], s)
     s = residual_block(E, sf[6], s)
     low, low_t = enhanced_unet(E, bh.bg_vs_fg_unet, s)
     fg = bh.fg_gate
-    g = ops.conv2d(E.conv(fg[0], None, act_code(fg[1])), low_t)
-    g = ops.conv2d(E.conv(fg[3], None, act_code(fg[4])), g)
+    g = cna(E, fg[0], None, act_code(fg[1]), low_t)
+    g = cna(E, fg[3], None, act_code(fg[4]), g)
     gated = ops.conv2d(E.conv(fg[5], None, ACT_SIGMOID), g, mul=s)
     tb = bh.target_vs_nontarget_branch
     if bh.use_attention_module:
         t = residual_block(E, tb[0], gated)
         t = ops.attn_spatial(t, E.f32(tb[1].conv.weight))
-        t = ops.conv2d(E.convT(tb[3], tb[4], act_code(tb[5])), t)
+        t = cna(E, tb[3], tb[4], act_code(tb[5]), t, convT=True)
         ca = tb[6]
         gate = ops.se_gate(t, E.f32(ca.fc1.weight, (ca.fc1.out_channels, ca.fc1.in_channels)), None,
                            E.f32(ca.fc2.weight, (ca.fc2.out_channels, ca.fc2.in_channels)), None,
@@ -229,19 +251,28 @@ def hier_head(E: Ctx, head: nn.Module, feat: Act, aux: str) -> Tuple[torch.Tenso
         last = tb[9]
     else:
         t = residual_block(E, tb[0], gated)
-        t = ops.conv2d(E.convT(tb[2], tb[3], act_code(tb[4])), t)
+        t = cna(E, tb[2], tb[3], act_code(tb[4]), t, convT=True)
         t = residual_block(E, tb[6], t)
         last = tb[7]
     mh, mw = bh.mask_height, bh.mask_width
     if (t.H, t.W) != (mh, mw) or (2 * low.H, 2 * low.W) != (mh, mw):
         raise NotImplementedError(f"mask size {mh}x{mw} must be 2x the ROI size {low.H}x{low.W} on the hiseg path")
     up = bh.upsample_bg_fg
-    ut_s, ut_h = E.affine(("ut", id(up[0])), up[0].out_channels, up[0].bias, up[1])
+    per_sample = isinstance(up[1], LayerNorm2d)
+    if per_sample:   # LayerNorm2d over the ConvTranspose output: per-ROI tables [N][32]
+        ut_s = torch.empty(low.N * 32, dtype=torch.float32, device=E.device)
+        ut_h = torch.empty_like(ut_s)
+        L.check(L.lib().hiseg_ubf_ln_tables(low.t.data_ptr(), low.N, low.H, low.W, E.f32(up[0].weight).data_ptr(),
+                                            E.f32(up[0].bias).data_ptr(), E.f32(up[1].weight, (32,)).data_ptr(),
+                                            E.f32(up[1].bias, (32,)).data_ptr(), float(up[1].eps), 1, None, None,
+                                            ut_s.data_ptr(), ut_h.data_ptr(), L.stream_ptr()), "ubf_ln_tables")
+    else:
+        ut_s, ut_h = E.affine(("ut", id(up[0])), up[0].out_channels, up[0].bias, up[1])
     want = aux == "full"
     logits, bgfg, tn = ops.hier_combine(
         low.t, low.N, low.H, low.W, t, E.f32(up[0].weight), ut_s, ut_h, act_code(up[2]),
         E.f32(up[3].weight, (2, up[3].in_channels)), E.f32(up[3].bias),
-        E.f32(last.weight, (2, last.in_channels)), E.f32(last.bias), want)
+        E.f32(last.weight, (2, last.in_channels)), E.f32(last.bias), want, per_sample=per_sample)
     auxd: Dict[str, torch.Tensor] = {}
     if not want:
         return logits, auxd
@@ -253,15 +284,15 @@ def hier_head(E: Ctx, head: nn.Module, feat: Act, aux: str) -> Tuple[torch.Tenso
     lib = L.lib()
     if head.use_contour_detection:
         cb = head.contour_branch.contour_branch
-        c = ops.conv2d(E.conv(cb[0], cb[1], act_code(cb[2])), s)
-        c = ops.conv2d(E.conv(cb[3], cb[4], act_code(cb[5])), c)
+        c = cna(E, cb[0], cb[1], act_code(cb[2]), s)
+        c = cna(E, cb[3], cb[4], act_code(cb[5]), c)
         cm = Act.new(c.N, c.H, c.W, 1, torch.float32, E.device, cpad=1, zero=False)
         ops.conv2d(E.conv(cb[6], None, ACT_SIGMOID), c, out=cm)
         auxd["contours"] = _resize(cm.t.view(c.N, 1, c.H, c.W), mh, mw, lib)
     if head.use_distance_transform:
         dd = head.distance_decoder
         dh = dd.distance_head
-        dx = ops.conv2d(E.conv(dh[0], dh[1], act_code(dh[2])), s)
+        dx = cna(E, dh[0], dh[1], act_code(dh[2]), s)
         dx = residual_block(E, dh[3], dx)
         dm = Act.new(dx.N, dx.H, dx.W, 1, torch.float32, E.device, cpad=1, zero=False)
         ops.conv2d(E.conv(dh[4]), dx, out=dm)

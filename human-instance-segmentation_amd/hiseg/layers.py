@@ -61,6 +61,19 @@ def make_act(name: str, beta: float = 1.0) -> nn.Module:
     raise ValueError(f"Unknown activation function: {name}")
 
 
+def make_act_unet(name: str, beta: float = 1.0) -> nn.Module:
+    """get_activation_function of hierarchical_segmentation_unet.py:13-32 (== rgb.py:21-40): 'swish' is
+    nn.SiLU there -- beta is ignored -- unlike the refinement modules' get_activation (make_act)."""
+    n = name.lower()
+    if n == "relu":
+        return nn.ReLU(inplace=True)
+    if n in ("swish", "silu"):
+        return nn.SiLU(inplace=True)
+    if n == "gelu":
+        return nn.GELU()
+    raise ValueError(f"Unsupported activation function: {name}")
+
+
 class ResidualBlock(nn.Module):
     """relu(bn2(conv2(relu(bn1(conv1 x)))) + x).
 
@@ -79,8 +92,8 @@ class ResidualBlock(nn.Module):
         if two_acts:
             self.activation1 = make_act(act, beta)
             self.activation2 = make_act(act, beta)
-        else:
-            self.activation = make_act(act, beta)
+        else:   # the UNet variant builds its activation with unet.py's factory (Swish -> SiLU)
+            self.activation = make_act_unet(act, beta)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return _engine().residual_block_nchw(self, x)
@@ -128,17 +141,17 @@ class EnhancedUNet(nn.Module):
         for i in range(depth):
             if i == 0:
                 self.encoders.append(nn.Sequential(
-                    nn.Conv2d(ch[0], ch[1], 3, padding=1), make_norm(norm, ch[1], groups), make_act(act, beta),
+                    nn.Conv2d(ch[0], ch[1], 3, padding=1), make_norm(norm, ch[1], groups), make_act_unet(act, beta),
                     res(ch[1]), res(ch[1])))
             else:
                 self.encoders.append(nn.Sequential(
                     res(ch[i]), res(ch[i]), nn.Conv2d(ch[i], ch[i + 1], 3, padding=1),
-                    make_norm(norm, ch[i + 1], groups), make_act(act, beta)))
+                    make_norm(norm, ch[i + 1], groups), make_act_unet(act, beta)))
             if i < depth - 1:
                 self.pools.append(nn.MaxPool2d(2))
         top = ch[-1]
         self.bottleneck = nn.Sequential(
-            res(top), res(top), nn.Conv2d(top, top, 3, padding=1), make_norm(norm, top, groups), make_act(act, beta),
+            res(top), res(top), nn.Conv2d(top, top, 3, padding=1), make_norm(norm, top, groups), make_act_unet(act, beta),
             nn.Conv2d(top, top, 1), nn.Sigmoid())
         self.bottleneck_conv = nn.Conv2d(top, top, 3, padding=1)
         self.upconvs = nn.ModuleList()
@@ -146,10 +159,10 @@ class EnhancedUNet(nn.Module):
         for i in range(depth - 1, 0, -1):
             self.upconvs.append(nn.ConvTranspose2d(ch[i + 1], ch[i], 2, stride=2))
             self.decoders.append(nn.Sequential(
-                nn.Conv2d(2 * ch[i], ch[i], 3, padding=1), make_norm(norm, ch[i], groups), make_act(act, beta),
+                nn.Conv2d(2 * ch[i], ch[i], 3, padding=1), make_norm(norm, ch[i], groups), make_act_unet(act, beta),
                 res(ch[i]), res(ch[i])))
         self.final = nn.Sequential(
-            nn.Conv2d(ch[1], ch[1] // 2, 3, padding=1), make_norm(norm, ch[1] // 2, groups), make_act(act, beta),
+            nn.Conv2d(ch[1], ch[1] // 2, 3, padding=1), make_norm(norm, ch[1] // 2, groups), make_act_unet(act, beta),
             nn.Conv2d(ch[1] // 2, 2, 1))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:

@@ -17,7 +17,7 @@ import torch.nn as nn
 
 from . import engine
 from .effunet import EfficientNetUnet
-from .layers import RefinedHierarchicalSegmentationHead, ResidualBlock, make_act, make_norm
+from .layers import RefinedHierarchicalSegmentationHead, ResidualBlock, make_act_unet, make_norm
 
 
 class DynamicRoIAlign(nn.Module):
@@ -145,13 +145,13 @@ class HierarchicalRGBSegmentationModelWithFullImagePretrainedUNet(nn.Module):
         fd = 256
         norm, g, act, beta = normalization_type, normalization_groups, activation_function, activation_beta
         self.rgb_feature_extractor = nn.Sequential(
-            nn.Conv2d(3, 64, 3, padding=1), make_norm(norm, 64, min(g, 64)), make_act(act, beta),
+            nn.Conv2d(3, 64, 3, padding=1), make_norm(norm, 64, min(g, 64)), make_act_unet(act, beta),
             ResidualBlock(64, norm, min(g, 64), act, beta),
-            nn.Conv2d(64, 128, 3, padding=1), make_norm(norm, 128, min(g, 128)), make_act(act, beta),
+            nn.Conv2d(64, 128, 3, padding=1), make_norm(norm, 128, min(g, 128)), make_act_unet(act, beta),
             ResidualBlock(128, norm, min(g, 128), act, beta),
-            nn.Conv2d(128, 256, 3, padding=1), make_norm(norm, 256, min(g, 256)), make_act(act, beta),
+            nn.Conv2d(128, 256, 3, padding=1), make_norm(norm, 256, min(g, 256)), make_act_unet(act, beta),
             ResidualBlock(256, norm, min(g, 256), act, beta),
-            nn.Conv2d(256, fd, 1), make_norm(norm, fd, min(g, fd)), make_act(act, beta))
+            nn.Conv2d(256, fd, 1), make_norm(norm, fd, min(g, fd)), make_act_unet(act, beta))
         use_refinement = any([use_boundary_refinement, use_progressive_upsampling, use_subpixel_conv,
                               use_contour_detection, use_distance_transform])
         if not use_refinement:

@@ -302,7 +302,7 @@ def conv2d(p: ConvPlan, xa: Act, xb: Optional[Act] = None, out: Optional[Act] = 
     if in_scale is not None:
         d.in_scale = in_scale.data_ptr()
     d.weight, d.Cout, d.Cout_pad, d.K_pad = p.weight.data_ptr(), p.gemm_cols, p.cout_pad, p.k_pad
-    d.scale, d.shift, d.act = p.scale.data_ptr(), p.shift.data_ptr(), p.act
+    d.scale, d.shift, d.act, d.act_beta = p.scale.data_ptr(), p.shift.data_ptr(), int(p.act), L.act_beta(p.act)
     if residual is not None:
         d.residual, d.r_cstride, d.r_coff = residual.ptr(), residual.cstride, residual.coff
     if mul is not None:
@@ -366,7 +366,7 @@ def se_gate(x: Act, w1, b1, w2, b2, act: int) -> torch.Tensor:
     gate = torch.empty(x.N, x.C, dtype=torch.float32, device=x.t.device)
     cr = w1.shape[0]
     L.check(lib.hiseg_se_gate_fwd(hdtype(x.dtype), x.ptr(), x.N, HW, x.C, w1.data_ptr(), _ptr(b1), cr,
-                                  w2.data_ptr(), _ptr(b2), act, partial.data_ptr(), gate.data_ptr(),
+                                  w2.data_ptr(), _ptr(b2), int(act), L.act_beta(act), partial.data_ptr(), gate.data_ptr(),
                                   L.stream_ptr()), "se_gate")
     return gate
 
@@ -427,17 +427,48 @@ def input_norm(images: torch.Tensor, mean: torch.Tensor, std: torch.Tensor, dtyp
 
 
 def hier_combine(low: torch.Tensor, N: int, h: int, w: int, tfeat: Act, ut_w, ut_scale, ut_shift, ut_act, u1_w, u1_b,
-                 t_w, t_b, want_aux: bool):
+                 t_w, t_b, want_aux: bool, per_sample: bool = False):
+    """Fused upsample_bg_fg + target 1x1 + hierarchical combine; ``per_sample``: ut_scale/ut_shift are the
+    [N][32] LayerNorm2d tables of hiseg_ubf_ln_tables."""
     assert tfeat.coff == 0 and tfeat.cstride == tfeat.C and (tfeat.H, tfeat.W) == (2 * h, 2 * w)
     dev = low.device
     logits = torch.empty(N, 3, 2 * h, 2 * w, dtype=torch.float32, device=dev)
     bgfg = torch.empty(N, 2, 2 * h, 2 * w, dtype=torch.float32, device=dev) if want_aux else None
     tn = torch.empty(N, 2, 2 * h, 2 * w, dtype=torch.float32, device=dev) if want_aux else None
     L.check(L.lib().hiseg_hier_combine_fwd(hdtype(tfeat.dtype), low.data_ptr(), N, h, w, tfeat.ptr(), tfeat.C,
-                                           ut_w.data_ptr(), ut_scale.data_ptr(), ut_shift.data_ptr(), ut_act,
-                                           u1_w.data_ptr(), u1_b.data_ptr(), t_w.data_ptr(), t_b.data_ptr(),
+                                           ut_w.data_ptr(), ut_scale.data_ptr(), ut_shift.data_ptr(), int(ut_act),
+                                           L.act_beta(ut_act), int(per_sample), u1_w.data_ptr(), u1_b.data_ptr(), t_w.data_ptr(), t_b.data_ptr(),
                                            logits.data_ptr(), _ptr(bgfg), _ptr(tn), L.stream_ptr()), "hier_combine")
     return logits, bgfg, tn
+
+
+def layernorm2d(z: Act, weight: torch.Tensor, bias: torch.Tensor, eps: float, act: int,
+                residual: Optional[Act] = None, out: Optional[Act] = None) -> Act:
+    """LayerNorm2d (model.py:18-38) of a conv output z, then (+ residual) and the activation:
+    per-sample statistics over (C, H, W) (hiseg_ln_fwd_stats) and one apply pass with the folded
+    per-sample tables (hiseg_bn_apply, per_sample = 1).  weight / bias: f32 [C]."""
+    lib = L.lib()
+    dev = z.t.device
+    N, HW, C = z.N, z.H * z.W, z.C
+    ws = torch.empty(int(lib.hiseg_ln_ws(N, HW, C)), dtype=torch.float32, device=dev)
+    mean = torch.empty(N, dtype=torch.float32, device=dev)
+    invstd = torch.empty_like(mean)
+    scale = torch.empty(N * C, dtype=torch.float32, device=dev)
+    shift = torch.empty_like(scale)
+    L.check(lib.hiseg_ln_fwd_stats(hdtype(z.dtype), z.ptr(), N, HW, C, z.cstride, z.coff, weight.data_ptr(),
+                                   bias.data_ptr(), float(eps), ws.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                                   scale.data_ptr(), shift.data_ptr(), L.stream_ptr()), "ln_fwd_stats")
+    y = out if out is not None else Act.new(N, z.H, z.W, C, z.dtype, dev, cpad=z.cstride)
+    d = L.BnApplyDesc()
+    d.dtype, d.P, d.HW, d.C = hdtype(z.dtype), N * HW, HW, C
+    d.z, d.z_cstride, d.z_coff = z.ptr(), z.cstride, z.coff
+    d.scale, d.shift, d.per_sample = scale.data_ptr(), shift.data_ptr(), 1
+    if residual is not None:
+        d.residual, d.r_cstride, d.r_coff = residual.ptr(), residual.cstride, residual.coff
+    d.act, d.act_beta = int(act), L.act_beta(act)
+    d.y, d.y_cstride, d.y_coff = y.ptr(), y.cstride, y.coff
+    L.check(lib.hiseg_bn_apply(ctypes.byref(d), L.stream_ptr()), "ln_apply")
+    return y
 
 
 def instance_masks(logits: torch.Tensor, dilation: int = 0) -> torch.Tensor:

@@ -33,6 +33,8 @@ from .layers import LayerNorm2d
 from .ops import Act, chunk_elems, hdtype, round_up
 
 ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_SILU = L.ACT_NONE, L.ACT_RELU, L.ACT_SIGMOID, L.ACT_SILU
+ACT_GELU, ACT_SWISH = L.ACT_GELU, L.ACT_SWISH
+SMOOTH_ACTS = (ACT_SILU, ACT_GELU, ACT_SWISH)   # derivative needs the pre-activation
 _P = ctypes.c_void_p
 # developer knob: force a conv kernel variant for the data-gradient convs (0 = automatic, -1 = generic)
 _DGRAD_VARIANT = int(os.environ.get("HISEG_DGRAD_VARIANT", "0"))
@@ -312,7 +314,8 @@ def _desc(S: TrainState, p: TConv, xa: Act, xb: Optional[Act], out: Act, *, act=
     if xb is not None:
         d.srcB, d.b_cstride, d.b_coff, d.Cb = xb.ptr(), xb.cstride, xb.coff, p.cb
     d.weight, d.Cout, d.Cout_pad, d.K_pad = p.w_fwd.data_ptr(), p.gemm_cols, p.cout_pad, p.k_pad
-    d.scale, d.shift, d.act = p.ones.data_ptr(), (shift if shift is not None else p.shift).data_ptr(), act
+    d.scale, d.shift = p.ones.data_ptr(), (shift if shift is not None else p.shift).data_ptr()
+    d.act, d.act_beta = int(act), L.act_beta(act)
     if residual is not None:
         d.residual, d.r_cstride, d.r_coff = residual.ptr(), residual.cstride, residual.coff
     if mul is not None:
@@ -422,16 +425,78 @@ class BNState:
         self.shift = torch.empty_like(self.mean)
 
 
+class LNState:
+    """LayerNorm2d forward state: per-sample mean / invstd [N], folded tables scale / shift [N][C], workspace."""
+
+    def __init__(self, N, HW, C, device):
+        self.mean = torch.empty(N, dtype=torch.float32, device=device)
+        self.invstd = torch.empty_like(self.mean)
+        self.scale = torch.empty(N * C, dtype=torch.float32, device=device)
+        self.shift = torch.empty_like(self.scale)
+        self.ws = torch.empty(int(L.lib().hiseg_ln_ws(N, HW, C)), dtype=torch.float32, device=device)
+
+
 def _bn_module(bn):
-    if isinstance(bn, LayerNorm2d):
-        raise NotImplementedError("layernorm2d training is not on the hiseg path (batchnorm configs only)")
-    assert isinstance(bn, nn.BatchNorm2d)
+    assert isinstance(bn, (nn.BatchNorm2d, LayerNorm2d)), type(bn)
     return bn
+
+
+def ln_forward(T: Tape, ln: LayerNorm2d, z: Act, *, act: int, residual: Optional[Act] = None,
+               drop: Optional[torch.Tensor] = None, out: Optional[Act] = None) -> Tuple[Act, LNState]:
+    """LayerNorm2d (model.py:18-38): per-sample statistics of z over (C, H, W), y = act(ln(z) + residual) * drop."""
+    lib = L.lib()
+    N, HW, C = z.N, z.H * z.W, z.C
+    st = LNState(N, HW, C, z.t.device)
+    _chk(lib.hiseg_ln_fwd_stats(hdtype(z.dtype), z.ptr(), N, HW, C, z.cstride, z.coff, ln.weight.data_ptr(),
+                                ln.bias.data_ptr(), float(ln.eps), st.ws.data_ptr(), st.mean.data_ptr(),
+                                st.invstd.data_ptr(), st.scale.data_ptr(), st.shift.data_ptr(), _stream()),
+         "ln_fwd_stats")
+    y = out if out is not None else Act.new(N, z.H, z.W, C, z.dtype, z.t.device, cpad=z.cstride)
+    d = L.BnApplyDesc()
+    d.dtype, d.P, d.HW, d.C = hdtype(z.dtype), N * HW, HW, C
+    d.z, d.z_cstride, d.z_coff = z.ptr(), z.cstride, z.coff
+    d.scale, d.shift, d.per_sample = st.scale.data_ptr(), st.shift.data_ptr(), 1
+    if residual is not None:
+        d.residual, d.r_cstride, d.r_coff = residual.ptr(), residual.cstride, residual.coff
+    d.act, d.act_beta = int(act), L.act_beta(act)
+    d.chan_mul = _ptr(drop)
+    d.y, d.y_cstride, d.y_coff = y.ptr(), y.cstride, y.coff
+    _chk(lib.hiseg_bn_apply(ctypes.byref(d), _stream()), "ln_apply")
+    return y, st
+
+
+def ln_backward(T: Tape, ln: LayerNorm2d, z: Act, y: Act, st: LNState, dz: Act, *, act: int,
+                residual: Optional[Act] = None, drop=None, conv_bias: Optional[torch.Tensor] = None):
+    lib, S = L.lib(), T.S
+    gy, _ = T.grad(y)
+    d = L.LnBwdDesc()
+    d.dtype, d.N, d.HW, d.C = hdtype(z.dtype), z.N, z.H * z.W, z.C
+    d.dy, d.dy_cstride, d.dy_coff = gy.ptr(), gy.cstride, gy.coff
+    d.z, d.z_cstride, d.z_coff = z.ptr(), z.cstride, z.coff
+    d.chan_mul, d.act, d.act_beta = _ptr(drop), int(act), L.act_beta(act)
+    d.mean, d.invstd, d.scale, d.shift = st.mean.data_ptr(), st.invstd.data_ptr(), st.scale.data_ptr(), \
+        st.shift.data_ptr()
+    d.gamma = ln.weight.data_ptr()
+    d.dgamma = _ptr(S.grad(ln.weight)) if ln.weight.requires_grad else None
+    d.dbeta = _ptr(S.grad(ln.bias)) if ln.bias.requires_grad else None
+    d.dconv_bias = _ptr(conv_bias)
+    d.accumulate_params = 1
+    d.dz, d.dz_cstride, d.dz_coff = dz.ptr(), dz.cstride, dz.coff
+    d.ws = st.ws.data_ptr()
+    if residual is not None:
+        gr, acc = T.grad(residual)
+        d.residual, d.r_cstride, d.r_coff = residual.ptr(), residual.cstride, residual.coff
+        d.dres, d.dres_cstride, d.dres_coff, d.dres_accumulate = gr.ptr(), gr.cstride, gr.coff, int(acc)
+    _chk(lib.hiseg_ln_bwd(ctypes.byref(d), _stream()), "ln_bwd")
+    if residual is not None:
+        T.mark(residual)
 
 
 def bn_forward(T: Tape, bn: nn.BatchNorm2d, z: Act, *, act: int, residual: Optional[Act] = None,
                drop: Optional[torch.Tensor] = None, out: Optional[Act] = None) -> Tuple[Act, BNState]:
     """Batch statistics of z (+ running update), y = act(bn(z) + residual) * drop."""
+    if isinstance(bn, LayerNorm2d):
+        return ln_forward(T, bn, z, act=act, residual=residual, drop=drop, out=out)
     lib = L.lib()
     C = z.C
     P = z.N * z.H * z.W
@@ -455,7 +520,7 @@ def bn_forward(T: Tape, bn: nn.BatchNorm2d, z: Act, *, act: int, residual: Optio
     d.scale, d.shift = st.scale.data_ptr(), st.shift.data_ptr()
     if residual is not None:
         d.residual, d.r_cstride, d.r_coff = residual.ptr(), residual.cstride, residual.coff
-    d.act = act
+    d.act, d.act_beta = int(act), L.act_beta(act)
     d.chan_mul = _ptr(drop)
     d.y, d.y_cstride, d.y_coff = y.ptr(), y.cstride, y.coff
     _chk(lib.hiseg_bn_apply(ctypes.byref(d), _stream()), "bn_apply")
@@ -464,6 +529,8 @@ def bn_forward(T: Tape, bn: nn.BatchNorm2d, z: Act, *, act: int, residual: Optio
 
 def bn_backward(T: Tape, bn: nn.BatchNorm2d, z: Act, y: Act, st: BNState, dz: Act, *, act: int,
                 residual: Optional[Act] = None, drop=None, conv_bias: Optional[torch.Tensor] = None):
+    if isinstance(bn, LayerNorm2d):
+        return ln_backward(T, bn, z, y, st, dz, act=act, residual=residual, drop=drop, conv_bias=conv_bias)
     lib, S = L.lib(), T.S
     gy, _ = T.grad(y)
     C = z.C
@@ -474,7 +541,7 @@ def bn_backward(T: Tape, bn: nn.BatchNorm2d, z: Act, y: Act, st: BNState, dz: Ac
     d.dy, d.dy_cstride, d.dy_coff = gy.ptr(), gy.cstride, gy.coff
     d.y, d.y_cstride, d.y_coff = y.ptr(), y.cstride, y.coff
     d.z, d.z_cstride, d.z_coff = z.ptr(), z.cstride, z.coff
-    d.chan_mul, d.act = _ptr(drop), act
+    d.chan_mul, d.act, d.act_beta = _ptr(drop), int(act), L.act_beta(act)
     d.mean, d.invstd, d.gamma, d.beta = st.mean.data_ptr(), st.invstd.data_ptr(), _ptr(bn.weight), _ptr(bn.bias)
     d.partial = part.data_ptr()
     d.dgamma = _ptr(S.grad(bn.weight)) if bn.weight is not None and bn.weight.requires_grad else None
@@ -487,6 +554,11 @@ def bn_backward(T: Tape, bn: nn.BatchNorm2d, z: Act, y: Act, st: BNState, dz: Ac
         d.dres, d.dres_cstride, d.dres_coff, d.dres_accumulate = gr.ptr(), gr.cstride, gr.coff, int(acc)
     elif act == ACT_RELU:   # ReLU mask recomputed from z with the forward's folded affine: y is not re-read
         d.fwd_scale, d.fwd_shift = st.scale.data_ptr(), st.shift.data_ptr()
+    if int(act) in (ACT_GELU, ACT_SWISH) or (int(act) == ACT_SILU and residual is not None):
+        # derivative at the forward's own pre-activation z*scale + shift (+ residual)
+        d.fwd_scale, d.fwd_shift = st.scale.data_ptr(), st.shift.data_ptr()
+        if residual is not None:
+            d.residual, d.r_cstride, d.r_coff = residual.ptr(), residual.cstride, residual.coff
     _chk(lib.hiseg_bn_bwd(ctypes.byref(d), _stream()), "bn_bwd")
     if residual is not None:
         T.mark(residual)
@@ -513,9 +585,13 @@ def conv_bn_act(T: Tape, conv: nn.Conv2d, bn, act: int, x: Act, xb: Optional[Act
 
 def conv_plain(T: Tape, conv: nn.Conv2d, act: int, x: Act, xb: Optional[Act] = None, *, split=None,
                convT: bool = False, out_dtype=None, out: Optional[Act] = None, out2: Optional[Act] = None) -> Act:
-    """Conv (+bias) (+act ReLU/Sigmoid fused in the epilogue), no normalisation."""
+    """Conv (+bias) (+act ReLU/Sigmoid fused in the epilogue), no normalisation.  SiLU / GELU / Swish: the
+    conv writes the pre-activation, one element-wise pass the activation (its derivative needs the former)."""
     S = T.S
     p = S.conv(conv, split=split, convT=convT)
+    if int(act) in SMOOTH_ACTS:
+        assert out is None and out2 is None and out_dtype is None
+        return _conv_smooth_act(T, p, act, x, xb)
     y, d = conv_fwd(S, p, x, xb, act=act, out_dtype=out_dtype, out=out, out2=out2)
 
     def back():
@@ -535,6 +611,30 @@ def conv_plain(T: Tape, conv: nn.Conv2d, act: int, x: Act, xb: Optional[Act] = N
                  "relu_bwd")
         else:
             dz = gy
+        conv_bwd(T, p, d, x, xb, dz)
+    T.push(back)
+    return y
+
+
+def _conv_smooth_act(T: Tape, p: TConv, act: int, x: Act, xb: Optional[Act]) -> Act:
+    S, lib = T.S, L.lib()
+    z, d = conv_fwd(S, p, x, xb)
+    y = Act.new(z.N, z.H, z.W, z.C, z.dtype, z.t.device, cpad=z.cstride)
+    one = torch.ones(z.C, dtype=torch.float32, device=z.t.device)
+    zero = torch.zeros(z.C, dtype=torch.float32, device=z.t.device)
+    a = L.BnApplyDesc()
+    a.dtype, a.P, a.HW, a.C = hdtype(z.dtype), z.N * z.H * z.W, z.H * z.W, z.C
+    a.z, a.z_cstride, a.z_coff = z.ptr(), z.cstride, z.coff
+    a.scale, a.shift, a.act, a.act_beta = one.data_ptr(), zero.data_ptr(), int(act), L.act_beta(act)
+    a.y, a.y_cstride, a.y_coff = y.ptr(), y.cstride, y.coff
+    _chk(lib.hiseg_bn_apply(ctypes.byref(a), _stream()), "act_apply")
+    T.keep.extend([one, zero])
+
+    def back():
+        gy, _ = T.grad(y)
+        dz = Act.new(z.N, z.H, z.W, z.C, z.dtype, z.t.device, cpad=z.cstride, zero=z.cstride != z.C)
+        _chk(lib.hiseg_act_bwd_pre(hdtype(z.dtype), z.N * z.H * z.W, z.C, ew(gy), ew(z), int(act), L.act_beta(act),
+                                   ew(dz), 0, _stream()), "act_bwd_pre")
         conv_bwd(T, p, d, x, xb, dz)
     T.push(back)
     return y
@@ -724,16 +824,16 @@ def channel_attention(T: Tape, m: nn.Module, x: Act, drop) -> Act:
     hpre = torch.empty(x.N * Cr, dtype=torch.float32, device=dev)
     g = torch.empty(x.N * C, dtype=torch.float32, device=dev)
     out = Act.new(x.N, x.H, x.W, C, x.dtype, dev, zero=False)
-    _chk(lib.hiseg_attn_channel_train_fwd(hdtype(x.dtype), x.ptr(), x.N, HW, C, w1.data_ptr(), Cr, w2.data_ptr(), act,
-                                          _ptr(drop), ws.data_ptr(), gap.data_ptr(), hpre.data_ptr(), g.data_ptr(),
+    _chk(lib.hiseg_attn_channel_train_fwd(hdtype(x.dtype), x.ptr(), x.N, HW, C, w1.data_ptr(), Cr, w2.data_ptr(),
+                                          int(act), L.act_beta(act), _ptr(drop), ws.data_ptr(), gap.data_ptr(), hpre.data_ptr(), g.data_ptr(),
                                           out.ptr(), _stream()), "attn_channel_train_fwd")
 
     def back():
         gy, _ = T.grad(out)
         gx, acc = T.grad(x)
         target = gx if not acc else Act.new(x.N, x.H, x.W, C, x.dtype, dev, zero=False)
-        _chk(lib.hiseg_attn_channel_bwd(hdtype(x.dtype), x.ptr(), x.N, HW, C, w1.data_ptr(), Cr, w2.data_ptr(), act,
-                                        _ptr(drop), gap.data_ptr(), hpre.data_ptr(), g.data_ptr(), gy.ptr(),
+        _chk(lib.hiseg_attn_channel_bwd(hdtype(x.dtype), x.ptr(), x.N, HW, C, w1.data_ptr(), Cr, w2.data_ptr(),
+                                        int(act), L.act_beta(act), _ptr(drop), gap.data_ptr(), hpre.data_ptr(), g.data_ptr(), gy.ptr(),
                                         target.ptr(), ws.data_ptr(), S.grad(w1).data_ptr(), S.grad(w2).data_ptr(),
                                         _stream()), "attn_channel_bwd")
         if acc:
@@ -807,11 +907,18 @@ def hier_head_train(T: Tape, head: nn.Module, feat: Act):
         raise NotImplementedError(f"mask size {mh}x{mw} must be 2x the ROI size {low.H}x{low.W} on the hiseg path")
     up = bh.upsample_bg_fg
     ubn = _bn_module(up[1])
+    uln = isinstance(ubn, LayerNorm2d)
+    uact = act_of(up[2])
     h, w = low.H, low.W
     logits = torch.empty(N, 3, mh, mw, dtype=torch.float32, device=dev)
     bgfg = torch.empty(N, 2, mh, mw, dtype=torch.float32, device=dev)
     tn = torch.empty(N, 2, mh, mw, dtype=torch.float32, device=dev)
     bst = BNState(32, dev)
+    if uln:   # per-sample statistics: mean / invstd [N], tables [N][32]
+        bst.mean = torch.empty(N, dtype=torch.float32, device=dev)
+        bst.invstd = torch.empty_like(bst.mean)
+        bst.scale = torch.empty(N * 32, dtype=torch.float32, device=dev)
+        bst.shift = torch.empty_like(bst.scale)
     ud = L.UbfDesc()
     ud.dtype = hdtype(S.dtype)
     ud.low, ud.N, ud.h, ud.w = low.ptr(), N, h, w
@@ -822,13 +929,18 @@ def hier_head_train(T: Tape, head: nn.Module, feat: Act):
     ud.u1_w, ud.u1_b = up[3].weight.data_ptr(), up[3].bias.data_ptr()
     ud.tfeat, ud.Ct, ud.t_w, ud.t_b = t.ptr(), t.C, last.weight.data_ptr(), last.bias.data_ptr()
     ud.logits, ud.bgfg, ud.tn = logits.data_ptr(), bgfg.data_ptr(), tn.data_ptr()
-    ws = torch.empty(lib.hiseg_ubf_ws(), dtype=torch.float32, device=dev)
-    if ubn.num_batches_tracked is not None:
-        ubn.num_batches_tracked.add_(1)
-    _chk(lib.hiseg_ubf_train_fwd(ctypes.byref(ud), float(ubn.eps), float(ubn.momentum or 0.1),
-                                 ubn.running_mean.data_ptr(), ubn.running_var.data_ptr(), ws.data_ptr(), _stream()),
-         "ubf_train_fwd")
-    torch.autograd.graph.increment_version([ubn.running_mean, ubn.running_var])
+    ud.act, ud.act_beta, ud.layernorm = int(uact), L.act_beta(uact), int(uln)
+    ws = torch.empty(lib.hiseg_ubf_ws(N), dtype=torch.float32, device=dev)
+    if uln:
+        _chk(lib.hiseg_ubf_train_fwd(ctypes.byref(ud), float(ubn.eps), 0.0, None, None, ws.data_ptr(), _stream()),
+             "ubf_train_fwd")
+    else:
+        if ubn.num_batches_tracked is not None:
+            ubn.num_batches_tracked.add_(1)
+        _chk(lib.hiseg_ubf_train_fwd(ctypes.byref(ud), float(ubn.eps), float(ubn.momentum or 0.1),
+                                     ubn.running_mean.data_ptr(), ubn.running_var.data_ptr(), ws.data_ptr(),
+                                     _stream()), "ubf_train_fwd")
+        torch.autograd.graph.increment_version([ubn.running_mean, ubn.running_var])
     T.keep.extend([bst, ws])
     aux = {"bg_fg_logits": bgfg, "target_nontarget_logits": tn}
 

@@ -28,7 +28,10 @@ typedef void* hiseg_stream_t; /* hipStream_t */
 
 enum hiseg_dtype { HISEG_F32 = 0, HISEG_BF16 = 1 };
 
-enum hiseg_act { HISEG_ACT_NONE = 0, HISEG_ACT_RELU = 1, HISEG_ACT_SIGMOID = 2, HISEG_ACT_SILU = 3 };
+/* Activations (advanced/activation_utils.py:71-101): GELU is nn.GELU's exact erf form,
+ * SWISH is x * sigmoid(beta * x) with beta taken from the caller's act_beta (SILU == SWISH, beta 1). */
+enum hiseg_act { HISEG_ACT_NONE = 0, HISEG_ACT_RELU = 1, HISEG_ACT_SIGMOID = 2, HISEG_ACT_SILU = 3,
+                 HISEG_ACT_GELU = 4, HISEG_ACT_SWISH = 5 };
 
 enum hiseg_status {
   HISEG_OK = 0,
@@ -114,6 +117,7 @@ typedef struct hiseg_conv2d_desc {
    * nK = K_pad/64 K blocks in channel-block-major / tap-minor order) used by the 3x3 halo
    * kernel that streams weights straight into registers; null disables that kernel. */
   const void* weight_frag;
+  float act_beta;           /* Swish beta (act == HISEG_ACT_SWISH); ignored otherwise        */
 } hiseg_conv2d_desc;
 int hiseg_conv2d_fwd(const hiseg_conv2d_desc* d, hiseg_stream_t stream);
 /* Tuning/test entry: variant -1 forces the generic kernel, 0 = automatic choice (as
@@ -138,7 +142,7 @@ int hiseg_attn_spatial_fwd(int dtype, const void* x, int N, int H, int W, int C,
  * `partial` is workspace of N*splits*C floats (splits = hiseg_gap_splits(HW)). */
 int hiseg_gap_splits(int HW);
 int hiseg_se_gate_fwd(int dtype, const void* x, int N, int HW, int C, const float* w1,
-                      const float* b1, int Cr, const float* w2, const float* b2, int act,
+                      const float* b1, int Cr, const float* w2, const float* b2, int act, float act_beta,
                       float* partial, float* gate, hiseg_stream_t stream);
 
 /* y[n, p, c] = x[n, p, c] * gate[n, c]  (attention_modules.py:64). */
@@ -180,14 +184,23 @@ int hiseg_input_norm_fwd(int dtype, const float* x, int B, int C, int H, int W, 
  * final 1x1 128->2 of the target branch (:521).
  *   low  : f32 NHWC [N, h, w, 2]       bg_fg_logits_low
  *   tfeat: dtype NHWC [N, 2h, 2w, Ct]  target-branch features before its last 1x1 (cstride Ct)
- *   ut_w [2][32][2][2], ut_scale/ut_shift [32] (convT bias + BN folded), u1_w [2][32], u1_b[2]
+ *   ut_w [2][32][2][2], ut_scale/ut_shift [32] (convT bias + BN folded; [N][32] per-sample
+ *   tables when ut_per_sample), ut_act / ut_beta the branch activation, u1_w [2][32], u1_b[2]
  *   t_w [2][Ct], t_b [2]
  * Outputs (f32 NCHW): logits [N,3,2h,2w]; optional bgfg [N,2,2h,2w], tn [N,2,2h,2w]. */
 int hiseg_hier_combine_fwd(int dtype, const float* low, int N, int h, int w, const void* tfeat,
                            int Ct, const float* ut_w, const float* ut_scale, const float* ut_shift,
-                           int ut_act, const float* u1_w, const float* u1_b, const float* t_w,
-                           const float* t_b, float* logits, float* bgfg, float* tn,
-                           hiseg_stream_t stream);
+                           int ut_act, float ut_beta, int ut_per_sample, const float* u1_w,
+                           const float* u1_b, const float* t_w, const float* t_b, float* logits,
+                           float* bgfg, float* tn, hiseg_stream_t stream);
+/* upsample_bg_fg with LayerNorm2d (normalization_type 'layernorm2d', model.py:18-38): per-sample
+ * statistics of z = ConvTranspose2d(low) (+ bias) over (32, 2h, 2w) -> mean/invstd [N] (optional)
+ * and the folded tables scale/shift [N][32]: act(z * scale + shift) -- or, with fold_bias = 1, the
+ * tables for the bias-free ConvTranspose sum that hiseg_hier_combine_fwd takes with
+ * ut_per_sample = 1. */
+int hiseg_ubf_ln_tables(const float* low, int N, int h, int w, const float* ut_w, const float* ut_b,
+                        const float* gamma, const float* beta, float eps, int fold_bias, float* mean,
+                        float* invstd, float* scale, float* shift, hiseg_stream_t stream);
 
 /* NHWC(dtype, cstride, coff) -> NCHW f32 copy of C channels (aux outputs of the reference's
  * forward dict are NCHW f32). */

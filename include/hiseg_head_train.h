@@ -31,12 +31,13 @@ int hiseg_attn_spatial_bwd(int dtype, const void* x, int N, int H, int W, int C,
  * Saves gap [N][C], hpre [N][Cr] (pre-activation), gate [N][C]. */
 int hiseg_attn_channel_ws(int N, int C, int Cr);
 int hiseg_attn_channel_train_fwd(int dtype, const void* x, int N, int HW, int C, const float* w1, int Cr,
-                                 const float* w2, int act, const float* chan_mul, float* ws, float* gap, float* hpre,
-                                 float* gate, void* out, hiseg_stream_t stream);
+                                 const float* w2, int act, float act_beta, const float* chan_mul, float* ws, float* gap,
+                                 float* hpre, float* gate, void* out, hiseg_stream_t stream);
 /* dx written; dw1 [Cr][C] += ..., dw2 [C][Cr] += ... */
 int hiseg_attn_channel_bwd(int dtype, const void* x, int N, int HW, int C, const float* w1, int Cr, const float* w2,
-                           int act, const float* chan_mul, const float* gap, const float* hpre, const float* gate,
-                           const void* dout, void* dx, float* ws, float* dw1, float* dw2, hiseg_stream_t stream);
+                           int act, float act_beta, const float* chan_mul, const float* gap, const float* hpre,
+                           const float* gate, const void* dout, void* dx, float* ws, float* dw1, float* dw2,
+                           hiseg_stream_t stream);
 
 /* upsample_bg_fg [ConvTranspose2d(2,32,2,s2), BatchNorm2d(32) train, ReLU, Conv2d(32,2,1)],
  * softmax, the target branch's last Conv2d(Ct,2,1) and the hierarchical combine
@@ -45,7 +46,8 @@ int hiseg_attn_channel_bwd(int dtype, const void* x, int N, int HW, int C, const
  * low: f32 [N][h][w][2] (EnhancedUNet output); tfeat: [N][2h][2w][Ct] compute dtype;
  * logits/bgfg/tn: NCHW f32 [N][3|2|2][2h][2w].  The train forward computes the BN batch
  * statistics of the ConvTranspose output into mean/invstd/scale/shift (caller buffers of 32)
- * and updates the running statistics. */
+ * and updates the running statistics -- or, with layernorm = 1, the per-sample LayerNorm2d
+ * statistics (buffers of N and N*32, running_mean/var unused). */
 typedef struct hiseg_ubf_desc {
   int dtype;
   const float* low; int N, h, w;
@@ -55,11 +57,14 @@ typedef struct hiseg_ubf_desc {
   const float* u1_w; const float* u1_b;
   const void* tfeat; int Ct; const float* t_w; const float* t_b;
   float* logits; float* bgfg; float* tn;
+  int act; float act_beta;        /* branch activation (refinement.py:503): ReLU in every preset */
+  int layernorm;                  /* 0: BatchNorm2d(32) train (mean/invstd/scale/shift [32], running update);
+                                   * 1: LayerNorm2d (model.py:18-38): mean/invstd [N], scale/shift [N][32] */
 } hiseg_ubf_desc;
 typedef struct hiseg_ubf_grads {
   float* dut_w; float* dut_b; float* dgamma; float* dbeta; float* du1_w; float* du1_b;   /* accumulated */
 } hiseg_ubf_grads;
-int hiseg_ubf_ws(void);
+int hiseg_ubf_ws(int N);
 int hiseg_ubf_train_fwd(const hiseg_ubf_desc* d, float eps, float momentum, float* running_mean, float* running_var,
                         float* ws, hiseg_stream_t stream);
 /* dlogits: NCHW f32 gradient of logits; dbgfg_ext / dtn_ext: extra gradients of the bgfg / tn

@@ -80,6 +80,8 @@ typedef struct hiseg_bn_apply_desc {
   int act;
   const float* chan_mul;          /* [N][C] or null (Dropout2d mask, 0 or 1/(1-p)) */
   void* y; int y_cstride, y_coff;
+  float act_beta;                 /* Swish beta (act == HISEG_ACT_SWISH) */
+  int per_sample;                 /* scale / shift are [N][C] per-sample tables (LayerNorm2d), n = p / HW */
 } hiseg_bn_apply_desc;
 int hiseg_bn_apply(const hiseg_bn_apply_desc* d, hiseg_stream_t stream);
 
@@ -106,8 +108,47 @@ typedef struct hiseg_bn_bwd_desc {
    * ReLU mask is then recomputed from z as z*scale + shift > 0 -- exactly the forward's expression -- and
    * y is not read (one activation stream less in each pass) */
   const float* fwd_scale; const float* fwd_shift;
+  float act_beta;                 /* Swish beta */
+  /* the forward's residual input (optional): with fwd_scale / fwd_shift the activation derivative is taken at
+   * the forward's pre-activation z*fwd_scale + fwd_shift + residual -- required for GELU / Swish / SiLU / ReLU
+   * after a residual add; GELU and Swish always need fwd_scale / fwd_shift */
+  const void* residual; int r_cstride, r_coff;
 } hiseg_bn_bwd_desc;
 int hiseg_bn_bwd(const hiseg_bn_bwd_desc* d, hiseg_stream_t stream);
+
+/* ----------------------------------------------------------------------------------------
+ * Train-mode LayerNorm2d (model.py:18-38, normalization_type 'layernorm2d' of
+ * advanced/normalization_comparison.py:159-206): per sample n, mean and biased variance of the
+ * conv output z over (C, H, W), eps 1e-5; no running statistics.
+ *   hiseg_ln_fwd_stats: mean/invstd [N] and the folded per-sample tables scale/shift [N][C]
+ *     (scale = w_c * invstd_n, shift = b_c - mean_n * scale); the output is then
+ *     hiseg_bn_apply with per_sample = 1 (+ residual, act, Dropout2d mask).
+ *   hiseg_ln_bwd: g = dy * chan_mul * act'(z*scale + shift [+ residual]), xhat = (z - mean_n)*invstd_n,
+ *     dz = invstd_n * (w_c g - a_n - xhat b_n) with a_n = mean over (C,H,W) of w_c g and
+ *     b_n = mean of w_c g xhat; dw (+)= sum g xhat, db (+)= sum g, dconv_bias (+)= sum dz,
+ *     dres (+)= g.
+ * ws: hiseg_ln_ws(N, HW, C) floats, 16-B aligned (shared by the two calls of one layer).
+ * -------------------------------------------------------------------------------------- */
+long long hiseg_ln_ws(int N, int HW, int C);
+int hiseg_ln_fwd_stats(int dtype, const void* z, int N, int HW, int C, int cstride, int coff, const float* gamma,
+                       const float* beta, float eps, float* ws, float* mean, float* invstd, float* scale, float* shift,
+                       hiseg_stream_t stream);
+typedef struct hiseg_ln_bwd_desc {
+  int dtype; int N, HW, C;
+  const void* dy; int dy_cstride, dy_coff;
+  const void* z; int z_cstride, z_coff;
+  const void* residual; int r_cstride, r_coff;
+  const float* chan_mul;          /* [N][C] or null */
+  int act; float act_beta;
+  const float* mean; const float* invstd;   /* [N] */
+  const float* scale; const float* shift;   /* [N][C] forward tables */
+  const float* gamma;
+  float* dgamma; float* dbeta; float* dconv_bias; int accumulate_params;
+  void* dz; int dz_cstride, dz_coff;
+  void* dres; int dres_cstride, dres_coff; int dres_accumulate;
+  float* ws;
+} hiseg_ln_bwd_desc;
+int hiseg_ln_bwd(const hiseg_ln_bwd_desc* d, hiseg_stream_t stream);
 
 /* Dropout2d mask (nn.Dropout2d in refinement.py:484,486,519,525,540): per (n, c) 0 with
  * probability p else 1/(1-p), from a counter-based hash of (seed, n*C + c). */
@@ -135,6 +176,10 @@ int hiseg_gate_bwd(int dtype, long long P, int C, hiseg_ew_view dy, hiseg_ew_vie
 int hiseg_act_bwd_cvt(int dtype, long long P, int C, hiseg_ew_view dy, hiseg_ew_view y, int act, hiseg_ew_view dz,
                       int accumulate, hiseg_stream_t stream);
 int hiseg_add_inplace(int dtype, long long P, int C, hiseg_ew_view dst, hiseg_ew_view src, hiseg_stream_t stream);
+/* dz (+= if accumulate) = dy * act'(z) at the pre-activation z (compute dtype views): the backward of an
+ * activation applied without normalisation (GELU / Swish(act_beta) / SiLU after a plain conv). */
+int hiseg_act_bwd_pre(int dtype, long long P, int C, hiseg_ew_view dy, hiseg_ew_view z, int act, float act_beta,
+                      hiseg_ew_view dz, int accumulate, hiseg_stream_t stream);
 
 /* MaxPool2d(2) backward (EnhancedUNet, hierarchical_segmentation_unet.py:366,384): dx (+)= dy
  * routed to the first maximum of each 2x2 window (PyTorch's tie rule). */

@@ -27,9 +27,20 @@ def conv(sd: SD, p: str, x, stride=1, pad=None):
     return F.conv2d(x, w, b, stride=stride, padding=pad)
 
 
+def layernorm2d(sd: SD, p: str, x, eps=1e-5):
+    """LayerNorm2d (src/human_edge_detection/model.py:18-38): per-sample mean / biased variance over
+    (C, H, W), weight / bias [1, C, 1, 1].  Same in train and eval (no running statistics)."""
+    mean = x.mean(dim=(1, 2, 3), keepdim=True)
+    var = x.var(dim=(1, 2, 3), keepdim=True, unbiased=False)
+    return (x - mean) / torch.sqrt(var + eps) * sd[p + ".weight"] + sd[p + ".bias"]
+
+
 def bn(sd: SD, p: str, x, eps=1e-5):
-    """nn.BatchNorm2d (advanced/normalization_comparison.py:181-182): running statistics (eval), or
-    batch statistics + running-stat update inside oracle.train.train_mode()."""
+    """The normalisation layer of get_normalization_layer (advanced/normalization_comparison.py:159-206):
+    nn.BatchNorm2d (:181-182) with running statistics (eval), or batch statistics + running-stat update
+    inside oracle.train.train_mode(); 'layernorm2d' (no running statistics in the state) -> layernorm2d."""
+    if p + ".running_mean" not in sd:
+        return layernorm2d(sd, p, x, eps)
     from . import train as _T
     if _T.is_train():
         return _T.bn_train(sd, p, x, eps)
@@ -38,7 +49,10 @@ def bn(sd: SD, p: str, x, eps=1e-5):
 
 
 def act(x, kind: str, beta: float = 1.0):
-    """advanced/activation_utils.py:71-101."""
+    """advanced/activation_utils.py:71-101.  kind may carry Swish's beta as 'swish:<beta>' (cfg_from_kwargs)."""
+    if ":" in kind:
+        kind, b = kind.split(":")
+        beta = float(b)
     if kind == "relu":
         return F.relu(x)
     if kind == "silu" or (kind == "swish" and beta == 1.0):
@@ -48,6 +62,12 @@ def act(x, kind: str, beta: float = 1.0):
     if kind == "gelu":
         return F.gelu(x)
     raise ValueError(kind)
+
+
+def plain(a: str) -> str:
+    """The activation of get_activation_function in unet.py:13-32 / rgb.py:21-40: 'swish' -> nn.SiLU
+    (Swish's beta dropped), unlike activation_utils.get_activation used by the refinement modules."""
+    return a.split(":")[0]
 
 
 def residual(sd: SD, p: str, x, a: str):
@@ -69,18 +89,21 @@ def roi_align(feat: torch.Tensor, rois: torch.Tensor, oh: int, ow: int, scale_h,
 
 # ---------------------------------------------------------------------------------------- ROI path
 def rgb_feature_extractor(sd: SD, p: str, x, a: str):
-    """advanced/hierarchical_segmentation_rgb.py:657-673."""
-    x = act(bn(sd, p + ".1", conv(sd, p + ".0", x)), a)
+    """advanced/hierarchical_segmentation_rgb.py:657-673 (stand-alone activations from rgb.py:21-40,
+    the residual blocks are refinement.py's with get_activation)."""
+    x = act(bn(sd, p + ".1", conv(sd, p + ".0", x)), plain(a))
     x = residual(sd, p + ".3", x, a)
-    x = act(bn(sd, p + ".5", conv(sd, p + ".4", x)), a)
+    x = act(bn(sd, p + ".5", conv(sd, p + ".4", x)), plain(a))
     x = residual(sd, p + ".7", x, a)
-    x = act(bn(sd, p + ".9", conv(sd, p + ".8", x)), a)
+    x = act(bn(sd, p + ".9", conv(sd, p + ".8", x)), plain(a))
     x = residual(sd, p + ".11", x, a)
-    return act(bn(sd, p + ".13", conv(sd, p + ".12", x)), a)
+    return act(bn(sd, p + ".13", conv(sd, p + ".12", x)), plain(a))
 
 
 def enhanced_unet(sd: SD, p: str, x, depth: int, a: str):
-    """EnhancedUNet.forward, advanced/hierarchical_segmentation_unet.py:375-417."""
+    """EnhancedUNet.forward, advanced/hierarchical_segmentation_unet.py:375-417 (every activation from
+    unet.py's get_activation_function)."""
+    a = plain(a)
     feats = []
     for i in range(depth):
         e = f"{p}.encoders.{i}"
@@ -213,6 +236,8 @@ def cfg_from_kwargs(kw: dict) -> dict:
         return (int(v[0]), int(v[1])) if isinstance(v, (list, tuple)) else (int(v), int(v))
     c = dict(kw)
     c["roi_hw"], c["mask_hw"] = hw(kw["roi_size"]), hw(kw["mask_size"])
+    if c.get("activation_function") == "swish" and float(c.get("activation_beta", 1.0)) != 1.0:
+        c["activation_function"] = f"swish:{float(c['activation_beta'])}"
     return c
 
 

@@ -202,7 +202,55 @@ def gen_state_keys(kw):
     print("state keys", len(keys))
 
 
-if __name__ == "__main__":
+# Normalisation / activation variants of the factory (normalization_comparison.py:159-206,
+# activation_utils.py:71-101): the presets all use batchnorm + relu; these pin layernorm2d, GELU and
+# Swish(beta != 1) on the same modules.  `python tests/golden/gen_golden.py variants` -> variants.npz
+VARIANTS = {"ln_gelu": ("layernorm2d", "gelu", 1.0), "bn_swish": ("batchnorm", "swish", 1.5),
+            "ln_swish": ("layernorm2d", "swish", 0.75)}
+
+
+def small_head_kwargs(norm, act, beta):
+    return dict(in_channels=64, mid_channels=64, num_classes=3, mask_size=(32, 24), use_attention_module=True,
+                use_contour_detection=True, use_distance_transform=True, normalization_type=norm,
+                normalization_groups=8, activation_function=act, activation_beta=beta,
+                hierarchical_base_channels=32, hierarchical_depth=3)
+
+
+def gen_variants(kw):
+    out = {}
+    x = torch.from_numpy(filler.normal(61, (2, 64, 12, 10)))
+    xu = torch.from_numpy(filler.normal(62, (2, 64, 16, 12)))
+    xh = torch.from_numpy(filler.normal(63, (2, 64, 16, 12)))
+    for key, (norm, act, beta) in VARIANTS.items():
+        blk = filler.fill_module(R.ResidualBlock(64, norm, 8, act, beta)).eval()
+        unet = filler.fill_module(U.EnhancedUNet(64, base_channels=32, depth=3, normalization_type=norm,
+                                                 normalization_groups=8, activation_function=act,
+                                                 activation_beta=beta)).eval()
+        head = filler.fill_module(R.RefinedHierarchicalSegmentationHead(**small_head_kwargs(norm, act, beta))).eval()
+        with torch.no_grad():
+            out[f"{key}_res_y"] = blk(x)
+            out[f"{key}_unet_y"] = unet(xu)
+            logits, aux = head(xh)
+        out[f"{key}_head_logits"] = logits
+        summarize(f"{key}_head_aux_", aux, out)
+    # the whole ROI path (rgb_feature_extractor, feature_combiner, full-size head) with layernorm2d + GELU
+    mkw = dict(kw, normalization_type="layernorm2d", activation_function="gelu")
+    model = build_ref_model(mkw)
+    images = torch.from_numpy(filler.uniform(64, (2, 3, 96, 128)))
+    u = torch.from_numpy(filler.normal(65, (2, 1, 96, 128)) * 2.0)
+    rois = torch.tensor([[0, .10, .10, .40, .90], [1, .35, .15, .80, .95]], dtype=torch.float32)
+    for m in (model.roi_align_mask, model.roi_align_rgb):
+        m.spatial_scale, m.spatial_scale_h, m.spatial_scale_w = (96, 128), 96, 128
+    _InjectedUnet.injected = u
+    with torch.no_grad():
+        logits, _ = model(images, rois)
+    out.update(model_images=images, model_u=u, model_rois=rois, model_logits=logits)
+    save("variants", **out)
+
+
+if __name__ == "__main__" and sys.argv[1:] == ["variants"]:
+    gen_variants(gen_configs()["b0"]["model_kwargs"])
+elif __name__ == "__main__":
     cfgs = gen_configs()
     kw = cfgs["b0"]["model_kwargs"]
     gen_roi_align()

@@ -145,3 +145,35 @@ def test_instance_and_binary_mask_semantics():
     logits = torch.tensor([[[[0.0, 1.0]], [[1.0, 1.0]], [[0.5, 1.0]]]])  # ties resolve to the first index
     m = O.instance_masks(logits)
     assert m.tolist() == [[[[1.0, 0.0]]]]
+
+
+@pytest.mark.parametrize("key", ["ln_gelu", "bn_swish", "ln_swish"])
+def test_norm_act_variants_match_reference(key):
+    """LayerNorm2d (model.py:18-38), GELU and Swish(beta) (activation_utils.py:71-101) in the residual
+    block, EnhancedUNet and the refined head, against the reference's own outputs."""
+    from helpers import VARIANTS, act_tag, small_head_cfg, variant_modules
+    norm, act, beta = VARIANTS[key]
+    g = load("variants")
+    blk, unet, head = variant_modules(norm, act, beta)
+    a = act_tag(act, beta)
+    with torch.no_grad():
+        y = O.residual({"b." + k: v for k, v in O.np_state(blk).items()}, "b",
+                       torch.from_numpy(filler.normal(61, (2, 64, 12, 10))), a)
+        assert max_abs(y, g[f"{key}_res_y"]) < 1e-5
+        y = O.enhanced_unet({"u." + k: v for k, v in O.np_state(unet).items()}, "u",
+                            torch.from_numpy(filler.normal(62, (2, 64, 16, 12))), 3, a)
+        assert max_abs(y, g[f"{key}_unet_y"]) < 1e-4
+        logits, aux = O.hier_head({"h." + k: v for k, v in O.np_state(head).items()}, "h",
+                                  torch.from_numpy(filler.normal(63, (2, 64, 16, 12))), small_head_cfg(norm, act, beta))
+    assert max_abs(logits, g[f"{key}_head_logits"]) < 2e-4 * float(np.abs(g[f"{key}_head_logits"]).max())
+    check_aux(aux, g, prefix=f"{key}_head_aux_")
+
+
+def test_layernorm_gelu_model_matches_reference():
+    kw = dict(b0_kwargs(), normalization_type="layernorm2d", activation_function="gelu")
+    g = load("variants")
+    sd = O.np_state(_hiseg_model(kw))
+    with torch.no_grad():
+        logits, _ = O.rgb_model_from_unet(sd, torch.from_numpy(g["model_images"]), torch.from_numpy(g["model_rois"]),
+                                          torch.from_numpy(g["model_u"]), O.cfg_from_kwargs(kw), (96, 128))
+    assert max_abs(logits, g["model_logits"]) < 2e-4 * float(np.abs(g["model_logits"]).max())
