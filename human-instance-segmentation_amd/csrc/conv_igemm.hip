@@ -260,7 +260,7 @@ extern "C" int hiseg_conv2d_fwd(const hiseg_conv2d_desc* d, hiseg_stream_t strea
 // -DHISEG_DIAG build (Makefile DIAG=1).
 static bool release_variant(int v) {
   return v == -1 || v == 0 || (v >= 1 && v <= 8) || v == 50 || v == 51 || v == 52 || v == 54 || v == 58 ||
-         (v >= 60 && v <= 69) || v == 70 || v == 71 || v == 72;
+         (v >= 60 && v <= 69) || v == 70 || v == 71 || v == 72 || v == 74;
 }
 
 extern "C" int hiseg_conv2d_fwd_variant(const hiseg_conv2d_desc* d, int variant, hiseg_stream_t stream) {

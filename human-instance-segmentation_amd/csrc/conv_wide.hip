@@ -467,6 +467,12 @@ static int launch_wide(const ConvArgs& a, hipStream_t s) {
   return hiseg_check_launch("conv_wide");
 }
 
+// Automatic BCO-256 configuration: 70 = tap-major K order (bit-identical to the generic kernel), 74 =
+// channel-major K order (the 9 taps of a 32-channel slice back to back: 0.42x the L2 fetch of 70).
+#ifndef HISEG_WIDE_AUTO
+#define HISEG_WIDE_AUTO 70
+#endif
+
 // Returns 1 if launched, 0 if the layer does not qualify (caller falls back), <0 on error.
 // variant 0 = automatic (BCO 256 when 256 | Cout_pad, else 128), 70 = BCO 256, 72 = BCO 128.
 int conv_wide_try(const ConvArgs& a, hipStream_t s, int variant) {
@@ -487,7 +493,7 @@ int conv_wide_try(const ConvArgs& a, hipStream_t s, int variant) {
   const long long span_w = (long long)d.Cout_pad * d.K_pad * 2;
   const long long span_r = d.residual ? (long long)a.M * d.r_cstride * 2 : 0;
   if (span_a >= 0x7fffffffll || span_b >= 0x7fffffffll || span_w >= 0x7fffffffll || span_r >= 0x7fffffffll) return 0;
-  if (variant == 0) variant = (d.Cout % 256 == 0) ? 70 : 72;
+  if (variant == 0) variant = (d.Cout % 256 == 0) ? HISEG_WIDE_AUTO : 72;
   int r;
   switch (variant) {
     case 70: if (d.Cout % 256) return 0; r = launch_wide<256>(a, s); break;
@@ -504,8 +510,8 @@ int conv_wide_try(const ConvArgs& a, hipStream_t s, int variant) {
       if (d.Cout % 256) return 0;
       r = launch_wide<256, true>(a, s);
       break;
-    case 74: if (d.Cout % 256) return 0; r = launch_wide<256, false, 0, true>(a, s); break;   // channel-major K
 #endif
+    case 74: if (d.Cout % 256) return 0; r = launch_wide<256, false, 0, true>(a, s); break;   // channel-major K
     case 71: if (d.Cout % 256) return 0; r = launch_wide<256, false, 0, false, 5>(a, s); break;   // 5-deep ring
     default: return 0;
   }

@@ -248,7 +248,61 @@ def gen_variants(kw):
     save("variants", **out)
 
 
-if __name__ == "__main__" and sys.argv[1:] == ["variants"]:
+def _import_export_script():
+    """export_hierarchical_instance_peopleseg_onnx (reference root) for MaskDilationModule / ModelWithDilation.
+    Its import chain (export_onnx_advanced, train_advanced) pulls in packages absent from this image -- onnx,
+    onnxruntime, tensorboard, pycocotools, cv2, seaborn -- none of which the dilation path executes: they are
+    stubbed as empty modules for the import only."""
+    class _Stub(types.ModuleType):
+        def __getattr__(self, k):
+            if k.startswith("__"):
+                raise AttributeError(k)
+            return type(k, (), {"__init__": lambda s, *a, **kw: None})
+
+    for name in ("onnx", "onnxruntime", "onnxsim", "pycocotools", "pycocotools.coco", "pycocotools.mask", "cv2",
+                 "seaborn", "torch.utils.tensorboard"):
+        if name not in sys.modules:
+            m = _Stub(name)
+            m.__path__ = []
+            sys.modules[name] = m
+    import export_hierarchical_instance_peopleseg_onnx as E  # noqa: E402
+    return E
+
+
+def gen_export(kw):
+    """ModelWithDilation (export_hierarchical_instance_peopleseg_onnx.py:144-181) around the reference model at
+    dilation 0 / 1 / 2, the instance masks of the export wrapper (export_onnx_advanced.py:358-362: argmax == 1)
+    and its binary masks (:374-387: softmax of pretrained_unet(images), channel 0); MaskDilationModule alone on
+    synthetic logits with larger radii."""
+    E = _import_export_script()
+    model = build_ref_model(kw)
+    images = torch.from_numpy(filler.uniform(71, (2, 3, 96, 128)))
+    u = torch.from_numpy(filler.normal(72, (2, 1, 96, 128)) * 2.0)
+    rois = torch.from_numpy(filler.box_rois(73, 2, 3))
+    for m in (model.roi_align_mask, model.roi_align_rgb):
+        m.spatial_scale, m.spatial_scale_h, m.spatial_scale_w = (96, 128), 96, 128
+    _InjectedUnet.injected = u
+    out = dict(rois=rois)   # images / u are regenerated from the filler seeds by the tests
+    with torch.no_grad():
+        for d in (0, 1, 2):
+            o = E.ModelWithDilation(model, d)(images, rois)
+            masks = o[0] if isinstance(o, tuple) else o
+            if d == 0:
+                out["d0_logits"] = masks
+            out[f"d{d}_instance"] = (torch.argmax(masks, dim=1, keepdim=True) == 1).to(torch.uint8)
+        pu = model.pretrained_unet(images)
+        pu = pu[0] if isinstance(pu, tuple) else pu
+        out["binary"] = torch.softmax(pu, dim=1)[:, 0:1]
+        z = torch.from_numpy(filler.normal(74, (3, 3, 20, 16)) * 3.0)
+        out["syn_logits"] = z
+        for d in (1, 2, 3):
+            out[f"syn_d{d}"] = E.MaskDilationModule(d)(z)
+    save("export", **out)
+
+
+if __name__ == "__main__" and sys.argv[1:] == ["export"]:
+    gen_export(gen_configs()["b0"]["model_kwargs"])
+elif __name__ == "__main__" and sys.argv[1:] == ["variants"]:
     gen_variants(gen_configs()["b0"]["model_kwargs"])
 elif __name__ == "__main__":
     cfgs = gen_configs()

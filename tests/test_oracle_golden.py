@@ -177,3 +177,30 @@ def test_layernorm_gelu_model_matches_reference():
         logits, _ = O.rgb_model_from_unet(sd, torch.from_numpy(g["model_images"]), torch.from_numpy(g["model_rois"]),
                                           torch.from_numpy(g["model_u"]), O.cfg_from_kwargs(kw), (96, 128))
     assert max_abs(logits, g["model_logits"]) < 2e-4 * float(np.abs(g["model_logits"]).max())
+
+
+def test_export_dilation_matches_reference():
+    """MaskDilationModule / ModelWithDilation (export_hierarchical_instance_peopleseg_onnx.py:85-181) at
+    dilation 0 / 1 / 2 and the export wrapper's instance / binary masks (export_onnx_advanced.py:358-387),
+    against the reference's own outputs (tests/golden/export.npz)."""
+    kw = b0_kwargs()
+    g = load("export")
+    for d in (1, 2, 3):
+        z = torch.from_numpy(g["syn_logits"])
+        ref = torch.from_numpy(g[f"syn_d{d}"])
+        mine = O.instance_masks(z, d)
+        assert torch.equal(mine, (ref.argmax(1, keepdim=True) == 1).float()), d
+    logits0 = torch.from_numpy(g["d0_logits"])
+    for d in (0, 1, 2):
+        assert torch.equal(O.instance_masks(logits0, d), torch.from_numpy(g[f"d{d}_instance"]).float()), d
+    # the whole path from the injected UNet map to the dilated masks and the binary masks
+    sd = O.np_state(_hiseg_model(kw))
+    images = torch.from_numpy(filler.uniform(71, (2, 3, 96, 128)))
+    u = torch.from_numpy(filler.normal(72, (2, 1, 96, 128)) * 2.0)
+    with torch.no_grad():
+        logits, _ = O.rgb_model_from_unet(sd, images, torch.from_numpy(g["rois"]), u, O.cfg_from_kwargs(kw), (96, 128))
+        assert max_abs(logits, logits0) < 2e-4 * float(np.abs(g["d0_logits"]).max())
+        for d in (0, 1, 2):
+            agree = (O.instance_masks(logits, d) == torch.from_numpy(g[f"d{d}_instance"]).float()).float().mean()
+            assert agree.item() > 0.999, d
+        assert max_abs(O.binary_masks(sd, u), g["binary"]) < 1e-5
