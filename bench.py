@@ -183,6 +183,7 @@ def train_bench(device, dtype, rank, world, dist, steps, warmup, preset=None, ba
         local = steps / el
     if world > 1:
         HD.enable_grad_sync(model)
+        HD.sync_loss_class_weights(loss_fn)   # class weights from the counts of the whole (all-rank) batch
     elapsed, first, last = timed()
     sps = steps / elapsed
     gflop = GFLOP_PER_TRAIN_ROI if preset is None else GFLOP_PER_TRAIN_SAMPLE[preset]

@@ -138,12 +138,22 @@ __global__ void __launch_bounds__(256) loss_dist_kernel(const float* d, int N, i
 
 __device__ __forceinline__ double clampd(double v, double lo, double hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
-__global__ void loss_weights_kernel(hiseg_loss_cfg cfg, const float* cnt, int nblk, double* st, float* coef) {
+// the 4 class pixel counts (bg, fg, target, non-target) of this batch -> counts[4]
+__global__ void loss_counts_kernel(const float* cnt, int nblk, double* counts) {
   if (threadIdx.x != 0) return;
   double c[4] = {0, 0, 0, 0};
   for (int b = 0; b < nblk; ++b)
     for (int k = 0; k < 4; ++k) c[k] += cnt[b * 4 + k];
-  const double bg = c[0], fg = c[1], tc = c[2], nt = c[3];
+  for (int k = 0; k < 4; ++k) counts[k] = c[k];
+}
+
+// class weights + EMA update from counts (this batch's, or their all-reduced sum over data-parallel ranks);
+// local_fg = this batch's foreground count (the loss terms' own normalisation)
+__global__ void loss_weights_kernel(hiseg_loss_cfg cfg, const double* counts, const double* local, double* st,
+                                    float* coef) {
+  if (threadIdx.x != 0) return;
+  const double bg = counts[0], fg = counts[1], tc = counts[2], nt = counts[3];
+  const double fg_local = local[1];
   float wb0, wb1;
   if (cfg.use_dynamic_weights) {
     const double tot = bg + fg;
@@ -172,7 +182,7 @@ __global__ void loss_weights_kernel(hiseg_loss_cfg cfg, const float* cnt, int nb
     }
   }
   coef[C_WTN0] = wt0; coef[C_WTN1] = wt1; coef[C_TNACT] = active;
-  coef[C_FGCNT] = (float)fg;
+  coef[C_FGCNT] = (float)fg_local;
   st[7] += 1.0;
 }
 
@@ -426,7 +436,12 @@ extern "C" int hiseg_loss_state_init(double* state, hiseg_stream_t stream) {
 
 extern "C" long long hiseg_loss_ws(int N, int H, int W) {
   const long long NP = (long long)N * H * W;
-  return 5 * NP + kCntBlocks * 4 + (long long)N * kSpl * kNS + kCoef + 2LL * N;
+  return 5 * NP + kCntBlocks * 4 + (long long)N * kSpl * kNS + kCoef + 2LL * N + 10;   // + local counts (double[4])
+}
+
+static double* local_counts(float* ws, int N, int H, int W) {   // after the partials, 8-B aligned (ws is)
+  const long long n = hiseg_loss_ws(N, H, W) - 10;
+  return reinterpret_cast<double*>(ws + ((n + 1) & ~1LL));
 }
 
 extern "C" int hiseg_loss_fwd(const hiseg_loss_cfg* cfg, int N, int H, int W, const float* pred, const float* bgfg,
@@ -436,10 +451,22 @@ extern "C" int hiseg_loss_fwd(const hiseg_loss_cfg* cfg, int N, int H, int W, co
                 HISEG_ERR_BAD_ARG, "loss_fwd: bad arguments");
   HISEG_REQUIRE(!cfg->use_contour || cont, HISEG_ERR_BAD_ARG, "loss_fwd: contour term needs cont");
   HISEG_REQUIRE(!cfg->use_distance || dist, HISEG_ERR_BAD_ARG, "loss_fwd: distance term needs dist");
+  int r = hiseg_loss_fwd_begin(cfg, N, H, W, targets, ws, nullptr, stream);
+  if (r) return r;
+  return hiseg_loss_fwd_end(cfg, N, H, W, pred, bgfg, tn, cont, dist, targets, nullptr, state, ws, out, stream);
+}
+
+extern "C" int hiseg_loss_fwd_begin(const hiseg_loss_cfg* cfg, int N, int H, int W, const long long* targets, float* ws,
+                                    double* counts, hiseg_stream_t stream) {
+  HISEG_REQUIRE(cfg && targets && ws && N > 0 && H > 0 && W > 0, HISEG_ERR_BAD_ARG, "loss_fwd_begin: bad arguments");
+  HISEG_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 7) == 0, HISEG_ERR_BAD_ARG, "loss_fwd_begin: ws alignment");
   hipStream_t s = (hipStream_t)stream;
   const long long NP = (long long)N * H * W;
   LossWS w = loss_ws(ws, N, NP);
+  double* lc = local_counts(ws, N, H, W);
   hipLaunchKernelGGL(loss_targets_kernel, dim3(kCntBlocks), dim3(256), 0, s, targets, N, H, W, w.bw, w.craw, w.dA, w.cnt);
+  hipLaunchKernelGGL(loss_counts_kernel, dim3(1), dim3(64), 0, s, w.cnt, kCntBlocks, lc);
+  if (counts) (void)hipMemcpyAsync(counts, lc, 4 * sizeof(double), hipMemcpyDeviceToDevice, s);
   if (cfg->use_contour)
     hipLaunchKernelGGL(loss_contour_kernel, dim3(gblocks(NP)), dim3(256), 0, s, w.craw, N, H, W, cfg->contour_ks, w.ct);
   if (cfg->use_distance) {
@@ -449,7 +476,19 @@ extern "C" int hiseg_loss_fwd(const hiseg_loss_cfg* cfg, int N, int H, int W, co
       hipLaunchKernelGGL(loss_dist_kernel, dim3(gblocks(NP)), dim3(256), 0, s, src, N, H, W, dst);
     }
   }
-  hipLaunchKernelGGL(loss_weights_kernel, dim3(1), dim3(64), 0, s, *cfg, w.cnt, kCntBlocks, state, w.coef);
+  return hiseg_check_launch("loss_fwd_begin");
+}
+
+extern "C" int hiseg_loss_fwd_end(const hiseg_loss_cfg* cfg, int N, int H, int W, const float* pred, const float* bgfg,
+                                  const float* tn, const float* cont, const float* dist, const long long* targets,
+                                  const double* counts, double* state, float* ws, float* out, hiseg_stream_t stream) {
+  HISEG_REQUIRE(cfg && pred && bgfg && tn && targets && state && ws && out && N > 0 && H > 0 && W > 0,
+                HISEG_ERR_BAD_ARG, "loss_fwd_end: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  const long long NP = (long long)N * H * W;
+  LossWS w = loss_ws(ws, N, NP);
+  const double* lc = local_counts(ws, N, H, W);
+  hipLaunchKernelGGL(loss_weights_kernel, dim3(1), dim3(64), 0, s, *cfg, counts ? counts : lc, lc, state, w.coef);
   hipLaunchKernelGGL(loss_main_kernel, dim3(kSpl, N), dim3(256), 0, s, *cfg, N, H, W, pred, bgfg, tn, cont, dist,
                      targets, w);
   hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, *cfg, N, H, W, w, state, out);

@@ -262,6 +262,9 @@ def _declare(lib):
         "hiseg_loss_state_init": ([P, P], c_int),
         "hiseg_loss_ws": ([c_int, c_int, c_int], c_ll),
         "hiseg_loss_fwd": ([ctypes.POINTER(LossCfg), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P], c_int),
+        "hiseg_loss_fwd_begin": ([ctypes.POINTER(LossCfg), c_int, c_int, c_int, P, P, P, P], c_int),
+        "hiseg_loss_fwd_end": ([ctypes.POINTER(LossCfg), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P],
+                               c_int),
         "hiseg_loss_bwd": ([ctypes.POINTER(LossCfg), c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
                            c_int),
         "hiseg_distill_ws": ([c_int, c_int, c_int], c_ll),

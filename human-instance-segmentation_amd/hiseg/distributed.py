@@ -130,6 +130,24 @@ def enable_grad_sync(model: nn.Module, process_group=None, bucket_mb: float = 25
     return sync
 
 
+def all_reduce_counts(counts: torch.Tensor, process_group=None) -> torch.Tensor:
+    """Sum a count vector over the process group in place (float64; RCCL on the GPU, gloo on the CPU)."""
+    dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=process_group)
+    return counts
+
+
+def sync_loss_class_weights(loss_fn: nn.Module, process_group=None) -> nn.Module:
+    """Data-parallel semantics of the loss's dynamic class weights (hierarchical_segmentation.py:227-255,
+    286-309): the reference derives them (and their EMA) from the class pixel counts of the whole batch, which
+    under data parallelism is spread over the ranks.  With this, every rank's RefinedHierarchicalLoss
+    all-reduces its 4 counts (bg, fg, target, non-target) before the EMA update, so all ranks carry the
+    weights a single process would compute on the concatenated batch."""
+    if not dist.is_initialized():
+        raise RuntimeError("hiseg.distributed: torch.distributed is not initialised")
+    loss_fn.count_sync = lambda c: all_reduce_counts(c, process_group)
+    return loss_fn
+
+
 def grad_sync_of(model: nn.Module) -> Optional[GradBucketSync]:
     return model.__dict__.get(_SYNC_KEY)
 

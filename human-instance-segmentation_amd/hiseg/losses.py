@@ -78,10 +78,20 @@ class _LossFunction(torch.autograd.Function):
         ws = torch.empty(int(lib.hiseg_loss_ws(N, H, W)), dtype=torch.float32, device=dev)
         out = torch.empty(L.LOSS_NOUT + 1, dtype=torch.float32, device=dev)
         st = handle["state"]
-        L.check(lib.hiseg_loss_fwd(ctypes.byref(cfg), N, H, W, pred.data_ptr(), bgfg.data_ptr(), tn.data_ptr(),
-                                   cont.data_ptr() if cont is not None else None,
-                                   dist.data_ptr() if dist is not None else None, target.data_ptr(), st.data_ptr(),
-                                   ws.data_ptr(), out.data_ptr(), L.stream_ptr()), "loss_fwd")
+        counts = None
+        if handle.get("count_sync") is not None:   # data parallel: class weights from the counts of all ranks
+            counts = torch.empty(4, dtype=torch.float64, device=dev)
+            L.check(lib.hiseg_loss_fwd_begin(ctypes.byref(cfg), N, H, W, target.data_ptr(), ws.data_ptr(),
+                                             counts.data_ptr(), L.stream_ptr()), "loss_fwd_begin")
+            handle["count_sync"](counts)
+        else:
+            L.check(lib.hiseg_loss_fwd_begin(ctypes.byref(cfg), N, H, W, target.data_ptr(), ws.data_ptr(), None,
+                                             L.stream_ptr()), "loss_fwd_begin")
+        L.check(lib.hiseg_loss_fwd_end(ctypes.byref(cfg), N, H, W, pred.data_ptr(), bgfg.data_ptr(), tn.data_ptr(),
+                                       cont.data_ptr() if cont is not None else None,
+                                       dist.data_ptr() if dist is not None else None, target.data_ptr(),
+                                       counts.data_ptr() if counts is not None else None, st.data_ptr(),
+                                       ws.data_ptr(), out.data_ptr(), L.stream_ptr()), "loss_fwd")
         ctx.save_for_backward(pred, bgfg, tn, cont, dist, target, ws)
         ctx.cfg = cfg
         ctx.mark_non_differentiable(out)
@@ -130,6 +140,7 @@ class RefinedHierarchicalLoss(nn.Module):
         self.auto_adjust_contour_weight = auto_adjust_contour_weight
         self.base_resolution = base_mask_size[0] * base_mask_size[1]
         self._state: Optional[torch.Tensor] = None   # device EMA state (double[8])
+        self.count_sync = None   # callable(counts double[4]) summing the class pixel counts over ranks, or None
 
     def _cfg(self, H: int, W: int, has_c: bool, has_d: bool) -> Tuple[L.LossCfg, Optional[float]]:
         c = L.LossCfg()
@@ -168,7 +179,7 @@ class RefinedHierarchicalLoss(nn.Module):
 
         def f32(t):
             return None if t is None else t.float().contiguous()
-        handle = {"cfg": cfg, "state": self._state}
+        handle = {"cfg": cfg, "state": self._state, "count_sync": self.count_sync}
         total, out = _LossFunction.apply(handle, f32(pred), f32(aux["bg_fg_logits"]),
                                          f32(aux["target_nontarget_logits"]), f32(cont), f32(dist),
                                          target.to(device=pred.device, dtype=torch.int64).contiguous())

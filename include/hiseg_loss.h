@@ -40,6 +40,17 @@ long long hiseg_loss_ws(int N, int H, int W);
 int hiseg_loss_fwd(const hiseg_loss_cfg* cfg, int N, int H, int W, const float* pred, const float* bgfg,
                    const float* tn, const float* cont, const float* dist, const long long* targets, double* state,
                    float* ws, float* out, hiseg_stream_t stream);
+/* hiseg_loss_fwd in two phases, for data-parallel training: _begin rasterises the per-pixel targets and
+ * writes this batch's 4 class pixel counts (bg, fg, target, non-target; double[4], optional) -- the caller
+ * all-reduces them over the ranks -- and _end updates the dynamic class weights' EMA from `counts` (null:
+ * this batch's own counts, i.e. hiseg_loss_fwd) before the loss terms (hierarchical_segmentation.py:227-255,
+ * 286-309: the weights come from the counts of the whole batch, which under data parallelism spans the
+ * ranks).  Same ws for both phases and for hiseg_loss_bwd. */
+int hiseg_loss_fwd_begin(const hiseg_loss_cfg* cfg, int N, int H, int W, const long long* targets, float* ws,
+                         double* counts, hiseg_stream_t stream);
+int hiseg_loss_fwd_end(const hiseg_loss_cfg* cfg, int N, int H, int W, const float* pred, const float* bgfg,
+                       const float* tn, const float* cont, const float* dist, const long long* targets,
+                       const double* counts, double* state, float* ws, float* out, hiseg_stream_t stream);
 /* Gradients (written, NCHW f32, same shapes) of grad_out[0] * total; any output may be null. Uses the
  * coefficients hiseg_loss_fwd left in ws. */
 int hiseg_loss_bwd(const hiseg_loss_cfg* cfg, int N, int H, int W, const float* pred, const float* bgfg,

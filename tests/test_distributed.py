@@ -107,3 +107,41 @@ def test_grad_bucket_sync_gloo_world2():
     assert sorted(order) == list(range(nb))
     assert any(k >= 0 for k in launch_after), launch_after
     assert order[0] != 0 and order.index(nb - 1) < order.index(0)
+
+
+def _count_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from hiseg import distributed as HD
+        seen = []
+
+        class _Loss(nn.Module):   # the hook sync_loss_class_weights installs on RefinedHierarchicalLoss
+            count_sync = None
+
+        loss = HD.sync_loss_class_weights(_Loss())
+        c = torch.tensor([10.0 + rank, 20.0 * (rank + 1), 3.0, 4.0 + 2 * rank], dtype=torch.float64)
+        loss.count_sync(c)
+        seen.append(c.tolist())
+        q.put((rank, seen))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e)))
+
+
+def test_loss_class_counts_all_reduced_gloo_world2():
+    """sync_loss_class_weights: each rank's 4 class pixel counts become their sum over the ranks before the
+    loss's EMA update (the GPU side of the same hook: tests/test_gpu_train.py
+    test_loss_class_weights_data_parallel_equal_single_process)."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_count_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=120) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+    for rank, res in out:
+        assert not isinstance(res, str), res
+        assert res[0] == [21.0, 60.0, 6.0, 10.0]

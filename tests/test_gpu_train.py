@@ -660,3 +660,50 @@ def test_eval_after_training_sees_the_updated_weights():
         ref, _ = fresh.eval()(images, rois)
     assert not torch.equal(before, after)
     assert torch.equal(after, ref)
+
+
+def test_loss_class_weights_data_parallel_equal_single_process():
+    """Two data-parallel ranks (each half of the ROI batch) with their class pixel counts summed -- what
+    hiseg.distributed.sync_loss_class_weights does over RCCL -- carry, step after step, the dynamic class
+    weights (and their EMA) of one process on the whole batch (hierarchical_segmentation.py:227-255, 286-309);
+    without the sum they differ."""
+    import ctypes
+    import hiseg
+    from hiseg import _lib as L
+    N, H, W = 6, 64, 48
+    g = torch.Generator().manual_seed(5)
+
+    def batch(k):
+        pred = torch.randn(N, 3, H, W, generator=g).to(DEV)
+        aux = {"bg_fg_logits": torch.randn(N, 2, H, W, generator=g).to(DEV),
+               "target_nontarget_logits": torch.randn(N, 2, H, W, generator=g).to(DEV)}
+        tgt = torch.from_numpy(filler.ellipse_targets(40 + k, N, H, W)).to(DEV)
+        return pred, aux, tgt
+
+    def make():
+        return hiseg.RefinedHierarchicalLoss(use_boundary_aware_loss=False)
+
+    def counts_of(loss, tgt):   # hiseg_loss_fwd_begin on another rank's half
+        cfg, _ = loss._cfg(H, W, False, False)
+        n = tgt.shape[0]
+        ws = torch.empty(int(L.lib().hiseg_loss_ws(n, H, W)), dtype=torch.float32, device=DEV)
+        c = torch.empty(4, dtype=torch.float64, device=DEV)
+        L.check(L.lib().hiseg_loss_fwd_begin(ctypes.byref(cfg), n, H, W, tgt.contiguous().data_ptr(), ws.data_ptr(),
+                                             c.data_ptr(), L.stream_ptr()), "begin")
+        return c
+
+    full, r0, r1, solo = make(), make(), make(), make()
+    keys = ("bg_weight", "fg_weight", "target_weight", "nontarget_weight")
+    for k in range(3):
+        pred, aux, tgt = batch(k)
+        h0, h1 = slice(0, N // 2), slice(N // 2, N)
+        _, d_full = full(pred, tgt, aux)
+        r0.count_sync = lambda c, t=tgt[h1]: c.add_(counts_of(r0, t))
+        r1.count_sync = lambda c, t=tgt[h0]: c.add_(counts_of(r1, t))
+        _, d0 = r0(pred[h0].contiguous(), tgt[h0].contiguous(), {a: v[h0].contiguous() for a, v in aux.items()})
+        _, d1 = r1(pred[h1].contiguous(), tgt[h1].contiguous(), {a: v[h1].contiguous() for a, v in aux.items()})
+        _, ds = solo(pred[h0].contiguous(), tgt[h0].contiguous(), {a: v[h0].contiguous() for a, v in aux.items()})
+        for key in keys:
+            assert d0[key] == pytest.approx(d_full[key], rel=1e-6), (k, key)
+            assert d1[key] == pytest.approx(d_full[key], rel=1e-6), (k, key)
+    assert any(abs(ds[key] - d_full[key]) > 1e-4 for key in keys)
