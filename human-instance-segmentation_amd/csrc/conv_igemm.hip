@@ -295,6 +295,43 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
   HISEG_REQUIRE(!d->convT || (d->KH == 1 && d->KW == 1 && d->stride == 1 && d->pad == 0 && d->Cout % 16 == 0 &&
                               d->Ho == d->H && d->Wo == d->W),
                 HISEG_ERR_BAD_SHAPE, "conv2d: convT requires a 1x1 GEMM with Cout = 4*C, C %% 4 == 0");
+  // Operands of >= 2 GiB: the LDS-DMA kernels address through 32-bit buffer offsets, so the launch is split
+  // into image ranges whose every operand spans < 2 GiB (NHWC images are contiguous blocks; the conv never
+  // mixes images), each range a launch of its own on the same stream.
+  {
+    const long long ea = d->dtype == HISEG_BF16 ? 2 : 4, eo = d->out_dtype == HISEG_BF16 ? 2 : 4;
+    const long long in_px = (long long)(d->H / d->a_up) * (d->W / d->a_up);
+    const long long out_px = (long long)d->Ho * d->Wo * (d->convT ? 4 : 1);
+    long long per = in_px * d->a_cstride * ea;
+    auto upd = [&](long long v) { if (v > per) per = v; };
+    if (d->srcB) upd((long long)d->H * d->W * d->b_cstride * ea);
+    if (d->residual) upd(out_px * d->r_cstride * ea);
+    if (d->mul) upd(out_px * d->m_cstride * ea);
+    upd(out_px * d->o_cstride * eo);
+    if (d->out2) upd(out_px * d->o2_cstride * ea);
+    const long long lim = (1ll << 31) - (1ll << 20);
+    if (per * d->N > lim) {
+      HISEG_REQUIRE(per <= lim, HISEG_ERR_BAD_SHAPE, "conv2d: one image's operand exceeds 2 GiB");
+      const int step = (int)(lim / per);
+      for (int n0 = 0; n0 < d->N; n0 += step) {
+        hiseg_conv2d_desc c = *d;
+        c.N = d->N - n0 < step ? d->N - n0 : step;
+        auto at = [&](const void* p, long long bytes_per_image) {
+          return p ? (const void*)((const char*)p + bytes_per_image * n0) : p;
+        };
+        c.srcA = at(d->srcA, in_px * d->a_cstride * ea);
+        c.srcB = at(d->srcB, (long long)d->H * d->W * d->b_cstride * ea);
+        c.residual = at(d->residual, out_px * d->r_cstride * ea);
+        c.mul = at(d->mul, out_px * d->m_cstride * ea);
+        c.out = const_cast<void*>(at(d->out, out_px * d->o_cstride * eo));
+        c.out2 = const_cast<void*>(at(d->out2, out_px * d->o2_cstride * ea));
+        if (d->in_scale) c.in_scale = d->in_scale + (long long)n0 * d->Ca;   // per-image SE gate [N][Ca]
+        const int r = conv2d_impl(&c, stream, variant);
+        if (r) return r;
+      }
+      return HISEG_OK;
+    }
+  }
   const long long M = (long long)d->N * d->Ho * d->Wo;
   HISEG_REQUIRE(M < (1ll << 31), HISEG_ERR_BAD_SHAPE, "conv2d: too many pixels");
   ConvArgs a;

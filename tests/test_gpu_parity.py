@@ -591,3 +591,33 @@ def test_export_dilation_matches_reference_golden(dilation):
     oc = model.pretrained_unet.output_conv
     binary = ops.binary_masks(u, oc.weight.detach().float().reshape(2).contiguous(), oc.bias.detach().float())
     assert max_abs(binary.cpu(), g["binary"]) < 1e-5
+
+
+def test_conv_operands_over_2gib_split_by_image_range():
+    """A conv whose input and output each span 2.26 GB (360 images x 128x96 x 256 ch bf16): the LDS-DMA kernels
+    address through 32-bit buffer offsets, so hiseg_conv2d_fwd splits the launch into image ranges.  Images are
+    independent, so the first, a middle and the last images equal the same conv run on those images alone."""
+    from hiseg import ops
+    dt = torch.bfloat16
+    N, C, H, W = 360, 256, 128, 96
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = ops.Act.new(N, H, W, C, dt, DEV, zero=False)
+    x.t.copy_(torch.randn(x.t.numel(), device=DEV, generator=g, dtype=torch.float32).to(dt))
+    assert x.t.numel() * 2 > (1 << 31)
+    w = torch.randn(C, C, 3, 3, device=DEV, generator=g) / (C * 9) ** 0.5
+    p = ops.pack_conv(w, torch.randn(C, device=DEV, generator=g) * 0.1, None, 1, dt, DEV, pad=1)
+    r = ops.Act.new(N, H, W, C, dt, DEV, zero=False)
+    r.t.copy_(torch.randn(r.t.numel(), device=DEV, generator=g, dtype=torch.float32).to(dt))
+    y = ops.conv2d(p, x, residual=r)
+    torch.cuda.synchronize()
+    per = H * W * C
+    for n in (0, 1, 179, 358, 359):
+        xi = ops.Act.new(1, H, W, C, dt, DEV, zero=False)
+        xi.t.copy_(x.t[n * per:(n + 1) * per])
+        ri = ops.Act.new(1, H, W, C, dt, DEV, zero=False)
+        ri.t.copy_(r.t[n * per:(n + 1) * per])
+        yi = ops.conv2d(p, xi, residual=ri)
+        torch.cuda.synchronize()
+        assert torch.equal(yi.t, y.t[n * per:(n + 1) * per]), n
+    del x, r, y
+    torch.cuda.empty_cache()
