@@ -109,7 +109,7 @@ GFLOP_PER_TRAIN_SAMPLE = {"b1": 279.0 + 40.0, "b7": 835.3 + 120.3}
 
 
 def train_bench(device, dtype, rank, world, dist, steps, warmup, preset=None, batch=B, rois_per_img=R,
-                hw=(H, W), local_first=False):
+                hw=(H, W), local_first=False, eager_train=False):
     """Train steps/s of an ROI model (module docstring).  preset None: the B0-std model on the C2-shaped batch
     (32 images 640x480 x 8 ROIs, RoIAlign scale (H, W)); preset "b1"/"b7": the C3/C4 preset on `batch` 640x640
     images with one ROI each (the reference's training semantics: dataset.py:74-80, RoIAlign scale 640).
@@ -152,9 +152,15 @@ def train_bench(device, dtype, rank, world, dist, steps, warmup, preset=None, ba
         state["opt"].step()
         return loss
 
+    # one HIP graph per step (hiseg.GraphedStep: the ~1 000 launches of a step replayed at once; every
+    # per-step state lives on the device) -- single-rank runs; the data-parallel step stays eager
+    run = step
+    if world == 1 and not eager_train:
+        run = hiseg.GraphedStep(step, lambda: state["opt"])
+
     def timed():
-        for _ in range(warmup):
-            loss = step()
+        for _ in range(max(warmup, 3 if run is not step else 1)):
+            loss = run()
         torch.cuda.synchronize()
         first = float(loss.detach())
         if dist:
@@ -162,7 +168,7 @@ def train_bench(device, dtype, rank, world, dist, steps, warmup, preset=None, ba
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
-            loss = step()
+            loss = run()
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
@@ -202,7 +208,8 @@ def train_bench(device, dtype, rank, world, dist, steps, warmup, preset=None, ba
            "loss_first_last": [round(first, 4), round(last, 4)],
            "config": {"workload": workload, "global_batch": int(images.shape[0]) * world,
                       "roi_samples_per_step": n_samples * world,
-                      "parallelism": f"dp{world} (DDP, bucketed RCCL grad all-reduce)" if world > 1 else "dp1"}}
+                      "parallelism": f"dp{world} (DDP, bucketed RCCL grad all-reduce)" if world > 1 else "dp1",
+                      "schedule": "eager" if run is step else "one HIP graph per step (hiseg.GraphedStep)"}}
     if local is not None:
         out["local_step_per_s"] = round(local, 3)
         out["ddp_over_local"] = round(sps / local, 4)   # 1.0 = the gradient exchange is fully hidden
@@ -500,6 +507,7 @@ def main():
     ap.add_argument("--no-presets", action="store_true", help="skip the C3 (B1) / C4 (B7) train lines")
     ap.add_argument("--distill-only", action="store_true", help="only the C5 distillation line (profiling)")
     ap.add_argument("--serial", action="store_true", help="one stream (no UNet/head overlap across steps)")
+    ap.add_argument("--eager-train", action="store_true", help="train legs without the whole-step HIP graph")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher + rendezvous check only (no GPU work): CPU tests of the multi-rank path")
@@ -551,14 +559,14 @@ def main():
     if not args.no_train:
         torch.cuda.empty_cache()
         out["train"] = train_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), max(2, args.warmup),
-                                   local_first=True)
+                                   local_first=True, eager_train=args.eager_train)
         if not args.no_presets:
             torch.cuda.empty_cache()
             out["train_c3"] = train_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2, preset="b1",
-                                          batch=32, rois_per_img=1, hw=(640, 640))
+                                          batch=32, rois_per_img=1, hw=(640, 640), eager_train=args.eager_train)
             torch.cuda.empty_cache()
             out["train_c4"] = train_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2, preset="b7",
-                                          batch=8, rois_per_img=1, hw=(640, 640))
+                                          batch=8, rois_per_img=1, hw=(640, 640), eager_train=args.eager_train)
     if not args.no_distill and not args.train_only:
         torch.cuda.empty_cache()
         out["distill"] = distill_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2)
@@ -625,7 +633,7 @@ def infer_bench(args, device, dtype, rank, world, dist):
         achieved = summ["flops"] / (summ["avg_ms"] * 1e-3) / 1e12
         roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": load_traffic(),
-                    "kernel": "conv_wide_kernel<256,4> (256x256 workgroup tile, 4-stage LDS-DMA ring, 128x128 wave tiles in AGPRs, LDS-staged epilogue) 256->256 3x3 @64x48 x256 ROIs",
+                    "kernel": "conv_hw_kernel<128> (halo-tiled: 16x16-pixel x 128-Cout workgroup tiles, one 18x18 halo per 32-channel slice for all 9 taps, 4-stage weight ring, 2 workgroups per CU, LDS-staged epilogue) 256->256 3x3 @64x48 x256 ROIs",
                     "launches_timed": summ["launches"], "avg_launch_ms": round(summ["avg_ms"], 4),
                     "flop_per_launch": summ["flops"]}
     pipeline_tflops = value * GFLOP_PER_ROI_MASK / 1e3

@@ -462,7 +462,12 @@ static int launch_wide(const ConvArgs& a, hipStream_t s) {
                                            : conv_wide_kernel<BCO, STAGES, HISEG_ACT_NONE, true, STAMP, NOLOAD, CM>)
                   : (act == HISEG_ACT_RELU ? conv_wide_kernel<BCO, STAGES, HISEG_ACT_RELU, false, STAMP, NOLOAD, CM>
                                            : conv_wide_kernel<BCO, STAGES, HISEG_ACT_NONE, false, STAMP, NOLOAD, CM>);
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  static bool attr_set[2][2] = {};   // once per instantiation (no API call but the launch per layer: capturable)
+  bool& done = attr_set[res ? 1 : 0][act == HISEG_ACT_RELU ? 1 : 0];
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    done = true;
+  }
   hipLaunchKernelGGL(kern, dim3(npx * nco), dim3(256), lds, s, a);
   return hiseg_check_launch("conv_wide");
 }

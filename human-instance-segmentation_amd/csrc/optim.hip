@@ -104,6 +104,11 @@ __global__ void __launch_bounds__(256) adamw_guarded_kernel(float* p, float* g, 
   }
 }
 
+// Commit the new step count into the slot the next step reads (the graph-safe form: the host never flips parity).
+__global__ void adamw_commit_kernel(int* steps, int parity) {
+  if (threadIdx.x == 0) steps[parity] = steps[parity ^ 1];
+}
+
 }  // namespace hiseg
 
 using namespace hiseg;
@@ -115,6 +120,7 @@ extern "C" int hiseg_adamw_step_guarded(float* p, float* g, float* m, float* v, 
                 HISEG_ERR_BAD_ARG, "adamw_step_guarded: bad arguments");
   hipLaunchKernelGGL(adamw_guarded_kernel, dim3(kOptBlocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, lr,
                      beta1, beta2, eps, weight_decay, partial, max_norm, norm_out, steps, parity, skipped);
+  hipLaunchKernelGGL(adamw_commit_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, steps, parity);
   return hiseg_check_launch("adamw_step_guarded");
 }
 

@@ -481,6 +481,21 @@ __global__ void dropout2d_mask_kernel(int n, float p, unsigned long long seed, f
   out[i] = u < p ? 0.f : 1.f / (1.f - p);
 }
 
+// Device-resident seed: seed = (base * 0x9E3779B1 + offset) masked to 48 bits, base read from device memory, so
+// a captured step replays with fresh masks once hiseg_seed_advance (captured with it) moved the base on.
+__global__ void dropout2d_mask_dev_kernel(int n, float p, const unsigned long long* base, unsigned long long offset,
+                                          float* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const unsigned long long seed = (base[0] * 0x9E3779B1ull + offset) & 0xFFFFFFFFFFFFull;
+  const float u = (float)(splitmix64(seed ^ splitmix64((unsigned long long)i)) >> 40) * (1.0f / 16777216.0f);
+  out[i] = u < p ? 0.f : 1.f / (1.f - p);
+}
+
+__global__ void seed_advance_kernel(unsigned long long* base) {
+  if (threadIdx.x == 0) base[0] += 1ull;
+}
+
 // ---------------------------------------------------------------------------------------- element-wise
 #define EW_LOOP(P, C)                                                                                   \
   const long long n_ = (P) * (C);                                                                      \
@@ -1051,6 +1066,21 @@ extern "C" int hiseg_bn_bwd(const hiseg_bn_bwd_desc* d, hiseg_stream_t stream) {
   hipLaunchKernelGGL(bn_bwd_finalize_par_kernel, dim3(C), dim3(256), 0, s, *d, S);
   DISPATCH_T(d->dtype, hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(ew_blocks(d->P * d->C)), dim3(256), 0, s, *d, S));
   return hiseg_check_launch("bn_bwd");
+}
+
+extern "C" int hiseg_dropout2d_mask_dev(int N, int C, float p, const unsigned long long* seed_base,
+                                        unsigned long long offset, float* out, hiseg_stream_t stream) {
+  HISEG_REQUIRE(seed_base && out && N > 0 && C > 0 && p >= 0.f && p < 1.f, HISEG_ERR_BAD_ARG, "dropout2d_mask_dev: bad args");
+  const int n = N * C;
+  hipLaunchKernelGGL(dropout2d_mask_dev_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, n, p,
+                     seed_base, offset, out);
+  return hiseg_check_launch("dropout2d_mask_dev");
+}
+
+extern "C" int hiseg_seed_advance(unsigned long long* seed_base, hiseg_stream_t stream) {
+  HISEG_REQUIRE(seed_base, HISEG_ERR_BAD_ARG, "seed_advance: null");
+  hipLaunchKernelGGL(seed_advance_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, seed_base);
+  return hiseg_check_launch("seed_advance");
 }
 
 extern "C" int hiseg_dropout2d_mask(int N, int C, float p, unsigned long long seed, float* out, hiseg_stream_t stream) {

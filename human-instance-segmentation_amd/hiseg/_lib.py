@@ -220,6 +220,8 @@ def _declare(lib):
         "hiseg_bn_apply": ([ctypes.POINTER(BnApplyDesc), P], c_int),
         "hiseg_bn_bwd": ([ctypes.POINTER(BnBwdDesc), P], c_int),
         "hiseg_dropout2d_mask": ([c_int, c_int, c_float, ctypes.c_ulonglong, P, P], c_int),
+        "hiseg_dropout2d_mask_dev": ([c_int, c_int, c_float, P, ctypes.c_ulonglong, P, P], c_int),
+        "hiseg_seed_advance": ([P, P], c_int),
         "hiseg_relu_bwd": ([c_int, c_ll, c_int, c_int, EwView, EwView, P, EwView, P], c_int),
         "hiseg_sigmoid_bwd": ([c_int, c_ll, c_int, EwView, EwView, EwView, P], c_int),
         "hiseg_gate_fwd": ([c_int, c_ll, c_int, EwView, EwView, EwView, P], c_int),

@@ -1,0 +1,69 @@
+"""Whole-step HIP graphs for training.
+
+A training step on the hiseg path is ~1 000 kernel launches issued from Python (tape engine, ctypes
+descriptors); on one MI355X the B0-std step's kernels take ~80 ms while issuing them takes longer, so the
+GPU idles between launches.  GraphedStep captures one step -- forward, loss, backward and the optimizer --
+into a HIP graph (torch.cuda.graph on the step's stream) and replays it: one launch per step.
+
+Every piece of per-step state the kernels use lives on the device, so a replayed step is the next step:
+the Dropout2d seed base (TrainState.begin_step), the loss's dynamic-weight EMA, FusedAdamW's step count and
+skip counter (fixed slot, committed by the library).  Host-side values are frozen into the graph: the
+learning rate, the inputs' addresses (the step must read the same input tensors, refilled in place between
+steps) and the shapes -- GraphedStep re-captures when the optimizer's learning rate changes.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+
+
+class GraphedStep:
+    """``gs = GraphedStep(step_fn, optimizer_fn)``; every ``gs()`` runs exactly one training step and returns
+    step_fn's outputs (for replays: the tensors captured, refreshed in place).
+
+    The first ``eager`` calls (default 2: the first step creates the conv plans, the second builds the one
+    packing table from them) run step_fn eagerly on a side stream -- host-to-device uploads, allocator
+    warm-up, optimizer creation; torch.cuda.graph's warm-up rule -- the next call captures it and replays it
+    once, later calls replay.  ``optimizer_fn`` returns the optimizer (or None): its learning rate is watched and
+    its parameters' version counters are bumped after each replay (eval plans packed from the weights must
+    see the update, as after an eager step)."""
+
+    def __init__(self, step_fn: Callable, optimizer_fn: Optional[Callable] = None, eager: int = 2):
+        self.fn, self.opt_fn, self.eager = step_fn, optimizer_fn, max(1, int(eager))
+        self.calls = 0
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.out = None
+        self.lr = None
+        self.captures = 0
+
+    def _opt(self):
+        return self.opt_fn() if self.opt_fn is not None else None
+
+    def _lr(self):
+        o = self._opt()
+        return None if o is None else tuple(g["lr"] for g in o.param_groups)
+
+    def __call__(self):
+        self.calls += 1
+        if self.calls <= self.eager:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                out = self.fn()
+            torch.cuda.current_stream().wait_stream(s)
+            return out
+        if self.graph is None or self._lr() != self.lr:
+            self.graph = None
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.out = self.fn()
+            self.graph, self.lr = g, self._lr()
+            self.captures += 1
+        self.graph.replay()
+        o = self._opt()
+        bump = getattr(o, "_bump", None)
+        if bump:
+            torch.autograd.graph.increment_version(bump)
+        return self.out

@@ -258,7 +258,8 @@ class FusedAdamW(torch.optim.Optimizer):
                                              self.partial.data_ptr(), float(self.max_grad_norm) if clip else 0.0,
                                              self.last_norm.data_ptr(), self._steps.data_ptr(), self._parity,
                                              self._skipped.data_ptr(), s), "adamw_step")
-        self._parity ^= 1
+        # the count stays in slot _parity (the library commits it): no host-side state changes per step, so the
+        # whole step can be captured into a HIP graph (hiseg.graphs.GraphedStep)
         # the kernel wrote the parameters in place: bump their versions so plans packed from them (eval
         # forward, frozen-layer caches keyed by tensor version) are rebuilt
         if self._bump is None:

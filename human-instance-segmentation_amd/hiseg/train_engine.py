@@ -18,7 +18,6 @@ RoIAlign backward.
 from __future__ import annotations
 
 import ctypes
-import itertools
 import os
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Tuple
@@ -160,7 +159,10 @@ class TrainState:
         self.entries: List[L.PackEntry] = []
         self.table: Optional[torch.Tensor] = None
         self.max_total = 0
-        self.seed = itertools.count(int(torch.initial_seed()) & 0xFFFFFFFF)
+        # Dropout2d seeds: a device-resident base advanced once per step (begin_step) + the draw's index within
+        # the step, so a step captured into a HIP graph draws fresh masks on every replay
+        self.seed_base = torch.full((1,), int(torch.initial_seed()) & 0xFFFFFFFF, dtype=torch.int64, device=device)
+        self.seed_offset = 0
         self.cached: Dict = {}
         self.sync = None          # hiseg.distributed.GradBucketSync (data-parallel gradient exchange)
         self.op_index: Optional[int] = None
@@ -243,8 +245,15 @@ class TrainState:
             self.sync.record(p, self.op_index)
         return self.flat.grad_view(p)
 
+    def begin_step(self):
+        """Start of a training step (the ROI path's forward): advance the device seed base (a kernel)."""
+        _chk(L.lib().hiseg_seed_advance(self.seed_base.data_ptr(), _stream()), "seed_advance")
+        self.seed_offset = 0
+
     def next_seed(self) -> int:
-        return next(self.seed) * 0x9E3779B1 & 0xFFFFFFFFFFFF
+        """Offset of the next Dropout2d draw within the step."""
+        self.seed_offset += 1
+        return self.seed_offset
 
 
 def _copy_bias(shift: torch.Tensor, b: torch.Tensor, n: int, convT: bool):
@@ -660,7 +669,8 @@ def dropout_mask(T: Tape, m: nn.Module, N: int, C: int, device) -> Optional[torc
     if p <= 0.0:
         return None
     out = torch.empty(N * C, dtype=torch.float32, device=device)
-    _chk(L.lib().hiseg_dropout2d_mask(N, C, p, T.S.next_seed(), out.data_ptr(), _stream()), "dropout2d_mask")
+    _chk(L.lib().hiseg_dropout2d_mask_dev(N, C, p, T.S.seed_base.data_ptr(), T.S.next_seed(), out.data_ptr(),
+                                          _stream()), "dropout2d_mask")
     return out
 
 
@@ -1073,6 +1083,7 @@ class _RoiPathFunction(torch.autograd.Function):
     def forward(ctx, handle, images, rois, *params):
         model, S = handle["model"], handle["state"]
         T = Tape(S)
+        S.begin_step()
         S.pack()
         u = handle["u"]
         logits, aux = roi_path_train(model, S, T, images, rois, u)

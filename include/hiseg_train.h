@@ -153,6 +153,11 @@ int hiseg_ln_bwd(const hiseg_ln_bwd_desc* d, hiseg_stream_t stream);
 /* Dropout2d mask (nn.Dropout2d in refinement.py:484,486,519,525,540): per (n, c) 0 with
  * probability p else 1/(1-p), from a counter-based hash of (seed, n*C + c). */
 int hiseg_dropout2d_mask(int N, int C, float p, unsigned long long seed, float* out, hiseg_stream_t stream);
+/* The same mask from a device-resident seed base (seed = (*seed_base * 0x9E3779B1 + offset) mod 2^48), and the
+ * one-thread kernel that advances the base: a step captured into a HIP graph draws fresh masks per replay. */
+int hiseg_dropout2d_mask_dev(int N, int C, float p, const unsigned long long* seed_base, unsigned long long offset,
+                             float* out, hiseg_stream_t stream);
+int hiseg_seed_advance(unsigned long long* seed_base, hiseg_stream_t stream);
 
 /* ----------------------------------------------------------------------------------------
  * Element-wise backward helpers (NHWC views, dtype = compute dtype, f32 math).
@@ -239,8 +244,10 @@ int hiseg_adamw_step(float* p, float* g, float* m, float* v, long long n, float 
  *   total = sqrt(sum partial) is NaN or Inf, p, g, m, v are left untouched, the step count is not
  *   advanced and *skipped is incremented; otherwise t = steps[parity] + 1 drives the bias corrections
  *   (computed in double as torch.optim.AdamW does) and steps[parity ^ 1] receives the new count
- *   (steps[parity] otherwise).  The caller flips `parity` every call (two slots: every block reads slot
- *   `parity` while block 0 writes the other).  norm_out (optional) receives total. */
+ *   (steps[parity] otherwise) -- two slots: every block reads slot `parity` while block 0 writes the
+ *   other -- and a one-thread commit launch then copies it back into slot `parity`, so the count always
+ *   lives in slot `parity` and a fixed parity (0) serves every call: the step can be captured into a HIP
+ *   graph and replayed.  norm_out (optional) receives total. */
 int hiseg_adamw_step_guarded(float* p, float* g, float* m, float* v, long long n, float lr, float beta1, float beta2,
                              float eps, float weight_decay, const float* partial, float max_norm, float* norm_out,
                              int* steps, int parity, int* skipped, hiseg_stream_t stream);

@@ -150,7 +150,7 @@ def test_conv_transpose_and_in_scale(dt):
     assert _rel(y, ref) < (2e-5 if dt == torch.float32 else 1e-2)
 
 
-# Every bf16 kernel variant must reproduce the generic kernel bit for bit: same K order per
+# Every tap-major bf16 kernel variant must reproduce the generic kernel bit for bit: same K order per
 # accumulator, same fp32 epilogue.  name: (N, Ca, Cb, Cout, H, W, k, convT, residual, mul, out2)
 VARIANT_CASES = {
     "3x3_256_res_mul_out2": (3, 256, 0, 256, 13, 11, 3, False, True, True, True),
@@ -193,7 +193,9 @@ def test_conv_kernel_variants_bit_identical(name):
     R = ops.Act.from_nchw(torch.randn(N, Cout, oH, oW, device=DEV, generator=g), dt) if res else None
     M = ops.Act.from_nchw(torch.rand(N, Cout, oH, oW, device=DEV, generator=g), dt) if mul else None
     outs = {}
-    for v in (-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 61, 62, 66, 67, 68, 69, 70, 71, 72):
+    # the automatic choice (variant 0) may take the channel-major halo kernel: checked within bf16 rounding by
+    # test_conv_halo_wide_within_bf16 / test_conv_automatic_choice_within_bf16
+    for v in (-1, 1, 2, 3, 4, 5, 6, 7, 8, 61, 62, 66, 67, 68, 69, 70, 71, 72):
         o2a = ops.Act.new(N, oH, oW, Cout, dt, DEV) if o2 else None
         y = ops.conv2d(p, xa, xb, residual=R, mul=M, out2=o2a, variant=v)
         torch.cuda.synchronize()
@@ -621,3 +623,66 @@ def test_conv_operands_over_2gib_split_by_image_range():
         assert torch.equal(yi.t, y.t[n * per:(n + 1) * per]), n
     del x, r, y
     torch.cuda.empty_cache()
+
+
+# The halo-tiled wide kernel (conv_hw.hip, variants 80 = BCO 256, 82 = BCO 128): channel-major K order, so
+# within bf16 output rounding of the generic kernel.  name: (N, Cin, Cout, H, W, residual, relu, a_coff)
+HW_CASES = {
+    "256_res_ragged_13x11": (3, 256, 256, 13, 11, True, True, 0),
+    "256_roi_64x48": (4, 256, 256, 64, 48, True, True, 0),
+    "256_plain_relu_30x40": (2, 256, 256, 30, 40, False, True, 0),
+    "128_to_128_res_37x20": (2, 128, 128, 37, 20, True, True, 0),
+    "64_to_128_16x12": (3, 64, 128, 16, 12, False, False, 0),
+    "128_to_384_offset_view_9x23": (2, 128, 384, 9, 23, True, False, 64),
+}
+
+
+@pytest.mark.parametrize("variant", [80, 82])
+@pytest.mark.parametrize("name", list(HW_CASES))
+def test_conv_halo_wide_within_bf16(name, variant):
+    from hiseg import ops
+    N, Cin, Cout, H, W, res, relu, coff = HW_CASES[name]
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(11)
+    full = ops.Act.new(N, H, W, Cin + coff, dt, DEV, zero=False)
+    full.t.copy_(torch.randn(full.t.numel(), device=DEV, generator=g).to(dt))
+    xa = full.slice(coff, Cin) if coff else full
+    w = torch.randn(Cout, Cin, 3, 3, device=DEV, generator=g) / (Cin * 9) ** 0.5
+    p = ops.pack_conv(w, torch.randn(Cout, device=DEV, generator=g) * 0.1, None, int(relu), dt, DEV, pad=1)
+    R = ops.Act.from_nchw(torch.randn(N, Cout, H, W, device=DEV, generator=g), dt) if res else None
+    ref = ops.conv2d(p, xa, residual=R, variant=-1).to_nchw().float()
+    y = ops.conv2d(p, xa, residual=R, variant=variant).to_nchw().float()
+    torch.cuda.synchronize()
+    assert torch.isfinite(y).all()
+    assert ((y - ref).abs().max() / ref.abs().max()).item() < 8e-3
+
+
+@pytest.mark.parametrize("name", list(VARIANT_CASES))
+def test_conv_automatic_choice_within_bf16(name):
+    """hiseg_conv2d_fwd's automatic kernel choice on every VARIANT_CASES layer: bit-identical to the generic kernel
+    where it takes a tap-major kernel, within bf16 rounding where it takes the channel-major halo kernel."""
+    from hiseg import ops
+    N, Ca, Cb, Cout, H, W, k, convT, res, mul, o2 = VARIANT_CASES[name]
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(7)
+    xa = ops.Act.from_nchw(torch.randn(N, Ca, H, W, device=DEV, generator=g), dt)
+    xb = ops.Act.from_nchw(torch.randn(N, Cb, H, W, device=DEV, generator=g), dt) if Cb else None
+    if convT:
+        w = torch.randn(Ca, Cout, 2, 2, device=DEV, generator=g) / Ca ** 0.5
+        p = ops.pack_convT2x2(w, torch.randn(Cout, device=DEV, generator=g), None, 1, dt, DEV)
+        oH, oW = 2 * H, 2 * W
+    else:
+        w = torch.randn(Cout, Ca + Cb, k, k, device=DEV, generator=g) / ((Ca + Cb) * k * k) ** 0.5
+        p = ops.pack_conv(w, torch.randn(Cout, device=DEV, generator=g) * 0.1, None, 1, dt, DEV, pad=k // 2,
+                          split=(Ca, Cb) if Cb else None)
+        oH, oW = H, W
+    R = ops.Act.from_nchw(torch.randn(N, Cout, oH, oW, device=DEV, generator=g), dt) if res else None
+    M = ops.Act.from_nchw(torch.rand(N, Cout, oH, oW, device=DEV, generator=g), dt) if mul else None
+    ref = ops.conv2d(p, xa, xb, residual=R, mul=M, variant=-1).to_nchw().float()
+    y = ops.conv2d(p, xa, xb, residual=R, mul=M, variant=0).to_nchw().float()
+    torch.cuda.synchronize()
+    halo = (not convT and k == 3 and not Cb and not mul and not o2 and Cout % 128 == 0 and Ca % 32 == 0 and Ca >= 64)
+    if halo:
+        assert ((y - ref).abs().max() / ref.abs().max()).item() < 8e-3
+    else:
+        assert torch.equal(y, ref)

@@ -707,3 +707,47 @@ def test_loss_class_weights_data_parallel_equal_single_process():
             assert d0[key] == pytest.approx(d_full[key], rel=1e-6), (k, key)
             assert d1[key] == pytest.approx(d_full[key], rel=1e-6), (k, key)
     assert any(abs(ds[key] - d_full[key]) > 1e-4 for key in keys)
+
+
+def test_graphed_train_step_equals_eager():
+    """hiseg.GraphedStep (one HIP graph per training step) against eager steps from the same initial state:
+    Dropout2d on (device seed base), FusedAdamW with clipping (device step count), the loss's EMA (device state)
+    -- after 4 steps the parameters, the optimizer moments and the loss are identical."""
+    import hiseg
+    torch.manual_seed(0)
+    images = torch.from_numpy(filler.uniform(31, (2, 3, 96, 128))).to(DEV)
+    rois = torch.from_numpy(filler.box_rois(32, 2, 2)).to(DEV)
+    tgt = torch.from_numpy(filler.ellipse_targets(33, 4, 128, 96)).to(DEV)
+    runs = []
+    for graphed in (False, True):
+        torch.manual_seed(0)
+        m = _model(torch.bfloat16, p_drop_zero=False).to(DEV).train()
+        for mm in (m.roi_align_mask, m.roi_align_rgb):
+            mm.spatial_scale_h, mm.spatial_scale_w = 96, 128
+        loss_fn = hiseg.RefinedHierarchicalLoss(use_boundary_aware_loss=True, use_contour_detection=True,
+                                                use_distance_transform=True, boundary_aware_weight=0.1,
+                                                contour_loss_weight=0.1, distance_loss_weight=0.1)
+        st = {"opt": None}
+
+        def step():
+            logits, aux = m(images, rois)
+            loss, _ = loss_fn(logits, tgt, aux)
+            if st["opt"] is None:
+                st["opt"] = hiseg.FusedAdamW(m, lr=5e-4, weight_decay=0.01, max_grad_norm=1.0)
+            st["opt"].zero_grad()
+            loss.backward()
+            st["opt"].step()
+            return loss
+
+        run = hiseg.GraphedStep(step, lambda: st["opt"]) if graphed else step
+        losses = [float(run().detach()) for _ in range(4)]
+        torch.cuda.synchronize()
+        if graphed:
+            assert run.captures == 1
+        params = torch.cat([p.detach().float().reshape(-1) for p in m.parameters()]).cpu()
+        runs.append((losses, params, st["opt"].exp_avg.cpu(), st["opt"].step_count))
+    (l0, p0, m0, s0), (l1, p1, m1, s1) = runs
+    assert l0 == l1, (l0, l1)
+    assert s0 == s1 == 4
+    assert torch.equal(p0, p1) and torch.equal(m0, m1)
+    assert l0[-1] != l0[0]
