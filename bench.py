@@ -109,7 +109,7 @@ GFLOP_PER_TRAIN_SAMPLE = {"b1": 279.0 + 40.0, "b7": 835.3 + 120.3}
 
 
 def train_bench(device, dtype, rank, world, dist, steps, warmup, preset=None, batch=B, rois_per_img=R,
-                hw=(H, W), local_first=False, eager_train=False):
+                hw=(H, W), local_first=False, graph_train=False):
     """Train steps/s of an ROI model (module docstring).  preset None: the B0-std model on the C2-shaped batch
     (32 images 640x480 x 8 ROIs, RoIAlign scale (H, W)); preset "b1"/"b7": the C3/C4 preset on `batch` 640x640
     images with one ROI each (the reference's training semantics: dataset.py:74-80, RoIAlign scale 640).
@@ -152,10 +152,11 @@ def train_bench(device, dtype, rank, world, dist, steps, warmup, preset=None, ba
         state["opt"].step()
         return loss
 
-    # one HIP graph per step (hiseg.GraphedStep: the ~1 000 launches of a step replayed at once; every
-    # per-step state lives on the device) -- single-rank runs; the data-parallel step stays eager
+    # --graph-train: one HIP graph per step (hiseg.GraphedStep; every per-step state lives on the device).  Off
+    # by default: the step is kernel-bound (the trace shows no launch gaps) and on this ROCm the replayed graph
+    # of ~1 000 kernels ran slower than eager launches (137 vs 118 ms)
     run = step
-    if world == 1 and not eager_train:
+    if world == 1 and graph_train:
         run = hiseg.GraphedStep(step, lambda: state["opt"])
 
     def timed():
@@ -507,7 +508,7 @@ def main():
     ap.add_argument("--no-presets", action="store_true", help="skip the C3 (B1) / C4 (B7) train lines")
     ap.add_argument("--distill-only", action="store_true", help="only the C5 distillation line (profiling)")
     ap.add_argument("--serial", action="store_true", help="one stream (no UNet/head overlap across steps)")
-    ap.add_argument("--eager-train", action="store_true", help="train legs without the whole-step HIP graph")
+    ap.add_argument("--graph-train", action="store_true", help="train legs as one replayed HIP graph per step")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher + rendezvous check only (no GPU work): CPU tests of the multi-rank path")
@@ -559,14 +560,14 @@ def main():
     if not args.no_train:
         torch.cuda.empty_cache()
         out["train"] = train_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), max(2, args.warmup),
-                                   local_first=True, eager_train=args.eager_train)
+                                   local_first=True, graph_train=args.graph_train)
         if not args.no_presets:
             torch.cuda.empty_cache()
             out["train_c3"] = train_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2, preset="b1",
-                                          batch=32, rois_per_img=1, hw=(640, 640), eager_train=args.eager_train)
+                                          batch=32, rois_per_img=1, hw=(640, 640), graph_train=args.graph_train)
             torch.cuda.empty_cache()
             out["train_c4"] = train_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2, preset="b7",
-                                          batch=8, rois_per_img=1, hw=(640, 640), eager_train=args.eager_train)
+                                          batch=8, rois_per_img=1, hw=(640, 640), graph_train=args.graph_train)
     if not args.no_distill and not args.train_only:
         torch.cuda.empty_cache()
         out["distill"] = distill_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2)

@@ -385,7 +385,9 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
     // 3x3 single-source layers with 128-multiple Cout: the halo-tiled kernel, BCO 128 (conv_hw.hip: two
     // workgroups per CU; tools/conv_bench.py: 0.92 vs 1.02 ms on the 256->256 @64x48 x256 ROI class, 1.11 vs
     // 1.37 ms on 128->128 @128x96, 0.49 vs 0.54 ms on 128->256; channel-major K order, within bf16 rounding)
-    if (v == 0 && !four_waves) {
+    // HISEG_CONV_HALO=0 keeps the tap-major kernels (A/B timing only)
+    static const bool halo = [] { const char* e = getenv("HISEG_CONV_HALO"); return !(e && atoi(e) == 0); }();
+    if (v == 0 && !four_waves && halo) {
       const int r = conv_hw_try(a, s, 82);
       if (r != 0) return r < 0 ? r : HISEG_OK;
     }
