@@ -634,7 +634,7 @@ def infer_bench(args, device, dtype, rank, world, dist):
         achieved = summ["flops"] / (summ["avg_ms"] * 1e-3) / 1e12
         roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": load_traffic(),
-                    "kernel": "conv_hw_kernel<128> (halo-tiled: 16x16-pixel x 128-Cout workgroup tiles, one 18x18 halo per 32-channel slice for all 9 taps, 4-stage weight ring, 2 workgroups per CU, LDS-staged epilogue) 256->256 3x3 @64x48 x256 ROIs",
+                    "kernel": "conv_hw_kernel<128, reuse> (halo-tiled: 16x16-pixel x 128-Cout workgroup tiles, one 18x18 halo per 32-channel slice for all 9 taps, B fragments reused across ky, 4-stage weight ring, 2 workgroups per CU, LDS-staged epilogue) 256->256 3x3 @64x48 x256 ROIs",
                     "launches_timed": summ["launches"], "avg_launch_ms": round(summ["avg_ms"], 4),
                     "flop_per_launch": summ["flops"]}
     pipeline_tflops = value * GFLOP_PER_ROI_MASK / 1e3

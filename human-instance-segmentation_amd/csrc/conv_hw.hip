@@ -18,9 +18,18 @@
 // finished reading slice c-1's halo (the barrier of the hand-over into tap 0 of slice c) and landed by the
 // hand-over into tap 8.  Halo rows are swizzled chunk c -> slot c ^ 2((r >> 2) & 1), conflict-free for a
 // ds_read_b128 fragment read of 16 consecutive rows from any start (a tap's window starts anywhere).
+//
+// Built twice (Makefile): this file (HISEG_HW_PART 1: BCO 256, accumulators in AGPRs, and conv_hw_try) and
+// conv_hw128.hip (HISEG_HW_PART 2: BCO 128 with -amdgpu-mfma-vgpr-form -- 128 accumulators in VGPRs keep
+// every configuration at two waves per SIMD; the AGPR form allocates 192 AGPRs and drops the B-reuse
+// residual kernels to one).
 #include <type_traits>
 
 #include "conv_common.h"
+
+#ifndef HISEG_HW_PART
+#define HISEG_HW_PART 1
+#endif
 
 namespace hiseg {
 
@@ -42,7 +51,11 @@ __device__ __forceinline__ int hhswz(int r) { return ((r >> 2) & 1) << 1; }     
 constexpr int kHaloRows = 324;             // 18 x 18
 constexpr int kHaloBytes = 24 * 1024;      // 24 pieces of 16 rows x 64 B (rows 324..383: padding)
 
-template <int BCO, int ACT, bool RES>
+// REUSE: taps ordered kx-major within a slice (tap t = (kx = t / 3, ky = t % 3)), so the three ky taps of a
+// kx read the same 10 halo rows shifted by one row each: the wave keeps B fragments for tile rows 0..9 in
+// registers across them and reads 10 per three stages instead of 24 (LDS read traffic per MFMA -39 % at
+// BCO 128, where the fragment reads are what bounds the two co-resident workgroups).
+template <int BCO, int ACT, bool RES, bool REUSE>
 __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
   constexpr int STAGES = 4;
   constexpr int TM = BCO / 32;        // A (Cout) fragments per wave
@@ -114,7 +127,8 @@ __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
   for (int k = 0; k < NAI; ++k) p_voff[k] = OOB;
   auto prepare_live = [&](int s) __attribute__((always_inline)) {
     p_sbase = lds_base + (unsigned)((s & (STAGES - 1)) * STAGE_BYTES);
-    const unsigned kofs = (unsigned)(n_tap * a.Cin + 32 * n_sl) * 2u;
+    const int wtap = REUSE ? (n_tap % 3) * 3 + n_tap / 3 : n_tap;   // packed weights: tap = ky * 3 + kx
+    const unsigned kofs = (unsigned)(wtap * a.Cin + 32 * n_sl) * 2u;
 #pragma unroll
     for (int k = 0; k < NAI; ++k) p_voff[k] = woff[k] + kofs;
     p_halo = n_tap >= 3 && n_sl + 1 < nsl;
@@ -161,10 +175,14 @@ __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
                                            a_lane_off);
   };
   const int bcol = lane & 15, bch = lane >> 4;
+  // B fragment of halo tile row k (= output tile row + ky) at column shift kx
+  auto rdBk = [&](int sl, int kx, int k) __attribute__((always_inline)) {
+    const int hr = (wpx * 8 + k) * 18 + bcol + kx;
+    return *reinterpret_cast<const uint4*>(lds_c + RING + (sl & 1) * kHaloBytes + hr * 64 + ((bch ^ hhswz(hr)) << 4));
+  };
   auto rdB = [&](int sl, int tap, int j) __attribute__((always_inline)) {
     const int ky = tap / 3, kx = tap - 3 * (tap / 3);
-    const int hr = (wpx * 8 + j + ky) * 18 + bcol + kx;
-    return *reinterpret_cast<const uint4*>(lds_c + RING + (sl & 1) * kHaloBytes + hr * 64 + ((bch ^ hhswz(hr)) << 4));
+    return rdBk(sl, kx, j + ky);
   };
 
   floatx4 acc[TM][TN];
@@ -191,32 +209,36 @@ __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 
-  uint4 af[TM], bf[TN];
+  constexpr int NB = REUSE ? TN + 2 : TN;
+  uint4 af[TM], bf[NB];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) bf[j] = rdB(0, 0, j);
+  for (int j = 0; j < NB; ++j) bf[j] = rdBk(0, 0, j);
 #pragma unroll
   for (int i = 0; i < GA; ++i) af[i] = rdA(0, i);
 
-  auto mfma = [&](int i, int j) __attribute__((always_inline)) {
+  // MFMA of A fragment i and output column group j at B register b (j + ky under REUSE, else j)
+  auto mfma = [&](int i, int j, int b) __attribute__((always_inline)) {
     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[i]),
-                                                         __builtin_bit_cast(bf16x8_t, bf[j]), acc[i][j], 0, 0, 0);
+                                                         __builtin_bit_cast(bf16x8_t, bf[b]), acc[i][j], 0, 0, 0);
   };
 
-  // the stage whose B fragments are read next (stage s + 1 during body(s)): slice / tap counters
-  int r_sl = 0, r_tap = 1;
+  // the stage whose B fragments are read next (stage s + 1 during body(s); REUSE: the next kx group during
+  // its last stage): slice / tap counters
+  int r_sl = 0, r_tap = REUSE ? 3 : 1;
   // One K stage s.  Groups 0..2: A fragments of the next group read ahead; DMA slots 2..NAI of set s+2 go out
   // after groups 0 and 1.  Hand-over: set s+1 landed (set s+2 may stay in flight: NAI or NAI + 1 DMAs),
   // barrier (every wave is done with stage s-1's ring buffer and, at tap 0, with the previous slice's halo),
   // set s+3 prepared.  Group 3: stage s+1's B fragments read column by column, slots 0..1 of set s+3.
-  auto body = [&](int s, auto tailc) __attribute__((always_inline)) {
+  auto body = [&](int s, auto tailc, auto kyc) __attribute__((always_inline)) {
     constexpr bool TAIL = decltype(tailc)::value;
+    constexpr int KY = decltype(kyc)::value;          // REUSE: the stage's ky (B register shift); else 0
 #pragma unroll
     for (int g = 0; g < 3; ++g) {
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
 #pragma unroll
-        for (int i = 0; i < GA; ++i) mfma(g * GA + i, j);
+        for (int i = 0; i < GA; ++i) mfma(g * GA + i, j, j + KY);
         if (j == 1) {
 #pragma unroll
           for (int i = 0; i < GA; ++i) af[(g + 1) * GA + i] = rdA(s, (g + 1) * GA + i);
@@ -235,11 +257,16 @@ __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
     else prepare_live(s + STAGES - 1);
     const int rsl = r_sl, rtp = r_tap;
     __builtin_amdgcn_s_setprio(1);
+    if constexpr (REUSE && KY == 2) {   // the next kx group's 10 rows: 0..1 now (unused by ky 2), k + 2 after column k
+      bf[0] = rdBk(rsl, rtp / 3, 0);
+      bf[1] = rdBk(rsl, rtp / 3, 1);
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
 #pragma unroll
-      for (int i = 0; i < GA; ++i) mfma(3 * GA + i, j);
-      bf[j] = rdB(rsl, rtp, j);
+      for (int i = 0; i < GA; ++i) mfma(3 * GA + i, j, j + KY);
+      if constexpr (!REUSE) bf[j] = rdB(rsl, rtp, j);
+      else if constexpr (KY == 2) bf[j + 2] = rdBk(rsl, rtp / 3, j + 2);
       if (j == 1) {
 #pragma unroll
         for (int i = 0; i < GA; ++i) af[i] = rdA(s + 1, i);
@@ -248,13 +275,31 @@ __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
       if (j == 5) slot_dma(std::integral_constant<int, 1>{});
     }
     __builtin_amdgcn_s_setprio(0);
-    const int tp = r_tap + 1;
-    r_tap = tp == 9 ? 0 : tp;
-    r_sl += tp == 9 ? 1 : 0;
+    if (!REUSE || KY == 2) {
+      const int tp = r_tap + (REUSE ? 3 : 1);
+      r_tap = tp == 9 ? 0 : tp;
+      r_sl += tp == 9 ? 1 : 0;
+    }
   };
-  for (int s = 0; s < nS - (STAGES - 1); ++s) body(s, std::false_type{});
+  using F = std::false_type;
+  using T = std::true_type;
+  using K0 = std::integral_constant<int, 0>;
+  using K1 = std::integral_constant<int, 1>;
+  using K2 = std::integral_constant<int, 2>;
+  if constexpr (REUSE) {   // kx groups of three stages; the last group prepares the sets past the end
+    for (int s = 0; s < nS - 3; s += 3) {
+      body(s, F{}, K0{});
+      body(s + 1, F{}, K1{});
+      body(s + 2, F{}, K2{});
+    }
+    body(nS - 3, T{}, K0{});
+    body(nS - 2, T{}, K1{});
+    body(nS - 1, T{}, K2{});
+  } else {
+    for (int s = 0; s < nS - (STAGES - 1); ++s) body(s, F{}, K0{});
 #pragma unroll
-  for (int q = STAGES - 1; q >= 1; --q) body(nS - q, std::true_type{});
+    for (int q = STAGES - 1; q >= 1; --q) body(nS - q, T{}, K0{});
+  }
   hvm<0>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -332,7 +377,7 @@ __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
   }
 }
 
-template <int BCO>
+template <int BCO, bool REUSE>
 static int launch_hw(const ConvArgs& a, hipStream_t s) {
   const hiseg_conv2d_desc& d = a.d;
   const int tiles = d.N * ((d.H + 15) / 16) * ((d.W + 15) / 16);
@@ -342,8 +387,9 @@ static int launch_hw(const ConvArgs& a, hipStream_t s) {
   const size_t lds = ring_halo > epi ? ring_halo : epi;
   const bool res = d.residual != nullptr;
   const bool relu = d.act == HISEG_ACT_RELU;
-  auto kern = res ? (relu ? conv_hw_kernel<BCO, HISEG_ACT_RELU, true> : conv_hw_kernel<BCO, HISEG_ACT_NONE, true>)
-                  : (relu ? conv_hw_kernel<BCO, HISEG_ACT_RELU, false> : conv_hw_kernel<BCO, HISEG_ACT_NONE, false>);
+  auto kern = res ? (relu ? conv_hw_kernel<BCO, HISEG_ACT_RELU, true, REUSE> : conv_hw_kernel<BCO, HISEG_ACT_NONE, true, REUSE>)
+                  : (relu ? conv_hw_kernel<BCO, HISEG_ACT_RELU, false, REUSE>
+                          : conv_hw_kernel<BCO, HISEG_ACT_NONE, false, REUSE>);
   static bool attr_set[2][2] = {};
   bool& done = attr_set[res ? 1 : 0][relu ? 1 : 0];
   if (!done) {
@@ -354,8 +400,16 @@ static int launch_hw(const ConvArgs& a, hipStream_t s) {
   return hiseg_check_launch("conv_hw");
 }
 
+#if HISEG_HW_PART == 2
+int launch_hw128(const ConvArgs& a, hipStream_t s, bool reuse) {
+  return reuse ? launch_hw<128, true>(a, s) : launch_hw<128, false>(a, s);
+}
+#else
+int launch_hw128(const ConvArgs& a, hipStream_t s, bool reuse);   // conv_hw128.hip
+
 // Returns 1 if launched, 0 if the layer does not qualify (caller falls back), <0 on error.
-// variant 80 = BCO 256 (Cout a multiple of 256), 82 = BCO 128.
+// variant 80 = BCO 256 (Cout a multiple of 256), 82 = BCO 128; 84 / 86 the same with the kx-major tap order and
+// B-fragment reuse across ky.
 int conv_hw_try(const ConvArgs& a, hipStream_t s, int variant) {
   const hiseg_conv2d_desc& d = a.d;
   if (d.dtype != HISEG_BF16 || d.out_dtype != HISEG_BF16) return 0;
@@ -372,11 +426,14 @@ int conv_hw_try(const ConvArgs& a, hipStream_t s, int variant) {
   if (span_a >= 0x7fffffffll || span_w >= 0x7fffffffll || span_r >= 0x7fffffffll) return 0;
   int r;
   switch (variant) {
-    case 80: if (d.Cout % 256) return 0; r = launch_hw<256>(a, s); break;
-    case 82: r = launch_hw<128>(a, s); break;
+    case 80: if (d.Cout % 256) return 0; r = launch_hw<256, false>(a, s); break;
+    case 82: r = launch_hw128(a, s, false); break;
+    case 84: if (d.Cout % 256) return 0; r = launch_hw<256, true>(a, s); break;
+    case 86: r = launch_hw128(a, s, true); break;
     default: return 0;
   }
   return r < 0 ? r : 1;
 }
+#endif
 
 }  // namespace hiseg

@@ -637,7 +637,7 @@ HW_CASES = {
 }
 
 
-@pytest.mark.parametrize("variant", [80, 82])
+@pytest.mark.parametrize("variant", [80, 82, 84, 86])
 @pytest.mark.parametrize("name", list(HW_CASES))
 def test_conv_halo_wide_within_bf16(name, variant):
     from hiseg import ops

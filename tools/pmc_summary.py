@@ -5,8 +5,8 @@ FETCH_SIZE counts half the bytes of wide coalesced reads (MI355X_MICROARCH.md §
 side is doubled.  Launches are selected by kernel-name substring and grid size; only the top
 duration cluster (>= 0.7 x the longest) is kept, which drops cold first launches' outliers.
 
-Round-2 dominant class: tools/conv_one.py --shape res256_3x3_64x48 --variants 82, i.e. the halo-tiled
-kernel conv_hw_kernel<128, 1, true> on the residual 256->256 3x3 conv at the 64x48 ROI grid over 256 ROIs
+Round-2 dominant class: tools/conv_one.py --shape res256_3x3_64x48 --variants 86, i.e. the halo-tiled
+kernel conv_hw_kernel<128, 1, true, true> (B-fragment reuse across ky) on the residual 256->256 3x3 conv at the 64x48 ROI grid over 256 ROIs
 (grid 3072 pixel tiles x 2 Cout tiles = 6144 workgroups x 256 lanes); v1 of round 2 (profiles/r2_v1_*)
 measured conv_wide_kernel<256, 4, 1, true> (--variants 70, "conv_wide_kernel<256, 4" 786432).
 Usage: python tools/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write [kernel-substring grid alg-bytes]
@@ -16,7 +16,7 @@ import json
 import statistics
 import sys
 
-KERNEL = "conv_hw_kernel<128, 1, true>"
+KERNEL = "conv_hw_kernel<128, 1, true, true>"
 GRID = 6144 * 256
 PX = 256 * 64 * 48
 # in + residual + out activations (bf16) + weights: the algorithmic bytes of the residual launch
