@@ -20,9 +20,10 @@
 // ds_read_b128 fragment read of 16 consecutive rows from any start (a tap's window starts anywhere).
 //
 // Built twice (Makefile): this file (HISEG_HW_PART 1: BCO 256, accumulators in AGPRs, and conv_hw_try) and
-// conv_hw128.hip (HISEG_HW_PART 2: BCO 128 with -amdgpu-mfma-vgpr-form -- 128 accumulators in VGPRs keep
+// conv_hw128.hip (HISEG_HW_PART 2: BCO 128 and 64 with -amdgpu-mfma-vgpr-form -- 128 accumulators in VGPRs keep
 // every configuration at two waves per SIMD; the AGPR form allocates 192 AGPRs and drops the B-reuse
-// residual kernels to one).
+// residual kernels to one).  BCO 64 arranges the 4 waves as 1 (Cout) x 4 (pixel): 64 Cout x 64 pixels per wave,
+// one weight piece per wave per stage, the same halo.
 #include <type_traits>
 
 #include "conv_common.h"
@@ -58,8 +59,10 @@ constexpr int kHaloBytes = 24 * 1024;      // 24 pieces of 16 rows x 64 B (rows 
 template <int BCO, int ACT, bool RES, bool REUSE>
 __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
   constexpr int STAGES = 4;
-  constexpr int TM = BCO / 32;        // A (Cout) fragments per wave
-  constexpr int TN = 8;               // B (pixel) fragments per wave: 8 tile rows of 16 pixels
+  constexpr int WPX = BCO == 64 ? 4 : 2;   // pixel waves (BCO 64: 1 x 4 waves, else 2 x 2)
+  constexpr int TM = BCO * WPX / 64;  // A (Cout) fragments per wave
+  constexpr int TN = 16 / WPX;        // B (pixel) fragments per wave: TN tile rows of 16 pixels
+  constexpr int J0 = TN >= 8 ? 3 : 1, J1 = TN >= 8 ? 5 : 2;   // columns of group 3 issuing DMA slots 0 / 1
   constexpr int GA = TM / 4;          // A fragments per MFMA group
   constexpr int NAI = BCO / 64;       // weight DMA pieces per wave per stage
   constexpr int STAGE_BYTES = BCO * 64;
@@ -71,7 +74,7 @@ __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wco = w >> 1, wpx = w & 1;
+  const int wco = w / WPX, wpx = w % WPX;
 
   // ---- XCD-major bijective remap; Cout tiles fastest, then the 16 x 16 pixel tiles of an image row-major
   const int nco = d.Cout_pad / BCO;
@@ -177,7 +180,7 @@ __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
   const int bcol = lane & 15, bch = lane >> 4;
   // B fragment of halo tile row k (= output tile row + ky) at column shift kx
   auto rdBk = [&](int sl, int kx, int k) __attribute__((always_inline)) {
-    const int hr = (wpx * 8 + k) * 18 + bcol + kx;
+    const int hr = (wpx * TN + k) * 18 + bcol + kx;
     return *reinterpret_cast<const uint4*>(lds_c + RING + (sl & 1) * kHaloBytes + hr * 64 + ((bch ^ hhswz(hr)) << 4));
   };
   auto rdB = [&](int sl, int tap, int j) __attribute__((always_inline)) {
@@ -204,8 +207,9 @@ __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
   }
   prepare(STAGES - 2);
   slot_dma(std::integral_constant<int, 0>{}); slot_dma(std::integral_constant<int, 1>{});
-  // halo 0 and set 0 landed; set 1 (NAI, tap 1: no halo) and set 2's slots 0..1 may stay in flight
-  hvm<NAI + 2>();
+  // halo 0 and set 0 landed; set 1 (NAI, tap 1: no halo) and set 2's slots 0..1 (min(NAI, 2) weight pieces:
+  // tap 2 has no halo piece) may stay in flight
+  hvm<NAI + (NAI < 2 ? NAI : 2)>();
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 
@@ -271,8 +275,8 @@ __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
 #pragma unroll
         for (int i = 0; i < GA; ++i) af[i] = rdA(s + 1, i);
       }
-      if (j == 3) slot_dma(std::integral_constant<int, 0>{});
-      if (j == 5) slot_dma(std::integral_constant<int, 1>{});
+      if (j == J0) slot_dma(std::integral_constant<int, 0>{});
+      if (j == J1) slot_dma(std::integral_constant<int, 1>{});
     }
     __builtin_amdgcn_s_setprio(0);
     if (!REUSE || KY == 2) {
@@ -306,12 +310,13 @@ __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
   asm volatile("" ::: "memory");
 
   // ---- epilogue through LDS (as conv_wide's non-prefetching path): the output tile as 256 pixel rows x BCO
-  // bf16, 16-B chunk c of row r at slot c ^ (r & 15); the residual tile arrives there by LDS-DMA, each lane
+  // bf16, 16-B chunk c of row r at slot c ^ (r & SWM) (SWM = min(BCO / 8, 16) - 1); the residual tile arrives there by LDS-DMA, each lane
   // turns its accumulator quads into bf16 output quads in place, whole rows leave by 16-B stores.  Tile row
   // r = pixel (y0 + r / 16, x0 + r % 16); rows outside the image are neither read nor written.
   constexpr int EROWB = BCO * 2;
   constexpr int CPR = BCO / 8;
   constexpr int RPI = 64 / CPR;
+  constexpr int SWM = (CPR < 16 ? CPR : 16) - 1;   // chunk swizzle mask (stays inside the row)
   char* tile = reinterpret_cast<char*>(smem);
   auto px_of = [&](int r) __attribute__((always_inline)) -> int {   // GEMM row of tile row r, or -1
     const int y = y0 + (r >> 4), x = x0 + (r & 15);
@@ -327,7 +332,7 @@ __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
     for (int k = 0; k < NRI; ++k) {
       const int r = RPI * (w + 4 * k) + lane / CPR;
       const int px = px_of(r);
-      const unsigned off = px >= 0 ? (unsigned)((px * d.r_cstride + d.r_coff + co0 + ((c ^ (r & 15)) * 8)) * 2) : OOB;
+      const unsigned off = px >= 0 ? (unsigned)((px * d.r_cstride + d.r_coff + co0 + ((c ^ (r & SWM)) * 8)) * 2) : OOB;
       dma16h(rR, lds_base + (unsigned)(RPI * (w + 4 * k) * EROWB), off);
     }
     hvm<0>();
@@ -348,7 +353,7 @@ __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
     for (int j = 0; j < TN; ++j) {
       const int cl = wco * TM * 16 + i * 16 + (lane >> 4) * 4;
       const int r = wpx * TN * 16 + j * 16 + (lane & 15);
-      char* q = tile + r * EROWB + ((((cl >> 3) ^ (r & 15)) << 4) | ((cl & 4) << 1));
+      char* q = tile + r * EROWB + ((((cl >> 3) ^ (r & SWM)) << 4) | ((cl & 4) << 1));
       const floatx4 ac = acc[i][j];
       float v[4];
       uint2 rv = make_uint2(0u, 0u);
@@ -371,7 +376,7 @@ __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
     const int idx = t + 256 * k;
     const int r = idx / CPR, c = idx % CPR;
     const int px = px_of(r), co = co0 + 8 * c;
-    const uint4 v = *reinterpret_cast<const uint4*>(tile + r * EROWB + ((c ^ (r & 15)) << 4));
+    const uint4 v = *reinterpret_cast<const uint4*>(tile + r * EROWB + ((c ^ (r & SWM)) << 4));
     if (px >= 0 && co < d.Cout)
       *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(d.out) + (long long)px * d.o_cstride + d.o_coff + co) = v;
   }
@@ -404,12 +409,17 @@ static int launch_hw(const ConvArgs& a, hipStream_t s) {
 int launch_hw128(const ConvArgs& a, hipStream_t s, bool reuse) {
   return reuse ? launch_hw<128, true>(a, s) : launch_hw<128, false>(a, s);
 }
+int launch_hw64(const ConvArgs& a, hipStream_t s, bool reuse) {
+  return reuse ? launch_hw<64, true>(a, s) : launch_hw<64, false>(a, s);
+}
 #else
 int launch_hw128(const ConvArgs& a, hipStream_t s, bool reuse);   // conv_hw128.hip
+int launch_hw64(const ConvArgs& a, hipStream_t s, bool reuse);
 
 // Returns 1 if launched, 0 if the layer does not qualify (caller falls back), <0 on error.
 // variant 80 = BCO 256 (Cout a multiple of 256), 82 = BCO 128; 84 / 86 the same with the kx-major tap order and
-// B-fragment reuse across ky.
+// B-fragment reuse across ky; 88 / 89 = BCO 64 (1 x 4 waves of 64 Cout x 64 pixels; 64-multiple Cout) without /
+// with the reuse.
 int conv_hw_try(const ConvArgs& a, hipStream_t s, int variant) {
   const hiseg_conv2d_desc& d = a.d;
   if (d.dtype != HISEG_BF16 || d.out_dtype != HISEG_BF16) return 0;
@@ -418,7 +428,8 @@ int conv_hw_try(const ConvArgs& a, hipStream_t s, int variant) {
   if (d.act != HISEG_ACT_NONE && d.act != HISEG_ACT_RELU) return 0;
   if (d.Ca % 32 != 0 || d.Ca < 64 || d.K_pad != 9 * d.Ca) return 0;
   if ((d.a_cstride | d.a_coff) & 7) return 0;
-  if ((d.Cout & 127) || ((d.o_cstride | d.o_coff) & 7) || (d.residual && ((d.r_cstride | d.r_coff) & 7))) return 0;
+  const int cmul = variant >= 88 ? 63 : 127;
+  if ((d.Cout & cmul) || ((d.o_cstride | d.o_coff) & 7) || (d.residual && ((d.r_cstride | d.r_coff) & 7))) return 0;
   if ((((uintptr_t)d.scale | (uintptr_t)d.shift | (uintptr_t)d.out | (uintptr_t)d.residual) & 15)) return 0;
   const long long span_a = (long long)d.N * d.H * d.W * d.a_cstride * 2;
   const long long span_w = (long long)d.Cout_pad * d.K_pad * 2;
@@ -430,6 +441,8 @@ int conv_hw_try(const ConvArgs& a, hipStream_t s, int variant) {
     case 82: r = launch_hw128(a, s, false); break;
     case 84: if (d.Cout % 256) return 0; r = launch_hw<256, true>(a, s); break;
     case 86: r = launch_hw128(a, s, true); break;
+    case 88: r = launch_hw64(a, s, false); break;
+    case 89: r = launch_hw64(a, s, true); break;
     default: return 0;
   }
   return r < 0 ? r : 1;

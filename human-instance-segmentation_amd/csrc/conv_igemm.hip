@@ -261,7 +261,8 @@ extern "C" int hiseg_conv2d_fwd(const hiseg_conv2d_desc* d, hiseg_stream_t strea
 // -DHISEG_DIAG build (Makefile DIAG=1).
 static bool release_variant(int v) {
   return v == -1 || v == 0 || (v >= 1 && v <= 8) || v == 50 || v == 51 || v == 52 || v == 54 || v == 58 ||
-         (v >= 60 && v <= 69) || v == 70 || v == 71 || v == 72 || v == 74 || v == 80 || v == 82 || v == 84 || v == 86;
+         (v >= 60 && v <= 69) || v == 70 || v == 71 || v == 72 || v == 74 || v == 80 || v == 82 || v == 84 || v == 86 ||
+         v == 88 || v == 89;
 }
 
 extern "C" int hiseg_conv2d_fwd_variant(const hiseg_conv2d_desc* d, int variant, hiseg_stream_t stream) {
@@ -385,11 +386,12 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
     // 3x3 single-source layers with 128-multiple Cout: the halo-tiled kernel, BCO 128 with B-fragment reuse
     // across ky (conv_hw.hip, variant 86: two workgroups per CU; tools/conv_bench.py: 0.85 vs 1.02 ms (wide
     // kernel) on the 256->256 @64x48 x256 ROI class, 1.01 vs 1.37 ms on 128->128 @128x96, 0.44 vs 0.54 ms on
-    // 128->256; channel-major K order, within bf16 rounding)
+    // 128->256; channel-major K order, within bf16 rounding); 64-multiple Cout: its BCO-64 configuration (variant
+    // 89: 0.104 vs 0.140 ms on the 64->64 residual class, 0.26 vs 0.43 ms on 256->64)
     // HISEG_CONV_HALO=0 keeps the tap-major kernels (A/B timing only)
     static const bool halo = [] { const char* e = getenv("HISEG_CONV_HALO"); return !(e && atoi(e) == 0); }();
     if (v == 0 && !four_waves && halo) {
-      const int r = conv_hw_try(a, s, 86);
+      const int r = conv_hw_try(a, s, d->Cout % 128 ? 89 : 86);
       if (r != 0) return r < 0 ? r : HISEG_OK;
     }
     if (v == 0 && d->Cout % 256 == 0 && d->KH * d->KW > 1 && !four_waves) {

@@ -94,7 +94,7 @@ __device__ __forceinline__ float silu_grad_pre(const hiseg_bn_bwd_desc& d, float
 
 // The derivative is taken at the forward's own pre-activation z*fwd_scale + fwd_shift (+ residual) when the
 // folded affine is given and the activation needs it (smooth ones; ReLU after a residual add with the residual).
-__device__ __forceinline__ bool bn_pre_path(const hiseg_bn_bwd_desc& d) {
+__host__ __device__ __forceinline__ bool bn_pre_path(const hiseg_bn_bwd_desc& d) {
   return d.fwd_scale && (act_smooth(d.act) || (d.act == HISEG_ACT_RELU && (!d.dres || d.residual)));
 }
 
@@ -314,40 +314,67 @@ __global__ void __launch_bounds__(256) bn_apply_vec_kernel(hiseg_bn_apply_desc d
   }
 }
 
+// How the backward pass gets act'(.) (bn_bwd_mode on the host; a template argument so the per-element loop
+// carries no activation switch and the per-channel tables live in registers, loaded once per thread):
+//   kGNone  identity;  kGY  act'(y) from the stored output (ReLU / Sigmoid, no folded affine given);
+//   kGReLU  ReLU mask at the forward's pre-activation z*fwd_scale + fwd_shift (+ residual);
+//   kGPre   any activation's derivative at that pre-activation (smooth ones; SiLU without the forward's tables
+//           folds them here from mean / invstd / gamma / beta).
+enum { kGNone = 0, kGY = 1, kGReLU = 2, kGPre = 3 };
+
+__host__ __device__ __forceinline__ int bn_bwd_mode(const hiseg_bn_bwd_desc& d) {
+  if (d.act == HISEG_ACT_NONE) return kGNone;
+  if (bn_pre_path(d)) return d.act == HISEG_ACT_RELU ? kGReLU : kGPre;
+  if (d.act == HISEG_ACT_SILU) return kGPre;
+  return kGY;
+}
+
+// the pre-activation's per-channel affine of chunk c (modes kGReLU / kGPre)
+template <int V>
+__device__ __forceinline__ void bn_pre_tables(const hiseg_bn_bwd_desc& d, int c, float* fs, float* fh) {
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    if (d.fwd_scale) {
+      fs[k] = d.fwd_scale[c + k];
+      fh[k] = d.fwd_shift[c + k];
+    } else {
+      const float kk = d.invstd[c + k] * (d.gamma ? d.gamma[c + k] : 1.f);
+      fs[k] = kk;
+      fh[k] = (d.beta ? d.beta[c + k] : 0.f) - d.mean[c + k] * kk;
+    }
+  }
+}
+
 // g = dy (* chan_mul) * act'(.) for one 16-B chunk; z = the chunk's pre-BN values (already loaded)
-template <typename T>
-__device__ __forceinline__ void bn_gv(const hiseg_bn_bwd_desc& d, long long p, int c, float* g, const float* z) {
+template <typename T, int MODE>
+__device__ __forceinline__ void bn_gv(const hiseg_bn_bwd_desc& d, int p, int c, float* g, const float* z,
+                                      const float* fs, const float* fh) {
   constexpr int V = Chunk<T>::N;
-  ldv<T>(d.dy, p * d.dy_cstride + d.dy_coff + c, g);
+  ldv<T>(d.dy, (long long)p * d.dy_cstride + d.dy_coff + c, g);
   if (d.chan_mul) {
-    const float* cm = d.chan_mul + (long long)((int)p / d.HW) * d.C + c;
+    const float* cm = d.chan_mul + (long long)(p / d.HW) * d.C + c;
 #pragma unroll
     for (int k = 0; k < V; ++k) g[k] *= cm[k];
   }
-  if (bn_pre_path(d)) {   // at the forward's pre-activation (+ residual)
+  if constexpr (MODE == kGReLU || MODE == kGPre) {
     float rr[V];
-    if (d.residual) ldv<T>(d.residual, p * d.r_cstride + d.r_coff + c, rr);
+    if (d.residual) ldv<T>(d.residual, (long long)p * d.r_cstride + d.r_coff + c, rr);
 #pragma unroll
     for (int k = 0; k < V; ++k) {
-      float v = z[k] * d.fwd_scale[c + k] + d.fwd_shift[c + k];
+      float v = z[k] * fs[k] + fh[k];
       if (d.residual) v += rr[k];
-      g[k] *= act_grad_pre(v, d.act, d.act_beta);
+      if constexpr (MODE == kGReLU) g[k] = v > 0.f ? g[k] : 0.f;
+      else g[k] *= act_grad_pre(v, d.act, d.act_beta);
     }
-  } else if (d.act == HISEG_ACT_SILU) {   // SiLU'(v) needs the pre-activation: v = xhat * gamma + beta from z
-#pragma unroll
-    for (int k = 0; k < V; ++k) g[k] *= silu_grad_pre(d, z[k], c + k);
-  } else if (d.act == HISEG_ACT_RELU && d.fwd_scale && !d.dres) {   // the forward's mask, from z
-#pragma unroll
-    for (int k = 0; k < V; ++k) g[k] = (z[k] * d.fwd_scale[c + k] + d.fwd_shift[c + k] > 0.f) ? g[k] : 0.f;
-  } else if (d.act != HISEG_ACT_NONE) {
+  } else if constexpr (MODE == kGY) {
     float y[V];
-    ldv<T>(d.y, p * d.y_cstride + d.y_coff + c, y);
+    ldv<T>(d.y, (long long)p * d.y_cstride + d.y_coff + c, y);
 #pragma unroll
     for (int k = 0; k < V; ++k) g[k] *= act_grad(y[k], d.act);
   }
 }
 
-template <typename T>
+template <typename T, int MODE>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_vec_kernel(hiseg_bn_bwd_desc d) {
   constexpr int V = Chunk<T>::N;
   __shared__ float sh[256 * 3 * V];
@@ -365,13 +392,14 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_vec_kernel(hiseg_bn_bwd_des
 #pragma unroll
   for (int k = 0; k < V; ++k) s1[k] = s2[k] = s3[k] = 0.f;
   if (r < R && ch < NCH) {
-    float mu[V], inv[V];
+    float mu[V], inv[V], fs[V], fh[V];
 #pragma unroll
     for (int k = 0; k < V; ++k) { mu[k] = d.mean[c + k]; inv[k] = d.invstd[c + k]; }
-    for (long long p = b + r; p < e; p += R) {
+    if constexpr (MODE == kGReLU || MODE == kGPre) bn_pre_tables<V>(d, c, fs, fh);
+    for (int p = (int)b + r; p < (int)e; p += R) {
       float g[V], z[V];
-      ldv<T>(d.z, p * d.z_cstride + d.z_coff + c, z);
-      bn_gv<T>(d, p, c, g, z);
+      ldv<T>(d.z, (long long)p * d.z_cstride + d.z_coff + c, z);
+      bn_gv<T, MODE>(d, p, c, g, z, fs, fh);
 #pragma unroll
       for (int k = 0; k < V; ++k) {
         const float xh = (z[k] - mu[k]) * inv[k];
@@ -426,7 +454,7 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_par_kernel(hiseg_bn_bwd_d
   }
 }
 
-template <typename T>
+template <typename T, int MODE>
 __global__ void __launch_bounds__(256) bn_bwd_apply_vec_kernel(hiseg_bn_bwd_desc d, int S) {
   constexpr int V = Chunk<T>::N;
   const int C = d.C;
@@ -439,17 +467,18 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_vec_kernel(hiseg_bn_bwd_desc
   if (r >= R || ch >= NCH) return;
   const int c = ch * V;
   const float* coef = d.partial + (long long)S * 3 * C;
-  float k0[V], k1[V], k2[V], mu[V], inv[V];
+  float k0[V], k1[V], k2[V], mu[V], inv[V], fs[V], fh[V];
 #pragma unroll
   for (int k = 0; k < V; ++k) {
     k0[k] = coef[c + k]; k1[k] = coef[C + c + k]; k2[k] = coef[2 * C + c + k];
     mu[k] = d.mean[c + k]; inv[k] = d.invstd[c + k];
   }
+  if constexpr (MODE == kGReLU || MODE == kGPre) bn_pre_tables<V>(d, c, fs, fh);
   const int P = (int)d.P;
   for (int p = blockIdx.x * R + r; p < P; p += gridDim.x * R) {
     float g[V], z[V], o[V];
     ldv<T>(d.z, (long long)p * d.z_cstride + d.z_coff + c, z);
-    bn_gv<T>(d, p, c, g, z);
+    bn_gv<T, MODE>(d, p, c, g, z, fs, fh);
 #pragma unroll
     for (int k = 0; k < V; ++k) o[k] = k0[k] * (g[k] - k1[k] - (z[k] - mu[k]) * inv[k] * k2[k]);
     stv<T>(d.dz, (long long)p * d.dz_cstride + d.dz_coff + c, o);
@@ -1057,9 +1086,21 @@ extern "C" int hiseg_bn_bwd(const hiseg_bn_bwd_desc* d, hiseg_stream_t stream) {
       vec_ok(dt, C, d->z, d->z_cstride, d->z_coff) && vec_ok(dt, C, d->dz, d->dz_cstride, d->dz_coff) &&
       vec_ok(dt, C, d->dres, d->dres_cstride, d->dres_coff) && vec_ok(dt, C, d->residual, d->r_cstride, d->r_coff)) {
     const int V = dt == HISEG_BF16 ? 8 : 4;
-    DISPATCH_T(dt, hipLaunchKernelGGL(bn_bwd_reduce_vec_kernel<T>, dim3(S, (C / V + 255) / 256), dim3(256), 0, s, *d));
-    hipLaunchKernelGGL(bn_bwd_finalize_par_kernel, dim3(C), dim3(256), 0, s, *d, S);
-    DISPATCH_T(dt, hipLaunchKernelGGL(bn_bwd_apply_vec_kernel<T>, vec_grid(d->P, C, dt), dim3(256), 0, s, *d, S));
+    const dim3 rgrid(S, (C / V + 255) / 256), agrid = vec_grid(d->P, C, dt);
+    const int mode = bn_bwd_mode(*d);
+#define BN_BWD_VEC(M)                                                                                         \
+  do {                                                                                                        \
+    DISPATCH_T(dt, hipLaunchKernelGGL((bn_bwd_reduce_vec_kernel<T, M>), rgrid, dim3(256), 0, s, *d));         \
+    hipLaunchKernelGGL(bn_bwd_finalize_par_kernel, dim3(C), dim3(256), 0, s, *d, S);                          \
+    DISPATCH_T(dt, hipLaunchKernelGGL((bn_bwd_apply_vec_kernel<T, M>), agrid, dim3(256), 0, s, *d, S));       \
+  } while (0)
+    switch (mode) {
+      case kGNone: BN_BWD_VEC(kGNone); break;
+      case kGY: BN_BWD_VEC(kGY); break;
+      case kGReLU: BN_BWD_VEC(kGReLU); break;
+      default: BN_BWD_VEC(kGPre); break;
+    }
+#undef BN_BWD_VEC
     return hiseg_check_launch("bn_bwd");
   }
   DISPATCH_T(d->dtype, hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(S, (d->C + 255) / 256), dim3(256), 0, s, *d));
