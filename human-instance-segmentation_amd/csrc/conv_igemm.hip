@@ -244,6 +244,7 @@ int conv_8ph_try(const ConvArgs& a, hipStream_t s, int variant);
 #endif
 int conv_wide_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_hw_try(const ConvArgs& a, hipStream_t s, int variant);
+int conv_pw_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_small_try(const ConvArgs& a, hipStream_t s, int variant);
 }
 
@@ -262,7 +263,7 @@ extern "C" int hiseg_conv2d_fwd(const hiseg_conv2d_desc* d, hiseg_stream_t strea
 static bool release_variant(int v) {
   return v == -1 || v == 0 || (v >= 1 && v <= 8) || v == 50 || v == 51 || v == 52 || v == 54 || v == 58 ||
          (v >= 60 && v <= 69) || v == 70 || v == 71 || v == 72 || v == 74 || v == 80 || v == 82 || v == 84 || v == 86 ||
-         v == 88 || v == 89;
+         v == 88 || v == 89 || v == 90;
 }
 
 extern "C" int hiseg_conv2d_fwd_variant(const hiseg_conv2d_desc* d, int variant, hiseg_stream_t stream) {
@@ -347,7 +348,10 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
   // Automatic choice (variant 0) = the fastest measured configuration per layer class
   // (tools/conv_bench.py): LDS-DMA ring kernel, 128x128 tiles for Cout >= 128, 64x128 for 64.
   // Experimental kernels (halo / halo2 / halo3) run only when forced by variant.
-  if (variant >= 80 && variant < 90) {
+  if (variant == 90) {
+    const int r = conv_pw_try(a, s, variant);
+    if (r != 0) return r < 0 ? r : HISEG_OK;
+  } else if (variant >= 80 && variant < 90) {
     const int r = conv_hw_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
   } else if (variant >= 70 && variant < 80) {
@@ -390,6 +394,14 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
     // 89: 0.104 vs 0.140 ms on the 64->64 residual class, 0.26 vs 0.43 ms on 256->64)
     // HISEG_CONV_HALO=0 keeps the tap-major kernels (A/B timing only)
     static const bool halo = [] { const char* e = getenv("HISEG_CONV_HALO"); return !(e && atoi(e) == 0); }();
+    // 1x1 layers and the ConvTranspose GEMM with 256-multiple GEMM columns: the persistent pointwise kernel
+    // (conv_pw.hip, variant 90: weights resident in LDS, activations streamed into MFMA registers;
+    // tools/conv_bench.py: 0.205 vs 0.308 ms on 256->256 @64x48 x256 ROIs, 0.21 vs 0.34 ms on the 256+8
+    // combiner, 0.16 vs 0.24 ms on 128->256; bit-identical)
+    if (v == 0 && d->KH == 1 && d->KW == 1) {
+      const int r = conv_pw_try(a, s, 90);
+      if (r != 0) return r < 0 ? r : HISEG_OK;
+    }
     if (v == 0 && !four_waves && halo) {
       const int r = conv_hw_try(a, s, d->Cout % 128 ? 89 : 86);
       if (r != 0) return r < 0 ? r : HISEG_OK;

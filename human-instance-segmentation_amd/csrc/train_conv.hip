@@ -500,7 +500,10 @@ static int wgrad_geometry(const hiseg_conv2d_desc* d, int want_bias, int* Cg, in
   const int BK = *Kg >= 128 ? 128 : 64;
   const int BC = *Cg >= 128 ? 128 : *Cg >= 64 ? 64 : *Cg >= 32 ? 32 : 16;
   const long long tiles = (long long)((*Kg + BK - 1) / BK) * ((*Cg + BC - 1) / BC);
-  int sp = (int)((1024 + tiles - 1) / tiles);
+  // about 1024 workgroups but never past it: the wgrad kernels run two workgroups per CU, so 1024 = two full
+  // rounds on 256 CUs, and rounding up (36 tiles x 29 splits = 1044) added a third, nearly empty round that cost
+  // a third of the layer's time
+  int sp = (int)(1024 / tiles);
   if (sp > nblocks) sp = nblocks;
   if (sp < 1) sp = 1;
   *bps = (nblocks + sp - 1) / sp;
@@ -539,56 +542,80 @@ extern "C" int hiseg_conv2d_wgrad(const hiseg_conv2d_desc* fwd, const void* dy, 
   return fwd->dtype == HISEG_BF16 ? wgrad_typed<bf16_t>(a, s) : wgrad_typed<float>(a, s);
 }
 
+// One thread per 4 consecutive K columns of one GEMM column j: float4 partial loads (Kg is a multiple of 64),
+// four splits in flight, then each of the 4 sums scattered to its reference-layout slot.
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* ws, int splits, hiseg_wgrad_map m, float* gw,
                                                            float* gb, int acc) {
   const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
   const int Cin = m.ca + m.cb;
   const int Ktot = m.KH * m.KW * Cin;
   const int ncol = Ktot + (m.want_bias ? 1 : 0);
-  if (idx >= (long long)m.Cout * ncol) return;
-  const int j = (int)(idx / ncol);
-  const int k = (int)(idx - (long long)j * ncol);
+  const int nq4 = (ncol + 3) >> 2;
+  if (idx >= (long long)m.Cout * nq4) return;
+  const int j = (int)(idx / nq4);
+  const int k0 = 4 * (int)(idx - (long long)j * nq4);
   const long long plane = (long long)m.Cg * m.Kg;
-  if (k == Ktot) {  // bias column
-    if (!gb) return;
-    int co = j;
+  const float* src = ws + (long long)j * m.Kg + k0;
+  float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0, s3 = s0;
+  int sp = 0;
+  for (; sp + 4 <= splits; sp += 4) {
+    const float4 a0 = *reinterpret_cast<const float4*>(src + sp * plane);
+    const float4 a1 = *reinterpret_cast<const float4*>(src + (sp + 1) * plane);
+    const float4 a2 = *reinterpret_cast<const float4*>(src + (sp + 2) * plane);
+    const float4 a3 = *reinterpret_cast<const float4*>(src + (sp + 3) * plane);
+    s0.x += a0.x; s0.y += a0.y; s0.z += a0.z; s0.w += a0.w;
+    s1.x += a1.x; s1.y += a1.y; s1.z += a1.z; s1.w += a1.w;
+    s2.x += a2.x; s2.y += a2.y; s2.z += a2.z; s2.w += a2.w;
+    s3.x += a3.x; s3.y += a3.y; s3.z += a3.z; s3.w += a3.w;
+  }
+  for (; sp < splits; ++sp) {
+    const float4 a0 = *reinterpret_cast<const float4*>(src + sp * plane);
+    s0.x += a0.x; s0.y += a0.y; s0.z += a0.z; s0.w += a0.w;
+  }
+  const float tot[4] = {(s0.x + s1.x) + (s2.x + s3.x), (s0.y + s1.y) + (s2.y + s3.y), (s0.z + s1.z) + (s2.z + s3.z),
+                        (s0.w + s1.w) + (s2.w + s3.w)};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int k = k0 + e;
+    if (k >= ncol) break;
+    if (k == Ktot) {  // bias column
+      if (!gb) continue;
+      if (m.convT) {
+        const int C = m.Cout / 4;
+        if (j >= C) continue;  // the q == 0 thread sums the 4 sub-pixel columns
+        float b = 0.f;
+        for (int q = 0; q < 4; ++q) {
+          const int jj = j + q * C;
+          for (int p = 0; p < splits; ++p) b += ws[p * plane + (long long)jj * m.Kg + k];
+        }
+        gb[j] = acc ? gb[j] + b : b;
+      } else {
+        gb[j] = acc ? gb[j] + tot[e] : tot[e];
+      }
+      continue;
+    }
+    long long dst;
     if (m.convT) {
       const int C = m.Cout / 4;
-      if (j >= C) return;  // the q == 0 thread sums the 4 sub-pixel columns
-      co = j;
-    }
-    float s = 0.f;
-    const int nq = m.convT ? 4 : 1;
-    for (int q = 0; q < nq; ++q) {
-      const int jj = j + q * (m.convT ? m.Cout / 4 : 0);
-      for (int sp = 0; sp < splits; ++sp) s += ws[sp * plane + (long long)jj * m.Kg + k];
-    }
-    gb[co] = acc ? gb[co] + s : s;
-    return;
-  }
-  float s = 0.f;
-  for (int sp = 0; sp < splits; ++sp) s += ws[sp * plane + (long long)j * m.Kg + k];
-  long long dst;
-  if (m.convT) {
-    const int C = m.Cout / 4;
-    const int q = j / C, co = j - q * C;
-    if (k >= m.ca_real) return;
-    dst = (((long long)k * C + co) * 2 + (q >> 1)) * 2 + (q & 1);
-  } else {
-    const int tap = k / Cin, cp = k - tap * Cin;
-    int ci;
-    if (cp < m.ca) {
-      if (cp >= m.ca_real) return;
-      ci = cp;
+      const int q = j / C, co = j - q * C;
+      if (k >= m.ca_real) continue;
+      dst = (((long long)k * C + co) * 2 + (q >> 1)) * 2 + (q & 1);
     } else {
-      const int b = cp - m.ca;
-      if (b >= m.cb_real) return;
-      ci = m.ca_real + b;
+      const int tap = k / Cin, cp = k - tap * Cin;
+      int ci;
+      if (cp < m.ca) {
+        if (cp >= m.ca_real) continue;
+        ci = cp;
+      } else {
+        const int b = cp - m.ca;
+        if (b >= m.cb_real) continue;
+        ci = m.ca_real + b;
+      }
+      const int ky = tap / m.KW, kx = tap - ky * m.KW;
+      dst = (((long long)j * (m.ca_real + m.cb_real) + ci) * m.KH + ky) * m.KW + kx;
     }
-    const int ky = tap / m.KW, kx = tap - ky * m.KW;
-    dst = (((long long)j * (m.ca_real + m.cb_real) + ci) * m.KH + ky) * m.KW + kx;
+    gw[dst] = acc ? gw[dst] + tot[e] : tot[e];
   }
-  gw[dst] = acc ? gw[dst] + s : s;
 }
 
 extern "C" int hiseg_conv2d_wgrad_reduce(const float* ws, int splits, const hiseg_wgrad_map* map, float* gw, float* gb,
@@ -596,7 +623,8 @@ extern "C" int hiseg_conv2d_wgrad_reduce(const float* ws, int splits, const hise
   HISEG_REQUIRE(ws && map && gw && splits > 0, HISEG_ERR_BAD_ARG, "wgrad_reduce: null argument");
   const hiseg_wgrad_map m = *map;
   HISEG_REQUIRE(!m.convT || m.Cout % 4 == 0, HISEG_ERR_BAD_SHAPE, "wgrad_reduce: convT Cout");
-  const long long n = (long long)m.Cout * (m.KH * m.KW * (m.ca + m.cb) + (m.want_bias ? 1 : 0));
+  HISEG_REQUIRE(m.Kg % 4 == 0 && al16(ws), HISEG_ERR_BAD_SHAPE, "wgrad_reduce: partial rows must be 16-B aligned");
+  const long long n = (long long)m.Cout * ((m.KH * m.KW * (m.ca + m.cb) + (m.want_bias ? 1 : 0) + 3) / 4);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ws,
                      splits, m, gw, gb, accumulate);
   return hiseg_check_launch("wgrad_reduce");

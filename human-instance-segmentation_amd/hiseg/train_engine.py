@@ -195,7 +195,8 @@ class TrainState:
             dg_cols, dg_k = ca + cb, round_up(kh * kw * cop, 64)
             stride, pad = 1, conv.padding[0]
         cout_pad = round_up(cols, 16)
-        dg_cout_pad = round_up(dg_cols, 16)
+        # data-gradient GEMM columns padded to 64 past 64 (e.g. 256+8 -> 320) so the LDS-DMA kernels take them
+        dg_cout_pad = round_up(dg_cols, 64) if dg_cols > 64 else round_up(dg_cols, 16)
         wf = torch.empty(cout_pad, k_pad, dtype=self.dtype, device=dev)
         wd = torch.empty(dg_cout_pad, dg_k, dtype=self.dtype, device=dev)
         ones = torch.ones(cout_pad, dtype=torch.float32, device=dev)

@@ -169,6 +169,11 @@ VARIANT_CASES = {
     "3x3_128+128_to_256": (2, 128, 128, 256, 9, 7, 3, False, False, False, False),
     "1x1_256_to_128_res": (2, 256, 0, 128, 10, 9, 1, False, True, False, False),
     "3x3_256_smp_decoder0_30x40": (2, 256, 0, 256, 30, 40, 3, False, False, False, False),
+    # the persistent pointwise kernel's classes (variant 90): 4 / 8 / 9 k-steps, ConvTranspose column tiles
+    "1x1_256_to_256_res_ragged": (3, 256, 0, 256, 13, 11, 1, False, True, False, False),
+    "1x1_128_to_256": (2, 128, 0, 256, 9, 7, 1, False, False, False, False),
+    "1x1_256+8_combiner": (2, 256, 8, 256, 9, 7, 1, False, False, False, False),
+    "convT_256_to_128": (2, 256, 0, 128, 5, 7, 1, True, False, False, False),
 }
 
 
@@ -195,7 +200,7 @@ def test_conv_kernel_variants_bit_identical(name):
     outs = {}
     # the automatic choice (variant 0) may take the channel-major halo kernel: checked within bf16 rounding by
     # test_conv_halo_wide_within_bf16 / test_conv_automatic_choice_within_bf16
-    for v in (-1, 1, 2, 3, 4, 5, 6, 7, 8, 61, 62, 66, 67, 68, 69, 70, 71, 72):
+    for v in (-1, 1, 2, 3, 4, 5, 6, 7, 8, 61, 62, 66, 67, 68, 69, 70, 71, 72, 90):
         o2a = ops.Act.new(N, oH, oW, Cout, dt, DEV) if o2 else None
         y = ops.conv2d(p, xa, xb, residual=R, mul=M, out2=o2a, variant=v)
         torch.cuda.synchronize()
@@ -206,6 +211,27 @@ def test_conv_kernel_variants_bit_identical(name):
         assert torch.equal(y, ref), f"variant {v} differs from the generic kernel"
         if o2:
             assert torch.equal(y2, ref2), f"variant {v} out2 differs"
+
+
+@pytest.mark.parametrize("act", [0, 2])
+@pytest.mark.parametrize("shape", [(3, 128, 256, 13, 11), (2, 256, 256, 64, 48)])
+def test_conv_pointwise_gate_mul_bit_identical(shape, act):
+    """The fg_gate form (refinement.py:255-268: 1x1 conv, sigmoid, times the shared features) on the persistent
+    pointwise kernel (variant 90) vs the generic kernel, bit for bit."""
+    from hiseg import ops
+    N, Cin, Cout, H, W = shape
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = ops.Act.from_nchw(torch.randn(N, Cin, H, W, device=DEV, generator=g), dt)
+    w = torch.randn(Cout, Cin, 1, 1, device=DEV, generator=g) / Cin ** 0.5
+    p = ops.pack_conv(w, torch.randn(Cout, device=DEV, generator=g) * 0.1, None, act, dt, DEV, pad=0)
+    m = ops.Act.from_nchw(torch.randn(N, Cout, H, W, device=DEV, generator=g), dt)
+    ref = ops.conv2d(p, x, mul=m, variant=-1).t.clone()
+    y = ops.conv2d(p, x, mul=m, variant=90).t.clone()
+    auto = ops.conv2d(p, x, mul=m, variant=0).t.clone()
+    torch.cuda.synchronize()
+    assert torch.isfinite(ref.float()).all()
+    assert torch.equal(y, ref) and torch.equal(auto, ref)
 
 
 # Narrow / ragged layers (full-resolution decoder, EfficientNet projections) on the halo-tiled

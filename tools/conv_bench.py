@@ -29,6 +29,8 @@ SHAPES = {
     "dec_128+128to128_3x3_32x24": (256, 128, 128, 128, 32, 24, 3, False),
     "c256to256_1x1_64x48": (256, 256, 0, 256, 64, 48, 1, False),
     "comb_256+8to256_1x1_64x48": (256, 256, 8, 256, 64, 48, 1, False),
+    "c128to256_1x1_64x48": (256, 128, 0, 256, 64, 48, 1, False),
+    "res256_1x1_64x48": (256, 256, 0, 256, 64, 48, 1, True),
     "c256to64_3x3_64x48": (256, 256, 0, 64, 64, 48, 3, False),
     "res256_3x3_16x12": (256, 256, 0, 256, 16, 12, 3, True),
     "dec16_3x3_480x640": (32, 16, 0, 16, 480, 640, 3, False),
