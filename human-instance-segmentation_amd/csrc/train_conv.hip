@@ -13,9 +13,10 @@
 // forward kernel's.  Register-staged double buffering, one barrier per pixel block.
 // The pixel dimension is split across workgroups (split-K); every split writes its own f32
 // partial tile (deterministic, no atomics) and hiseg_conv2d_wgrad_reduce sums them.
-// That register-transpose kernel serves f32 (parity), ConvTranspose and GEMM-bias columns; every other
-// bf16 layer takes conv_wgrad_tr_kernel below (LDS-DMA + ds_read_b64_tr_b16, 4.5x faster on the ROI
-// head's 256-channel 3x3 layers).
+// That register-transpose kernel serves f32 (parity) and bf16 two-source layers whose sources are not
+// 128-channel multiples; every other bf16 layer (GEMM-bias columns and ConvTranspose included) takes
+// conv_wgrad_tr_kernel below (LDS-DMA + ds_read_b64_tr_b16, 4.5x faster on the ROI head's 256-channel 3x3
+// layers).
 #include <cstdlib>
 
 #include "conv_common.h"
@@ -260,6 +261,8 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
 typedef short v4s_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4s_t lds_v4s_t;
 typedef __attribute__((address_space(3))) void lds_void_t;
+typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4u_t lds_v4u_t;
 
 __device__ __forceinline__ unsigned trswz(int row, int ch) {
   return 256u * (unsigned)row + 16u * (unsigned)(ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
@@ -310,6 +313,8 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
   // per-lane DMA state: instruction i fills rows 4(w + 4i) .. +3; this lane row (lane >> 4), slot lane & 15
   int xo[4], ky[4], kx[4], yo[4];       // X channel offset (or -1 = zero column), tap; dY column offset (or -1)
   int pn[4], py[4], px[4], pp[4];       // pixel (n, oy, ox) and flat index of the lane's row
+  int yq[4];                            // ConvTranspose: the column's sub-pixel q (output pixel 2y + q/2, 2x + q%2)
+  unsigned bias_lanes = 0;              // bit i: this lane's chunk of instruction i is the GEMM-bias column's
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int r = 4 * (w + 4 * i) + (lane >> 4);
@@ -318,10 +323,18 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
     const int tap = k / a.Cin;
     const int ci = k - tap * a.Cin;
     xo[i] = k < a.Ktot ? coff + ci : -1;
+    if (a.want_bias && k == a.Ktot) bias_lanes |= 1u << i;
     ky[i] = tap / d.KW;
     kx[i] = tap - ky[i] * d.KW;
     const int j = j0 + 8 * c;
-    yo[i] = j < d.Cout ? a.dy_coff + j : -1;
+    yq[i] = 0;
+    if (d.convT) {   // GEMM column j = q * C + co (C % 8 == 0: a chunk never straddles two q)
+      const int C = d.Cout >> 2, q = j / C;
+      yq[i] = q;
+      yo[i] = j < d.Cout ? a.dy_coff + (j - q * C) : -1;
+    } else {
+      yo[i] = j < d.Cout ? a.dy_coff + j : -1;
+    }
     const int p = pb_begin * PB + r;
     pp[i] = p;
     px[i] = p % d.Wo;
@@ -343,7 +356,10 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
       const unsigned offx = okx ? (unsigned)((((pn[i] * Hs + (iy >> sh)) * Ws + (ix >> sh)) * cs + xo[i]) * 2) : OOB;
       wg_dma16(rX, sb + row_base, offx);
       const bool oky = yo[i] >= 0 && pp[i] < a.M;
-      const unsigned offy = oky ? (unsigned)((pp[i] * a.dy_cs + yo[i]) * 2) : OOB;
+      int yp = pp[i];
+      if (d.convT)   // the dY pixel of sub-pixel q: (n, 2y + q/2, 2x + q%2) of the 2H x 2W output grid
+        yp = (pn[i] * (2 * d.Ho) + 2 * py[i] + (yq[i] >> 1)) * (2 * d.Wo) + 2 * px[i] + (yq[i] & 1);
+      const unsigned offy = oky ? (unsigned)((yp * a.dy_cs + yo[i]) * 2) : OOB;
       wg_dma16(rY, sb + IMG + row_base, offy);
       // advance this row by PB pixels
       pp[i] += PB;
@@ -375,6 +391,15 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
       else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * NL) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (bias_lanes) {   // the GEMM-bias column: X = 1 in every row (rows past M meet zero dY), written over the
+                        // DMA's zeros once this stage landed
+      const unsigned sb = lds_base + (unsigned)((it % STAGES) * STAGE);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (bias_lanes & (1u << i))
+          *reinterpret_cast<lds_v4u_t*>((uintptr_t)(sb + 256u * (unsigned)(4 * (w + 4 * i)) + 16u * (unsigned)lane)) =
+              v4u_t{0x3f80u, 0u, 0u, 0u};
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -450,16 +475,20 @@ static int wgrad_tr_mode() {
 static int wgrad_tr_try(const WgradArgs& a, hipStream_t s) {
   const hiseg_conv2d_desc& d = a.d;
   if (!wgrad_tr_mode()) return 0;
-  if (d.dtype != HISEG_BF16 || d.convT || a.want_bias) return 0;
-  if (!(d.Cb == 0 || (d.Ca % 128 == 0 && d.Cb % 128 == 0))) return 0;
+  if (d.dtype != HISEG_BF16) return 0;
+  // one source per 128-column K tile: A ends on a tile boundary and (with more than one tap) so does each tap
+  if (!(d.Cb == 0 || (d.Ca % 128 == 0 && (d.KH * d.KW == 1 || d.Cb % 128 == 0)))) return 0;
   if (a.Cin % 8 || a.dy_cs % 8 || a.dy_coff % 8 || d.a_cstride % 8 || d.a_coff % 8) return 0;
   if (d.Cb && (d.b_cstride % 8 || d.b_coff % 8)) return 0;
-  if (a.Cg < 64) return 0;
+  if (d.convT && (d.Cout % 32 || d.a_up != 1)) return 0;   // C = Cout / 4 a multiple of 8
   const long long span_a = (long long)d.N * d.H * d.W * d.a_cstride * 2;
   const long long span_b = d.Cb ? (long long)d.N * d.H * d.W * d.b_cstride * 2 : 0;
-  const long long span_y = ((long long)a.M * a.dy_cs + a.dy_coff + a.Cg) * 2;
+  const long long span_y = ((long long)a.M * (d.convT ? 4 : 1) * a.dy_cs + a.dy_coff + a.Cg) * 2;
   if (span_a >= 0x7fffffffll || span_b >= 0x7fffffffll || span_y >= 0x7fffffffll) return 0;
-  const int r = a.Cg >= 128 ? wgrad_tr_launch<128, 2, 2, 2>(a, s) : wgrad_tr_launch<64, 4, 1, 2>(a, s);
+  const int r = a.Cg >= 128 ? wgrad_tr_launch<128, 2, 2, 2>(a, s)
+              : a.Cg >= 64  ? wgrad_tr_launch<64, 4, 1, 2>(a, s)
+              : a.Cg >= 32  ? wgrad_tr_launch<32, 4, 1, 2>(a, s)
+                            : wgrad_tr_launch<16, 4, 1, 2>(a, s);
   return r < 0 ? r : 1;
 }
 

@@ -79,6 +79,10 @@ CONV_CASES = [  # (cin, cout, k, H, W, N, bias, two-source split)
     (3, 64, 3, 16, 12, 2, True, None),
     (128, 2, 1, 8, 6, 3, True, None),
     (128, 64, 3, 8, 6, 2, True, (64, 64)),
+    # transposed-read wgrad forms: GEMM-bias column in a K tile of its own (Ktot = 1152), narrow Cout 32 / 8
+    (128, 128, 3, 9, 7, 2, True, None),
+    (64, 32, 3, 10, 9, 2, False, None),
+    (128, 8, 1, 12, 10, 3, True, None),
 ]
 
 
@@ -117,15 +121,18 @@ def test_conv_backward_matches_autograd(case, dt):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-def test_convT_backward_matches_autograd(dt):
+@pytest.mark.parametrize("cio", [(256, 128), (128, 64), (64, 32)])
+def test_convT_backward_matches_autograd(dt, cio):
+    """ConvTranspose2d(k=2, s=2) backward; 128 -> 64 has two sub-pixels per 128-column wgrad tile."""
     from hiseg.ops import Act
-    conv = nn.ConvTranspose2d(256, 128, 2, stride=2)
+    cin, cout = cio
+    conv = nn.ConvTranspose2d(cin, cout, 2, stride=2)
     filler.fill_module(conv, seed=9)
     TE, S, T = engine(_Holder(c=conv), dt)
-    x = torch.from_numpy(filler.normal(3, (2, 256, 8, 6))).to(DEV)
+    x = torch.from_numpy(filler.normal(3, (2, cin, 8, 6))).to(DEV)
     xa = Act.from_nchw(x, dt)
     y = TE.conv_plain(T, conv, TE.ACT_NONE, xa, convT=True)
-    g = torch.from_numpy(filler.normal(4, (2, 128, 16, 12))).to(DEV)
+    g = torch.from_numpy(filler.normal(4, (2, cout, 16, 12))).to(DEV)
     inject(T, y, g, dt)
     S.flat.prepare_backward()
     T.run_backward()

@@ -38,8 +38,9 @@ def conv_key(d):
 
 
 def wgrad_family(d, want_bias):
-    tr = (d.dtype == 1 and not d.convT and not want_bias and (d.Cb == 0 or (d.Ca % 128 == 0 and d.Cb % 128 == 0))
-          and d.Cout >= 64)
+    """The kernel family csrc/train_conv.hip wgrad_tr_try picks (shape rules only)."""
+    tr = (d.dtype == 1 and (d.Cb == 0 or (d.Ca % 128 == 0 and (d.KH * d.KW == 1 or d.Cb % 128 == 0)))
+          and (not d.convT or d.Cout % 32 == 0))
     return "tr" if tr else "legacy"
 
 
