@@ -290,7 +290,15 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wk = w / WC, wc = w % WC;
-  const int k0 = blockIdx.x * BK, j0 = blockIdx.y * BC, split = blockIdx.z;
+  // 1-D grid, XCD-major bijective remap: the hardware deals consecutive workgroups round-robin over the 8 XCDs,
+  // so consecutive remapped ids -- the K / Cout tiles of one pixel split, fastest -- run on one XCD at about
+  // the same time and share its L2: every tap tile of a split re-reads the same (shifted) activation rows
+  // and the same dY rows, which otherwise came from HBM once per tile
+  const int nkt = (a.Kg + BK - 1) / BK, nct = (a.Cg + BC - 1) / BC;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = orig & 7, loc = orig >> 3;
+  const int wgi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int k0 = (wgi % nkt) * BK, j0 = ((wgi / nkt) % nct) * BC, split = wgi / (nkt * nct);
   const int pb_begin = split * a.blocks_per_split;
   const int nblocks = (a.M + PB - 1) / PB;
   int pb_end = pb_begin + a.blocks_per_split;
@@ -456,8 +464,8 @@ static int wgrad_tr_launch(const WgradArgs& a, hipStream_t s) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  dim3 grid((a.Kg + 127) / 128, (a.Cg + BC - 1) / BC, a.splits);
-  hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a);
+  const int nwg = ((a.Kg + 127) / 128) * ((a.Cg + BC - 1) / BC) * a.splits;
+  hipLaunchKernelGGL(kern, dim3(nwg), dim3(256), lds, s, a);
   return hiseg_check_launch("conv_wgrad_tr");
 }
 
