@@ -11,12 +11,15 @@ struct bf16_t { uint16_t x; };
 
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 
-// Round-to-nearest-even, NaN kept a NaN (MI355X_MICROARCH.md "Correctness boundaries").
-__device__ __forceinline__ uint16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
+// Round-to-nearest-even by the gfx950 conversion instruction v_cvt_pk_bf16_f32 (a plain cast at -O3), NaN kept
+// a NaN (MI355X_MICROARCH.md "Correctness boundaries"); one instruction per PAIR with f2bf2 -- the integer
+// rounding sequence it replaces cost ~5 VALU instructions per value, which bound the narrow-input 1x1 layers'
+// epilogues.
+typedef __bf16 hiseg_bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float hiseg_f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+__device__ __forceinline__ uint32_t f2bf2(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((hiseg_f32x2_t){lo, hi}, hiseg_bf16x2_t));
 }
 
 template <typename T> struct Elem;
@@ -39,7 +42,9 @@ template <> struct Elem<bf16_t> {
   }
 };
 
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// 1 / (1 + e^-x) with the hardware reciprocal (v_rcp_f32, 1 ulp) instead of the correctly rounded division's
+// 11-instruction sequence: sigmoid / SiLU epilogues are VALU-bound on the wide EfficientNet expansions
+__device__ __forceinline__ float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 
 // nn.GELU() (approximate='none'): x * Phi(x) with the exact erf
 __device__ __forceinline__ float gelu_(float v) { return 0.5f * v * (1.f + erff(v * 0.70710678118654752f)); }
@@ -100,7 +105,7 @@ template <> struct Chunk<bf16_t> {
   __device__ static __forceinline__ uint4 pack(const float* v) {
     uint32_t w[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+    for (int i = 0; i < 4; ++i) w[i] = f2bf2(v[2 * i], v[2 * i + 1]);
     return make_uint4(w[0], w[1], w[2], w[3]);
   }
 };

@@ -294,8 +294,8 @@ __global__ void __launch_bounds__(512) conv_8ph_kernel(ConvArgs a) {
             v[2] *= __uint_as_float(qv.y << 16); v[3] *= __uint_as_float(qv.y & 0xffff0000u);
           }
           uint2 o;
-          o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-          o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          o.x = f2bf2(v[0], v[1]);
+          o.y = f2bf2(v[2], v[3]);
           *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(d.out) + op * d.o_cstride + d.o_coff + oc) = o;
           if (out2)
             *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out2) + op * d.o2_cstride + d.o2_coff + oc) = o;

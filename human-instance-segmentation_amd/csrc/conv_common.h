@@ -42,8 +42,8 @@ __device__ __forceinline__ void store4(void* base, long long idx, bool vec, int 
           make_float4(v[0], v[1], v[2], v[3]);
     } else {
       uint2 q;
-      q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-      q.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      q.x = f2bf2(v[0], v[1]);
+      q.y = f2bf2(v[2], v[3]);
       *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(base) + idx) = q;
     }
   } else {
@@ -127,8 +127,8 @@ template <> struct Quad<bf16_t> {
   __device__ static __forceinline__ V zero() { return make_uint2(0u, 0u); }
   __device__ static __forceinline__ void store(void* p, long long i, const float* f) {
     uint2 o;
-    o.x = (uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16);
-    o.y = (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16);
+    o.x = f2bf2(f[0], f[1]);
+    o.y = f2bf2(f[2], f[3]);
     *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p) + i) = o;
   }
 };

@@ -365,8 +365,8 @@ __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
         if constexpr (ACT == HISEG_ACT_RELU) v[e] = v[e] > 0.f ? v[e] : 0.f;
       }
       uint2 o;
-      o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-      o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      o.x = f2bf2(v[0], v[1]);
+      o.y = f2bf2(v[2], v[3]);
       *reinterpret_cast<uint2*>(q) = o;
     }
   __syncthreads();

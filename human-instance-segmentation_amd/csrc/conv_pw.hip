@@ -6,42 +6,56 @@
 // (tools/conv_bench.py): every 128x128 or 256x256 workgroup tile re-stages its weight block and pays
 // a ring prologue and an LDS epilogue for only 8-9 K stages.
 //
-// Here one persistent workgroup per CU keeps its 256-column weight tile (<= 147 KiB) in LDS for the
-// whole launch and streams pixels: each wave owns 32-pixel blocks (block b, b + #waves, ...), loads the
-// block's activations straight into MFMA B-fragment registers (a lane's 8 consecutive channels of one
-// pixel are 16 contiguous bytes of the NHWC row), prefetches the next block's while the current one's
-// 16 x 2 x NKS MFMAs run (A = weight fragments read from LDS), and stores the epilogue straight from
-// the accumulators (4 consecutive output channels = 8 bytes per lane).  Weight rows are padded by 16 B
-// in LDS (row stride = 33 / 37 chunks), which makes the 16 rows of a fragment read hit distinct banks.
+// Here persistent workgroups keep their column tile of the weights (<= 147 KiB) in LDS for the whole
+// launch and stream pixels: each wave owns 32-pixel blocks (block b, b + #waves, ...), loads the block's
+// activations straight into MFMA B-fragment registers (a lane's 8 consecutive channels of one pixel are 16
+// contiguous bytes of the NHWC row), prefetches the next block's while the current one's RB x 2 x nks MFMAs
+// run (A = weight fragments read from LDS), and stores the epilogue straight from the accumulators (4
+// consecutive output channels = 8 bytes per lane).  Weight rows are padded by 16 B in LDS (row stride =
+// 4 NKS + 1 chunks), which makes the 16 rows of a fragment read hit distinct banks.
+//
+// Column tiles of CT = 16 RB columns: RB = 16 for the head's 256-multiple layers; the EfficientNet encoder's
+// 1x1 layers (timm InvertedResidual conv_pw / conv_pwl, DepthwiseSeparableConv conv_pw; efficientnet.py in
+// timm 1.0.19) have 16..1152 columns and 16..240 input channels (K <= 256: nks <= 8 k-steps, a runtime count
+// up to the template's NKS): RB 1..8 for narrow projections, RB 16 with ragged last tiles for the wide
+// expansions (672 = 3 tiles, the third half empty).  Input channel tails (Ca a multiple of 8, not of 32) read
+// zeros through out-of-range offsets.  INS: the squeeze-excite gate of the projection's input (in_scale
+// [N][Ca], f32) is staged in LDS once per workgroup and applied to each fragment in registers, rounded to
+// bf16 exactly as the generic kernel's loader does (conv_igemm.hip gather), so results stay bit-identical.
 //
 // ConvTranspose2d: GEMM column j = q * C + co (q = 2 dy + dx) of input pixel (n, y, x) lands at output
 // pixel (n, 2y + dy, 2x + dx), channel co; a 512-column layer runs as two column tiles.
+//
+// Built twice (Makefile): this file (HISEG_PW_PART 1: RB 16, and conv_pw_try) and conv_pw_n.hip
+// (HISEG_PW_PART 2: RB 1, 2, 4, 8).
 #include "conv_common.h"
+
+#ifndef HISEG_PW_PART
+#define HISEG_PW_PART 1
+#endif
 
 namespace hiseg {
 
-constexpr int kPwCT = 256;     // output columns per workgroup tile
 constexpr int kPwBlk = 32;     // pixels per wave block (two 16-pixel MFMA columns)
-
-// f2bf without the early return (a select, so the epilogue stays free of exec-mask branches)
-__device__ __forceinline__ uint32_t pw_bf(float f) {
-  const uint32_t u = __float_as_uint(f);
-  const uint32_t r = (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
-  return (u & 0x7fffffffu) > 0x7f800000u ? ((u >> 16) | 0x40u) : r;
-}
+constexpr int kPwActRt = -1;   // ACT template value: activation read from the descriptor at run time
 
 typedef unsigned pw_u4 __attribute__((ext_vector_type(4)));
 typedef unsigned pw_u2 __attribute__((ext_vector_type(2)));
 
-// NKS k-steps of 32 channels; NKS == 9: k-steps 0..7 from source A (Ca == 256), k-step 8 from source B
-// (Cb <= 32 channels, the rest zero).  Every global access is a buffer instruction whose out-of-range lanes
-// (pixel tail, channel tail, the block past the last) carry an offset beyond num_records: loads return zeros,
-// stores are dropped -- no divergent branches, so the compiler's vmcnt waits stay counted.
+// NKS: k-steps of 32 channels held in registers (nks <= NKS of them used); NKS == 9:
+// k-steps 0..7 from source A (Ca == 256), k-step 8 from source B (Cb <= 32 channels, the rest zero).  Every
+// global access is a buffer instruction whose out-of-range lanes (pixel tail, channel tail, the block past
+// the last) carry an offset beyond num_records: loads return zeros, stores are dropped -- no divergent
+// branches, so the compiler's vmcnt waits stay counted.
 // EPI: 0 plain, 1 residual added before the activation, 2 mul applied after it (include/hiseg.h epilogue).
-template <int NKS, int EPI, int ACT, bool CONVT>
-__global__ void __launch_bounds__(256, 1) conv_pw_kernel(ConvArgs a, int nct) {
+template <int NKSA, int EPI, int ACT, bool CONVT, int RB, bool INS>
+__global__ void __launch_bounds__(256, 1) conv_pw_kernel(ConvArgs a, int nct, int nks_arg) {
+  // NKSA > 0: exactly NKSA k-steps (the head's layers: no run-time guards, which cost the residual / mul
+  // forms registers); NKSA < 0: a run-time count nks_arg <= -NKSA
+  constexpr int NKS = NKSA < 0 ? -NKSA : NKSA;
+  const int nks = NKSA < 0 ? nks_arg : NKSA;
   constexpr bool RES = EPI == 1, MUL = EPI == 2, XOP = EPI != 0;
-  constexpr int RB = kPwCT / 16;               // 16-row blocks of the column tile
+  constexpr int CT = 16 * RB;                  // output columns per workgroup tile
   constexpr int ROWC = NKS * 4 + 1;            // LDS row stride in 16-B chunks (one chunk of padding)
   constexpr int NA = NKS == 9 ? 8 : NKS;       // k-steps from source A
   constexpr unsigned OOB = 0x80000000u;
@@ -50,22 +64,29 @@ __global__ void __launch_bounds__(256, 1) conv_pw_kernel(ConvArgs a, int nct) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int ct = blockIdx.x % nct;             // column tile
   const int grp = blockIdx.x / nct, ngrp = gridDim.x / nct;
-  const int c0 = ct * kPwCT;
+  const int c0 = ct * CT;
+  const int act = ACT == kPwActRt ? d.act : ACT;
 
-  // ---- weights of the column tile -> LDS (row r, chunk c at r * ROWC + c); scale / shift after them
+  // ---- weights of the column tile -> LDS (row r, chunk c at r * ROWC + c; rows past Cout_pad zero); scale /
+  // shift after them, then (INS) the gate table [N][Ca]
   uint4* wl = smem;
-  float* ssc = reinterpret_cast<float*>(smem + kPwCT * ROWC);
-  float* ssh = ssc + kPwCT;
+  float* ssc = reinterpret_cast<float*>(smem + CT * ROWC);
+  float* ssh = ssc + CT;
+  float* gl = ssh + CT;
   const uint4* wg = reinterpret_cast<const uint4*>(d.weight);
   const int kc = d.K_pad >> 3;                 // 16-B chunks per global weight row
-  for (int i = t; i < kPwCT * NKS * 4; i += 256) {
-    const int r = i / (NKS * 4), c = i - r * (NKS * 4);
-    wl[r * ROWC + c] = wg[(long long)(c0 + r) * kc + c];
+  const int wch = nks * 4;                     // chunks per row that are used
+  for (int i = t; i < CT * wch; i += 256) {
+    const int r = i / wch, c = i - r * wch;
+    wl[r * ROWC + c] = c0 + r < d.Cout_pad ? wg[(long long)(c0 + r) * kc + c] : make_uint4(0u, 0u, 0u, 0u);
   }
-  for (int i = t; i < kPwCT; i += 256) {
+  for (int i = t; i < CT; i += 256) {
     const int j = c0 + i < d.Cout ? c0 + i : 0;
     ssc[i] = d.scale[j];
     ssh[i] = d.shift[j];
+  }
+  if constexpr (INS) {
+    for (int i = t; i < d.N * d.Ca; i += 256) gl[i] = d.in_scale[i];
   }
   __syncthreads();
 
@@ -89,12 +110,13 @@ __global__ void __launch_bounds__(256, 1) conv_pw_kernel(ConvArgs a, int nct) {
 
   // B fragments of block b: lane (g, pl) holds pixel b*32 + 16j + pl, channels 32 ks + 8 g .. + 7
   auto load_ks = [&](int b, int ks, uint4 (&bk)[2]) __attribute__((always_inline)) {
+    const bool ch_ok = 32 * ks + 8 * g < d.Ca;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int p = b * kPwBlk + 16 * j + pl;
       pw_u4 v;
       if (ks < NA) {
-        const unsigned off = p < M ? (unsigned)((p * d.a_cstride + d.a_coff + 32 * ks + 8 * g) * 2) : OOB;
+        const unsigned off = (p < M && ch_ok) ? (unsigned)((p * d.a_cstride + d.a_coff + 32 * ks + 8 * g) * 2) : OOB;
         v = __builtin_amdgcn_raw_buffer_load_b128(rA, off, 0, 0);
       } else {
         const unsigned off = (p < M && bch_ok) ? (unsigned)((p * d.b_cstride + d.b_coff + 8 * g) * 2) : OOB;
@@ -129,6 +151,7 @@ __global__ void __launch_bounds__(256, 1) conv_pw_kernel(ConvArgs a, int nct) {
       return (unsigned)((pbase[j] * cs + coff + col) * 2);
     }
   };
+  const int hw = d.H * d.W;
 
   // blocks of this wave: grp * 4 + w, then strides of all waves of the column tile's groups.  Two B buffers
   // in a loop unrolled by two: block b computes from one while block b + stride's fragments load into the
@@ -138,11 +161,37 @@ __global__ void __launch_bounds__(256, 1) conv_pw_kernel(ConvArgs a, int nct) {
   int b = grp * 4 + w;
   uint4 b0[NKS][2], b1[NKS][2];
 #pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) load_ks(b, ks, b0[ks]);
-  auto process = [&](int b, const uint4 (&bf)[NKS][2], uint4 (&bn)[NKS][2]) __attribute__((always_inline)) {
+  for (int ks = 0; ks < NKS; ++ks)
+    if (ks < nks) load_ks(b, ks, b0[ks]);
+  auto process = [&](int b, uint4 (&bf)[NKS][2], uint4 (&bn)[NKS][2]) __attribute__((always_inline)) {
     const int nb = b + stride;
+    if constexpr (INS) {   // gate the current block's fragments before the next block's loads reuse registers
+      int gofs[2];
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) load_ks(nb, ks, bn[ks]);
+      for (int j = 0; j < 2; ++j) {
+        const int p = b * kPwBlk + 16 * j + pl;
+        const int n = p < M ? p / hw : 0;
+        gofs[j] = n * d.Ca;
+      }
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        if (ks >= nks) continue;
+        const int ch = 32 * ks + 8 * g < d.Ca ? 32 * ks + 8 * g : d.Ca - 8;   // masked lanes hold zeros
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float4* gp = reinterpret_cast<const float4*>(gl + gofs[j] + ch);
+          const float4 s0 = gp[0], s1 = gp[1];
+          float f[8];
+          Chunk<bf16_t>::unpack(bf[ks][j], f);
+          f[0] *= s0.x; f[1] *= s0.y; f[2] *= s0.z; f[3] *= s0.w;
+          f[4] *= s1.x; f[5] *= s1.y; f[6] *= s1.z; f[7] *= s1.w;
+          bf[ks][j] = Chunk<bf16_t>::pack(f);
+        }
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+      if (ks < nks) load_ks(nb, ks, bn[ks]);
     set_block(b);
     pw_u2 rv[XOP ? RB : 1][2];
     if constexpr (XOP) {
@@ -152,7 +201,7 @@ __global__ void __launch_bounds__(256, 1) conv_pw_kernel(ConvArgs a, int nct) {
         for (int j = 0; j < 2; ++j) rv[i][j] = __builtin_amdgcn_raw_buffer_load_b64(rR, offset(j, i, x_cs, x_coff), 0, 0);
     }
     // the weight fragments are loop-invariant: an opaque base per block keeps the compiler from hoisting all
-    // 16 x NKS of them (64 registers each k-step) out of the pixel loop
+    // RB x NKS of them (4 registers each) out of the pixel loop
     int wofs = pl * ROWC + g;   // (an index, not a pointer: the asm would turn an LDS pointer into a flat one)
     asm volatile("" : "+v"(wofs));
     const uint4* wrow = smem + wofs;
@@ -161,6 +210,7 @@ __global__ void __launch_bounds__(256, 1) conv_pw_kernel(ConvArgs a, int nct) {
     for (int i = 0; i < RB; ++i) acc[i][0] = acc[i][1] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
+      if (ks >= nks) continue;
 #pragma unroll
       for (int i = 0; i < RB; ++i) {
         const uint4 af = wrow[16 * i * ROWC + 4 * ks];
@@ -183,12 +233,12 @@ __global__ void __launch_bounds__(256, 1) conv_pw_kernel(ConvArgs a, int nct) {
         for (int e = 0; e < 4; ++e) {
           v[e] = acc[i][j][e] * sc[e] + sh[e];
           if constexpr (RES) v[e] += Quad<bf16_t>::get(make_uint2(rv[i][j].x, rv[i][j].y), e);
-          v[e] = apply_act(v[e], ACT);
+          v[e] = apply_act(v[e], act);
           if constexpr (MUL) v[e] *= Quad<bf16_t>::get(make_uint2(rv[i][j].x, rv[i][j].y), e);
         }
         pw_u2 q;
-        q.x = pw_bf(v[0]) | (pw_bf(v[1]) << 16);
-        q.y = pw_bf(v[2]) | (pw_bf(v[3]) << 16);
+        q.x = f2bf2(v[0], v[1]);
+        q.y = f2bf2(v[2], v[3]);
         __builtin_amdgcn_raw_buffer_store_b64(q, rO, offset(j, i, d.o_cstride, d.o_coff), 0, 0);
       }
     }
@@ -210,39 +260,87 @@ static int cu_count() {
   return n;
 }
 
-template <int NKS, int EPI, int ACT, bool CONVT>
-static int launch_pw(const ConvArgs& a, hipStream_t s) {
+static size_t pw_lds_bytes(int NKS, int RB, bool ins, const hiseg_conv2d_desc& d) {
+  return (size_t)16 * RB * (NKS * 4 + 1) * 16 + 2 * 16 * RB * 4 + (ins ? (size_t)d.N * d.Ca * 4 : 0);
+}
+
+template <int NKSA, int EPI, int ACT, bool CONVT, int RB, bool INS>
+static int launch_pw(const ConvArgs& a, hipStream_t s, int nks) {
   const hiseg_conv2d_desc& d = a.d;
-  const size_t lds = (size_t)kPwCT * (NKS * 4 + 1) * 16 + 2 * kPwCT * 4;
-  auto kern = conv_pw_kernel<NKS, EPI, ACT, CONVT>;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr = true;
+  const size_t lds = pw_lds_bytes(NKSA < 0 ? -NKSA : NKSA, RB, INS, d);
+  auto kern = conv_pw_kernel<NKSA, EPI, ACT, CONVT, RB, INS>;
+  static int occ = 0;   // resident workgroups per CU at the largest LDS request seen (the gate table varies)
+  static size_t occ_lds = 0;
+  if (lds > occ_lds) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kern, 256, lds) != hipSuccess || nb < 1) nb = 1;
+    occ = nb > 4 ? 4 : nb;
+    occ_lds = lds;
   }
-  const int nct = d.Cout_pad / kPwCT;
+  const int nct = (d.Cout_pad + 16 * RB - 1) / (16 * RB);
   const int nblk = (a.M + kPwBlk - 1) / kPwBlk;
-  int groups = cu_count() / nct;                       // one workgroup per CU in all
+  int groups = cu_count() * occ / nct;                  // every resident slot of the chip in all
   const int need = (nblk + 3) / 4;
   if (groups > need) groups = need;
   if (groups < 1) groups = 1;
-  hipLaunchKernelGGL(kern, dim3(groups * nct), dim3(256), lds, s, a, nct);
+  hipLaunchKernelGGL(kern, dim3(groups * nct), dim3(256), lds, s, a, nct, nks);
   return hiseg_check_launch("conv_pw");
 }
 
-template <int NKS>
-static int launch_pw_k(const ConvArgs& a, hipStream_t s) {
+// narrow column tiles (conv_pw_n.hip): RB 1, 2, 4 or 8; plain / residual epilogue, optional SE gate
+int launch_pw_narrow(const ConvArgs& a, hipStream_t s, int rb, int nks_max, int nks);
+
+#if HISEG_PW_PART == 2
+template <int RB, int NKS>
+static int launch_pw_n2(const ConvArgs& a, hipStream_t s, int nks) {
   const hiseg_conv2d_desc& d = a.d;
-  constexpr int N = HISEG_ACT_NONE, R = HISEG_ACT_RELU, S = HISEG_ACT_SIGMOID;
+  const bool ins = d.in_scale != nullptr;
+  if (d.residual) return ins ? launch_pw<-NKS, 1, kPwActRt, false, RB, true>(a, s, nks)
+                             : launch_pw<-NKS, 1, kPwActRt, false, RB, false>(a, s, nks);
+  return ins ? launch_pw<-NKS, 0, kPwActRt, false, RB, true>(a, s, nks)
+             : launch_pw<-NKS, 0, kPwActRt, false, RB, false>(a, s, nks);
+}
+template <int RB>
+static int launch_pw_n1(const ConvArgs& a, hipStream_t s, int nks_max, int nks) {
+  if (nks_max == 2) return launch_pw_n2<RB, 2>(a, s, nks);
+  if (nks_max == 4) return launch_pw_n2<RB, 4>(a, s, nks);
+  return launch_pw_n2<RB, 8>(a, s, nks);
+}
+int launch_pw_narrow(const ConvArgs& a, hipStream_t s, int rb, int nks_max, int nks) {
+  switch (rb) {
+    case 1: return launch_pw_n1<1>(a, s, nks_max, nks);
+    case 2: return launch_pw_n1<2>(a, s, nks_max, nks);
+    case 4: return launch_pw_n1<4>(a, s, nks_max, nks);
+    default: return launch_pw_n1<8>(a, s, nks_max, nks);
+  }
+}
+#else
+template <int NKS>
+static int launch_pw_k(const ConvArgs& a, hipStream_t s, int nks) {
+  const hiseg_conv2d_desc& d = a.d;
+  constexpr int N = HISEG_ACT_NONE, R = HISEG_ACT_RELU, S = HISEG_ACT_SIGMOID, SI = HISEG_ACT_SILU;
   const int act = d.act;
   if constexpr (NKS == 9) {   // the 256 + 8 combiner: plain outputs only (the other forms would spill)
-    return act == R ? launch_pw<NKS, 0, R, false>(a, s) : launch_pw<NKS, 0, N, false>(a, s);
+    return act == R ? launch_pw<NKS, 0, R, false, 16, false>(a, s, nks) : launch_pw<NKS, 0, N, false, 16, false>(a, s, nks);
   } else {
-    if (d.convT) return act == R ? launch_pw<NKS, 0, R, true>(a, s) : launch_pw<NKS, 0, N, true>(a, s);
-    if (d.residual) return act == R ? launch_pw<NKS, 1, R, false>(a, s) : launch_pw<NKS, 1, N, false>(a, s);
-    if (d.mul) return act == S ? launch_pw<NKS, 2, S, false>(a, s) : launch_pw<NKS, 2, N, false>(a, s);
-    return act == R ? launch_pw<NKS, 0, R, false>(a, s)
-         : act == S ? launch_pw<NKS, 0, S, false>(a, s) : launch_pw<NKS, 0, N, false>(a, s);
+    if (nks != NKS) {   // a k-step count below the register tile: plain epilogue (EfficientNet expansions)
+      if (d.convT || d.residual || d.mul) return 0;
+      return act == R ? launch_pw<-NKS, 0, R, false, 16, false>(a, s, nks)
+           : act == S ? launch_pw<-NKS, 0, S, false, 16, false>(a, s, nks)
+           : act == SI ? launch_pw<-NKS, 0, SI, false, 16, false>(a, s, nks)
+                       : launch_pw<-NKS, 0, N, false, 16, false>(a, s, nks);
+    }
+    if (d.convT) return act == R ? launch_pw<NKS, 0, R, true, 16, false>(a, s, nks)
+                                 : launch_pw<NKS, 0, N, true, 16, false>(a, s, nks);
+    if (d.residual) return act == R ? launch_pw<NKS, 1, R, false, 16, false>(a, s, nks)
+                                    : launch_pw<NKS, 1, N, false, 16, false>(a, s, nks);
+    if (d.mul) return act == S ? launch_pw<NKS, 2, S, false, 16, false>(a, s, nks)
+                               : launch_pw<NKS, 2, N, false, 16, false>(a, s, nks);
+    return act == R ? launch_pw<NKS, 0, R, false, 16, false>(a, s, nks)
+         : act == S ? launch_pw<NKS, 0, S, false, 16, false>(a, s, nks)
+         : act == SI ? launch_pw<NKS, 0, SI, false, 16, false>(a, s, nks)
+                     : launch_pw<NKS, 0, N, false, 16, false>(a, s, nks);
   }
 }
 
@@ -252,18 +350,36 @@ int conv_pw_try(const ConvArgs& a, hipStream_t s, int variant) {
   if (variant != 90) return 0;
   if (d.dtype != HISEG_BF16 || d.out_dtype != HISEG_BF16) return 0;
   if (d.KH != 1 || d.KW != 1 || d.stride != 1 || d.pad != 0 || d.a_up != 1) return 0;
-  if (d.in_scale || d.out2) return 0;
+  if (d.out2) return 0;
   if (d.residual && d.mul) return 0;
-  if (d.act == HISEG_ACT_SIGMOID ? (d.convT || d.residual) : (d.act != HISEG_ACT_NONE && d.act != HISEG_ACT_RELU))
-    return 0;
-  if (d.mul && (d.act == HISEG_ACT_RELU || d.convT || ((d.m_cstride | d.m_coff) & 3))) return 0;
-  if (d.convT && d.residual) return 0;
-  if (d.Ca % 32 || d.Cb % 8 || d.Cout % 4 || d.Cout_pad % kPwCT) return 0;
+  if (d.Ca % 8 || d.Cb % 8 || d.Cout % 4) return 0;
   if (d.convT && (d.Cout / 4) % 4) return 0;
+  if (d.convT && d.residual) return 0;
   const int nks = (a.Cin + 31) / 32;
-  if (d.K_pad < nks * 32) return 0;
-  if (nks == 9 ? (d.Ca != 256 || d.Cb > 32 || d.convT || d.residual || d.mul || d.act == HISEG_ACT_SIGMOID) : d.Cb != 0)
+  if (d.K_pad < nks * 32 || nks > 9) return 0;
+  const bool comb = nks == 9;
+  if (comb ? (d.Ca != 256 || d.Cb > 32 || d.convT || d.residual || d.mul || d.in_scale ||
+              (d.act != HISEG_ACT_NONE && d.act != HISEG_ACT_RELU))
+           : d.Cb != 0)
     return 0;
+  // column tile: 16 RB columns, RB the smallest power of two covering Cout_pad (at most 16; wider layers take
+  // ceil(Cout_pad / 256) tiles of 256, the last one ragged)
+  int rb = 16;
+  if (d.Cout_pad <= 128) rb = d.Cout_pad <= 16 ? 1 : d.Cout_pad <= 32 ? 2 : d.Cout_pad <= 64 ? 4 : 8;
+  if (rb == 16) {
+    // the head's forms (ReLU / sigmoid / none; residual, mul, ConvTranspose) and the EfficientNet expansion
+    // (SiLU); no SE gate at 256-column tiles
+    if (d.in_scale) return 0;
+    if (d.act == HISEG_ACT_SIGMOID ? (d.convT || d.residual)
+                                   : (d.act != HISEG_ACT_NONE && d.act != HISEG_ACT_RELU &&
+                                      !(d.act == HISEG_ACT_SILU && !d.convT && !d.residual && !d.mul)))
+      return 0;
+    if (d.mul && (d.act == HISEG_ACT_RELU || d.convT || ((d.m_cstride | d.m_coff) & 3))) return 0;
+  } else {
+    // narrow tiles: plain or residual epilogue with any elementwise activation, optional SE gate
+    if (d.convT || d.mul || d.act == HISEG_ACT_SWISH || comb) return 0;
+    if (d.in_scale && (((uintptr_t)d.in_scale & 15) || (long long)d.N * d.Ca * 4 > 64 * 1024)) return 0;
+  }
   const long long out_px = (long long)a.M * (d.convT ? 4 : 1);
   const long long lim = 0x7fffffffll;
   if ((long long)a.M * d.a_cstride * 2 >= lim || (d.Cb && (long long)a.M * d.b_cstride * 2 >= lim) ||
@@ -274,14 +390,20 @@ int conv_pw_try(const ConvArgs& a, hipStream_t s, int variant) {
   if (d.Cb && ((d.b_cstride | d.b_coff) & 7)) return 0;
   if (((d.o_cstride | d.o_coff) & 3) || (d.residual && ((d.r_cstride | d.r_coff) & 3))) return 0;
   if (((uintptr_t)d.out | (uintptr_t)d.residual | (uintptr_t)d.mul) & 7) return 0;
+  const int nks_max = comb ? 9 : nks <= 2 ? 2 : nks <= 4 ? 4 : 8;
   int r;
-  switch (nks) {
-    case 4: r = launch_pw_k<4>(a, s); break;
-    case 8: r = launch_pw_k<8>(a, s); break;
-    case 9: r = launch_pw_k<9>(a, s); break;
-    default: return 0;
+  if (rb < 16) {
+    r = launch_pw_narrow(a, s, rb, nks_max, nks);
+  } else {
+    switch (nks_max) {
+      case 2: r = launch_pw_k<2>(a, s, nks); break;
+      case 4: r = launch_pw_k<4>(a, s, nks); break;
+      case 8: r = launch_pw_k<8>(a, s, nks); break;
+      default: r = launch_pw_k<9>(a, s, nks); break;
+    }
   }
   return r < 0 ? r : 1;
 }
+#endif
 
 }  // namespace hiseg

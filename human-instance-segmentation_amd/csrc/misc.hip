@@ -321,6 +321,118 @@ __global__ void __launch_bounds__(256) dwconv_kernel(const void* in, int H, int 
   }
 }
 
+// bf16 depthwise conv, round 2: the kernel above re-reads a thread's K*K x 8 f32 weights (800 B at K = 5) for
+// every 4-output strip -- more L1/L2 traffic than the activations themselves on the low-resolution wide layers
+// (k5 s1 at 30x40 x 672 channels ran at ~0.5 TB/s).  Here a thread owns 4 channels (8 B of the NHWC row) and
+// holds their K*K x 4 weights in registers for all of its strips; a block is CT channel quads x R strip rows
+// (CT chosen on the host to fill the 256 threads), and the strip ranges are longer (hiseg_dw_gap_tiles).  Per
+// output the arithmetic is the kernel above's: same tap order, same fused multiply-adds, same epilogue.
+template <int KS, int ST>
+__global__ void __launch_bounds__(256) dwconv_q_kernel(const void* in, int H, int W, int C, const float* w,
+                                                       const float* scale, const float* shift, int act, void* out,
+                                                       int Ho, int Wo, float* gap, int CT) {
+  constexpr int NIN = (kDwXS - 1) * ST + KS;
+  __shared__ float red[256 * 4];
+  const int nq = C >> 2;
+  const int g0 = blockIdx.z * CT;
+  const int R = 256 / CT;
+  const int t = threadIdx.x;
+  const int cl = t % CT, r = t / CT;
+  const int q = g0 + cl < nq ? g0 + cl : nq - 1;   // (a ragged last group's spare lanes redo the last quad)
+  const bool live = r < R && g0 + cl < nq;
+  const int n = blockIdx.y, tiles = gridDim.x, tile = blockIdx.x;
+  const int sx = (Wo + kDwXS - 1) / kDwXS;
+  const int strips = Ho * sx;
+  const int s0 = (int)((long long)strips * tile / tiles), s1 = (int)((long long)strips * (tile + 1) / tiles);
+  const int c = q * 4;
+  const int pad = KS / 2;
+  float sc[4], sh[4], gs[4], wk[KS * KS][4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { sc[e] = scale[c + e]; sh[e] = shift[c + e]; gs[e] = 0.f; }
+#pragma unroll
+  for (int k = 0; k < KS * KS; ++k) {
+    const float4 f = *reinterpret_cast<const float4*>(w + k * C + c);
+    wk[k][0] = f.x; wk[k][1] = f.y; wk[k][2] = f.z; wk[k][3] = f.w;
+  }
+  const uint2* src = reinterpret_cast<const uint2*>(in) + (long long)n * H * W * nq;
+  uint2* dst = reinterpret_cast<uint2*>(out) + (long long)n * Ho * Wo * nq;
+  if (live) {
+    for (int st = s0 + r; st < s1; st += R) {
+      const int oy = st / sx;
+      const int ox0 = (st - oy * sx) * kDwXS;
+      float acc[kDwXS][4];
+#pragma unroll
+      for (int xo = 0; xo < kDwXS; ++xo)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[xo][e] = 0.f;
+#pragma unroll
+      for (int ky = 0; ky < KS; ++ky) {
+        const int iy = oy * ST - pad + ky;
+        if ((unsigned)iy >= (unsigned)H) continue;
+        const uint2* row = src + (long long)iy * W * nq + q;
+        const int ix0 = ox0 * ST - pad;
+        uint2 raw[NIN];
+#pragma unroll
+        for (int j = 0; j < NIN; ++j) {
+          const int ix = ix0 + j;
+          raw[j] = (unsigned)ix < (unsigned)W ? row[(long long)ix * nq] : make_uint2(0u, 0u);
+        }
+#pragma unroll
+        for (int j = 0; j < NIN; ++j) {
+          const int ix = ix0 + j;
+          if ((unsigned)ix >= (unsigned)W) continue;
+          const float v[4] = {__uint_as_float(raw[j].x << 16), __uint_as_float(raw[j].x & 0xffff0000u),
+                              __uint_as_float(raw[j].y << 16), __uint_as_float(raw[j].y & 0xffff0000u)};
+#pragma unroll
+          for (int xo = 0; xo < kDwXS; ++xo) {
+            const int kx = j - xo * ST;
+            if (kx < 0 || kx >= KS) continue;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[xo][e] += wk[ky * KS + kx][e] * v[e];
+          }
+        }
+      }
+#pragma unroll
+      for (int xo = 0; xo < kDwXS; ++xo) {
+        if (ox0 + xo >= Wo) break;
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[e] = apply_act(acc[xo][e] * sc[e] + sh[e], act);
+          gs[e] += o[e];
+        }
+        dst[((long long)oy * Wo + ox0 + xo) * nq + q] = make_uint2(f2bf2(o[0], o[1]), f2bf2(o[2], o[3]));
+      }
+    }
+  }
+  if (gap == nullptr) return;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) red[t * 4 + e] = gs[e];
+  __syncthreads();
+  if (r == 0 && live) {
+    for (int rr = 1; rr < R; ++rr)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gs[e] += red[(rr * CT + cl) * 4 + e];
+    float* gp = gap + ((long long)n * tiles + tile) * C + c;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) gp[e] = gs[e];
+  }
+}
+
+// channel quads per block for dwconv_q_kernel: the fewest z groups whose blocks keep >= 90 % of the 256 threads
+// busy (else the best fill seen)
+static int dw_quads_per_block(int nq) {
+  int best = nq < 256 ? nq : 256, best_fill = 0;
+  for (int d = 1; d <= 16; ++d) {
+    const int ct = (nq + d - 1) / d;
+    if (ct > 256) continue;
+    const int fill = (256 / ct) * ct;
+    if (fill > best_fill) { best = ct; best_fill = fill; }
+    if (fill >= 230) return ct;
+  }
+  return best;
+}
+
 // ------------------------------------------------------------------ input prologue
 __device__ __forceinline__ unsigned ord_enc(float f) {
   const unsigned u = __float_as_uint(f);
@@ -604,10 +716,14 @@ extern "C" int hiseg_channel_scale_fwd(int dtype, const void* x, int N, int HW, 
 }
 
 extern "C" int hiseg_dw_gap_tiles(int N, int Ho, int Wo) {
+  // strip ranges of >= 16 strips (a thread of dwconv_q_kernel keeps its weights in registers across them), at
+  // most 2048 / N per image
   const int strips = Ho * ((Wo + kDwXS - 1) / kDwXS);
   int t = 2048 / (N > 0 ? N : 1);
   if (t < 1) t = 1;
-  return t < strips ? t : strips;
+  int by_len = strips / 16;
+  if (by_len < 1) by_len = 1;
+  return t < by_len ? t : by_len;
 }
 
 static int dwconv_launch(int dtype, const void* in, int N, int H, int W, int C, int K, int stride, const float* w,
@@ -623,12 +739,15 @@ static int dwconv_launch(int dtype, const void* in, int N, int H, int W, int C, 
   HISEG_REQUIRE((reinterpret_cast<uintptr_t>(w) & 15) == 0 && (long long)H * W * C < (1ll << 31), HISEG_ERR_BAD_SHAPE,
                 "dwconv: weights must be 16-B aligned, image < 2^31 elements");
   const int nch = C / chunk_of(dtype);
-  dim3 grid(hiseg_dw_gap_tiles(N, Ho, Wo), N, (nch + 255) / 256);
+  const int nq = C / 4, ctq = dw_quads_per_block(nq);
+  const int tiles = hiseg_dw_gap_tiles(N, Ho, Wo);
+  dim3 grid(tiles, N, (nch + 255) / 256);
+  dim3 gridq(tiles, N, (nq + ctq - 1) / ctq);
 #define DW_L(KS, ST)                                                                                          \
   do {                                                                                                        \
     if (dtype == HISEG_BF16)                                                                                  \
-      hipLaunchKernelGGL((dwconv_kernel<bf16_t, KS, ST>), grid, dim3(256), 0, s, in, H, W, C, w, scale, shift, \
-                         act, out, Ho, Wo, gap);                                                              \
+      hipLaunchKernelGGL((dwconv_q_kernel<KS, ST>), gridq, dim3(256), 0, s, in, H, W, C, w, scale, shift,     \
+                         act, out, Ho, Wo, gap, ctq);                                                         \
     else                                                                                                      \
       hipLaunchKernelGGL((dwconv_kernel<float, KS, ST>), grid, dim3(256), 0, s, in, H, W, C, w, scale, shift,  \
                          act, out, Ho, Wo, gap);                                                              \

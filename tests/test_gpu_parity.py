@@ -278,6 +278,50 @@ def test_conv_small_kernel_bit_identical(name):
             assert torch.equal(y2, ref2), f"variant {v} out2 differs"
 
 
+# The EfficientNet encoder's 1x1 layers and the head's narrow 1x1 layers on the persistent pointwise kernel
+# (variant 90 and the automatic choice) vs the generic kernel, bit for bit: SiLU expansions (channel tails of
+# 24 / 40 input channels, ragged 256-column tiles at 672 / 1152, run-time k-step counts), SE-gated projections
+# with and without the skip (narrow column tiles of 16..80), the head's 8->64 / 64->128 forms.
+# name: (N, Ca, Cout, H, W, act, in_scale, residual)
+PW_EFF_CASES = {
+    "exp_16_96_silu": (2, 16, 96, 9, 70, 3, False, False),
+    "exp_24_144_silu": (3, 24, 144, 7, 9, 3, False, False),
+    "exp_40_240_silu": (2, 40, 240, 11, 13, 3, False, False),
+    "exp_112_672_silu": (2, 112, 672, 5, 7, 3, False, False),
+    "exp_192_1152_silu": (2, 192, 1152, 3, 5, 3, False, False),
+    "proj_144_24_ins_res": (3, 144, 24, 7, 9, 0, True, True),
+    "proj_96_24_ins": (2, 96, 24, 9, 11, 0, True, False),
+    "proj_240_40_ins_res": (2, 240, 40, 6, 10, 0, True, True),
+    "proj_240_80_ins": (2, 240, 80, 5, 6, 0, True, False),
+    "ds_32_16_ins": (2, 32, 16, 9, 70, 0, True, False),
+    "head_8_64_relu": (2, 8, 64, 6, 9, 1, False, False),
+    "head_64_128_relu_res": (2, 64, 128, 9, 7, 1, False, True),
+}
+
+
+@pytest.mark.parametrize("name", list(PW_EFF_CASES))
+def test_conv_pointwise_efficientnet_bit_identical(name):
+    from hiseg import ops
+    N, Ca, Cout, H, W, act, ins, res = PW_EFF_CASES[name]
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(13)
+    xa = ops.Act.from_nchw(torch.randn(N, Ca, H, W, device=DEV, generator=g), dt)
+    w = torch.randn(Cout, Ca, 1, 1, device=DEV, generator=g) / Ca ** 0.5
+    bn = torch.nn.BatchNorm2d(Cout).to(DEV).eval()
+    filler.fill_module(bn)
+    p = ops.pack_conv(w, None, bn, act, dt, DEV, pad=0)
+    gate = torch.rand(N, p.ca, device=DEV, generator=g) if ins else None
+    R = ops.Act.from_nchw(torch.randn(N, Cout, H, W, device=DEV, generator=g), dt) if res else None
+    outs = {}
+    for v in (-1, 0, 90):
+        y = ops.conv2d(p, xa, residual=R, in_scale=gate, variant=v)
+        torch.cuda.synchronize()
+        outs[v] = y.t.clone()
+    assert torch.isfinite(outs[-1].float()).all()
+    for v in (0, 90):
+        assert torch.equal(outs[v], outs[-1]), f"variant {v} differs from the generic kernel"
+
+
 # ------------------------------------------------------------------------------------------ misc kernels
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_pointwise_kernels(dt):
