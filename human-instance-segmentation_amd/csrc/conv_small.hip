@@ -18,6 +18,15 @@
 
 namespace hiseg {
 
+// i / d for 0 <= i < 2^32 / d by one multiply-high (m = ceil(2^32 / d)): the staging loops' run-time divisions by
+// the chunk counts were ~40 VALU instructions each, twice per staged 16-B chunk
+struct SmallDiv {
+  unsigned m;
+  int d;
+  __device__ explicit SmallDiv(int d_) : m(d_ > 1 ? 0xffffffffu / (unsigned)d_ + 1u : 0u), d(d_) {}
+  __device__ __forceinline__ int div(int i) const { return d > 1 ? (int)__umulhi((unsigned)i, m) : i; }
+};
+
 __device__ __forceinline__ unsigned long long stamp_small() {
   unsigned long long t;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
@@ -26,13 +35,14 @@ __device__ __forceinline__ unsigned long long stamp_small() {
 
 // STAMP (diagnostic): s_memtime at entry, after staging, after compute, at exit -> u64 x 4 per
 // workgroup in the buffer passed as desc.out2 (out2 itself is then not written).
-template <int KS, int TH, typename TO, int NJ, bool STAMP = false>
+// ST: stride (2: the EfficientNet stem, halo of (TH-1)*2+KS rows x 129 columns)
+template <int KS, int TH, typename TO, int NJ, bool STAMP = false, int ST = 1>
 __global__ void __launch_bounds__(256) conv_small_kernel(ConvArgs a, int WS, int PS) {
   unsigned long long st0 = 0, st1 = 0, st2 = 0;
   if constexpr (STAMP) st0 = stamp_small();
   unsigned long long* stamp_buf = STAMP ? reinterpret_cast<unsigned long long*>(a.d.out2) : nullptr;
   constexpr int TW = 64;
-  constexpr int HR = TH + KS - 1, HC = TW + KS - 1;
+  constexpr int HR = (TH - 1) * ST + KS, HC = (TW - 1) * ST + KS;
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   const hiseg_conv2d_desc& d = a.d;
   const int t = threadIdx.x;
@@ -56,20 +66,21 @@ __global__ void __launch_bounds__(256) conv_small_kernel(ConvArgs a, int WS, int
   // load) so that UB loads are in flight before the first LDS store.
   constexpr int UB = 8;
   const int nw = d.Cout_pad * kch;
+  const SmallDiv dkch(kch), dcch(cch);
   for (int i0 = t; i0 < nw; i0 += 256 * UB) {
     uint4 v[UB];
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
       int i = i0 + u * 256;
       i = i < nw ? i : nw - 1;
-      const int r = i / kch, c = i - r * kch;
+      const int r = dkch.div(i), c = i - r * kch;
       v[u] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(d.weight) + (long long)r * d.K_pad + c * 8);
     }
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
       const int i = i0 + u * 256;
       if (i < nw) {
-        const int r = i / kch, c = i - r * kch;
+        const int r = dkch.div(i), c = i - r * kch;
         sW[r * WS + c] = v[u];
       }
     }
@@ -83,10 +94,9 @@ __global__ void __launch_bounds__(256) conv_small_kernel(ConvArgs a, int WS, int
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
       const int i = i0 + u * 256;
-      const int c = i % cch;
-      const int pcol = (i / cch) % HC;
-      const int prow = i / (cch * HC);
-      const int iy = y0 + prow - pad, ix = x0 + pcol - pad;
+      const int pix = dcch.div(i), c = i - pix * cch;
+      const int prow = pix / HC, pcol = pix - prow * HC;
+      const int iy = y0 * ST + prow - pad, ix = x0 * ST + pcol - pad;
       ok[u] = i < nh && iy >= 0 && iy < d.H && ix >= 0 && ix < d.W;
       const int ciy = ok[u] ? iy : 0, cix = ok[u] ? ix : 0;
       const int ci = c * 8;
@@ -101,10 +111,8 @@ __global__ void __launch_bounds__(256) conv_small_kernel(ConvArgs a, int WS, int
     for (int u = 0; u < UB; ++u) {
       const int i = i0 + u * 256;
       if (i < nh) {
-        const int c = i % cch;
-        const int pcol = (i / cch) % HC;
-        const int prow = i / (cch * HC);
-        sX[(prow * HC + pcol) * PS + c] = ok[u] ? v[u] : make_uint4(0u, 0u, 0u, 0u);
+        const int pix = dcch.div(i), c = i - pix * cch;
+        sX[pix * PS + c] = ok[u] ? v[u] : make_uint4(0u, 0u, 0u, 0u);
       }
     }
   }
@@ -184,14 +192,14 @@ __global__ void __launch_bounds__(256) conv_small_kernel(ConvArgs a, int WS, int
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[q][j] = floatx4{0.f, 0.f, 0.f, 0.f};
       int tap = tap0, ci = ci0;
-      const uint4* xrow = sX + (r * HC + gx0 + lr) * PS;
+      const uint4* xrow = sX + (r * ST * HC + (gx0 + lr) * ST) * PS;
       for (int kc = 0; kc < nkc; ++kc) {
         const int dy = tap / KS, dx = tap - dy * KS;
         const bool kok = tap < KS * KS;
         const uint4* xb = xrow + (dy * HC + dx) * PS + (ci >> 3);
         uint4 b[G];
 #pragma unroll
-        for (int q = 0; q < G; ++q) b[q] = kok ? xb[q * 16 * PS] : make_uint4(0u, 0u, 0u, 0u);
+        for (int q = 0; q < G; ++q) b[q] = kok ? xb[q * 16 * ST * PS] : make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           if (p + j < nco) {
@@ -255,11 +263,11 @@ __global__ void __launch_bounds__(256) conv_small_kernel(ConvArgs a, int WS, int
 
 static int odd_slots(int n) { return (n & 1) ? n : n + 1; }
 
-template <int KS, int TH, typename TO, int NJ, bool STAMP>
+template <int KS, int TH, typename TO, int NJ, bool STAMP, int ST = 1>
 static int launch_small_nj(const ConvArgs& a, hipStream_t s, int WS, int PS, size_t lds) {
   const hiseg_conv2d_desc& d = a.d;
   const int ntx = (d.Wo + 63) / 64, nty = (d.Ho + TH - 1) / TH;
-  auto kern = conv_small_kernel<KS, TH, TO, NJ, STAMP>;
+  auto kern = conv_small_kernel<KS, TH, TO, NJ, STAMP, ST>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -275,6 +283,30 @@ static int launch_small(const ConvArgs& a, hipStream_t s, int WS, int PS, size_t
   if (nco == 1) return launch_small_nj<KS, TH, TO, 1, STAMP>(a, s, WS, PS, lds);
   if (nco == 2) return launch_small_nj<KS, TH, TO, 2, STAMP>(a, s, WS, PS, lds);
   return launch_small_nj<KS, TH, TO, 4, STAMP>(a, s, WS, PS, lds);
+}
+
+// stride 2 (3x3, bf16 out): 8 output rows when the halo fits two workgroups per CU, else 4.  Returns 1 if
+// launched, 0 if the layer does not fit, <0 on error.
+static int launch_small_s2(const ConvArgs& a, hipStream_t s, int WS, int PS) {
+  const hiseg_conv2d_desc& d = a.d;
+  const size_t wbytes = (size_t)d.Cout_pad * WS * 16;
+  auto lds_for = [&](int th) { return wbytes + (size_t)((th - 1) * 2 + 3) * (63 * 2 + 3) * PS * 16; };
+  const int nco = d.Cout_pad / 16;
+  int r;
+  if (lds_for(8) <= 80 * 1024) {
+    const size_t l = lds_for(8);
+    r = nco == 1 ? launch_small_nj<3, 8, bf16_t, 1, false, 2>(a, s, WS, PS, l)
+      : nco == 2 ? launch_small_nj<3, 8, bf16_t, 2, false, 2>(a, s, WS, PS, l)
+                 : launch_small_nj<3, 8, bf16_t, 4, false, 2>(a, s, WS, PS, l);
+  } else if (lds_for(4) <= 160 * 1024) {
+    const size_t l = lds_for(4);
+    r = nco == 1 ? launch_small_nj<3, 4, bf16_t, 1, false, 2>(a, s, WS, PS, l)
+      : nco == 2 ? launch_small_nj<3, 4, bf16_t, 2, false, 2>(a, s, WS, PS, l)
+                 : launch_small_nj<3, 4, bf16_t, 4, false, 2>(a, s, WS, PS, l);
+  } else {
+    return 0;
+  }
+  return r < 0 ? r : 1;
 }
 
 template <int KS, typename TO>
@@ -312,9 +344,13 @@ static int pick_th(const ConvArgs& a, hipStream_t s, int WS, int PS, int force_t
 // variant: 0 auto, 50 auto TH, 51/52/54/58 force TH = 1/2/4/8.
 int conv_small_try(const ConvArgs& a, hipStream_t s, int variant) {
   const hiseg_conv2d_desc& d = a.d;
-  if (d.dtype != HISEG_BF16 || d.convT || d.stride != 1) return 0;
+  if (d.dtype != HISEG_BF16 || d.convT || (d.stride != 1 && d.stride != 2)) return 0;
   if (!(d.KH == d.KW && (d.KH == 1 || d.KH == 3) && d.pad == d.KH / 2)) return 0;
-  if (d.Ho != d.H || d.Wo != d.W) return 0;
+  const bool s2 = d.stride == 2;
+  if (s2 ? (d.KH != 3 || d.a_up != 1 || d.out_dtype != HISEG_BF16 || d.Ho != (d.H - 1) / 2 + 1 ||
+            d.Wo != (d.W - 1) / 2 + 1)
+         : (d.Ho != d.H || d.Wo != d.W))
+    return 0;
   const int KS = d.KH;
   const int K = KS * KS * a.Cin;
   if (d.K_pad < K || d.K_pad % 64 != 0) return 0;
@@ -327,6 +363,10 @@ int conv_small_try(const ConvArgs& a, hipStream_t s, int variant) {
   const bool stamp = variant == 59;   // diagnostic: TH 8 with stamps (see conv_small_kernel)
   HISEG_REQUIRE(!stamp || a.d.out2 != nullptr, HISEG_ERR_BAD_ARG, "conv_small: stamp variant needs desc.out2");
   if (stamp) th = 8;
+  if (s2) {
+    if (stamp || variant != 0) return 0;
+    return launch_small_s2(a, s, WS, PS);
+  }
   if (variant >= 51 && variant <= 58) th = variant - 50;
   if (th != 0 && th != 1 && th != 2 && th != 4 && th != 8) return 0;
   int r;

@@ -278,6 +278,26 @@ def test_conv_small_kernel_bit_identical(name):
             assert torch.equal(y2, ref2), f"variant {v} out2 differs"
 
 
+@pytest.mark.parametrize("shape", [(2, 3, 32, 20, 150), (3, 16, 24, 9, 70), (1, 8, 64, 33, 17)])
+def test_conv_small_stride2_bit_identical(shape):
+    """The EfficientNet stem form (3x3 / stride 2 / pad 1, timm conv_stem + bn1 + SiLU) on the halo-tiled
+    direct kernel's stride-2 configuration (automatic choice) vs the generic kernel, bit for bit; odd sizes."""
+    from hiseg import ops
+    N, Cin, Cout, H, W = shape
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(17)
+    x = ops.Act.from_nchw(torch.randn(N, Cin, H, W, device=DEV, generator=g), dt)
+    w = torch.randn(Cout, Cin, 3, 3, device=DEV, generator=g) / (Cin * 9) ** 0.5
+    bn = torch.nn.BatchNorm2d(Cout).to(DEV).eval()
+    filler.fill_module(bn)
+    p = ops.pack_conv(w, None, bn, 3, dt, DEV, stride=2, pad=1)
+    ref = ops.conv2d(p, x, variant=-1).t.clone()
+    auto = ops.conv2d(p, x, variant=0).t.clone()
+    torch.cuda.synchronize()
+    assert torch.isfinite(ref.float()).all()
+    assert torch.equal(auto, ref)
+
+
 # The EfficientNet encoder's 1x1 layers and the head's narrow 1x1 layers on the persistent pointwise kernel
 # (variant 90 and the automatic choice) vs the generic kernel, bit for bit: SiLU expansions (channel tails of
 # 24 / 40 input channels, ragged 256-column tiles at 672 / 1152, run-time k-step counts), SE-gated projections
