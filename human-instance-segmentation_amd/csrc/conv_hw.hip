@@ -77,7 +77,7 @@ __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
   const int wco = w / WPX, wpx = w % WPX;
 
   // ---- XCD-major bijective remap; Cout tiles fastest, then the 16 x 16 pixel tiles of an image row-major
-  const int nco = d.Cout_pad / BCO;
+  const int nco = (d.Cout_pad + BCO - 1) / BCO;   // (BCO 64 over 16 / 32 / 48 columns: one partial tile)
   const int ntx = (d.W + 15) >> 4, nty = (d.H + 15) >> 4;
   const int nwg = gridDim.x;
   const int orig = blockIdx.x;
@@ -386,7 +386,7 @@ template <int BCO, bool REUSE>
 static int launch_hw(const ConvArgs& a, hipStream_t s) {
   const hiseg_conv2d_desc& d = a.d;
   const int tiles = d.N * ((d.H + 15) / 16) * ((d.W + 15) / 16);
-  const int nco = d.Cout_pad / BCO;
+  const int nco = (d.Cout_pad + BCO - 1) / BCO;
   const size_t ring_halo = (size_t)4 * BCO * 64 + 2 * kHaloBytes;
   const size_t epi = (size_t)256 * BCO * 2;
   const size_t lds = ring_halo > epi ? ring_halo : epi;
@@ -428,8 +428,12 @@ int conv_hw_try(const ConvArgs& a, hipStream_t s, int variant) {
   if (d.act != HISEG_ACT_NONE && d.act != HISEG_ACT_RELU) return 0;
   if (d.Ca % 32 != 0 || d.Ca < 64 || d.K_pad != 9 * d.Ca) return 0;
   if ((d.a_cstride | d.a_coff) & 7) return 0;
+  // BCO 64 also takes 16 / 32 / 48 output columns as one partial tile: weight rows past Cout_pad read zeros
+  // (exact num_records), columns past Cout are neither scaled from real tables nor stored
   const int cmul = variant >= 88 ? 63 : 127;
-  if ((d.Cout & cmul) || ((d.o_cstride | d.o_coff) & 7) || (d.residual && ((d.r_cstride | d.r_coff) & 7))) return 0;
+  const bool narrow = variant >= 88 && d.Cout < 64 && d.Cout % 16 == 0;
+  if (((d.Cout & cmul) && !narrow) || ((d.o_cstride | d.o_coff) & 7) || (d.residual && ((d.r_cstride | d.r_coff) & 7)))
+    return 0;
   if ((((uintptr_t)d.scale | (uintptr_t)d.shift | (uintptr_t)d.out | (uintptr_t)d.residual) & 15)) return 0;
   const long long span_a = (long long)d.N * d.H * d.W * d.a_cstride * 2;
   const long long span_w = (long long)d.Cout_pad * d.K_pad * 2;

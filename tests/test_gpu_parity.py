@@ -727,9 +727,12 @@ HW_CASES = {
     "64_res_roi_64x48": (3, 64, 64, 64, 48, True, True, 0),
     "256_to_64_ragged_21x13": (2, 256, 64, 21, 13, False, False, 0),
     "128_to_192_offset_view_17x9": (2, 128, 192, 17, 9, True, True, 32),
+    # BCO 64 over fewer than 64 output columns (EnhancedUNet final 64 -> 32): one partial Cout tile
+    "64_to_32_roi_64x48": (3, 64, 32, 64, 48, False, True, 0),
+    "128_to_16_res_13x9": (2, 128, 16, 13, 9, True, True, 0),
 }
 
-# BCO-128/256 configurations need a 128-multiple Cout, the BCO-64 ones (88 / 89) a 64-multiple
+# BCO-128/256 configurations need a 128-multiple Cout, the BCO-64 ones (88 / 89) a 64-multiple or 16 / 32 / 48
 HW_VARIANT_CMUL = {80: 256, 82: 128, 84: 256, 86: 128, 88: 64, 89: 64}
 
 
@@ -738,7 +741,8 @@ HW_VARIANT_CMUL = {80: 256, 82: 128, 84: 256, 86: 128, 88: 64, 89: 64}
 def test_conv_halo_wide_within_bf16(name, variant):
     from hiseg import ops
     N, Cin, Cout, H, W, res, relu, coff = HW_CASES[name]
-    if Cout % HW_VARIANT_CMUL[variant]:
+    narrow = variant in (88, 89) and Cout < 64 and Cout % 16 == 0
+    if Cout % HW_VARIANT_CMUL[variant] and not narrow:
         pytest.skip("configuration needs a larger Cout multiple (the kernel declines; covered by the fallback tests)")
     dt = torch.bfloat16
     g = torch.Generator(device=DEV).manual_seed(11)
