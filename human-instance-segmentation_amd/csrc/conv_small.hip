@@ -64,7 +64,7 @@ __global__ void __launch_bounds__(256) conv_small_kernel(ConvArgs a, int WS, int
   // ---- stage weights and the halo (zero padding, upsampling, in_scale).  Loads are issued
   // unconditionally in batches of UB per thread (clamped addresses, zero-select after the
   // load) so that UB loads are in flight before the first LDS store.
-  constexpr int UB = 8;
+  constexpr int UB = 16;   // 16 x 16 B per thread in flight: a workgroup stages up to 140 KB, at one CU per workgroup
   const int nw = d.Cout_pad * kch;
   const SmallDiv dkch(kch), dcch(cch);
   for (int i0 = t; i0 < nw; i0 += 256 * UB) {
