@@ -357,6 +357,10 @@ int conv_pw_try(const ConvArgs& a, hipStream_t s, int variant) {
   if (d.convT && d.residual) return 0;
   const int nks = (a.Cin + 31) / 32;
   if (d.K_pad < nks * 32 || nks > 9) return 0;
+  // HISEG_PW_EFF=0 restores the round-2 v5 coverage (256-multiple columns, 4 / 8 / 9 k-steps of whole 32-channel
+  // slices, no SE gate) for same-box A/B timing
+  static const bool eff = [] { const char* e = getenv("HISEG_PW_EFF"); return !(e && atoi(e) == 0); }();
+  if (!eff && (d.Cout_pad % 256 || d.Ca % 32 || d.in_scale || (nks != 4 && nks != 8 && nks != 9))) return 0;
   const bool comb = nks == 9;
   if (comb ? (d.Ca != 256 || d.Cb > 32 || d.convT || d.residual || d.mul || d.in_scale ||
               (d.act != HISEG_ACT_NONE && d.act != HISEG_ACT_RELU))

@@ -743,13 +743,18 @@ static int dwconv_launch(int dtype, const void* in, int N, int H, int W, int C, 
   const int tiles = hiseg_dw_gap_tiles(N, Ho, Wo);
   dim3 grid(tiles, N, (nch + 255) / 256);
   dim3 gridq(tiles, N, (nq + ctq - 1) / ctq);
+  // HISEG_DWCONV_Q=0: the round-2 v5 bf16 kernel (8 channels per thread, weights re-read per strip), A/B only
+  static const bool dwq = [] { const char* e = getenv("HISEG_DWCONV_Q"); return !(e && atoi(e) == 0); }();
 #define DW_L(KS, ST)                                                                                          \
   do {                                                                                                        \
-    if (dtype == HISEG_BF16)                                                                                  \
+    if (dtype == HISEG_BF16 && dwq)                                                                           \
       hipLaunchKernelGGL((dwconv_q_kernel<KS, ST>), gridq, dim3(256), 0, s, in, H, W, C, w, scale, shift,     \
                          act, out, Ho, Wo, gap, ctq);                                                         \
-    else                                                                                                      \
+    else if (dtype != HISEG_BF16)                                                                             \
       hipLaunchKernelGGL((dwconv_kernel<float, KS, ST>), grid, dim3(256), 0, s, in, H, W, C, w, scale, shift,  \
+                         act, out, Ho, Wo, gap);                                                              \
+    else                                                                                                      \
+      hipLaunchKernelGGL((dwconv_kernel<bf16_t, KS, ST>), grid, dim3(256), 0, s, in, H, W, C, w, scale, shift, \
                          act, out, Ho, Wo, gap);                                                              \
   } while (0)
   if (K == 3 && stride == 1) DW_L(3, 1);
