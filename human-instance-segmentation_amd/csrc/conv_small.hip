@@ -35,9 +35,12 @@ __device__ __forceinline__ unsigned long long stamp_small() {
 
 // STAMP (diagnostic): s_memtime at entry, after staging, after compute, at exit -> u64 x 4 per
 // workgroup in the buffer passed as desc.out2 (out2 itself is then not written).
-// ST: stride (2: the EfficientNet stem, halo of (TH-1)*2+KS rows x 129 columns)
-template <int KS, int TH, typename TO, int NJ, bool STAMP = false, int ST = 1>
-__global__ void __launch_bounds__(256) conv_small_kernel(ConvArgs a, int WS, int PS) {
+// ST: stride (2: the EfficientNet stem, halo of (TH-1)*2+KS rows x 129 columns).  NW: waves per workgroup -- 8
+// where the LDS footprint allows one workgroup per CU (wide-K two-source decoder convs: weights + halo > 80 KB),
+// so that each SIMD still has two waves to hide the staging loads' and the fragment reads' latency.
+template <int KS, int TH, typename TO, int NJ, bool STAMP = false, int ST = 1, int NW = 4>
+__global__ void __launch_bounds__(NW * 64) conv_small_kernel(ConvArgs a, int WS, int PS) {
+  constexpr int NT = NW * 64;
   unsigned long long st0 = 0, st1 = 0, st2 = 0;
   if constexpr (STAMP) st0 = stamp_small();
   unsigned long long* stamp_buf = STAMP ? reinterpret_cast<unsigned long long*>(a.d.out2) : nullptr;
@@ -67,18 +70,18 @@ __global__ void __launch_bounds__(256) conv_small_kernel(ConvArgs a, int WS, int
   constexpr int UB = 16;   // 16 x 16 B per thread in flight: a workgroup stages up to 140 KB, at one CU per workgroup
   const int nw = d.Cout_pad * kch;
   const SmallDiv dkch(kch), dcch(cch);
-  for (int i0 = t; i0 < nw; i0 += 256 * UB) {
+  for (int i0 = t; i0 < nw; i0 += NT * UB) {
     uint4 v[UB];
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
-      int i = i0 + u * 256;
+      int i = i0 + u * NT;
       i = i < nw ? i : nw - 1;
       const int r = dkch.div(i), c = i - r * kch;
       v[u] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(d.weight) + (long long)r * d.K_pad + c * 8);
     }
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
-      const int i = i0 + u * 256;
+      const int i = i0 + u * NT;
       if (i < nw) {
         const int r = dkch.div(i), c = i - r * kch;
         sW[r * WS + c] = v[u];
@@ -88,12 +91,12 @@ __global__ void __launch_bounds__(256) conv_small_kernel(ConvArgs a, int WS, int
   const int nh = HR * HC * cch;
   const uint16_t* srcA = reinterpret_cast<const uint16_t*>(d.srcA);
   const uint16_t* srcB = reinterpret_cast<const uint16_t*>(d.Cb ? d.srcB : d.srcA);
-  for (int i0 = t; i0 < nh; i0 += 256 * UB) {
+  for (int i0 = t; i0 < nh; i0 += NT * UB) {
     uint4 v[UB];
     bool ok[UB];
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
-      const int i = i0 + u * 256;
+      const int i = i0 + u * NT;
       const int pix = dcch.div(i), c = i - pix * cch;
       const int prow = pix / HC, pcol = pix - prow * HC;
       const int iy = y0 * ST + prow - pad, ix = x0 * ST + pcol - pad;
@@ -109,7 +112,7 @@ __global__ void __launch_bounds__(256) conv_small_kernel(ConvArgs a, int WS, int
     }
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
-      const int i = i0 + u * 256;
+      const int i = i0 + u * NT;
       if (i < nh) {
         const int pix = dcch.div(i), c = i - pix * cch;
         sX[pix * PS + c] = ok[u] ? v[u] : make_uint4(0u, 0u, 0u, 0u);
@@ -119,7 +122,7 @@ __global__ void __launch_bounds__(256) conv_small_kernel(ConvArgs a, int WS, int
   __syncthreads();
   if (d.in_scale) {   // squeeze-excite gate on the src-A channels, rounded to bf16 in place
     const int cha = d.Ca >> 3;
-    for (int i = t; i < HR * HC * cha; i += 256) {
+    for (int i = t; i < HR * HC * cha; i += NT) {
       const int c = i % cha, pix = i / cha;
       uint4* q = &sX[pix * PS + c];
       const float4* sp = reinterpret_cast<const float4*>(d.in_scale + (long long)n * d.Ca + c * 8);
@@ -139,7 +142,8 @@ __global__ void __launch_bounds__(256) conv_small_kernel(ConvArgs a, int WS, int
   // 4 blocks of 16: per 32-deep k chunk a wave reads G B fragments and (<= 4) A fragments and
   // issues G x 4 independent MFMAs.  The (tap, channel) of a lane's 8 k values advances
   // incrementally from chunk to chunk (no division in the loop).
-  constexpr int G = TH >= 4 ? 4 : (TH == 2 ? 2 : 1);
+  constexpr int G0 = TH * 4 / NW;
+  constexpr int G = G0 >= 4 ? 4 : (G0 >= 2 ? 2 : 1);
   constexpr int NI = TH * 4 / G;          // work items per tile
   const int K = KS * KS * Cin;
   const int nkc = (K + 31) >> 5;          // 32-deep chunks holding real k
@@ -165,7 +169,7 @@ __global__ void __launch_bounds__(256) conv_small_kernel(ConvArgs a, int WS, int
         sh[j] = *reinterpret_cast<const floatx4*>(d.shift + co);
       }
     }
-    for (int it = w; it < NI; it += 4) {
+    for (int it = w; it < NI; it += NW) {
       const int r = (it * G) >> 2;
       const int gx0 = ((it * G) & 3) * 16;
       const int oy = y0 + r;
@@ -263,23 +267,30 @@ __global__ void __launch_bounds__(256) conv_small_kernel(ConvArgs a, int WS, int
 
 static int odd_slots(int n) { return (n & 1) ? n : n + 1; }
 
-template <int KS, int TH, typename TO, int NJ, bool STAMP, int ST = 1>
+template <int KS, int TH, typename TO, int NJ, bool STAMP, int ST = 1, int NW = 4>
 static int launch_small_nj(const ConvArgs& a, hipStream_t s, int WS, int PS, size_t lds) {
   const hiseg_conv2d_desc& d = a.d;
   const int ntx = (d.Wo + 63) / 64, nty = (d.Ho + TH - 1) / TH;
-  auto kern = conv_small_kernel<KS, TH, TO, NJ, STAMP, ST>;
+  auto kern = conv_small_kernel<KS, TH, TO, NJ, STAMP, ST, NW>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3(ntx * nty * d.N), dim3(256), lds, s, a, WS, PS);
+  hipLaunchKernelGGL(kern, dim3(ntx * nty * d.N), dim3(NW * 64), lds, s, a, WS, PS);
   return hiseg_check_launch("conv_small");
 }
 
 template <int KS, int TH, typename TO, bool STAMP = false>
 static int launch_small(const ConvArgs& a, hipStream_t s, int WS, int PS, size_t lds) {
   const int nco = a.d.Cout_pad / 16;
+  if constexpr (!STAMP && KS == 3 && TH >= 2) {
+    if (lds > 80 * 1024) {   // one workgroup per CU: 8 waves
+      if (nco == 1) return launch_small_nj<KS, TH, TO, 1, STAMP, 1, 8>(a, s, WS, PS, lds);
+      if (nco == 2) return launch_small_nj<KS, TH, TO, 2, STAMP, 1, 8>(a, s, WS, PS, lds);
+      return launch_small_nj<KS, TH, TO, 4, STAMP, 1, 8>(a, s, WS, PS, lds);
+    }
+  }
   if (nco == 1) return launch_small_nj<KS, TH, TO, 1, STAMP>(a, s, WS, PS, lds);
   if (nco == 2) return launch_small_nj<KS, TH, TO, 2, STAMP>(a, s, WS, PS, lds);
   return launch_small_nj<KS, TH, TO, 4, STAMP>(a, s, WS, PS, lds);
