@@ -285,7 +285,9 @@ template <int KS, int TH, typename TO, bool STAMP = false>
 static int launch_small(const ConvArgs& a, hipStream_t s, int WS, int PS, size_t lds) {
   const int nco = a.d.Cout_pad / 16;
   if constexpr (!STAMP && KS == 3 && TH >= 2) {
-    if (lds > 80 * 1024) {   // one workgroup per CU: 8 waves
+    // HISEG_SMALL_NW8=0 keeps 4-wave workgroups (A/B timing only)
+    static const bool nw8 = [] { const char* e = getenv("HISEG_SMALL_NW8"); return !(e && atoi(e) == 0); }();
+    if (nw8 && lds > 80 * 1024) {   // one workgroup per CU: 8 waves
       if (nco == 1) return launch_small_nj<KS, TH, TO, 1, STAMP, 1, 8>(a, s, WS, PS, lds);
       if (nco == 2) return launch_small_nj<KS, TH, TO, 2, STAMP, 1, 8>(a, s, WS, PS, lds);
       return launch_small_nj<KS, TH, TO, 4, STAMP, 1, 8>(a, s, WS, PS, lds);

@@ -28,6 +28,10 @@ def main():
     pr.s_head = torch.cuda.Stream(priority=-1)
     pr.s_unet = torch.cuda.Stream(priority=0)
     runners["pipe_headprio"] = pr
+    pu = hiseg.StreamPipelinedExport(wrapper)
+    pu.s_head = torch.cuda.Stream(priority=0)
+    pu.s_unet = torch.cuda.Stream(priority=-1)
+    runners["pipe_unetprio"] = pu
     res = {k: [] for k in runners}
     with torch.no_grad():
         for _ in range(args.rounds):
