@@ -602,11 +602,20 @@ __global__ void __launch_bounds__(256) ubf_bwd1_kernel(UbfArgs u, const float* d
   const float scc = u.ln ? u.scale[ns * 32 + c] : u.scale[c], shc = u.ln ? u.shift[ns * 32 + c] : u.shift[c];
   const float w0 = u.u1_w[c], w1 = u.u1_w[32 + c];
   float sg = 0.f, sgx = 0.f, sx = 0.f, dw0 = 0.f, dw1 = 0.f, db0s = 0.f, db1s = 0.f;
-  for (long long p = b + r; p < e; p += 8) {
-    const int X = (int)(p % W);
-    const long long tt = p / W;
-    const int Y = (int)(tt % H);
-    const long long n = tt / H;
+  // (n, Y, X) of p advanced incrementally by the row stride 8: the 64-bit div / mod per pixel dominated the loop
+  int X, Y;
+  long long n;
+  {
+    const long long p0 = b + r, tt = p0 / W;
+    X = (int)(p0 - tt * W);
+    Y = (int)(tt % H);
+    n = tt / H;
+  }
+  for (long long p = b + r; p < e; p += 8, X += 8) {
+    while (X >= W) {
+      X -= W;
+      if (++Y == H) { Y = 0; ++n; }
+    }
     const long long pp = (long long)Y * W + X;
     const float* G = bgfg + n * 2 * plane + pp;
     const float* Tn = tn + n * 2 * plane + pp;
@@ -707,11 +716,19 @@ __global__ void __launch_bounds__(256) ubf_bwd2_kernel(UbfArgs u, const float* d
   float dw[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) dw[i] = 0.f;
-  for (long long p = b + r; p < e; p += 8) {
-    const int x = (int)(p % u.w);
-    const long long tt = p / u.w;
-    const int y = (int)(tt % u.h);
-    const long long n = tt / u.h;
+  int x, y;
+  long long n;
+  {
+    const long long p0 = b + r, tt = p0 / u.w;
+    x = (int)(p0 - tt * u.w);
+    y = (int)(tt % u.h);
+    n = tt / u.h;
+  }
+  for (long long p = b + r; p < e; p += 8, x += 8) {
+    while (x >= u.w) {
+      x -= u.w;
+      if (++y == u.h) { y = 0; ++n; }
+    }
     const float l0 = u.low[p * 2], l1 = u.low[p * 2 + 1];
     const float mu = u.ln ? u.mean[n] : u.mean[c], inv = u.ln ? u.invstd[n] : u.invstd[c];
     const float scc = u.ln ? u.scale[n * 32 + c] : u.scale[c], shc = u.ln ? u.shift[n * 32 + c] : u.shift[c];
@@ -948,9 +965,9 @@ static UbfArgs ubf_args(const hiseg_ubf_desc* d) {
 }
 
 // blocks of the pass-1 reduction: kUbfBlocks pixel ranges (BN), or sb ranges per sample (LN)
-static int ubf_sb(int N) { const int sb = 512 / (N > 0 ? N : 1); return sb < 1 ? 1 : sb; }
+static int ubf_sb(int N) { const int sb = 2048 / (N > 0 ? N : 1); return sb < 1 ? 1 : sb; }
 
-static const int kUbfBlocks = 512;
+static const int kUbfBlocks = 2048;   // 8 workgroups per CU: the per-pixel loops are latency-bound
 
 extern "C" int hiseg_ubf_ws(int N) {
   const long long nb1 = (long long)N * ubf_sb(N);
