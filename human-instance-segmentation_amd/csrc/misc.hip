@@ -446,7 +446,24 @@ __global__ void reset_max_kernel(unsigned* buf) { *buf = 0u; }  // encodes below
 
 __global__ void __launch_bounds__(256) image_max_kernel(const float* x, long long n, unsigned* buf) {
   float m = -FLT_MAX;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) m = fmaxf(m, x[i]);
+  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x, stride = (long long)gridDim.x * 256;
+  long long head = 0;
+  if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {   // 16-B loads, four in flight per thread (scalar: 1 TB/s)
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    const long long n4 = n >> 2;
+    long long i = gid;
+    for (; i + 3 * stride < n4; i += 4 * stride) {
+      const float4 a = x4[i], b = x4[i + stride], c = x4[i + 2 * stride], d = x4[i + 3 * stride];
+      m = fmaxf(m, fmaxf(fmaxf(fmaxf(a.x, a.y), fmaxf(a.z, a.w)), fmaxf(fmaxf(b.x, b.y), fmaxf(b.z, b.w))));
+      m = fmaxf(m, fmaxf(fmaxf(fmaxf(c.x, c.y), fmaxf(c.z, c.w)), fmaxf(fmaxf(d.x, d.y), fmaxf(d.z, d.w))));
+    }
+    for (; i < n4; i += stride) {
+      const float4 a = x4[i];
+      m = fmaxf(m, fmaxf(fmaxf(a.x, a.y), fmaxf(a.z, a.w)));
+    }
+    head = n4 << 2;
+  }
+  for (long long i = head + gid; i < n; i += stride) m = fmaxf(m, x[i]);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
   if ((threadIdx.x & 63) == 0) atomicMax(buf, ord_enc(m));
