@@ -305,21 +305,24 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
   if (pb_end > nblocks) pb_end = nblocks;
   const int nit = pb_end > pb_begin ? pb_end - pb_begin : 0;
 
-  // K tile source (wave-uniform by eligibility: one source per 128-column tile)
-  const int ci_tile = k0 % a.Cin;
-  const bool fromA = d.Cb == 0 || ci_tile < d.Ca;
-  const int cs = fromA ? d.a_cstride : d.b_cstride;
-  const int coff = fromA ? d.a_coff : d.b_coff - d.Ca;
-  const int sh = (fromA && d.a_up == 2) ? 1 : 0;   // nearest-x2 upsampled source (UNet decoder)
-  const int Hs = d.H >> sh, Ws = d.W >> sh;
-  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(fromA ? d.srcA : d.srcB),
-                                                                       (short)0, 0x7fffffff, 0x00020000);
+  // X source per lane chunk: a 128-column K tile may hold channels of both sources (the EnhancedUNet's 64 + 64
+  // decoder concat), so one buffer resource spans both tensors from the lower address (the launcher checks that
+  // the two fit in 2^31 bytes of it) and each lane carries its source's byte offset, channel stride and
+  // upsampling shift
+  const char* const pa = reinterpret_cast<const char*>(d.srcA);
+  const char* const pb = d.Cb ? reinterpret_cast<const char*>(d.srcB) : pa;
+  const char* const xbase = pa < pb ? pa : pb;
+  const unsigned dA = (unsigned)(pa - xbase), dB = (unsigned)(pb - xbase);
+  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(xbase), (short)0, 0x7fffffff,
+                                                                       0x00020000);
   const __amdgpu_buffer_rsrc_t rY = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.dy), (short)0, 0x7fffffff,
                                                                        0x00020000);
   const unsigned OOB = 0x80000000u;
 
   // per-lane DMA state: instruction i fills rows 4(w + 4i) .. +3; this lane row (lane >> 4), slot lane & 15
   int xo[4], ky[4], kx[4], yo[4];       // X channel offset (or -1 = zero column), tap; dY column offset (or -1)
+  int xcs[4], xsh[4];                   // X source's channel stride and upsampling shift (src A of a decoder: 1)
+  unsigned xd[4];                       // X source's byte offset from the resource base
   int pn[4], py[4], px[4], pp[4];       // pixel (n, oy, ox) and flat index of the lane's row
   int yq[4];                            // ConvTranspose: the column's sub-pixel q (output pixel 2y + q/2, 2x + q%2)
   unsigned bias_lanes = 0;              // bit i: this lane's chunk of instruction i is the GEMM-bias column's
@@ -330,7 +333,11 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
     const int k = k0 + 8 * c;
     const int tap = k / a.Cin;
     const int ci = k - tap * a.Cin;
-    xo[i] = k < a.Ktot ? coff + ci : -1;
+    const bool la = d.Cb == 0 || ci < d.Ca;
+    xo[i] = k < a.Ktot ? (la ? d.a_coff + ci : d.b_coff + ci - d.Ca) : -1;
+    xcs[i] = la ? d.a_cstride : d.b_cstride;
+    xsh[i] = (la && d.a_up == 2) ? 1 : 0;
+    xd[i] = la ? dA : dB;
     if (a.want_bias && k == a.Ktot) bias_lanes |= 1u << i;
     ky[i] = tap / d.KW;
     kx[i] = tap - ky[i] * d.KW;
@@ -361,7 +368,9 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
       const int iy = py[i] * d.stride - d.pad + ky[i];
       const int ix = px[i] * d.stride - d.pad + kx[i];
       const bool okx = xo[i] >= 0 && pp[i] < a.M && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
-      const unsigned offx = okx ? (unsigned)((((pn[i] * Hs + (iy >> sh)) * Ws + (ix >> sh)) * cs + xo[i]) * 2) : OOB;
+      const int sh = xsh[i], Hs = d.H >> sh, Ws = d.W >> sh;
+      const unsigned offx =
+          okx ? xd[i] + (unsigned)((((pn[i] * Hs + (iy >> sh)) * Ws + (ix >> sh)) * xcs[i] + xo[i]) * 2) : OOB;
       wg_dma16(rX, sb + row_base, offx);
       const bool oky = yo[i] >= 0 && pp[i] < a.M;
       int yp = pp[i];
@@ -484,15 +493,19 @@ static int wgrad_tr_try(const WgradArgs& a, hipStream_t s) {
   const hiseg_conv2d_desc& d = a.d;
   if (!wgrad_tr_mode()) return 0;
   if (d.dtype != HISEG_BF16) return 0;
-  // one source per 128-column K tile: A ends on a tile boundary and (with more than one tap) so does each tap
-  if (!(d.Cb == 0 || (d.Ca % 128 == 0 && (d.KH * d.KW == 1 || d.Cb % 128 == 0)))) return 0;
-  if (a.Cin % 8 || a.dy_cs % 8 || a.dy_coff % 8 || d.a_cstride % 8 || d.a_coff % 8) return 0;
+  // 8-channel chunks never straddle the two sources
+  if (d.Ca % 8 || a.Cin % 8 || a.dy_cs % 8 || a.dy_coff % 8 || d.a_cstride % 8 || d.a_coff % 8) return 0;
   if (d.Cb && (d.b_cstride % 8 || d.b_coff % 8)) return 0;
   if (d.convT && (d.Cout % 32 || d.a_up != 1)) return 0;   // C = Cout / 4 a multiple of 8
   const long long span_a = (long long)d.N * d.H * d.W * d.a_cstride * 2;
   const long long span_b = d.Cb ? (long long)d.N * d.H * d.W * d.b_cstride * 2 : 0;
   const long long span_y = ((long long)a.M * (d.convT ? 4 : 1) * a.dy_cs + a.dy_coff + a.Cg) * 2;
   if (span_a >= 0x7fffffffll || span_b >= 0x7fffffffll || span_y >= 0x7fffffffll) return 0;
+  if (d.Cb) {   // both sources within 2^31 bytes of the lower one (the kernel's single X resource)
+    const long long pa = (long long)(uintptr_t)d.srcA, pb = (long long)(uintptr_t)d.srcB;
+    const long long lo = pa < pb ? pa : pb;
+    if (pa - lo + span_a >= 0x7fffffffll || pb - lo + span_b >= 0x7fffffffll) return 0;
+  }
   const int r = a.Cg >= 128 ? wgrad_tr_launch<128, 2, 2, 2>(a, s)
               : a.Cg >= 64  ? wgrad_tr_launch<64, 4, 1, 2>(a, s)
               : a.Cg >= 32  ? wgrad_tr_launch<32, 4, 1, 2>(a, s)
