@@ -34,6 +34,8 @@ struct WgradArgs {
   int Cg, Kg;
   int splits, blocks_per_split;  // pixel blocks per split
   float* ws;
+  int x_tile_src;  // transposed-read kernel: 1 = one X source per K tile (two sources too far apart for one
+                   // buffer resource; the layer's tiles never mix them), 0 = per-lane source over one resource
 };
 
 // KCH x KCH transpose of 16-B chunks: in[i] = chunk of pixel i (KCH channels), out[e] = chunk of
@@ -311,8 +313,9 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
   // upsampling shift
   const char* const pa = reinterpret_cast<const char*>(d.srcA);
   const char* const pb = d.Cb ? reinterpret_cast<const char*>(d.srcB) : pa;
-  const char* const xbase = pa < pb ? pa : pb;
-  const unsigned dA = (unsigned)(pa - xbase), dB = (unsigned)(pb - xbase);
+  const bool tile_a = d.Cb == 0 || k0 % a.Cin < d.Ca;   // (x_tile_src: the K tile's one source)
+  const char* const xbase = a.x_tile_src ? (tile_a ? pa : pb) : (pa < pb ? pa : pb);
+  const unsigned dA = a.x_tile_src ? 0u : (unsigned)(pa - xbase), dB = a.x_tile_src ? 0u : (unsigned)(pb - xbase);
   const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(xbase), (short)0, 0x7fffffff,
                                                                        0x00020000);
   const __amdgpu_buffer_rsrc_t rY = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.dy), (short)0, 0x7fffffff,
@@ -501,15 +504,21 @@ static int wgrad_tr_try(const WgradArgs& a, hipStream_t s) {
   const long long span_b = d.Cb ? (long long)d.N * d.H * d.W * d.b_cstride * 2 : 0;
   const long long span_y = ((long long)a.M * (d.convT ? 4 : 1) * a.dy_cs + a.dy_coff + a.Cg) * 2;
   if (span_a >= 0x7fffffffll || span_b >= 0x7fffffffll || span_y >= 0x7fffffffll) return 0;
-  if (d.Cb) {   // both sources within 2^31 bytes of the lower one (the kernel's single X resource)
+  WgradArgs b = a;
+  b.x_tile_src = 0;
+  if (d.Cb) {   // both sources within 2^31 bytes of the lower one (one X resource), else one source per K tile
     const long long pa = (long long)(uintptr_t)d.srcA, pb = (long long)(uintptr_t)d.srcB;
     const long long lo = pa < pb ? pa : pb;
-    if (pa - lo + span_a >= 0x7fffffffll || pb - lo + span_b >= 0x7fffffffll) return 0;
+    if (pa - lo + span_a >= 0x7fffffffll || pb - lo + span_b >= 0x7fffffffll) {
+      // A ends on a 128-column tile boundary and (with more than one tap) so does each tap
+      if (!(d.Ca % 128 == 0 && (d.KH * d.KW == 1 || d.Cb % 128 == 0))) return 0;
+      b.x_tile_src = 1;
+    }
   }
-  const int r = a.Cg >= 128 ? wgrad_tr_launch<128, 2, 2, 2>(a, s)
-              : a.Cg >= 64  ? wgrad_tr_launch<64, 4, 1, 2>(a, s)
-              : a.Cg >= 32  ? wgrad_tr_launch<32, 4, 1, 2>(a, s)
-                            : wgrad_tr_launch<16, 4, 1, 2>(a, s);
+  const int r = b.Cg >= 128 ? wgrad_tr_launch<128, 2, 2, 2>(b, s)
+              : b.Cg >= 64  ? wgrad_tr_launch<64, 4, 1, 2>(b, s)
+              : b.Cg >= 32  ? wgrad_tr_launch<32, 4, 1, 2>(b, s)
+                            : wgrad_tr_launch<16, 4, 1, 2>(b, s);
   return r < 0 ? r : 1;
 }
 
