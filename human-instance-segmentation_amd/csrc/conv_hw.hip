@@ -103,15 +103,19 @@ __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
   // halo rows: piece h (0..23) = rows 16h + lane / 4; piece 4p + w belongs to wave w (p = 0..5).  The lane's
   // byte offset for piece p (slice 0; OOB outside the image / past row 324), computed where needed: a
   // precomputed array indexed by the stage's piece number would live in scratch
-  auto halo_off = [&](int p) __attribute__((always_inline)) -> unsigned {
+  // slice sl of a two-source layer (the EnhancedUNet decoder concat) comes from src B once 32 sl >= Ca
+  auto halo_off = [&](int p, int sl) __attribute__((always_inline)) -> unsigned {
     const int hr = 16 * (4 * p + w) + lrow;
     const int hy = hr / 18, hx = hr - 18 * hy;
     const int iy = y0 + hy - 1, ix = x0 + hx - 1;
     const bool ok = hr < kHaloRows && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
-    return ok ? (unsigned)((((n * d.H + iy) * d.W + ix) * d.a_cstride + d.a_coff + (slot ^ hhswz(hr)) * 8) * 2) : OOB;
+    const bool fb = 32 * sl >= d.Ca;
+    const int cs = fb ? d.b_cstride : d.a_cstride, coff = fb ? d.b_coff + 32 * sl - d.Ca : d.a_coff + 32 * sl;
+    return ok ? (unsigned)((((n * d.H + iy) * d.W + ix) * cs + coff + (slot ^ hhswz(hr)) * 8) * 2) : OOB;
   };
   const int nrec_w = d.Cout_pad * d.K_pad * 2;
   const int nrec_a = d.N * d.H * d.W * d.a_cstride * 2;
+  const int nrec_b = d.Cb ? d.N * d.H * d.W * d.b_cstride * 2 : 0;
   const int nsl = a.Cin >> 5;          // 32-channel slices
   const int nS = 9 * nsl;
   const unsigned lds_base = (unsigned)(uintptr_t)(lds_void_h*)smem;
@@ -120,12 +124,14 @@ __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
                                                                      0x00020000);
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(d.srcA), (short)0, nrec_a,
                                                                      0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(d.Cb ? d.srcB : d.srcA), (short)0,
+                                                                     nrec_b, 0x00020000);
 
   // ---- the DMA set to be issued next: stage (n_sl, n_tap); weights of that stage, plus, for taps 3..8 of
   // every slice but the last, halo piece (tap - 3) of slice n_sl + 1
   int n_sl = 0, n_tap = 0;
   unsigned p_sbase = lds_base, p_voff[NAI], p_hdst = halo_base, p_hoff = OOB;
-  bool p_halo = false;
+  bool p_halo = false, p_hb = false;
 #pragma unroll
   for (int k = 0; k < NAI; ++k) p_voff[k] = OOB;
   auto prepare_live = [&](int s) __attribute__((always_inline)) {
@@ -136,8 +142,8 @@ __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
     for (int k = 0; k < NAI; ++k) p_voff[k] = woff[k] + kofs;
     p_halo = n_tap >= 3 && n_sl + 1 < nsl;
     const int hp = n_tap >= 3 ? n_tap - 3 : 0;
-    const unsigned ho = halo_off(hp);
-    p_hoff = ho == OOB ? OOB : ho + (unsigned)(64 * (n_sl + 1));
+    p_hoff = halo_off(hp, n_sl + 1);
+    p_hb = 32 * (n_sl + 1) >= d.Ca;
     p_hdst = halo_base + (unsigned)(((n_sl + 1) & 1) * kHaloBytes + 1024 * (4 * hp + w));
     const int tp = n_tap + 1;
     const bool wrap = tp == 9;
@@ -160,7 +166,7 @@ __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
     if constexpr (k < NAI) {
       dma16h(rW, p_sbase + (unsigned)(1024 * (w + 4 * k)), p_voff[k]);
     } else if constexpr (k == NAI) {
-      if (p_halo) dma16h(rA, p_hdst, p_hoff);
+      if (p_halo) dma16h(p_hb ? rB : rA, p_hdst, p_hoff);
     }
   };
   // halo of a set: the hand-over waits count one DMA more when the set following the awaited one carries one
@@ -197,7 +203,7 @@ __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
   // ---- prologue: slice 0's halo (6 pieces per wave), sets 0 and 1 whole, slots 0..1 of set 2
 #pragma unroll
   for (int p = 0; p < 6; ++p)
-    dma16h(rA, halo_base + (unsigned)(1024 * (4 * p + w)), halo_off(p));
+    dma16h(rA, halo_base + (unsigned)(1024 * (4 * p + w)), halo_off(p, 0));
 #pragma unroll
   for (int s = 0; s < STAGES - 2; ++s) {
     prepare(s);
@@ -423,11 +429,13 @@ int launch_hw64(const ConvArgs& a, hipStream_t s, bool reuse);
 int conv_hw_try(const ConvArgs& a, hipStream_t s, int variant) {
   const hiseg_conv2d_desc& d = a.d;
   if (d.dtype != HISEG_BF16 || d.out_dtype != HISEG_BF16) return 0;
-  if (d.a_up != 1 || d.in_scale != nullptr || d.convT || d.mul != nullptr || d.out2 != nullptr || d.Cb != 0) return 0;
+  if (d.a_up != 1 || d.in_scale != nullptr || d.convT || d.mul != nullptr || d.out2 != nullptr) return 0;
   if (d.KH != 3 || d.KW != 3 || d.stride != 1 || d.pad != 1 || d.Ho != d.H || d.Wo != d.W) return 0;
   if (d.act != HISEG_ACT_NONE && d.act != HISEG_ACT_RELU) return 0;
-  if (d.Ca % 32 != 0 || d.Ca < 64 || d.K_pad != 9 * d.Ca) return 0;
+  // two sources (concat): each whole 32-channel slice from one of them
+  if (d.Ca % 32 != 0 || d.Cb % 32 != 0 || d.Ca < 64 || d.K_pad != 9 * (d.Ca + d.Cb)) return 0;
   if ((d.a_cstride | d.a_coff) & 7) return 0;
+  if (d.Cb && (d.srcB == nullptr || ((d.b_cstride | d.b_coff) & 7))) return 0;
   // BCO 64 also takes 16 / 32 / 48 output columns as one partial tile: weight rows past Cout_pad read zeros
   // (exact num_records), columns past Cout are neither scaled from real tables nor stored
   const int cmul = variant >= 88 ? 63 : 127;
@@ -436,9 +444,10 @@ int conv_hw_try(const ConvArgs& a, hipStream_t s, int variant) {
     return 0;
   if ((((uintptr_t)d.scale | (uintptr_t)d.shift | (uintptr_t)d.out | (uintptr_t)d.residual) & 15)) return 0;
   const long long span_a = (long long)d.N * d.H * d.W * d.a_cstride * 2;
+  const long long span_b = d.Cb ? (long long)d.N * d.H * d.W * d.b_cstride * 2 : 0;
   const long long span_w = (long long)d.Cout_pad * d.K_pad * 2;
   const long long span_r = d.residual ? (long long)a.M * d.r_cstride * 2 : 0;
-  if (span_a >= 0x7fffffffll || span_w >= 0x7fffffffll || span_r >= 0x7fffffffll) return 0;
+  if (span_a >= 0x7fffffffll || span_b >= 0x7fffffffll || span_w >= 0x7fffffffll || span_r >= 0x7fffffffll) return 0;
   int r;
   switch (variant) {
     case 80: if (d.Cout % 256) return 0; r = launch_hw<256, false>(a, s); break;

@@ -759,6 +759,32 @@ def test_conv_halo_wide_within_bf16(name, variant):
     assert ((y - ref).abs().max() / ref.abs().max()).item() < 8e-3
 
 
+@pytest.mark.parametrize("variant", [86, 89])
+@pytest.mark.parametrize("shape", [(3, 64, 64, 64, 64, 48, True), (2, 128, 128, 128, 32, 24, False),
+                                   (2, 64, 32, 64, 21, 13, True), (2, 96, 64, 128, 9, 23, False)])
+def test_conv_halo_two_source_within_bf16(shape, variant):
+    """The halo-tiled kernel over a two-source concat (EnhancedUNet decoder: up ++ skip, hierarchical_segmentation_unet.py
+    decoders) -- each 32-channel slice read from its own source -- vs the generic kernel within bf16 rounding."""
+    from hiseg import ops
+    N, Ca, Cb, Cout, H, W, res = shape
+    if variant == 86 and Cout % 128:
+        pytest.skip("BCO 128 needs a 128-multiple Cout")
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(19)
+    xa = ops.Act.from_nchw(torch.randn(N, Ca, H, W, device=DEV, generator=g), dt)
+    xb = ops.Act.from_nchw(torch.randn(N, Cb, H, W, device=DEV, generator=g), dt)
+    w = torch.randn(Cout, Ca + Cb, 3, 3, device=DEV, generator=g) / ((Ca + Cb) * 9) ** 0.5
+    p = ops.pack_conv(w, torch.randn(Cout, device=DEV, generator=g) * 0.1, None, 1, dt, DEV, pad=1, split=(Ca, Cb))
+    R = ops.Act.from_nchw(torch.randn(N, Cout, H, W, device=DEV, generator=g), dt) if res else None
+    ref = ops.conv2d(p, xa, xb, residual=R, variant=-1).to_nchw().float()
+    y = ops.conv2d(p, xa, xb, residual=R, variant=variant).to_nchw().float()
+    auto = ops.conv2d(p, xa, xb, residual=R, variant=0).to_nchw().float()
+    torch.cuda.synchronize()
+    assert torch.isfinite(y).all()
+    assert ((y - ref).abs().max() / ref.abs().max()).item() < 8e-3
+    assert ((auto - ref).abs().max() / ref.abs().max()).item() < 8e-3
+
+
 @pytest.mark.parametrize("name", list(VARIANT_CASES))
 def test_conv_automatic_choice_within_bf16(name):
     """hiseg_conv2d_fwd's automatic kernel choice on every VARIANT_CASES layer: bit-identical to the generic kernel
@@ -783,7 +809,9 @@ def test_conv_automatic_choice_within_bf16(name):
     ref = ops.conv2d(p, xa, xb, residual=R, mul=M, variant=-1).to_nchw().float()
     y = ops.conv2d(p, xa, xb, residual=R, mul=M, variant=0).to_nchw().float()
     torch.cuda.synchronize()
-    halo = (not convT and k == 3 and not Cb and not mul and not o2 and Cout % 128 == 0 and Ca % 32 == 0 and Ca >= 64)
+    # the halo kernel also takes two-source layers whose sources are whole 32-channel slices (round 2 v10)
+    halo = (not convT and k == 3 and Cb % 32 == 0 and not mul and not o2 and Cout % 128 == 0 and Ca % 32 == 0
+            and Ca >= 64)
     if halo:
         assert ((y - ref).abs().max() / ref.abs().max()).item() < 8e-3
     else:
