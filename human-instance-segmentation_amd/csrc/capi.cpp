@@ -25,3 +25,27 @@ int hiseg_check_launch(const char* what) {
 extern "C" int hiseg_version(void) { return 100; }
 extern "C" const char* hiseg_last_error_string(void) { return g_err; }
 extern "C" int hiseg_built_for_gfx950(void) { return 1; }
+
+extern "C" int hiseg_stream_create_cu_mask(const unsigned* mask, int nwords, hiseg_stream_t* out) {
+  if (!mask || nwords <= 0 || !out) {
+    hiseg_set_error("stream_create_cu_mask: bad args");
+    return HISEG_ERR_BAD_ARG;
+  }
+  hipStream_t s = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)nwords, mask);
+  if (e != hipSuccess) {
+    hiseg_set_error("stream_create_cu_mask: %s", hipGetErrorString(e));
+    return HISEG_ERR_LAUNCH;
+  }
+  *out = (hiseg_stream_t)s;
+  return HISEG_OK;
+}
+
+extern "C" int hiseg_stream_destroy(hiseg_stream_t s) {
+  const hipError_t e = hipStreamDestroy((hipStream_t)s);
+  if (e != hipSuccess) {
+    hiseg_set_error("stream_destroy: %s", hipGetErrorString(e));
+    return HISEG_ERR_LAUNCH;
+  }
+  return HISEG_OK;
+}

@@ -183,6 +183,8 @@ def _declare(lib):
         "hiseg_version": ([], c_int),
         "hiseg_last_error_string": ([], ctypes.c_char_p),
         "hiseg_built_for_gfx950": ([], c_int),
+        "hiseg_stream_create_cu_mask": ([ctypes.POINTER(ctypes.c_uint), c_int, ctypes.POINTER(c_void_p)], c_int),
+        "hiseg_stream_destroy": ([P], c_int),
         "hiseg_roi_align_fwd": ([ctypes.POINTER(RoiAlignDesc), P], c_int),
         "hiseg_conv2d_fwd": ([ctypes.POINTER(Conv2dDesc), P], c_int),
         "hiseg_conv2d_fwd_variant": ([ctypes.POINTER(Conv2dDesc), c_int, P], c_int),

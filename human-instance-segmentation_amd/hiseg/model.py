@@ -15,6 +15,7 @@ from typing import Dict, Optional, Tuple, Union
 import torch
 import torch.nn as nn
 
+from . import _lib as L
 from . import engine
 from .effunet import EfficientNetUnet
 from .layers import RefinedHierarchicalSegmentationHead, ResidualBlock, make_act_unet, make_norm
@@ -217,10 +218,30 @@ class StreamPipelinedExport:
     ready on the caller's current stream when it returns (the caller synchronises as usual).
     """
 
-    def __init__(self, wrapper: "RGBHierarchicalExportWrapper"):
+    def __init__(self, wrapper: "RGBHierarchicalExportWrapper", unet_cu_mask=None):
+        """``unet_cu_mask``: optional list of 32-bit words; the UNet stream then runs only on the CUs whose bits
+        are set (hiseg_stream_create_cu_mask), leaving the rest to the head."""
         self.wrapper = wrapper
-        self.s_unet = torch.cuda.Stream()
+        self._raw_unet = None
+        if unet_cu_mask is None:
+            self.s_unet = torch.cuda.Stream()
+        else:
+            import ctypes
+            words = (ctypes.c_uint * len(unet_cu_mask))(*[int(w) & 0xFFFFFFFF for w in unet_cu_mask])
+            h = ctypes.c_void_p()
+            L.check(L.lib().hiseg_stream_create_cu_mask(words, len(unet_cu_mask), ctypes.byref(h)),
+                    "stream_create_cu_mask")
+            self._raw_unet = h.value
+            self.s_unet = torch.cuda.ExternalStream(h.value)
         self.s_head = torch.cuda.Stream()
+
+    def __del__(self):
+        if getattr(self, "_raw_unet", None):
+            try:
+                torch.cuda.synchronize()
+                L.lib().hiseg_stream_destroy(self._raw_unet)
+            except Exception:
+                pass
 
     def run(self, batches):
         w = self.wrapper

@@ -47,6 +47,12 @@ const char* hiseg_last_error_string(void);
 /* 1 if the library's code object contains gfx950 kernels (always true for this build). */
 int hiseg_built_for_gfx950(void);
 
+/* A HIP stream whose kernels run only on the CUs whose bits are set in mask[0..nwords) (hipExtStreamCreateWithCUMask),
+ * for the serving schedule's full-image UNet stream (hiseg.StreamPipelinedExport(cu_mask=...)); destroy with
+ * hiseg_stream_destroy. */
+int hiseg_stream_create_cu_mask(const unsigned* mask, int nwords, hiseg_stream_t* out);
+int hiseg_stream_destroy(hiseg_stream_t s);
+
 /* ----------------------------------------------------------------------------------------
  * Dynamic RoIAlign forward.
  * Replaces DynamicRoIAlign.forward (src/human_edge_detection/dynamic_roi_align.py:56-171):

@@ -32,6 +32,9 @@ def main():
     pu.s_head = torch.cuda.Stream(priority=0)
     pu.s_unet = torch.cuda.Stream(priority=-1)
     runners["pipe_unetprio"] = pu
+    # UNet stream restricted to a CU subset (bit patterns striped over the 8 words = 256 CUs)
+    for name, word in (("pipe_unet_3of4", 0x77777777), ("pipe_unet_half", 0x55555555), ("pipe_unet_quarter", 0x11111111)):
+        runners[name] = hiseg.StreamPipelinedExport(wrapper, unet_cu_mask=[word] * 8)
     res = {k: [] for k in runners}
     with torch.no_grad():
         for _ in range(args.rounds):
