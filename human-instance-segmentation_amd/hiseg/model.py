@@ -218,9 +218,12 @@ class StreamPipelinedExport:
     ready on the caller's current stream when it returns (the caller synchronises as usual).
     """
 
-    def __init__(self, wrapper: "RGBHierarchicalExportWrapper", unet_cu_mask=None):
+    def __init__(self, wrapper: "RGBHierarchicalExportWrapper", unet_cu_mask=None, head_priority: bool = True):
         """``unet_cu_mask``: optional list of 32-bit words; the UNet stream then runs only on the CUs whose bits
-        are set (hiseg_stream_create_cu_mask), leaving the rest to the head."""
+        are set (hiseg_stream_create_cu_mask), leaving the rest to the head.  ``head_priority``: the head -- the
+        critical path once the UNet got cheaper -- runs on a high-priority stream, so its workgroups are dispatched
+        ahead of the UNet's when both wait for CUs (tools/pipeline_ab.py, profiles/r2_v11_schedule_ab2.txt: 19.0-19.3
+        vs 19.5-19.7 ms per step on one box, 19.35-19.6 vs 19.8-20.0 on another)."""
         self.wrapper = wrapper
         self._raw_unet = None
         if unet_cu_mask is None:
@@ -233,7 +236,7 @@ class StreamPipelinedExport:
                     "stream_create_cu_mask")
             self._raw_unet = h.value
             self.s_unet = torch.cuda.ExternalStream(h.value)
-        self.s_head = torch.cuda.Stream()
+        self.s_head = torch.cuda.Stream(priority=-1) if head_priority else torch.cuda.Stream()
 
     def __del__(self):
         if getattr(self, "_raw_unet", None):

@@ -22,7 +22,7 @@ def main():
     model = bench.build_model(dev, torch.bfloat16)
     wrapper = hiseg.RGBHierarchicalExportWrapper(model)
     images, rois = bench.synthetic_batch(dev, 0)
-    runners = {"serial": None, "pipe": hiseg.StreamPipelinedExport(wrapper)}
+    runners = {"serial": None, "pipe": hiseg.StreamPipelinedExport(wrapper, head_priority=False)}
     pr = hiseg.StreamPipelinedExport(wrapper)
     lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") else (0, -1)
     pr.s_head = torch.cuda.Stream(priority=-1)
@@ -34,7 +34,7 @@ def main():
     runners["pipe_unetprio"] = pu
     # UNet stream restricted to a CU subset (bit patterns striped over the 8 words = 256 CUs)
     for name, word in (("pipe_unet_3of4", 0x77777777), ("pipe_unet_half", 0x55555555), ("pipe_unet_quarter", 0x11111111)):
-        runners[name] = hiseg.StreamPipelinedExport(wrapper, unet_cu_mask=[word] * 8)
+        runners[name] = hiseg.StreamPipelinedExport(wrapper, unet_cu_mask=[word] * 8, head_priority=False)
     res = {k: [] for k in runners}
     with torch.no_grad():
         for _ in range(args.rounds):
