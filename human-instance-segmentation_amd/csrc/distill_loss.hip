@@ -19,7 +19,8 @@ constexpr float kEps = 1e-5f;
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
 
-__device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+// torch.clamp semantics: NaN stays NaN (fminf / fmaxf alone would return a bound)
+__device__ __forceinline__ float clampf(float x, float lo, float hi) { return x != x ? x : fminf(fmaxf(x, lo), hi); }
 
 __global__ void __launch_bounds__(256) distill_partial_kernel(hiseg_distill_cfg c, long long HW, const float* s,
                                                               const float* te, const float* y, float* ws) {
@@ -85,8 +86,11 @@ __global__ void distill_finalize_kernel(hiseg_distill_cfg c, int B, int S, long 
   }
   const double n = (double)B * (double)HW;
   kl /= n; mse /= n; bce /= n;
+  // The reference's KL fallback (kl NaN/Inf -> 0.1 mean|pt - ps|, :560-564) is reachable only through a NaN
+  // probability (the clamped probabilities keep every finite term bounded), where |pt - ps| is NaN as well: kl
+  // stays NaN either way.  clamp(kl, 0, 5) keeps a NaN (:570).
   const bool kl_pass = kl >= 0.0 && kl <= 5.0;
-  const double klc = kl < 0.0 ? 0.0 : (kl > 5.0 ? 5.0 : kl);
+  const double klc = kl != kl ? kl : (kl < 0.0 ? 0.0 : (kl > 5.0 ? 5.0 : kl));
   const double sm = 1e-5;
   double coeff = 0;
   float* cf = ws + (long long)B * S * kDistQ;
@@ -102,18 +106,29 @@ __global__ void distill_finalize_kernel(hiseg_distill_cfg c, int B, int S, long 
   const double task = c.use_dice ? 0.7 * bce + 0.3 * dice : bce;
   const double kw = c.kl_weight, tw = c.task_weight;
   const double dist = c.distill_in_total ? kw * kl_v + (1.0 - kw) * mse_v : 0.0;
-  const double total = c.has_target ? tw * task + (1.0 - tw) * dist : dist;
+  double total = c.has_target ? tw * task + (1.0 - tw) * dist : dist;
+  // Final safety check (:650-659): a non-finite total falls back to the task loss (targets, task not NaN), else
+  // to the MSE term (not NaN), else to a constant 1.0 that carries no gradient.
+  int mode = 0;
+  if (!isfinite(total)) {
+    if (c.has_target && task == task) { mode = 1; total = task; }
+    else if (mse_v == mse_v) { mode = 2; total = mse_v; }
+    else { mode = 3; total = 1.0; }
+  }
+  auto nz = [](double v) { return v != v ? 0.f : (float)v; };   // loss_dict: NaN reported as 0.0
   out[HISEG_DISTILL_TOTAL] = (float)total;
-  out[HISEG_DISTILL_KL] = (float)kl_v;
-  out[HISEG_DISTILL_MSE] = (float)mse_v;
-  out[HISEG_DISTILL_BCE] = c.has_target ? (float)bce : 0.f;
-  out[HISEG_DISTILL_DICE] = (c.has_target && c.use_dice) ? (float)dice : 0.f;
+  out[HISEG_DISTILL_KL] = nz(kl_v);
+  out[HISEG_DISTILL_MSE] = nz(mse_v);
+  out[HISEG_DISTILL_BCE] = c.has_target ? nz(bce) : 0.f;
+  out[HISEG_DISTILL_DICE] = (c.has_target && c.use_dice) ? nz(dice) : 0.f;
   const double wd = c.has_target ? 1.0 - tw : 1.0;
   const bool dterms = c.distill_terms && c.distill_in_total;
-  cf[0] = (dterms && kl_pass) ? (float)(wd * kw / n) : 0.f;
-  cf[1] = dterms ? (float)(wd * (1.0 - kw) * 2.0 / n) : 0.f;
-  cf[2] = c.has_target ? (float)(tw * (c.use_dice ? 0.7 : 1.0) / n) : 0.f;
-  cf[3] = (c.has_target && c.use_dice) ? (float)(-tw * 0.3 / B) : 0.f;
+  const double wt = mode == 1 ? 1.0 : tw;   // weight of the task terms in the differentiated total
+  cf[0] = (mode == 0 && dterms && kl_pass) ? (float)(wd * kw / n) : 0.f;
+  cf[1] = mode == 0 ? (dterms ? (float)(wd * (1.0 - kw) * 2.0 / n) : 0.f)
+                    : ((mode == 2 && c.distill_terms) ? (float)(2.0 / n) : 0.f);
+  cf[2] = (c.has_target && mode <= 1) ? (float)(wt * (c.use_dice ? 0.7 : 1.0) / n) : 0.f;
+  cf[3] = (c.has_target && c.use_dice && mode <= 1) ? (float)(-wt * 0.3 / B) : 0.f;
 }
 
 __global__ void __launch_bounds__(256) distill_grad_kernel(hiseg_distill_cfg c, int B, int S, long long HW,

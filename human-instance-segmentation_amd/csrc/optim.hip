@@ -109,9 +109,94 @@ __global__ void adamw_commit_kernel(int* steps, int parity) {
   if (threadIdx.x == 0) steps[parity] = steps[parity ^ 1];
 }
 
+constexpr int kMaxSeg = 256;
+
+// Per-segment step counts (hiseg_adamw_step_segmented): the bias corrections of segment s come from its own
+// count; each thread walks its grid-stride indices upwards, so its segment index only advances.
+__global__ void __launch_bounds__(256) adamw_seg_kernel(float* p, float* g, float* m, float* v, long long n, float lr,
+                                                        float b1, float b2, float omb1, float omb2, float decay,
+                                                        float eps, const float* partial,
+                                                        float max_norm, float* norm_out, const long long* seg_start,
+                                                        int nseg, int* steps, int parity, int* skipped) {
+  __shared__ float s_step[kMaxSeg], s_sbc2[kMaxSeg];
+  __shared__ long long s_seg[kMaxSeg + 1];
+  __shared__ float s_coef;
+  __shared__ int s_skip;
+  if (threadIdx.x == 0) {
+    double acc = 0;
+    for (int b = 0; b < kOptBlocks; ++b) acc += partial[b];
+    const float total = (float)sqrt(acc);
+    const bool finite = isfinite(total);
+    float c = 1.f;
+    if (max_norm > 0.f && finite) {
+      const float cc = max_norm / (total + 1e-6f);
+      c = cc < 1.f ? cc : 1.f;
+    }
+    s_coef = c;
+    s_skip = finite ? 0 : 1;
+    if (blockIdx.x == 0) {
+      if (norm_out) norm_out[0] = total;
+      if (!finite) skipped[0] += 1;
+    }
+  }
+  for (int k = threadIdx.x; k <= nseg; k += blockDim.x) s_seg[k] = seg_start[k];
+  for (int k = threadIdx.x; k < nseg; k += blockDim.x) {
+    const int t = steps[parity * nseg + k] + 1;
+    const double bc1 = 1.0 - pow((double)b1, (double)t), bc2 = 1.0 - pow((double)b2, (double)t);
+    s_step[k] = (float)((double)lr / bc1);
+    s_sbc2[k] = (float)sqrt(bc2);
+  }
+  __syncthreads();
+  if (blockIdx.x == 0)
+    for (int k = threadIdx.x; k < nseg; k += blockDim.x)
+      steps[(parity ^ 1) * nseg + k] = steps[parity * nseg + k] + (s_skip ? 0 : 1);
+  if (s_skip) return;
+  const float c = s_coef;
+  const bool clip = max_norm > 0.f;
+  int sg = 0;
+  // torch.optim.AdamW's multi-tensor arithmetic, op for op: p *= 1 - lr wd; m = lerp(m, g, 1 - b1);
+  // v = v b2 + (1 - b2) g g; p -= (lr / bc1) m / (sqrt(v) / sqrt(bc2) + eps)  (complements from the host in double)
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    while (sg + 1 < nseg && i >= s_seg[sg + 1]) ++sg;
+    const float step = s_step[sg], sbc2 = s_sbc2[sg];
+    float gi = g[i];
+    if (clip) { gi *= c; g[i] = gi; }
+    const float pi = __fmul_rn(p[i], decay);
+    const float m0 = m[i];
+    const float mi = omb1 < 0.5f ? __fadd_rn(m0, __fmul_rn(omb1, __fsub_rn(gi, m0)))
+                                 : __fsub_rn(gi, __fmul_rn(__fsub_rn(gi, m0), __fsub_rn(1.f, omb1)));
+    const float vi = __fadd_rn(__fmul_rn(v[i], b2), __fmul_rn(__fmul_rn(omb2, gi), gi));
+    m[i] = mi;
+    v[i] = vi;
+    const float den = __fadd_rn(__fdiv_rn(__fsqrt_rn(vi), sbc2), eps);
+    p[i] = __fadd_rn(pi, __fmul_rn(-step, __fdiv_rn(mi, den)));
+  }
+}
+
+__global__ void adamw_seg_commit_kernel(int* steps, int nseg, int parity) {
+  for (int k = threadIdx.x; k < nseg; k += blockDim.x) steps[parity * nseg + k] = steps[(parity ^ 1) * nseg + k];
+}
+
 }  // namespace hiseg
 
 using namespace hiseg;
+
+extern "C" int hiseg_adamw_max_segments(void) { return kMaxSeg; }
+
+extern "C" int hiseg_adamw_step_segmented(float* p, float* g, float* m, float* v, long long n, float lr, float beta1,
+                                          float beta2, float one_minus_beta1, float one_minus_beta2, float decay,
+                                          float eps, const float* partial, float max_norm, float* norm_out,
+                                          const long long* seg_start, int nseg, int* steps, int parity,
+                                          int* skipped, hiseg_stream_t stream) {
+  HISEG_REQUIRE(p && g && m && v && n > 0 && partial && seg_start && steps && skipped && (parity == 0 || parity == 1),
+                HISEG_ERR_BAD_ARG, "adamw_step_segmented: bad arguments");
+  HISEG_REQUIRE(nseg >= 1 && nseg <= kMaxSeg, HISEG_ERR_BAD_SHAPE, "adamw_step_segmented: 1..256 segments");
+  hipLaunchKernelGGL(adamw_seg_kernel, dim3(kOptBlocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, lr, beta1,
+                     beta2, one_minus_beta1, one_minus_beta2, decay, eps, partial, max_norm, norm_out, seg_start, nseg,
+                     steps, parity, skipped);
+  hipLaunchKernelGGL(adamw_seg_commit_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, steps, nseg, parity);
+  return hiseg_check_launch("adamw_step_segmented");
+}
 
 extern "C" int hiseg_adamw_step_guarded(float* p, float* g, float* m, float* v, long long n, float lr, float beta1,
                                         float beta2, float eps, float weight_decay, const float* partial, float max_norm,

@@ -7,9 +7,11 @@ distillation weight, ``forward(student, teacher, masks) -> (total, loss_dict)``)
 ``create_unet_distillation_model``.  The loss terms, reductions and the gradient run as HIP kernels
 (include/hiseg_distill.h); the schedule state stays on the host exactly as in the reference (it is
 updated once per epoch), and ``loss_dict`` is materialised lazily (one device->host copy on first
-access instead of the reference's five ``.item()`` calls).  NaN/Inf fallbacks of the reference
-(:540-548, :640-650) are not reproduced: the kernels clamp exactly as the reference does, so a
-non-finite value can only come from non-finite logits.
+access instead of the reference's five ``.item()`` calls).  The reference's NaN/Inf fallbacks are
+reproduced on the device (:560-568, :650-659): a non-finite total becomes the task loss, else the MSE
+term, else a constant 1.0 without a gradient, and the backward differentiates the value returned;
+NaN terms are reported as 0.0 in loss_dict.  Pinned to the reference by the non-finite golden cases
+(tests/golden/distill_loss.npz: NaN / Inf teacher, NaN student, with and without targets).
 """
 from __future__ import annotations
 

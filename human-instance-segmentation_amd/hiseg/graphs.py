@@ -10,6 +10,13 @@ the Dropout2d seed base (TrainState.begin_step), the loss's dynamic-weight EMA, 
 skip counter (fixed slot, committed by the library).  Host-side values are frozen into the graph: the
 learning rate, the inputs' addresses (the step must read the same input tensors, refilled in place between
 steps) and the shapes -- GraphedStep re-captures when the optimizer's learning rate changes.
+
+The graph also holds raw pointers to the optimizer's buffers (moments, step counts, norm partials), the
+model's flat parameters and its conv packing table.  Anything that re-allocates them -- a new optimizer
+(the reference's pattern at progressive unfreezing), FusedAdamW re-binding to a new flat layout, a new
+trainable set or compute dtype -- changes GraphedStep's fingerprint of that state; the next call then
+drops the graph, runs ``eager`` steps again (the re-binding and re-packing happen there, for real) and
+captures anew.
 """
 from __future__ import annotations
 
@@ -36,6 +43,7 @@ class GraphedStep:
         self.out = None
         self.lr = None
         self.captures = 0
+        self.fp = None
 
     def _opt(self):
         return self.opt_fn() if self.opt_fn is not None else None
@@ -44,8 +52,31 @@ class GraphedStep:
         o = self._opt()
         return None if o is None else tuple(g["lr"] for g in o.param_groups)
 
+    def _fingerprint(self):
+        """Identities / addresses of the device state a captured step reads and writes."""
+        o = self._opt()
+        if o is None:
+            return None
+
+        def ptr(t):
+            return None if t is None else t.data_ptr()
+        fp = [id(o), id(getattr(o, "_flat", None)), getattr(o, "_nseg", None)]
+        fp += [ptr(getattr(o, k, None)) for k in ("exp_avg", "exp_avg_sq", "_steps", "_seg_start", "partial",
+                                                  "_skipped", "last_norm")]
+        model = getattr(o, "model", None)
+        if model is not None:
+            fp.append(tuple(id(p) for p in model.parameters() if p.requires_grad))
+            for m in model.modules():
+                S = m.__dict__.get("_hiseg_train")
+                if S is not None:
+                    fp += [id(m), id(S), id(S.flat), S.dtype, ptr(S.table), len(S.entries)]
+        return tuple(fp)
+
     def __call__(self):
         self.calls += 1
+        if self.graph is not None and self._fingerprint() != self.fp:
+            # the optimizer or the model's flat layout / packing table was re-allocated since the capture
+            self.graph, self.calls = None, 1
         if self.calls <= self.eager:
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
@@ -56,9 +87,14 @@ class GraphedStep:
         if self.graph is None or self._lr() != self.lr:
             self.graph = None
             torch.cuda.synchronize()
+            before = self._fingerprint()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self.out = self.fn()
+            self.fp = self._fingerprint()
+            if self.fp != before:
+                raise RuntimeError("GraphedStep: the step re-allocated optimizer / model state while it was being "
+                                   "captured; run more eager steps first (GraphedStep(..., eager=N))")
             self.graph, self.lr = g, self._lr()
             self.captures += 1
         self.graph.replay()

@@ -49,10 +49,11 @@ class _LiveState(MutableMapping):
     def __getitem__(self, p):
         o = self._opt
         off = self._off(p)
-        if off is None or o.step_count == 0:
+        t = 0 if off is None else o._param_steps().get(id(p), 0)
+        if t == 0:      # torch.optim.AdamW: no state before the parameter's first step
             raise KeyError(p)
         k = p.numel()
-        return {"step": torch.tensor(float(o.step_count)), "exp_avg": o.exp_avg[off:off + k].view(p.shape),
+        return {"step": torch.tensor(float(t)), "exp_avg": o.exp_avg[off:off + k].view(p.shape),
                 "exp_avg_sq": o.exp_avg_sq[off:off + k].view(p.shape)}
 
     def __setitem__(self, p, ent):
@@ -69,7 +70,9 @@ class _LiveState(MutableMapping):
         with torch.no_grad():
             o.exp_avg[off:off + k].copy_(ent["exp_avg"].reshape(-1))
             o.exp_avg_sq[off:off + k].copy_(ent["exp_avg_sq"].reshape(-1))
-        o.step_count = max(o.step_count, int(float(ent["step"])))
+        steps = o._param_steps()
+        steps[id(p)] = int(float(ent["step"]))
+        o._set_steps(steps)
 
     def __delitem__(self, p):
         off = self._off(p)
@@ -82,9 +85,10 @@ class _LiveState(MutableMapping):
     def __iter__(self):
         o = self._opt
         o._ensure(required=False)
-        if o._flat is None or o.step_count == 0:
+        if o._flat is None:
             return iter(())
-        return iter([q for _, q, _ in o._slots()])
+        steps = o._param_steps()
+        return iter([q for _, q, _ in o._slots() if steps.get(id(q), 0) > 0])
 
     def __len__(self):
         return sum(1 for _ in self)
@@ -116,9 +120,15 @@ class FusedAdamW(torch.optim.Optimizer):
     hiseg.distributed the gradients are averaged over the ranks before the step, so a non-finite gradient on any
     rank makes every rank skip the same step.
 
-    When the model's flat layout is rebuilt (a new trainable set after ``unfreeze_encoder_blocks``, a dtype
-    change), the next ``zero_grad`` / ``step`` re-binds to the new buffers and carries every kept parameter's
-    moments over."""
+    Inf-only gradients are skipped on purpose too, although the reference's fp32 path (train_advanced.py:815-832)
+    checks only for NaN loss / NaN gradients and would apply such a step (clip_grad_norm_ turns it into NaN).
+
+    Step counts are per parameter, as in torch.optim.AdamW: the device keeps one count per run of parameters
+    that share it (segments of the flat layout, hiseg_adamw_step_segmented).  When the model's flat layout is
+    rebuilt (a new trainable set after ``unfreeze_encoder_blocks``, a dtype change), the next ``zero_grad`` /
+    ``step`` re-binds to the new buffers and carries every kept parameter's moments and step count over; a
+    parameter new to the optimizer starts at step 0 with zero moments (the reference's new optimizer at
+    progressive unfreezing, train_distillation_staged.py:1531-1552)."""
 
     def __init__(self, model: torch.nn.Module, lr: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.01, max_grad_norm: Optional[float] = 1.0, params=None):
@@ -138,7 +148,10 @@ class FusedAdamW(torch.optim.Optimizer):
         self.exp_avg = self.exp_avg_sq = None
         self.partial = None
         self.last_norm: Optional[torch.Tensor] = None
-        self._steps: Optional[torch.Tensor] = None     # device step count, two slots (see hiseg_adamw_step_guarded)
+        self._steps: Optional[torch.Tensor] = None     # device step counts [2][nseg] (hiseg_adamw_step_segmented)
+        self._seg_start: Optional[torch.Tensor] = None  # int64 [nseg + 1] segment bounds in the moment buffers
+        self._nseg = 0
+        self._slot_list = None
         self._parity = 0
         self._host_steps = 0
         self._skipped: Optional[torch.Tensor] = None
@@ -151,17 +164,65 @@ class FusedAdamW(torch.optim.Optimizer):
 
     @property
     def step_count(self) -> int:
-        """Applied (not skipped) steps; reads the device counter (a host sync) once the buffers exist."""
+        """Applied (not skipped) steps of the longest-trained parameter (torch.optim.AdamW's per-parameter
+        ``step``: see ``param_steps``); reads the device counters (a host sync) once the buffers exist."""
         if self._steps is None:
             return self._host_steps
-        return int(self._steps[self._parity].item())
+        n = self._nseg
+        return int(self._steps[self._parity * n:(self._parity + 1) * n].max().item())
 
     @step_count.setter
     def step_count(self, v: int):
         if self._steps is None:
             self._host_steps = int(v)
         else:
-            self._steps[self._parity] = int(v)
+            self._set_steps({id(p): int(v) for _, p, _ in self._slots()})
+
+    def param_steps(self):
+        """{parameter: step count} (torch.optim.AdamW's state[p]['step']) for every parameter with moments here."""
+        steps = self._param_steps()
+        return {p: steps.get(id(p), 0) for _, p, _ in self._slots()}
+
+    def _param_steps(self):
+        """{id(parameter): step} from the device segments (host sync)."""
+        if self._steps is None:
+            return {}
+        n = self._nseg
+        counts = self._steps[self._parity * n:(self._parity + 1) * n].tolist()
+        bounds = self._seg_start.tolist()
+        out = {}
+        s = 0
+        for _, p, off in sorted(self._slots(), key=lambda e: e[2]):
+            while s + 1 < n and off >= bounds[s + 1]:
+                s += 1
+            out[id(p)] = int(counts[s])
+        return out
+
+    def _set_steps(self, steps):
+        """Per-parameter step counts (dict id(p) -> t) -> device segments: maximal runs of the flat layout whose
+        parameters share a count.  Rewrites the buffers in place when the segment count is unchanged."""
+        bounds, counts = [0], []
+        for _, p, off in sorted(self._slots(), key=lambda e: e[2]):
+            t = int(steps.get(id(p), 0))
+            if counts and counts[-1] == t:
+                continue
+            if counts:
+                bounds.append(off)
+            counts.append(t)
+        if not counts:
+            counts = [0]
+        bounds.append(self._range[1] - self._range[0])
+        if len(counts) > L.lib().hiseg_adamw_max_segments():
+            raise ValueError(f"FusedAdamW: {len(counts)} distinct per-parameter step runs exceed the device table")
+        dev = self._flat.data.device
+        seg = torch.tensor(bounds, dtype=torch.int64)
+        st = torch.tensor(counts + counts, dtype=torch.int32)
+        if self._steps is not None and self._nseg == len(counts):
+            self._seg_start.copy_(seg)
+            self._steps.copy_(st)
+        else:
+            self._seg_start, self._steps = seg.to(dev), st.to(dev)
+            self._nseg = len(counts)
 
     @property
     def skipped_steps(self) -> int:
@@ -194,8 +255,10 @@ class FusedAdamW(torch.optim.Optimizer):
         return (b, e)
 
     def _bind(self, f, carried):
-        steps = self.step_count if self._steps is not None else self._host_steps
+        first = carried is None
+        host_steps = self._host_steps
         self._flat = f
+        self._slot_list = None
         self._range = self._range_of(f)
         n = self._range[1] - self._range[0]
         dev = f.data.device
@@ -204,18 +267,19 @@ class FusedAdamW(torch.optim.Optimizer):
         self.partial = torch.empty(L.lib().hiseg_optim_blocks(), dtype=torch.float32, device=dev)
         self.last_norm = torch.zeros(1, dtype=torch.float32, device=dev)
         skipped = 0 if self._skipped is None else int(self._skipped.item())
-        self._steps = torch.zeros(2, dtype=torch.int32, device=dev)
+        self._steps = self._seg_start = None
         self._parity = 0
-        self._steps[0] = steps
         self._skipped = torch.full((1,), skipped, dtype=torch.int32, device=dev)
         self._bump = None
-        if carried:
-            for _, p, off in self._slots():
-                ent = carried.get(id(p))
-                if ent is not None:
-                    k = p.numel()
-                    self.exp_avg[off:off + k].copy_(ent[0])
-                    self.exp_avg_sq[off:off + k].copy_(ent[1])
+        steps = {}
+        for _, p, off in self._slots():
+            ent = None if first else carried.get(id(p))
+            if ent is not None:
+                k = p.numel()
+                self.exp_avg[off:off + k].copy_(ent[0])
+                self.exp_avg_sq[off:off + k].copy_(ent[1])
+            steps[id(p)] = host_steps if first else (ent[2] if ent is not None else 0)
+        self._set_steps(steps)
         if self._pending_state is not None:
             sd, self._pending_state = self._pending_state, None
             self._load_moments(sd)
@@ -224,9 +288,11 @@ class FusedAdamW(torch.optim.Optimizer):
     def _rebind(self, f):
         """The model re-laid its trainable parameters (new FlatParams): keep every parameter's moments."""
         carried = {}
+        steps = self._param_steps()
         for _, p, off in self._slots():
             k = p.numel()
-            carried[id(p)] = (self.exp_avg[off:off + k].clone(), self.exp_avg_sq[off:off + k].clone())
+            carried[id(p)] = (self.exp_avg[off:off + k].clone(), self.exp_avg_sq[off:off + k].clone(),
+                              steps.get(id(p), 0))
         self._bind(f, carried)
 
     def zero_grad(self, set_to_none: bool = False):
@@ -253,11 +319,13 @@ class FusedAdamW(torch.optim.Optimizer):
         b, e = self._range
         gp, dp = f.grad.data_ptr() + 4 * b, f.data.data_ptr() + 4 * b
         L.check(lib.hiseg_grad_norm_partials(gp, e - b, self.partial.data_ptr(), s), "grad_norm")
-        L.check(lib.hiseg_adamw_step_guarded(dp, gp, self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), e - b,
-                                             float(lr), float(b1), float(b2), float(eps), float(wd),
-                                             self.partial.data_ptr(), float(self.max_grad_norm) if clip else 0.0,
-                                             self.last_norm.data_ptr(), self._steps.data_ptr(), self._parity,
-                                             self._skipped.data_ptr(), s), "adamw_step")
+        L.check(lib.hiseg_adamw_step_segmented(dp, gp, self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), e - b,
+                                               float(lr), float(b1), float(b2), 1.0 - float(b1), 1.0 - float(b2),
+                                               1.0 - float(lr) * float(wd), float(eps),
+                                               self.partial.data_ptr(), float(self.max_grad_norm) if clip else 0.0,
+                                               self.last_norm.data_ptr(), self._seg_start.data_ptr(), self._nseg,
+                                               self._steps.data_ptr(), self._parity, self._skipped.data_ptr(), s),
+                "adamw_step")
         # the count stays in slot _parity (the library commits it): no host-side state changes per step, so the
         # whole step can be captured into a HIP graph (hiseg.graphs.GraphedStep)
         # the kernel wrote the parameters in place: bump their versions so plans packed from them (eval
@@ -272,23 +340,29 @@ class FusedAdamW(torch.optim.Optimizer):
         """(index in the optimizer's parameter list, parameter, flat offset relative to the moment buffers)
         for every parameter whose moments this optimiser keeps."""
         f = self._flat
+        plist = self.param_groups[0]["params"]
+        key = (id(f), len(plist))
+        if self._slot_list is not None and self._slot_list[0] == key:
+            return self._slot_list[1]
         b, e = self._range
         out = []
-        for i, p in enumerate(self.param_groups[0]["params"]):
+        for i, p in enumerate(plist):
             if id(p) in f.offsets:
                 off, k = f.offsets[id(p)]
                 if b <= off and off + k <= e:
                     out.append((i, p, off - b))
+        self._slot_list = (key, out)
         return out
 
     def state_dict(self):
         self._ensure()
         state = {}
-        steps = self.step_count
-        if steps > 0:
-            for i, p, off in self._slots():
+        steps = self._param_steps()
+        for i, p, off in self._slots():
+            t = steps.get(id(p), 0)
+            if t > 0:
                 k = p.numel()
-                state[i] = {"step": torch.tensor(float(steps)),
+                state[i] = {"step": torch.tensor(float(t)),
                             "exp_avg": self.exp_avg[off:off + k].view(p.shape).clone(),
                             "exp_avg_sq": self.exp_avg_sq[off:off + k].view(p.shape).clone()}
         groups = []
@@ -323,19 +397,18 @@ class FusedAdamW(torch.optim.Optimizer):
             return
         self.exp_avg.zero_()
         self.exp_avg_sq.zero_()
-        steps = set()
+        steps = {}
         st = sd["state"]
         for i, p, off in self._slots():
             ent = st.get(i, st.get(str(i)))
             if ent is None:
+                steps[id(p)] = 0
                 continue
             k = p.numel()
             self.exp_avg[off:off + k].copy_(ent["exp_avg"].reshape(-1))
             self.exp_avg_sq[off:off + k].copy_(ent["exp_avg_sq"].reshape(-1))
-            steps.add(int(float(ent["step"])))
-        if len(steps) > 1:
-            raise ValueError(f"per-parameter AdamW steps differ ({sorted(steps)}); one step count is kept")
-        self.step_count = steps.pop() if steps else 0
+            steps[id(p)] = int(float(ent["step"]))
+        self._set_steps(steps)
 
 
 def cosine_lr(base_lr: float, epoch: int, total_epochs: int, min_lr: float = 1e-6) -> float:

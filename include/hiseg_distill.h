@@ -12,6 +12,9 @@
  *   bce  = BCEWithLogits(s, y, pos_weight) (mean),  dice = 1 - mean_b (2 I_b + 1e-5) / (P_b + Y_b + 1e-5)
  *   task = 0.7 bce + 0.3 dice (or bce),  distill = kw kl + (1-kw) mse,  kw = min(alpha_eff, 0.1)
  *   total = tw task + (1-tw) distill  (targets) | distill (no targets)
+ * Non-finite totals take the reference's fallbacks (:650-659): the task loss (targets, task not NaN), else the
+ * MSE term (not NaN), else a constant 1.0 with a zero gradient; the gradient is that of the value returned.
+ * loss_dict values that are NaN are reported as 0 (:571-590); clamps keep NaN (torch.clamp).
  */
 #ifndef HISEG_DISTILL_H_
 #define HISEG_DISTILL_H_

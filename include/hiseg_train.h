@@ -251,6 +251,21 @@ int hiseg_adamw_step(float* p, float* g, float* m, float* v, long long n, float 
 int hiseg_adamw_step_guarded(float* p, float* g, float* m, float* v, long long n, float lr, float beta1, float beta2,
                              float eps, float weight_decay, const float* partial, float max_norm, float* norm_out,
                              int* steps, int parity, int* skipped, hiseg_stream_t stream);
+/* The guarded step with a step count per parameter segment, as torch.optim.AdamW keeps one per parameter
+ * (parameters added to the optimizer later -- progressive unfreezing, train_distillation_staged.py:1531-1552 --
+ * start at t = 0 while the others continue).  seg_start[0..nseg] (int64, device) cuts [0, n) into nseg <=
+ * hiseg_adamw_max_segments() runs of parameters that share a count; steps is [2][nseg] int32 (slot
+ * parity * nseg + s holds segment s's count, the other row is the staging row of the commit, as above).  A
+ * non-finite total skips the whole step (no segment advances).  Inf-only gradients are skipped here on purpose,
+ * although the reference's fp32 path (train_advanced.py:815-832) checks only for NaN.  The update follows
+ * torch.optim.AdamW's multi-tensor arithmetic op for op (p *= decay; m = lerp(m, g, 1 - beta1); v = v beta2 +
+ * (1 - beta2) g g; p -= lr / bc1 * m / (sqrt(v) / sqrt(bc2) + eps)), with one_minus_beta1/2 and decay = 1 - lr
+ * weight_decay rounded from double on the host as torch's Python scalars are. */
+int hiseg_adamw_max_segments(void);
+int hiseg_adamw_step_segmented(float* p, float* g, float* m, float* v, long long n, float lr, float beta1,
+                               float beta2, float one_minus_beta1, float one_minus_beta2, float decay, float eps,
+                               const float* partial, float max_norm, float* norm_out, const long long* seg_start,
+                               int nseg, int* steps, int parity, int* skipped, hiseg_stream_t stream);
 
 #ifdef __cplusplus
 }

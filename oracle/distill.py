@@ -35,19 +35,22 @@ def distill_loss(student, teacher, target, temperature, alpha, task_weight, adap
         pt = torch.sigmoid(torch.clamp(teacher, -10, 10) / temperature).clamp(eps, 1 - eps)
         t1 = pt * (torch.log(pt + eps) - torch.log(ps + eps))
         t2 = (1 - pt) * (torch.log(1 - pt + eps) - torch.log(1 - ps + eps))
-        kl = torch.clamp((t1 + t2).mean(), 0.0, 5.0)
+        kl = (t1 + t2).mean()
+        if not torch.isfinite(kl):                                     # :560-564
+            kl = torch.abs(pt - ps).mean() * 0.1
+        kl = torch.clamp(kl, 0.0, 5.0)
         mse = F.mse_loss(student, teacher)
-        d["kl_loss"], d["mse_loss"] = float(kl.detach()), float(mse.detach())
+        d["kl_loss"], d["mse_loss"] = _nz(kl), _nz(mse)
     if target is not None:                                             # :571-600
         pw = torch.tensor([math.sqrt((1.0 - fg_ratio) / fg_ratio)], dtype=student.dtype)
         bce = F.binary_cross_entropy_with_logits(student, target.to(student.dtype), pos_weight=pw)
-        d["bce_loss"] = float(bce.detach())
+        d["bce_loss"] = _nz(bce)
         if use_dice:                                                   # :471-508
             p = torch.sigmoid(student).reshape(student.shape[0], -1)
             y = target.to(student.dtype).reshape(student.shape[0], -1)
             coeff = (2 * (p * y).sum(1) + 1e-5) / (p.sum(1) + y.sum(1) + 1e-5)
             dice = 1.0 - coeff.mean()
-            d["dice_loss"] = float(dice.detach())
+            d["dice_loss"] = _nz(dice)
             task = 0.7 * bce + 0.3 * dice
         else:
             d["dice_loss"] = 0.0
@@ -62,8 +65,21 @@ def distill_loss(student, teacher, target, temperature, alpha, task_weight, adap
         kw = min(eff, 0.1)
         dist = kw * kl + (1 - kw) * mse
     total = task_weight * task + (1 - task_weight) * dist if task is not None else dist   # :617-628
+    if not torch.isfinite(total):                                      # :650-659
+        if task is not None and not torch.isnan(task):
+            total = task
+        elif not torch.isnan(mse):
+            total = mse
+        else:
+            total = student.new_tensor(1.0)   # a constant: no gradient reaches the student
     d["total_loss"] = float(total.detach())
     return total, d
+
+
+def _nz(v):
+    """loss_dict value: .item(), NaN reported as 0.0 (:567, :571, :585, :590)."""
+    x = float(v.detach())
+    return 0.0 if x != x else x
 
 
 def temperature_at(initial, final, epoch, total_epochs, schedule="linear"):

@@ -50,6 +50,23 @@ CASES = [
     ("no_dice", 9, (2, 16, 16), dict(temperature=2.0, alpha=0.2, task_weight=0.5, use_dice_loss=False), [], True),
 ]
 
+# Non-finite inputs: the reference's fallbacks (:560-568 KL -> L1, :650-659 total -> task loss, else MSE, else a
+# constant 1.0 without a gradient).  (name, seed, shape, ctor kwargs, use targets, [(tensor, flat index, value)])
+POISON_CASES = [
+    ("nan_teacher", 21, (2, 16, 16), dict(temperature=4.0, alpha=0.05, task_weight=0.7), True,
+     [("t", 5, float("nan")), ("t", 300, float("nan"))]),
+    ("inf_teacher", 22, (2, 16, 16), dict(temperature=4.0, alpha=0.05, task_weight=0.7), True,
+     [("t", 17, float("inf")), ("t", 400, float("-inf"))]),
+    ("nan_student", 23, (2, 16, 16), dict(temperature=4.0, alpha=0.05, task_weight=0.7), True,
+     [("s", 9, float("nan"))]),
+    ("nan_teacher_no_target", 24, (2, 16, 16), dict(temperature=3.0, alpha=0.3, task_weight=0.7), False,
+     [("t", 33, float("nan"))]),
+    ("inf_teacher_no_target", 25, (2, 16, 16), dict(temperature=3.0, alpha=0.3, task_weight=0.7), False,
+     [("t", 44, float("inf"))]),
+    ("nan_teacher_finetune", 26, (2, 16, 16), dict(temperature=1.0, alpha=0.0, task_weight=1.0,
+                                                   adaptive_distillation=False), True, [("t", 7, float("nan"))]),
+]
+
 
 def main():
     out = {"keys": np.array(KEYS)}
@@ -78,6 +95,31 @@ def main():
         out[f"{name}_loss"] = np.array(float(loss))
         out[f"{name}_dict"] = np.array([float(d.get(k, np.nan)) for k in KEYS])
         out[f"{name}_grad"] = s.grad.numpy().astype(np.float32)
+        print(name, float(loss), {k: round(float(v), 5) for k, v in d.items()})
+    for name, seed, (b, h, w), kw, with_t, poison in POISON_CASES:
+        fn = UNetDistillationLoss(**kw)
+        s, t, m = distill_inputs(seed, b, h, w)
+        for which, idx, val in poison:
+            (s if which == "s" else t).view(-1)[idx] = val
+        s.requires_grad_(True)
+        loss, d = fn(s, t, m if with_t else None)
+        if loss.requires_grad and loss.grad_fn is not None:
+            loss.backward()
+        grad = s.grad if s.grad is not None else torch.zeros_like(s)
+        names.append(name)
+        out[f"{name}_meta"] = np.array([seed, b, h, w, int(with_t)], dtype=np.int64)
+        out[f"{name}_state"] = np.array([fn.temperature, fn.alpha, fn.task_weight, float(fn.adaptive_distillation),
+                                         float(fn.distillation_eliminated), fn.performance_ratio,
+                                         float(fn.use_dice_loss), fn.initial_alpha, fn.initial_task_weight],
+                                        dtype=np.float64)
+        out[f"{name}_ctor"] = np.array([kw.get("temperature", 3.0), kw.get("alpha", 0.5), kw.get("task_weight", 0.3),
+                                        float(kw.get("use_dice_loss", True)),
+                                        float(kw.get("adaptive_distillation", True))], dtype=np.float64)
+        out[f"{name}_poison"] = np.array([[0 if wh == "s" else 1, idx, val] for wh, idx, val in poison],
+                                         dtype=np.float64)
+        out[f"{name}_loss"] = np.array(float(loss))
+        out[f"{name}_dict"] = np.array([float(d.get(k, np.nan)) for k in KEYS])
+        out[f"{name}_grad"] = grad.detach().numpy().astype(np.float32)
         print(name, float(loss), {k: round(float(v), 5) for k, v in d.items()})
     out["names"] = np.array(names)
     np.savez_compressed(os.path.join(HERE, "distill_loss.npz"), **out)

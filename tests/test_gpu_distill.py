@@ -5,7 +5,7 @@ import pytest
 import torch
 
 from helpers import load
-from test_oracle_distill import G, KEYS, NAMES, case_inputs
+from test_oracle_distill import G, KEYS, NAMES, assert_grad_close, case_inputs
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -32,8 +32,7 @@ def test_distill_loss_kernel_matches_reference_golden(name):
     assert total.item() == pytest.approx(float(G[f"{name}_loss"]), rel=1e-5, abs=1e-6)
     for k, v in zip(KEYS, G[f"{name}_dict"]):
         assert d[k] == pytest.approx(float(v), rel=1e-4, abs=1e-6), k
-    ref = torch.from_numpy(G[f"{name}_grad"])
-    assert (sd.grad.cpu() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item() + 1e-9
+    assert_grad_close(sd.grad.cpu(), torch.from_numpy(G[f"{name}_grad"]), 1e-5)
 
 
 def test_distill_schedule_methods_match_reference_state():

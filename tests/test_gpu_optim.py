@@ -78,7 +78,7 @@ def test_non_finite_gradient_skips_the_step():
 
 def test_rebind_after_the_flat_layout_changes_keeps_the_moments():
     """unfreeze_encoder_blocks / a dtype change build a new FlatParams: the optimizer re-binds on its next
-    zero_grad and every kept parameter's moments (and the step count) carry over."""
+    zero_grad and every kept parameter's moments and step count carry over; new parameters start at step 0."""
     import hiseg
     m = _model()
     m[0].weight.requires_grad_(False)
@@ -101,12 +101,70 @@ def test_rebind_after_the_flat_layout_changes_keeps_the_moments():
     opt.zero_grad()
     assert opt._flat is f2 and opt._flat is not old_flat
     assert opt.step_count == 2
+    steps = opt.param_steps()
     for p in m.parameters():
         if id(p) in before:
+            assert steps[p] == 2 and float(opt.state[p]["step"]) == 2.0
             assert torch.equal(opt.state[p]["exp_avg"], before[id(p)][0])
             assert torch.equal(opt.state[p]["exp_avg_sq"], before[id(p)][1])
-        else:
-            assert not opt.state[p]["exp_avg"].any()
+        else:   # torch.optim.AdamW: no state (step 0) before a new parameter's first step
+            assert steps[p] == 0 and p not in opt.state
+            off = opt._flat.offsets[id(p)][0]
+            assert not opt.exp_avg[off:off + p.numel()].any()
+
+
+def test_unfreeze_midway_matches_torch_adamw():
+    """a parameter that joins the optimizer partway through training gets its own step count, as in
+    torch.optim.AdamW (the reference's progressive unfreezing builds a new optimizer and transfers the kept
+    parameters' state, train_distillation_staged.py:1531-1552): its first update is lr * g / |g|-like, not the
+    bias-corrected update of the global step.  3 steps with m[0] frozen, then 3 with everything trainable."""
+    import hiseg
+    m, ref = _model(), _model()
+    ref.load_state_dict(m.state_dict())
+    for mm in (m, ref):
+        mm[0].weight.requires_grad_(False)
+        mm[0].bias.requires_grad_(False)
+    _flat(m)
+    opt = hiseg.FusedAdamW(m, lr=1e-2, weight_decay=0.01, max_grad_norm=None)
+    topt = torch.optim.AdamW([p for p in ref.parameters() if p.requires_grad], lr=1e-2, weight_decay=0.01)
+
+    def both(seed):
+        gs = _grads(m, seed)
+        opt.zero_grad()
+        for p, g in zip(m.parameters(), gs):
+            if p.requires_grad:
+                p.grad.copy_(g)
+        opt.step()
+        topt.zero_grad()
+        for p, g in zip(ref.parameters(), gs):
+            if p.requires_grad:
+                p.grad = g.clone()
+        topt.step()
+
+    for s in range(3):
+        both(20 + s)
+    for mm in (m, ref):
+        mm[0].weight.requires_grad_(True)
+        mm[0].bias.requires_grad_(True)
+    _flat(m)
+    old = topt   # the reference pattern: a new optimizer over all trainable params, old state transferred
+    topt = torch.optim.AdamW([p for p in ref.parameters() if p.requires_grad], lr=1e-2, weight_decay=0.01)
+    for p in topt.param_groups[0]["params"]:
+        if p in old.state:
+            topt.state[p] = old.state[p]
+    for s in range(3):
+        both(30 + s)
+    torch.cuda.synchronize()
+    for p, q in zip(m.parameters(), ref.parameters()):
+        torch.testing.assert_close(p.detach(), q.detach(), rtol=2e-6, atol=2e-7)
+    steps = opt.param_steps()
+    assert [steps[p] for p in m.parameters()] == [int(topt.state[q]["step"]) for q in ref.parameters()] \
+        == [3, 3, 6, 6, 6, 6, 6, 6]
+    sd = opt.state_dict()
+    tsd = topt.state_dict()
+    for i, st in tsd["state"].items():
+        assert float(sd["state"][i]["step"]) == float(st["step"])
+        torch.testing.assert_close(sd["state"][i]["exp_avg_sq"], st["exp_avg_sq"], rtol=1e-6, atol=1e-12)
 
 
 def test_reference_state_transfer_between_fused_optimizers():

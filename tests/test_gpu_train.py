@@ -758,3 +758,51 @@ def test_graphed_train_step_equals_eager():
     assert s0 == s1 == 4
     assert torch.equal(p0, p1) and torch.equal(m0, m1)
     assert l0[-1] != l0[0]
+
+
+def test_graphed_step_recaptures_after_optimizer_swap():
+    """the captured graph holds the optimizer's buffer addresses.  Replacing the optimizer between
+    replays (the reference's progressive-unfreezing pattern: a new AdamW with the old state transferred,
+    train_distillation_staged.py:1531-1552) must make GraphedStep run eagerly again and re-capture, so its
+    trajectory stays bit-identical to eager steps that do the same swap."""
+    import hiseg
+    images = torch.from_numpy(filler.uniform(131, (2, 3, 96, 128))).to(DEV)
+    rois = torch.from_numpy(filler.box_rois(132, 2, 2)).to(DEV)
+    tgt = torch.from_numpy(filler.ellipse_targets(133, 4, 128, 96)).to(DEV)
+    runs = []
+    for graphed in (False, True):
+        torch.manual_seed(0)
+        m = _model(torch.bfloat16).to(DEV).train()
+        for mm in (m.roi_align_mask, m.roi_align_rgb):
+            mm.spatial_scale_h, mm.spatial_scale_w = 96, 128
+        loss_fn = hiseg.RefinedHierarchicalLoss(use_contour_detection=True, use_distance_transform=True)
+        st = {"opt": None}
+
+        def step():
+            logits, aux = m(images, rois)
+            loss, _ = loss_fn(logits, tgt, aux)
+            if st["opt"] is None:
+                st["opt"] = hiseg.FusedAdamW(m, lr=5e-4, weight_decay=0.01, max_grad_norm=1.0)
+            st["opt"].zero_grad()
+            loss.backward()
+            st["opt"].step()
+            return loss
+
+        run = hiseg.GraphedStep(step, lambda: st["opt"]) if graphed else step
+        losses = [float(run().detach()) for _ in range(4)]
+        old = st["opt"]
+        new = hiseg.FusedAdamW(m, lr=5e-4, weight_decay=0.01, max_grad_norm=1.0)
+        for p in new.param_groups[0]["params"]:
+            if p in old.state:
+                new.state[p] = old.state[p]
+        st["opt"] = new
+        losses += [float(run().detach()) for _ in range(4)]
+        torch.cuda.synchronize()
+        if graphed:
+            assert run.captures == 2
+        params = torch.cat([p.detach().float().reshape(-1) for p in m.parameters()]).cpu()
+        runs.append((losses, params, new.exp_avg.cpu(), new.step_count))
+    (l0, p0, m0, s0), (l1, p1, m1, s1) = runs
+    assert l0 == l1, (l0, l1)
+    assert s0 == s1 == 8
+    assert torch.equal(p0, p1) and torch.equal(m0, m1)
