@@ -59,6 +59,8 @@ PEAK_HBM_GBS = 8000.0     # MI355X HBM3E (MI355X_MICROARCH.md)
 GFLOP_PER_ROI_MASK = 53.1 + 27.7 / 8
 # Algorithmic work per training sample: B0-std head fwd+bwd 173.5 GFLOP + UNet fwd per ROI
 GFLOP_PER_TRAIN_ROI = 173.5 + 27.7 / 8
+# Distillation unit = one 640x640 image: B7 teacher fwd 120.3 + B0 student fwd+bwd ~111 GFLOP
+GFLOP_PER_DISTILL_IMAGE = 120.3 + 111.0
 
 B0_KWARGS = dict(
     roi_size=ROI_HW, mask_size=MASK_HW, multi_scale=False, use_attention_module=True,
@@ -191,7 +193,10 @@ def train_bench(device, dtype, rank, world, dist, steps, warmup, preset=None, ba
     if world > 1:
         HD.enable_grad_sync(model)
         HD.sync_loss_class_weights(loss_fn)   # class weights from the counts of the whole (all-rank) batch
+        # the local leg left per-rank optimizer moments / loss EMA: start the DDP leg from rank 0's
+        HD.broadcast_training_state(state["opt"], loss_fn)
     elapsed, first, last = timed()
+    prof = call_profile(step) if world == 1 else None
     sps = steps / elapsed
     gflop = GFLOP_PER_TRAIN_ROI if preset is None else GFLOP_PER_TRAIN_SAMPLE[preset]
     if preset is None:
@@ -211,6 +216,11 @@ def train_bench(device, dtype, rank, world, dist, steps, warmup, preset=None, ba
                       "roi_samples_per_step": n_samples * world,
                       "parallelism": f"dp{world} (DDP, bucketed RCCL grad all-reduce)" if world > 1 else "dp1",
                       "schedule": "eager" if run is step else "one HIP graph per step (hiseg.GraphedStep)"}}
+    pipe = out["pipeline_tflops"] / world
+    out["pipeline_frac"] = round(pipe / PEAK_BF16_TFLOPS, 4)
+    if prof is not None:
+        out["roofline"] = prof.pop("roofline", None)
+        out["call_profile"] = prof
     if local is not None:
         out["local_step_per_s"] = round(local, 3)
         out["ddp_over_local"] = round(sps / local, 4)   # 1.0 = the gradient exchange is fully hidden
@@ -272,9 +282,16 @@ def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=6
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = tt.item()
     sps = steps / elapsed
+    prof = call_profile(step) if world == 1 else None
+    extra = {}
+    if prof is not None:
+        extra["roofline"] = prof.pop("roofline", None)
+        extra["call_profile"] = prof
+    extra["pipeline_tflops"] = round(sps * batch * world * GFLOP_PER_DISTILL_IMAGE / 1e3, 1)
+    extra["pipeline_frac"] = round(extra["pipeline_tflops"] / world / PEAK_BF16_TFLOPS, 4)
     return {"metric": "distillation step/s", "value": round(sps, 3), "unit": "steps/s",
             "ms_per_step": round(1e3 / sps, 2), "steps": steps, "warmup": warmup,
-            "images_per_s": round(sps * batch * world, 1), "loss_last": round(float(loss.detach()), 4),
+            "images_per_s": round(sps * batch * world, 1), "loss_last": round(float(loss.detach()), 4), **extra,
             "config": {"workload": f"C5: B7 teacher (eval) -> B0 student (train-mode BN, decoder-only phase), "
                                    f"{batch} img {hw}x{hw}/GPU, UNetDistillationLoss T=4 + BCE/Dice targets, "
                                    f"decoder FusedAdamW clip 1.0", "global_batch": batch * world,
@@ -449,16 +466,151 @@ def cpu_train_baseline(seconds_budget=30.0):
                                       f"median of {n} after 2 warm-ups, {t:.2f} s/step"}
 
 
+DOMINANT_KERNEL_ID = "conv_hwr_128_256x256_roi"
+
+
+def cpu_train_c3_baseline(bench_batch=32, seconds_budget=30.0, full_budget_s=90.0):
+    """the oracle's C3 (B1-enhanced, 80x60 ROI / 160x120 mask) train step on the host cores at the
+    reference batch (2 images 640x640 x 1 ROI: 2 warm-ups, median of >= 5) and at the bench batch (32) as a
+    bounded sample: one step after the batch-2 warm-ups, skipped when the batch-2 time predicts more than
+    `full_budget_s` for it."""
+    import filler
+    from oracle import rgb_model as O
+    from oracle import train as OT
+    import hiseg
+    torch.set_num_threads(cpu_threads())
+    kw = preset_kwargs("b1")
+    model = hiseg.create_rgb_hierarchical_model(**kw)
+    filler.fill_module(model)
+    for m in model.modules():
+        if isinstance(m, (torch.nn.Dropout, torch.nn.Dropout2d)):
+            m.p = 0.0
+    sd = OT.params_of(model)
+    cfg = O.cfg_from_kwargs(kw)
+    params = [v for v in sd.values() if v.requires_grad]
+
+    def make(b):
+        images = torch.rand(b, 3, 640, 640, generator=torch.Generator().manual_seed(0))
+        rois = torch.from_numpy(filler.box_rois(1, b, 1))
+        tgt = torch.from_numpy(filler.ellipse_targets(7, b, *kw["mask_size"]))
+        state, loss_fn = {}, OT.RefinedHierarchicalLoss()
+
+        def run():
+            with torch.no_grad():
+                u = O.pretrained_unet_logits(sd, images, "b1")
+            logits, aux = OT.forward_train(sd, images, rois, u, cfg, (640, 640))
+            loss, _ = loss_fn(logits, tgt, aux)
+            for p in params:
+                p.grad = None
+            loss.backward()
+            OT.adamw_step(params, [p.grad if p.grad is not None else torch.zeros_like(p) for p in params], state)
+        return run
+
+    t2, n2 = _median_runs(make(2), budget_s=seconds_budget)
+    out = {"value": round(1.0 / t2, 4), "unit": "steps/s", "batch": 2, "cores": torch.get_num_threads(),
+           "kind": "port", "sample": f"oracle/train.py fp32 CPU C3 B1-enhanced train step, 2 images 640x640 x 1 ROI, "
+                                     f"median of {n2} after 2 warm-ups, {t2:.2f} s/step"}
+    est = t2 * bench_batch / 2
+    if est <= full_budget_s:
+        run = make(bench_batch)
+        t0 = time.perf_counter()
+        run()
+        tb = time.perf_counter() - t0
+        out["bench_batch"] = {"value": round(1.0 / tb, 4), "unit": "steps/s", "batch": bench_batch,
+                              "sample": f"one step of {bench_batch} images 640x640 x 1 ROI after the batch-2 "
+                                        f"warm-ups (bounded sample), {tb:.2f} s/step"}
+    else:
+        out["bench_batch"] = {"value": None, "batch": bench_batch,
+                              "sample": f"skipped: the batch-2 step predicts ~{est:.0f} s per step (> {full_budget_s:.0f} s budget)"}
+    return out
+
+
 def load_traffic():
-    """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3 PMC summary, if any."""
-    path = os.path.join(ROOT, "profiles", "r2_pmc_traffic.json")
-    if not os.path.exists(path):
-        return None
+    """Per-launch HBM bytes of the dominant kernel (rocprofv3 FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected)
+    from roofline_traffic.json at the repository root -- a tracked file that travels with the tree (profiles/
+    does not); None when it describes another kernel than the one timed here."""
+    path = os.path.join(ROOT, "roofline_traffic.json")
     try:
         with open(path) as f:
-            return json.load(f).get("dominant_bytes_per_launch")
-    except Exception:
+            d = json.load(f)
+    except (OSError, ValueError):
         return None
+    if d.get("kernel_id") != DOMINANT_KERNEL_ID:
+        return None
+    return d.get("dominant_bytes_per_launch")
+
+
+def _conv_flops(d):
+    """Algorithmic FLOPs of one conv GEMM launch (forward, data gradient or weight gradient: the same
+    2 * pixels * K * columns) from its hiseg_conv2d_desc."""
+    if d.convT:
+        return 2.0 * d.N * d.H * d.W * d.Ca * d.Cout
+    return 2.0 * d.N * d.Ho * d.Wo * d.Cout * d.KH * d.KW * (d.Ca + d.Cb)
+
+
+def call_profile(step):
+    """One extra (untimed) step with HIP events around every libhiseg C-ABI call on its launch stream:
+    per-entry-point GPU time and the dominant conv kernel class (forward / data-gradient / weight-gradient
+    launches grouped by shape) with its MFMA roofline -- the `roofline` of the train and distill legs."""
+    from hiseg import _lib as L
+    lib = L.lib()
+    real, rec = {}, []
+    names = [n for n in (L.EXPORTED or []) if n.startswith("hiseg_")]
+    for name in names:
+        fn = getattr(lib, name, None)
+        if fn is None or not callable(fn):
+            continue
+        real[name] = fn
+
+        def wrap(*a, _n=name, _f=fn):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            r = _f(*a)
+            e1.record()
+            key, flops = None, 0.0
+            if _n in ("hiseg_conv2d_fwd", "hiseg_conv2d_fwd_variant", "hiseg_conv2d_wgrad"):
+                d = a[0]._obj
+                kind = "wgrad" if _n == "hiseg_conv2d_wgrad" else (
+                    "dgrad" if sys._getframe(1).f_code.co_name == "_dgrad_launch" else "fwd")
+                key = (f"{kind} {d.KH}x{d.KW}{' T' if d.convT else ''} {d.Ca}+{d.Cb}->{d.Cout} "
+                       f"{d.N}x{d.Ho}x{d.Wo}")
+                flops = _conv_flops(d)
+            rec.append((_n, key, flops, e0, e1))
+            return r
+        setattr(lib, name, wrap)
+    try:
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record()
+        step()
+        t1.record()
+        torch.cuda.synchronize()
+    finally:
+        for name, fn in real.items():
+            setattr(lib, name, fn)
+    step_ms = t0.elapsed_time(t1)
+    by_entry, groups = {}, {}
+    for n, k, fl, e0, e1 in rec:
+        ms = e0.elapsed_time(e1)
+        by_entry[n] = by_entry.get(n, 0.0) + ms
+        if k is not None:
+            g = groups.setdefault(k, [0, 0.0, fl])
+            g[0] += 1
+            g[1] += ms
+    conv_ms = sum(g[1] for g in groups.values())
+    out = {"step_ms_probed": round(step_ms, 3),
+           "conv_share": round(conv_ms / step_ms, 4) if step_ms > 0 else None,
+           "top_entry_points_ms": {n: round(ms, 3) for n, ms in sorted(by_entry.items(), key=lambda kv: -kv[1])[:6]}}
+    if groups:
+        key, (cnt, ms, fl) = max(groups.items(), key=lambda kv: kv[1][1])
+        avg = ms / cnt
+        ach = fl / (avg * 1e-3) / 1e12
+        out["roofline"] = {"bound": "mfma", "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                           "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None, "kernel": key,
+                           "launches_timed": cnt, "avg_launch_ms": round(avg, 4), "flop_per_launch": fl,
+                           "share_of_step": round(ms / step_ms, 4) if step_ms > 0 else None}
+        all_fl = sum(g[2] * g[0] for g in groups.values())
+        out["conv_tflops"] = round(all_fl / (conv_ms * 1e-3) / 1e12, 1) if conv_ms > 0 else None
+    return out
 
 
 def _free_port():
@@ -580,6 +732,8 @@ def main():
             out["cpu_baseline"] = cpu_baseline()
             if not args.no_train:
                 out["cpu_baseline_train"] = cpu_train_baseline()
+                if not args.no_presets:
+                    out["cpu_baseline_train_c3"] = cpu_train_c3_baseline()
         print(json.dumps(out))
     if dist:
         dist.destroy_process_group()
@@ -634,7 +788,8 @@ def infer_bench(args, device, dtype, rank, world, dist):
         achieved = summ["flops"] / (summ["avg_ms"] * 1e-3) / 1e12
         roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": load_traffic(),
-                    "kernel": "conv_hw_kernel<128, reuse> (halo-tiled: 16x16-pixel x 128-Cout workgroup tiles, one 18x18 halo per 32-channel slice for all 9 taps, B fragments reused across ky, 4-stage weight ring, 2 workgroups per CU, LDS-staged epilogue) 256->256 3x3 @64x48 x256 ROIs",
+                    "kernel_id": DOMINANT_KERNEL_ID,
+                    "kernel": "conv_hwr_kernel (halo-tiled: 16x16-pixel x 128-Cout workgroup tiles, one 18x18 halo per 32-channel slice in LDS, weights in MFMA fragment order streamed straight into registers, one barrier per slice, 2 workgroups per CU, LDS-staged epilogue) 256->256 3x3 @64x48 x256 ROIs",
                     "launches_timed": summ["launches"], "avg_launch_ms": round(summ["avg_ms"], 4),
                     "flop_per_launch": summ["flops"]}
     pipeline_tflops = value * GFLOP_PER_ROI_MASK / 1e3

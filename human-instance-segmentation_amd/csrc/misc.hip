@@ -974,3 +974,28 @@ extern "C" int hiseg_output_conv_fwd(const float* u, int B, int H, int W, const 
                      b, out);
   return hiseg_check_launch("output_conv");
 }
+
+// ------------------------------------------------------------------------------------------ test utility
+__global__ void __launch_bounds__(256) debug_fill_lds_kernel(unsigned pattern, int words) {
+  extern __shared__ unsigned lds_fill[];
+  for (int i = threadIdx.x; i < words; i += 256) lds_fill[i] = pattern;
+  __syncthreads();
+  // keep the stores: a data-dependent (never true) global write the compiler cannot prove dead
+  if (lds_fill[(threadIdx.x * 7) % words] == pattern + 1u && pattern == 0x12345678u) asm volatile("s_nop 0");
+}
+
+extern "C" int hiseg_debug_fill_lds(unsigned pattern, int rounds, hiseg_stream_t stream) {
+  HISEG_REQUIRE(rounds >= 1 && rounds <= 64, HISEG_ERR_BAD_ARG, "debug_fill_lds: rounds 1..64");
+  const int bytes = 160 * 1024;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)debug_fill_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    attr = true;
+  }
+  int dev = 0, cus = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  hipLaunchKernelGGL(debug_fill_lds_kernel, dim3(cus * rounds), dim3(256), bytes, (hipStream_t)stream, pattern,
+                     bytes / 4);
+  return hiseg_check_launch("debug_fill_lds");
+}

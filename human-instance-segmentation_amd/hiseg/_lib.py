@@ -286,6 +286,7 @@ def _declare(lib):
         "hiseg_adamw_step_guarded": ([P, P, P, P, c_ll, c_float, c_float, c_float, c_float, c_float, P, c_float, P,
                                       P, c_int, P, P], c_int),
         "hiseg_adamw_max_segments": ([], c_int),
+        "hiseg_debug_fill_lds": ([ctypes.c_uint, c_int, P], c_int),
         "hiseg_adamw_step_segmented": ([P, P, P, P, c_ll, c_float, c_float, c_float, c_float, c_float, c_float,
                                         c_float, P, c_float, P, P, c_int, P, c_int, P, P], c_int),
     }

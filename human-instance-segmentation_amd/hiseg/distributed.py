@@ -148,6 +148,22 @@ def sync_loss_class_weights(loss_fn: nn.Module, process_group=None) -> nn.Module
     return loss_fn
 
 
+def broadcast_training_state(optimizer=None, loss_fn: Optional[nn.Module] = None, src: int = 0,
+                             process_group=None) -> None:
+    """Copy rank `src`'s FusedAdamW moments and per-parameter step counts and the loss's dynamic-weight EMA state
+    to every rank (after enable_grad_sync broadcast the parameters): replicas that trained on their own before
+    continue as one data-parallel trajectory, as torch DDP replicas built from one checkpoint would."""
+    if not dist.is_initialized():
+        raise RuntimeError("hiseg.distributed: torch.distributed is not initialised")
+    with torch.no_grad():
+        if optimizer is not None and getattr(optimizer, "exp_avg", None) is not None:
+            for t in (optimizer.exp_avg, optimizer.exp_avg_sq, optimizer._seg_start, optimizer._steps):
+                dist.broadcast(t, src, group=process_group)
+        st = getattr(loss_fn, "_state", None) if loss_fn is not None else None
+        if st is not None:
+            dist.broadcast(st, src, group=process_group)
+
+
 def grad_sync_of(model: nn.Module) -> Optional[GradBucketSync]:
     return model.__dict__.get(_SYNC_KEY)
 

@@ -46,6 +46,10 @@ int hiseg_version(void);
 const char* hiseg_last_error_string(void);
 /* 1 if the library's code object contains gfx950 kernels (always true for this build). */
 int hiseg_built_for_gfx950(void);
+/* Test utility (tests/, tools/): fill the LDS of every CU with a 32-bit pattern -- 160 KB workgroups, `rounds`
+ * times the CU count of them -- so that a kernel which reads LDS it did not write in its own dispatch (stale data
+ * left by an earlier kernel: LDS is not cleared between dispatches) sees the pattern (e.g. a NaN). */
+int hiseg_debug_fill_lds(unsigned pattern, int rounds, hiseg_stream_t stream);
 
 /* A HIP stream whose kernels run only on the CUs whose bits are set in mask[0..nwords) (hipExtStreamCreateWithCUMask),
  * for the serving schedule's full-image UNet stream (hiseg.StreamPipelinedExport(cu_mask=...)); destroy with

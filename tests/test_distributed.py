@@ -145,3 +145,38 @@ def test_loss_class_counts_all_reduced_gloo_world2():
     for rank, res in out:
         assert not isinstance(res, str), res
         assert res[0] == [21.0, 60.0, 6.0, 10.0]
+
+
+def _state_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import types
+        from hiseg import distributed as HD
+        opt = types.SimpleNamespace(   # FusedAdamW's device state (moments, segment bounds, step counts)
+            exp_avg=torch.full((6,), float(rank + 1)), exp_avg_sq=torch.full((6,), 10.0 * (rank + 1)),
+            _seg_start=torch.tensor([0, 2, 6]), _steps=torch.tensor([3 + rank, 5 + rank, 3 + rank, 5 + rank],
+                                                                     dtype=torch.int32))
+        loss = types.SimpleNamespace(_state=torch.arange(8, dtype=torch.float64) * (rank + 1))
+        HD.broadcast_training_state(opt, loss)
+        q.put((rank, [opt.exp_avg.tolist(), opt.exp_avg_sq.tolist(), opt._steps.tolist(), loss._state.tolist()]))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e)))
+
+
+def test_broadcast_training_state_gloo_world2():
+    """the DDP bench leg starts from rank 0's optimizer moments, per-parameter step counts and loss
+    EMA state, not from each rank's own local-training state."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_state_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=120) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+    for rank, res in out:
+        assert not isinstance(res, str), res
+        assert res == [[1.0] * 6, [10.0] * 6, [3, 5, 3, 5], [float(i) for i in range(8)]]

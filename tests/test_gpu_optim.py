@@ -155,8 +155,10 @@ def test_unfreeze_midway_matches_torch_adamw():
     for s in range(3):
         both(30 + s)
     torch.cuda.synchronize()
+    # same arithmetic op for op; contraction / rounding differences stay ~1e-6 over 6 steps, whereas a global
+    # step count would move the new parameters' first updates by a factor 2.5-3 (~lr = 1e-2)
     for p, q in zip(m.parameters(), ref.parameters()):
-        torch.testing.assert_close(p.detach(), q.detach(), rtol=2e-6, atol=2e-7)
+        torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-5, atol=1e-6)
     steps = opt.param_steps()
     assert [steps[p] for p in m.parameters()] == [int(topt.state[q]["step"]) for q in ref.parameters()] \
         == [3, 3, 6, 6, 6, 6, 6, 6]
@@ -164,7 +166,7 @@ def test_unfreeze_midway_matches_torch_adamw():
     tsd = topt.state_dict()
     for i, st in tsd["state"].items():
         assert float(sd["state"][i]["step"]) == float(st["step"])
-        torch.testing.assert_close(sd["state"][i]["exp_avg_sq"], st["exp_avg_sq"], rtol=1e-6, atol=1e-12)
+        torch.testing.assert_close(sd["state"][i]["exp_avg_sq"], st["exp_avg_sq"], rtol=1e-5, atol=1e-12)
 
 
 def test_reference_state_transfer_between_fused_optimizers():

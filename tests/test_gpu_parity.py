@@ -759,6 +759,54 @@ def test_conv_halo_wide_within_bf16(name, variant):
     assert ((y - ref).abs().max() / ref.abs().max()).item() < 8e-3
 
 
+@pytest.mark.parametrize("name", list(HW_CASES))
+def test_conv_hwr_bit_identical_to_halo_kernel(name):
+    """The register-streamed-weight halo kernel (conv_hwr.hip, variant 92: weights in MFMA fragment order straight
+    into registers, one barrier per 32-channel slice) accumulates in conv_hw's non-reuse order (variant 82: slice,
+    then taps 0..8), so its output equals that kernel's bit for bit -- ragged tiles, offset views, residual / ReLU
+    epilogues, Cout 128 / 256 / 384."""
+    from hiseg import ops
+    N, Cin, Cout, H, W, res, relu, coff = HW_CASES[name]
+    if Cout % 128 or Cin % 64:
+        pytest.skip("variant 92 needs a 128-multiple Cout and fragment-packed weights (64-multiple Cin)")
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(13)
+    full = ops.Act.new(N, H, W, Cin + coff, dt, DEV, zero=False)
+    full.t.copy_(torch.randn(full.t.numel(), device=DEV, generator=g).to(dt))
+    xa = full.slice(coff, Cin) if coff else full
+    w = torch.randn(Cout, Cin, 3, 3, device=DEV, generator=g) / (Cin * 9) ** 0.5
+    p = ops.pack_conv(w, torch.randn(Cout, device=DEV, generator=g) * 0.1, None, int(relu), dt, DEV, pad=1)
+    assert p.weight_frag is not None
+    R = ops.Act.from_nchw(torch.randn(N, Cout, H, W, device=DEV, generator=g), dt) if res else None
+    y82 = ops.conv2d(p, xa, residual=R, variant=82).t.clone()
+    y92 = ops.conv2d(p, xa, residual=R, variant=92).t.clone()
+    auto = ops.conv2d(p, xa, residual=R, variant=0).t.clone()
+    torch.cuda.synchronize()
+    assert torch.isfinite(y92.float()).all()
+    assert torch.equal(y92, y82)
+    assert torch.equal(auto, y92)   # the automatic choice takes it
+
+
+@pytest.mark.parametrize("shape", [(2, 128, 128, 128, 32, 24, False), (3, 64, 64, 128, 21, 13, True),
+                                   (2, 192, 64, 256, 9, 23, True)])
+def test_conv_hwr_two_source_bit_identical(shape):
+    """Variant 92 over a two-source concat (EnhancedUNet decoder up ++ skip): bit-identical to variant 82."""
+    from hiseg import ops
+    N, Ca, Cb, Cout, H, W, res = shape
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(23)
+    xa = ops.Act.from_nchw(torch.randn(N, Ca, H, W, device=DEV, generator=g), dt)
+    xb = ops.Act.from_nchw(torch.randn(N, Cb, H, W, device=DEV, generator=g), dt)
+    w = torch.randn(Cout, Ca + Cb, 3, 3, device=DEV, generator=g) / ((Ca + Cb) * 9) ** 0.5
+    p = ops.pack_conv(w, torch.randn(Cout, device=DEV, generator=g) * 0.1, None, 1, dt, DEV, pad=1, split=(Ca, Cb))
+    assert p.weight_frag is not None
+    R = ops.Act.from_nchw(torch.randn(N, Cout, H, W, device=DEV, generator=g), dt) if res else None
+    y82 = ops.conv2d(p, xa, xb, residual=R, variant=82).t.clone()
+    y92 = ops.conv2d(p, xa, xb, residual=R, variant=92).t.clone()
+    torch.cuda.synchronize()
+    assert torch.equal(y92, y82)
+
+
 @pytest.mark.parametrize("variant", [86, 89])
 @pytest.mark.parametrize("shape", [(3, 64, 64, 64, 64, 48, True), (2, 128, 128, 128, 32, 24, False),
                                    (2, 64, 32, 64, 21, 13, True), (2, 96, 64, 128, 9, 23, False)])

@@ -725,7 +725,7 @@ def test_graphed_train_step_equals_eager():
     images = torch.from_numpy(filler.uniform(31, (2, 3, 96, 128))).to(DEV)
     rois = torch.from_numpy(filler.box_rois(32, 2, 2)).to(DEV)
     tgt = torch.from_numpy(filler.ellipse_targets(33, 4, 128, 96)).to(DEV)
-    runs = []
+    runs, diag = [], []
     for graphed in (False, True):
         torch.manual_seed(0)
         m = _model(torch.bfloat16, p_drop_zero=False).to(DEV).train()
@@ -747,14 +747,19 @@ def test_graphed_train_step_equals_eager():
             return loss
 
         run = hiseg.GraphedStep(step, lambda: st["opt"]) if graphed else step
-        losses = [float(run().detach()) for _ in range(4)]
+        losses, norms = [], []
+        for _ in range(4):
+            losses.append(float(run().detach()))
+            norms.append((float(st["opt"].last_norm), st["opt"].step_count, st["opt"].skipped_steps))
         torch.cuda.synchronize()
         if graphed:
             assert run.captures == 1
         params = torch.cat([p.detach().float().reshape(-1) for p in m.parameters()]).cpu()
         runs.append((losses, params, st["opt"].exp_avg.cpu(), st["opt"].step_count))
+        diag.append(norms)
     (l0, p0, m0, s0), (l1, p1, m1, s1) = runs
-    assert l0 == l1, (l0, l1)
+    # diag: per step (pre-clip gradient norm, applied steps, skipped steps) of the eager / graphed runs
+    assert l0 == l1, (l0, l1, diag)
     assert s0 == s1 == 4
     assert torch.equal(p0, p1) and torch.equal(m0, m1)
     assert l0[-1] != l0[0]
@@ -806,3 +811,44 @@ def test_graphed_step_recaptures_after_optimizer_swap():
     assert l0 == l1, (l0, l1)
     assert s0 == s1 == 8
     assert torch.equal(p0, p1) and torch.equal(m0, m1)
+
+
+def test_side_stream_train_step_equals_default_stream():
+    """a fresh model's bf16 train steps (Dropout2d on, FusedAdamW with clipping) issued on the default
+    stream and under torch.cuda.stream(side) -- every buffer created in the first step (flat parameters, packing
+    tables, optimizer state) then lives on the side stream -- are bit-identical over 3 steps."""
+    import hiseg
+    images = torch.from_numpy(filler.uniform(141, (2, 3, 96, 128))).to(DEV)
+    rois = torch.from_numpy(filler.box_rois(142, 2, 2)).to(DEV)
+    tgt = torch.from_numpy(filler.ellipse_targets(143, 4, 128, 96)).to(DEV)
+    runs = []
+    for side in (None, torch.cuda.Stream(), torch.cuda.Stream()):
+        torch.manual_seed(0)
+        m = _model(torch.bfloat16, p_drop_zero=False).to(DEV).train()
+        for mm in (m.roi_align_mask, m.roi_align_rgb):
+            mm.spatial_scale_h, mm.spatial_scale_w = 96, 128
+        loss_fn = hiseg.RefinedHierarchicalLoss(use_boundary_aware_loss=True, use_contour_detection=True,
+                                                use_distance_transform=True)
+        opt = None
+        losses = []
+        for _ in range(3):
+            if side is not None:
+                side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side) if side is not None else torch.cuda.stream(torch.cuda.current_stream()):
+                logits, aux = m(images, rois)
+                loss, _ = loss_fn(logits, tgt, aux)
+                if opt is None:
+                    opt = hiseg.FusedAdamW(m, lr=5e-4, weight_decay=0.01, max_grad_norm=1.0)
+                opt.zero_grad()
+                loss.backward()
+                opt.step()
+            if side is not None:
+                torch.cuda.current_stream().wait_stream(side)
+            losses.append(float(loss.detach()))
+        torch.cuda.synchronize()
+        params = torch.cat([p.detach().float().reshape(-1) for p in m.parameters()]).cpu()
+        runs.append((losses, params, opt.exp_avg_sq.cpu(), opt.step_count))
+    for l, p, v, s in runs[1:]:
+        assert l == runs[0][0]
+        assert s == runs[0][3] == 3
+        assert torch.equal(p, runs[0][1]) and torch.equal(v, runs[0][2])

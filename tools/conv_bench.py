@@ -93,6 +93,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--shapes", default=",".join(SHAPES))
+    ap.add_argument("--bitref", type=int, default=None, help="also report bit-equality against this variant")
     args = ap.parse_args()
     variants = [int(v) for v in args.variants.split(",")]
     results = {}
@@ -105,13 +106,21 @@ def main():
         run(d, -1)
         torch.cuda.synchronize()
         ref = out.t.float().clone()
-        ok = {}
+        ok, same = {}, {}
+        bref = None
+        if args.bitref is not None:
+            out.t.fill_(float("nan"))
+            run(d, args.bitref)
+            torch.cuda.synchronize()
+            bref = out.t.clone()
         for v in variants:
             out.t.fill_(float("nan"))
             run(d, v)
             torch.cuda.synchronize()
             err = ((out.t.float() - ref).abs().max() / ref.abs().max()).item()
             ok[v] = err
+            if bref is not None:
+                same[v] = bool(torch.equal(out.t, bref))
         times = {v: [] for v in variants}
         for _ in range(args.rounds):
             for v in variants:
@@ -128,6 +137,8 @@ def main():
         for v in variants:
             ms = min(times[v])
             row[str(v)] = {"ms": round(ms, 4), "tflops": round(flops / ms / 1e9, 1), "rel_err_vs_generic": ok[v]}
+            if v in same:
+                row[str(v)]["bit_equal_ref"] = same[v]
         results[name] = row
         print(name, json.dumps(row), flush=True)
     os.makedirs("gpurun_out", exist_ok=True)

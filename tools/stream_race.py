@@ -10,6 +10,8 @@ step, so a schedule-dependent result shows the step at which it first appears.  
   graphed      hiseg.GraphedStep
   poison_nan   default stream; before every step the caching allocator's free blocks are filled with NaN
   poison_rand  the same with random values (an uninitialised read then changes the result)
+  lds_nan      default stream; before every libhiseg call every CU's LDS is filled with NaN (f32 and bf16)
+  lds_big      the same with 8.5e37 (f32 and bf16): a kernel reading LDS it did not write then changes
 """
 import os
 import sys
@@ -68,6 +70,29 @@ def poison(kind):
     del held
 
 
+class LdsPoison:
+    """Wrap every libhiseg entry point: fill all LDS with `pattern` right before the call (same stream)."""
+
+    def __init__(self, pattern):
+        from hiseg import _lib as L
+        self.lib, self.real, self.pattern = L.lib(), {}, pattern
+        fill = self.lib.hiseg_debug_fill_lds
+        for name in L.EXPORTED:
+            if not name.startswith("hiseg_") or name == "hiseg_debug_fill_lds":
+                continue
+            fn = getattr(self.lib, name)
+            self.real[name] = fn
+
+            def wrap(*a, _f=fn):
+                fill(self.pattern, 2, L.stream_ptr())
+                return _f(*a)
+            setattr(self.lib, name, wrap)
+
+    def close(self):
+        for name, fn in self.real.items():
+            setattr(self.lib, name, fn)
+
+
 def run(schedule, steps=4):
     images = torch.from_numpy(filler.uniform(31, (2, 3, 96, 128))).to(DEV)
     rois = torch.from_numpy(filler.box_rois(32, 2, 2)).to(DEV)
@@ -89,10 +114,15 @@ def run(schedule, steps=4):
         return loss
 
     side = torch.cuda.Stream()
+    lp = None
+    if schedule.startswith("lds"):
+        lp = LdsPoison(0x7FC07FC0 if schedule == "lds_nan" else 0x7E807E80)
     gs = hiseg.GraphedStep(step, lambda: st["opt"]) if schedule == "graphed" else None
     rows = []
     for i in range(steps):
-        if schedule.startswith("poison"):
+        if schedule.startswith("lds"):
+            loss = step()
+        elif schedule.startswith("poison"):
             poison(schedule.split("_")[1])
             loss = step()
         elif schedule.startswith("default"):
@@ -114,6 +144,8 @@ def run(schedule, steps=4):
             loss = gs()
         torch.cuda.synchronize()
         rows.append((float(loss.detach()), checksum(m, st["opt"])))
+    if lp is not None:
+        lp.close()
     return rows
 
 
