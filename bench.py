@@ -154,9 +154,11 @@ def train_bench(device, dtype, rank, world, dist, steps, warmup, preset=None, ba
         state["opt"].step()
         return loss
 
-    # --graph-train: one HIP graph per step (hiseg.GraphedStep; every per-step state lives on the device).  Off
-    # by default: the step is kernel-bound (the trace shows no launch gaps) and on this ROCm the replayed graph
-    # of ~1 000 kernels ran slower than eager launches (137 vs 118 ms)
+    # One HIP graph per step on one GPU (hiseg.GraphedStep; every per-step state lives on the device): the eager
+    # C3 / C4 steps take 28 / 33 ms of Python enqueue for 38 / 41 ms of GPU work (tools/host_bound.py --train), so
+    # any host contention made them host-bound (C3 53-70 ms in full bench runs vs 38 ms alone); replayed, the
+    # step costs one launch.  Same GPU time as eager on a quiet host (profiles/r3_graph_vs_eager.txt).  Data-parallel
+    # legs stay eager (the bucketed all-reduce on the comm stream is not captured).  --eager-train: eager always.
     run = step
     if world == 1 and graph_train:
         run = hiseg.GraphedStep(step, lambda: state["opt"])
@@ -172,6 +174,9 @@ def train_bench(device, dtype, rank, world, dist, steps, warmup, preset=None, ba
         t0 = time.perf_counter()
         for _ in range(steps):
             loss = run()
+            if STEP_TIMES is not None:
+                torch.cuda.synchronize()
+                STEP_TIMES.append(time.perf_counter() - t0)
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
@@ -195,8 +200,11 @@ def train_bench(device, dtype, rank, world, dist, steps, warmup, preset=None, ba
         HD.sync_loss_class_weights(loss_fn)   # class weights from the counts of the whole (all-rank) batch
         # the local leg left per-rank optimizer moments / loss EMA: start the DDP leg from rank 0's
         HD.broadcast_training_state(state["opt"], loss_fn)
+    prof = None
+    if world == 1:   # per-call profile of one eager step (before any graph capture: its pool would skew it)
+        step()
+        prof = call_profile(step)
     elapsed, first, last = timed()
-    prof = call_profile(step) if world == 1 else None
     sps = steps / elapsed
     gflop = GFLOP_PER_TRAIN_ROI if preset is None else GFLOP_PER_TRAIN_SAMPLE[preset]
     if preset is None:
@@ -228,7 +236,7 @@ def train_bench(device, dtype, rank, world, dist, steps, warmup, preset=None, ba
     return out
 
 
-def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=640):
+def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=640, graph=True):
     """C5 (BASELINE.json configs[4]): B7 -> B0 staged distillation step, decoder-only phase of the progressive
     unfreezing schedule -- B7 teacher forward (eval), B0 student forward (train-mode BN) + decoder/head
     backward, UNetDistillationLoss (T = 4, targets), decoder-subset FusedAdamW with clip 1.0 -- 4 images
@@ -263,15 +271,21 @@ def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=6
         state["opt"].step()
         return loss
 
-    for _ in range(warmup):
-        loss = step()
+    prof = None
+    if world == 1:   # per-call profile of one eager step, before the graph capture
+        step()
+        step()
+        prof = call_profile(step)
+    run = hiseg.GraphedStep(step, lambda: state["opt"]) if (graph and world == 1) else step
+    for _ in range(max(warmup, 3 if run is not step else 1)):
+        loss = run()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        loss = step()
+        loss = run()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -282,7 +296,6 @@ def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=6
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = tt.item()
     sps = steps / elapsed
-    prof = call_profile(step) if world == 1 else None
     extra = {}
     if prof is not None:
         extra["roofline"] = prof.pop("roofline", None)
@@ -295,6 +308,7 @@ def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=6
             "config": {"workload": f"C5: B7 teacher (eval) -> B0 student (train-mode BN, decoder-only phase), "
                                    f"{batch} img {hw}x{hw}/GPU, UNetDistillationLoss T=4 + BCE/Dice targets, "
                                    f"decoder FusedAdamW clip 1.0", "global_batch": batch * world,
+                       "schedule": "eager" if run is step else "one HIP graph per step (hiseg.GraphedStep)",
                        "parallelism": f"dp{world} (bucketed RCCL grad all-reduce)" if world > 1 else "dp1"}}
 
 
@@ -466,6 +480,8 @@ def cpu_train_baseline(seconds_budget=30.0):
                                       f"median of {n} after 2 warm-ups, {t:.2f} s/step"}
 
 
+# developer hook (tools/c3_after_infer.py): a list collects the cumulative time after every timed train step
+STEP_TIMES = None
 DOMINANT_KERNEL_ID = "conv_hwr_128_256x256_roi"
 
 
@@ -660,7 +676,8 @@ def main():
     ap.add_argument("--no-presets", action="store_true", help="skip the C3 (B1) / C4 (B7) train lines")
     ap.add_argument("--distill-only", action="store_true", help="only the C5 distillation line (profiling)")
     ap.add_argument("--serial", action="store_true", help="one stream (no UNet/head overlap across steps)")
-    ap.add_argument("--graph-train", action="store_true", help="train legs as one replayed HIP graph per step")
+    ap.add_argument("--eager-train", action="store_true", help="train / distill legs as eager launches (default on one "
+                                                                "GPU: one replayed HIP graph per step)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher + rendezvous check only (no GPU work): CPU tests of the multi-rank path")
@@ -706,23 +723,25 @@ def main():
     out = {}
     if args.distill_only:
         args.train_only, args.no_train = True, True
-        out["distill"] = distill_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2)
+        out["distill"] = distill_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2,
+                                       graph=not args.eager_train)
     if not args.train_only:
         out = infer_bench(args, device, dtype, rank, world, dist)
     if not args.no_train:
         torch.cuda.empty_cache()
         out["train"] = train_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), max(2, args.warmup),
-                                   local_first=True, graph_train=args.graph_train)
+                                   local_first=True, graph_train=not args.eager_train)
         if not args.no_presets:
             torch.cuda.empty_cache()
             out["train_c3"] = train_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2, preset="b1",
-                                          batch=32, rois_per_img=1, hw=(640, 640), graph_train=args.graph_train)
+                                          batch=32, rois_per_img=1, hw=(640, 640), graph_train=not args.eager_train)
             torch.cuda.empty_cache()
             out["train_c4"] = train_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2, preset="b7",
-                                          batch=8, rois_per_img=1, hw=(640, 640), graph_train=args.graph_train)
+                                          batch=8, rois_per_img=1, hw=(640, 640), graph_train=not args.eager_train)
     if not args.no_distill and not args.train_only:
         torch.cuda.empty_cache()
-        out["distill"] = distill_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2)
+        out["distill"] = distill_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2,
+                                       graph=not args.eager_train)
     if not args.train_only and world == 1:
         torch.cuda.empty_cache()
         out["eval"] = eval_bench(device)

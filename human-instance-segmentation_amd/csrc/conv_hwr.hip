@@ -34,7 +34,10 @@ __device__ __forceinline__ void hr_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned l
 
 typedef __attribute__((address_space(3))) void hr_lds_void;
 
-template <int ACT, bool RES>
+// SCH (schedule of a K step): bit 1 -- s_setprio 1 around the MFMA groups (the co-resident workgroup's wave yields
+// its issue slots to them); bit 2 -- B-fragment reuse across ky (below).  Bit 0 is unused (an earlier interleaving
+// of the B reads between the last group's MFMAs measured slower: the variant numbers stay for the A/B record).
+template <int ACT, bool RES, int SCH>
 __global__ void __launch_bounds__(256, 2) conv_hwr_kernel(ConvArgs a) {
   constexpr int BCO = 128, TM = 4, TN = 8;
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
@@ -71,46 +74,49 @@ __global__ void __launch_bounds__(256, 2) conv_hwr_kernel(ConvArgs a) {
 
   // ---- A fragments: (Cout tile ct, slice sl, tap) at ((((ct * ncb + sl / 2) * 9 + tap) * 2 + sl % 2) * 64 + lane) * 16 B:
   // the lane / Cout-tile part in 4 VGPRs, the wave-uniform (slice, tap) part as the SGPR offset of the load
-  unsigned a_voff[TM];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-    a_voff[i] = ((unsigned)((co0 + wco * 64) >> 4) + (unsigned)i) * (unsigned)ncb * 18u * 1024u + (unsigned)lane * 16u;
+  // (recomputed per step from an opaque copy of the lane id: kept live across the unrolled slice, these loop
+  // invariants -- with the halo and B-fragment bases below -- push the kernel past 256 registers and spill)
+  const unsigned a_ct = (unsigned)((co0 + wco * 64) >> 4) * (unsigned)ncb * 18u * 1024u;
+  const unsigned a_ct_step = (unsigned)ncb * 18u * 1024u;
   auto load_a = [&](hr_u4 (&af)[TM], int sl, int tap) __attribute__((always_inline)) {
     const unsigned so = __builtin_amdgcn_readfirstlane((((unsigned)(sl >> 1) * 9u + (unsigned)tap) * 2u + (unsigned)(sl & 1)) * 1024u);
 #pragma unroll
-    for (int i = 0; i < TM; ++i) af[i] = __builtin_amdgcn_raw_buffer_load_b128(rF, a_voff[i], so, 0);
+    for (int i = 0; i < TM; ++i)
+      af[i] = __builtin_amdgcn_raw_buffer_load_b128(rF, a_ct + (unsigned)i * a_ct_step + (unsigned)lane * 16u, so, 0);
   };
 
-  // ---- halo pieces: piece p (0..5) of wave w = halo rows hr = 16 (4p + w) + lane / 4, one LDS-DMA (1 KiB) each:
-  // lane l lands at byte 16 l of the piece = row hr, slot l % 4, which holds chunk (l % 4) ^ swz(hr) (the swizzle is
-  // applied on the source side; swz(hr) = 2 ((hr >> 2) & 1) = 2 ((lane >> 4) & 1) for every piece).  Per piece,
-  // once: the source pixel, -1 outside the image / past row 324.
-  const int lrow = lane >> 2;
-  const int hchunk = (lane & 3) ^ (((lane >> 4) & 1) << 1);
-  int hpix[6];
-#pragma unroll
-  for (int p = 0; p < 6; ++p) {
-    const int hr = 16 * (4 * p + w) + lrow;
+  // ---- halo layout: row hr = hy * 18 + hx (64 B = 32 channels), 16-B chunk c stored at slot c ^ swz(hx),
+  // swz(hx) = 2 ((hx >> 2) & 1).  A B-fragment read (16 consecutive hx of one hy, 4 chunks) is conflict-free for
+  // every column shift kx (checked for all hy / kx by brute force over the ds_read_b128 lane groups), and the
+  // swizzle depends on the column only: a fragment's address is a per-lane base for its kx plus the row offset
+  // (j + ky) * 1152 as the instruction's immediate -- no per-read address arithmetic.
+  // Halo pieces: piece p (0..5) of wave w = halo rows hr = 16 (4p + w) + lane / 4, one LDS-DMA (1 KiB) each; lane l
+  // lands at byte 16 l of the piece = row hr, slot l % 4, so it fetches chunk (l % 4) ^ swz(hr % 18).  Per piece,
+  // once: the source pixel (-1 outside the image / past row 324) and that chunk.
+  const unsigned lds_base = (unsigned)(uintptr_t)(hr_lds_void*)smem;
+  auto halo_dma = [&](int p, int sl, int buf) __attribute__((always_inline)) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int hr = 16 * (4 * p + w) + (ln >> 2);
     const int hy = hr / 18, hx = hr - 18 * hy;
     const int iy = y0 + hy - 1, ix = x0 + hx - 1;
     const bool ok = hr < kHrHaloRows && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
-    hpix[p] = ok ? (n * d.H + iy) * d.W + ix : -1;
-  }
-  const unsigned lds_base = (unsigned)(uintptr_t)(hr_lds_void*)smem;
-  auto halo_dma = [&](int p, int sl, int buf) __attribute__((always_inline)) {
+    const int chunk = (ln & 3) ^ (((hx >> 2) & 1) << 1);
     const bool fb = 32 * sl >= d.Ca;
     const int cs = fb ? d.b_cstride : d.a_cstride, coff = fb ? d.b_coff + 32 * sl - d.Ca : d.a_coff + 32 * sl;
-    const unsigned off = hpix[p] >= 0 ? (unsigned)((hpix[p] * cs + coff + hchunk * 8) * 2) : OOB;
+    const unsigned off = ok ? (unsigned)((((n * d.H + iy) * d.W + ix) * cs + coff + chunk * 8) * 2) : OOB;
     hr_dma16(fb ? rB : rA, lds_base + (unsigned)(buf * kHrHaloBytes + 1024 * (4 * p + w)), off);
   };
   char* lds_c = reinterpret_cast<char*>(smem);
-  // B fragment: pixel (tile row wpx*8 + j, column lane % 16) at tap (ky, kx), channels 8 (lane / 16) .. + 7;
-  // halo row hr = bbase + (j + ky) * 18 + kx, from a per-step opaque copy of bbase (see halo_load)
-  const int bbase = wpx * TN * 18 + (lane & 15), bch = lane >> 4;
-  auto rdB = [&](int bb, int buf, int tap, int j) __attribute__((always_inline)) -> hr_u4 {
+  // B fragment: pixel (tile row wpx*8 + j, column lane % 16) at tap (ky, kx), channels 8 (lane / 16) .. + 7:
+  // halo row (wpx * 8 + j + ky, lane % 16 + kx)
+  auto bsw = [&](int ln, int kx) __attribute__((always_inline)) -> int {
+    const int hx = (ln & 15) + kx;
+    return (wpx * TN * 18 + hx) * 64 + (((ln >> 4) ^ (((hx >> 2) & 1) << 1)) << 4);
+  };
+  auto rdB = [&](int ln, int buf, int tap, int j) __attribute__((always_inline)) -> hr_u4 {
     const int ky = tap / 3, kx = tap - 3 * (tap / 3);
-    const int hr = bb + (j + ky) * 18 + kx;
-    return *reinterpret_cast<const hr_u4*>(lds_c + buf * kHrHaloBytes + hr * 64 + ((bch ^ hr_hswz(hr)) << 4));
+    return *reinterpret_cast<const hr_u4*>(lds_c + bsw(ln, kx) + buf * kHrHaloBytes + (j + ky) * 18 * 64);
   };
 
   floatx4 acc[TM][TN];
@@ -120,14 +126,15 @@ __global__ void __launch_bounds__(256, 2) conv_hwr_kernel(ConvArgs a) {
     for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   // ---- prologue: slice 0's halo into buffer 0, the first A fragments
-  hr_u4 af[TM], bf[TN];
+  constexpr int NBMAX = TN + 2;
+  hr_u4 af[TM], bf[NBMAX];
 #pragma unroll
   for (int p = 0; p < 6; ++p) halo_dma(p, 0, 0);
   load_a(af, 0, 0);
   asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // the 6 halo pieces (older than the 4 A loads)
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < TN; ++j) bf[j] = rdB(bbase, 0, 0, j);
+  for (int k = 0; k < ((SCH & 4) ? TN + 2 : TN); ++k) bf[k] = rdB(lane, 0, 0, k);
 
   // One K step (slice sl, tap), Cout fragment by Cout fragment: A fragment i's 8 MFMAs, then (registers free) the
   // next step's fragment i is loaded into it; the last fragment's MFMAs replace the B fragments column by column
@@ -135,39 +142,56 @@ __global__ void __launch_bounds__(256, 2) conv_hwr_kernel(ConvArgs a) {
   // piece p by LDS-DMA at the end of tap p (p = 0..5), after that step's A loads -- vmcnt counts in issue order,
   // so a piece is first waited for (by the compiler's wait for an A fragment issued after it) two steps later;
   // before the slice barrier every wave's pieces have landed (vmcnt(4): only the next slice's A loads may stay).
+  // REUSE (SCH & 4): steps run kx-major (step s: kx = s / 3, ky = s % 3), so the three ky steps of a kx read the
+  // halo tile rows j + ky of ONE set of 10 B fragments (rows 0..9 of the wave's window) kept in registers: 10
+  // fragment reads per three steps instead of 24 (conv_hw.hip's REUSE; the same accumulation order as its
+  // variant 86).  Without it step s is tap s (ky-major, variant 82's order).
+  constexpr bool REUSE = (SCH & 4) != 0;
+  constexpr int NB = REUSE ? TN + 2 : TN;
+  auto tap_of = [](int st) constexpr { return REUSE ? (st % 3) * 3 + st / 3 : st; };
   auto step = [&](int sl, auto tapc) __attribute__((always_inline)) {
-    constexpr int tap = decltype(tapc)::value;
+    constexpr int st = decltype(tapc)::value;
+    constexpr int KY = REUSE ? st % 3 : 0;          // B register shift of this step
+    constexpr bool read_b = REUSE ? (KY == 2 && st < 8) : st < 8;
     const int buf = sl & 1;
     const bool more = sl + 1 < nsl;
-    int bb = bbase;
-    asm volatile("" : "+v"(bb));
-    const int nsl_ = tap < 8 ? sl : sl + 1, ntap = tap < 8 ? tap + 1 : 0;
+    const int nsl_ = st < 8 ? sl : sl + 1, ntap = st < 8 ? tap_of(st + 1) : 0;
     const unsigned so = __builtin_amdgcn_readfirstlane(
         (((unsigned)(nsl_ >> 1) * 9u + (unsigned)ntap) * 2u + (unsigned)(nsl_ & 1)) * 1024u);
-    const bool load_next = tap < 8 || more;
+    const bool load_next = st < 8 || more;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const unsigned a_lane = a_ct + (unsigned)ln * 16u;
+    if constexpr ((SCH & 2) != 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
       for (int j = 0; j < TN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[i]),
-                                                             __builtin_bit_cast(bf16x8_t, bf[j]), acc[i][j], 0, 0, 0);
+                                                             __builtin_bit_cast(bf16x8_t, bf[j + KY]), acc[i][j], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
-      if (load_next) af[i] = __builtin_amdgcn_raw_buffer_load_b128(rF, a_voff[i], so, 0);
+      if (load_next) af[i] = __builtin_amdgcn_raw_buffer_load_b128(rF, a_lane + (unsigned)i * a_ct_step, so, 0);
     }
-    if constexpr (tap < 8) {
+    if constexpr ((SCH & 2) != 0) __builtin_amdgcn_s_setprio(0);
+    if constexpr (read_b) {
+      if constexpr (REUSE) {   // the next kx's window: rows 0..9 at column shift kx + 1
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bf[j] = rdB(bb, buf, tap + 1, j);
+        for (int k = 0; k < NB; ++k) bf[k] = rdB(ln, buf, st / 3 + 1, k);
+      } else {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bf[j] = rdB(ln, buf, st + 1, j);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (tap < 6) {
-      if (more) halo_dma(tap, sl + 1, buf ^ 1);
+    if constexpr (st < 6) {
+      if (more) halo_dma(st, sl + 1, buf ^ 1);
     }
-    if constexpr (tap == 8) {
+    if constexpr (st == 8) {
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       __syncthreads();   // slice sl+1's halo is in LDS; every wave is done reading slice sl's buffer
       if (more) {
 #pragma unroll
-        for (int j = 0; j < TN; ++j) bf[j] = rdB(bb, buf ^ 1, 0, j);
+        for (int k = 0; k < NB; ++k) bf[k] = rdB(ln, buf ^ 1, 0, k);
       }
     }
   };
@@ -256,13 +280,13 @@ __global__ void __launch_bounds__(256, 2) conv_hwr_kernel(ConvArgs a) {
   }
 }
 
-template <int ACT, bool RES>
+template <int ACT, bool RES, int SCH>
 static int launch_hwr(const ConvArgs& a, hipStream_t s) {
   const hiseg_conv2d_desc& d = a.d;
   const int tiles = d.N * ((d.H + 15) / 16) * ((d.W + 15) / 16);
   const int nco = d.Cout_pad / 128;
   const size_t lds = (size_t)256 * 128 * 2;   // >= 2 halo buffers (48 KiB)
-  auto kern = conv_hwr_kernel<ACT, RES>;
+  auto kern = conv_hwr_kernel<ACT, RES, SCH>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -272,10 +296,19 @@ static int launch_hwr(const ConvArgs& a, hipStream_t s) {
   return hiseg_check_launch("conv_hwr");
 }
 
-// 1 = launched, 0 = the layer does not qualify (caller falls back), <0 on error.  variant 92.
+template <int SCH>
+static int launch_hwr_sch(const ConvArgs& a, hipStream_t s) {
+  const hiseg_conv2d_desc& d = a.d;
+  const bool res = d.residual != nullptr, relu = d.act == HISEG_ACT_RELU;
+  return res ? (relu ? launch_hwr<HISEG_ACT_RELU, true, SCH>(a, s) : launch_hwr<HISEG_ACT_NONE, true, SCH>(a, s))
+             : (relu ? launch_hwr<HISEG_ACT_RELU, false, SCH>(a, s) : launch_hwr<HISEG_ACT_NONE, false, SCH>(a, s));
+}
+
+// 1 = launched, 0 = the layer does not qualify (caller falls back), <0 on error.  Variants 92..95 = SCH 0..3,
+// 96 = SCH 4 (B reuse across ky), 97 = SCH 6 (reuse + priority).
 int conv_hwr_try(const ConvArgs& a, hipStream_t s, int variant) {
   const hiseg_conv2d_desc& d = a.d;
-  if (variant != 92 || d.weight_frag == nullptr) return 0;
+  if (variant < 92 || variant > 97 || d.weight_frag == nullptr) return 0;
   if (d.dtype != HISEG_BF16 || d.out_dtype != HISEG_BF16) return 0;
   if (d.a_up != 1 || d.in_scale != nullptr || d.convT || d.mul != nullptr || d.out2 != nullptr) return 0;
   if (d.KH != 3 || d.KW != 3 || d.stride != 1 || d.pad != 1 || d.Ho != d.H || d.Wo != d.W) return 0;
@@ -295,9 +328,16 @@ int conv_hwr_try(const ConvArgs& a, hipStream_t s, int variant) {
   const long long span_w = (long long)d.Cout_pad * d.K_pad * 2;
   const long long span_r = d.residual ? (long long)a.M * d.r_cstride * 2 : 0;
   if (span_a >= 0x7fffffffll || span_b >= 0x7fffffffll || span_w >= 0x7fffffffll || span_r >= 0x7fffffffll) return 0;
-  const bool res = d.residual != nullptr, relu = d.act == HISEG_ACT_RELU;
-  const int r = res ? (relu ? launch_hwr<HISEG_ACT_RELU, true>(a, s) : launch_hwr<HISEG_ACT_NONE, true>(a, s))
-                    : (relu ? launch_hwr<HISEG_ACT_RELU, false>(a, s) : launch_hwr<HISEG_ACT_NONE, false>(a, s));
+  if ((long long)d.N * d.H * d.W >= (1ll << 29)) return 0;   // halo source pixel packed with its chunk in 31 bits
+  int r;
+  switch (variant) {
+    case 92: r = launch_hwr_sch<0>(a, s); break;
+    case 93: r = launch_hwr_sch<1>(a, s); break;
+    case 94: r = launch_hwr_sch<2>(a, s); break;
+    case 95: r = launch_hwr_sch<3>(a, s); break;
+    case 96: r = launch_hwr_sch<4>(a, s); break;
+    default: r = launch_hwr_sch<6>(a, s); break;
+  }
   return r < 0 ? r : 1;
 }
 

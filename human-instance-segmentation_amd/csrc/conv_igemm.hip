@@ -264,7 +264,7 @@ extern "C" int hiseg_conv2d_fwd(const hiseg_conv2d_desc* d, hiseg_stream_t strea
 static bool release_variant(int v) {
   return v == -1 || v == 0 || (v >= 1 && v <= 8) || v == 50 || v == 51 || v == 52 || v == 54 || v == 58 ||
          (v >= 60 && v <= 69) || v == 70 || v == 71 || v == 72 || v == 74 || v == 80 || v == 82 || v == 84 || v == 86 ||
-         v == 88 || v == 89 || v == 90 || v == 92;
+         v == 88 || v == 89 || v == 90 || (v >= 92 && v <= 97);
 }
 
 extern "C" int hiseg_conv2d_fwd_variant(const hiseg_conv2d_desc* d, int variant, hiseg_stream_t stream) {
@@ -352,7 +352,7 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
   if (variant == 90) {
     const int r = conv_pw_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
-  } else if (variant == 92) {
+  } else if (variant >= 92 && variant <= 97) {
     const int r = conv_hwr_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
   } else if (variant >= 80 && variant < 90) {
@@ -407,11 +407,12 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
       if (r != 0) return r < 0 ? r : HISEG_OK;
     }
     // 3x3 layers with weights also packed in MFMA fragment order (hiseg.ops.frag_pack) and 128-multiple Cout: the
-    // register-streamed-weight halo kernel (conv_hwr.hip, variant 92: one barrier per 32-channel slice;
-    // tools/conv_bench.py: 0.761 vs 0.793 ms (variant 86) on 256->256 @64x48 x256 ROIs, 0.894 vs 0.920 ms on
-    // 128->128 @128x96, 0.390 vs 0.415 ms on 128->256; bit-identical to variant 82)
+    // register-streamed-weight halo kernel (conv_hwr.hip: one barrier per 32-channel slice) in its B-reuse,
+    // MFMA-priority configuration (variant 97; tools/conv_bench.py, profiles/r3_conv_bench_hwr*.json: 0.732 vs
+    // 0.793 ms (variant 86) on 256->256 @64x48 x256 ROIs, 0.879 vs 0.930 ms on 128->128 @128x96, 0.364 vs 0.408 ms
+    // on 128->256; bit-identical to variant 86)
     if (v == 0 && !four_waves && halo && d->weight_frag != nullptr && d->Cout % 128 == 0) {
-      const int r = conv_hwr_try(a, s, 92);
+      const int r = conv_hwr_try(a, s, 97);
       if (r != 0) return r < 0 ? r : HISEG_OK;
     }
     if (v == 0 && !four_waves && halo) {

@@ -699,16 +699,33 @@ __device__ __forceinline__ int real_channel(const hiseg_pack_entry& e, int cp) {
 __global__ void __launch_bounds__(256) pack_weights_kernel(const hiseg_pack_entry* table) {
   const hiseg_pack_entry e = table[blockIdx.y];
   for (long long idx = (long long)blockIdx.x * 256 + threadIdx.x; idx < e.total; idx += (long long)gridDim.x * 256) {
-    const int row = (int)(idx / e.K_pad);
-    const int k = (int)(idx - (long long)row * e.K_pad);
-    float v = 0.f;
+    int row, k;
     const int cinp = e.ca + e.cb;
-    if (e.mode == 0) {            // conv forward: [co][tap*cinp + cp]
+    const int mode = e.mode & 7;
+    if (e.mode & HISEG_PACK_FRAG) {   // fragment order: idx = (((((ct*ncb + cb)*taps + tap)*2 + s)*4 + lg)*16 + r)*8 + el
+      const int kc = mode == 0 ? cinp : e.cop;   // K channels per tap
+      const int taps = e.KH * e.KW, ncb = kc >> 6;
+      long long t = idx;
+      const int el = (int)(t & 7); t >>= 3;
+      const int r = (int)(t & 15); t >>= 4;
+      const int lg = (int)(t & 3); t >>= 2;
+      const int s = (int)(t & 1); t >>= 1;
+      const int tap = (int)(t % taps); t /= taps;
+      const int cb = (int)(t % ncb);
+      const int ct = (int)(t / ncb);
+      row = ct * 16 + r;
+      k = tap * kc + cb * 64 + s * 32 + lg * 8 + el;
+    } else {
+      row = (int)(idx / e.K_pad);
+      k = (int)(idx - (long long)row * e.K_pad);
+    }
+    float v = 0.f;
+    if (mode == 0) {            // conv forward: [co][tap*cinp + cp]
       if (row < e.Cout && k < e.KH * e.KW * cinp) {
         const int tap = k / cinp, ci = real_channel(e, k - tap * cinp);
         if (ci >= 0) v = e.src[((long long)row * e.Cin_real + ci) * e.KH * e.KW + tap];
       }
-    } else if (e.mode == 1) {     // conv dgrad: [cp_in][tap'*cop + co], taps flipped
+    } else if (mode == 1) {       // conv dgrad: [cp_in][tap'*cop + co], taps flipped
       const int ci = row < cinp ? real_channel(e, row) : -1;
       if (ci >= 0 && k < e.KH * e.KW * e.cop) {
         const int tap2 = k / e.cop, co = k - tap2 * e.cop;
@@ -717,7 +734,7 @@ __global__ void __launch_bounds__(256) pack_weights_kernel(const hiseg_pack_entr
           v = e.src[(((long long)co * e.Cin_real + ci) * e.KH + ky) * e.KW + kx];
         }
       }
-    } else if (e.mode == 2) {     // convT forward: [q*C + co][ci], W [Cin][C][2][2]
+    } else if (mode == 2) {       // convT forward: [q*C + co][ci], W [Cin][C][2][2]
       if (row < 4 * e.Cout && k < e.Cin_real) {
         const int q = row / e.Cout, co = row - q * e.Cout;
         v = e.src[((long long)k * e.Cout + co) * 4 + q];

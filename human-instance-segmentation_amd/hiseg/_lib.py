@@ -83,6 +83,9 @@ class WgradMap(ctypes.Structure):
                                      "want_bias")]
 
 
+HISEG_PACK_FRAG = 8   # include/hiseg_train.h: pack mode flag, MFMA fragment order
+
+
 class PackEntry(ctypes.Structure):
     _fields_ = [("src", c_void_p), ("dst", c_void_p), ("dtype", c_int), ("mode", c_int),
                 ("Cout", c_int), ("Cin_real", c_int), ("KH", c_int), ("KW", c_int),

@@ -147,6 +147,8 @@ class TConv:
     ones: torch.Tensor
     shift: torch.Tensor  # bias or zeros (f32, padded to cout_pad)
     has_bias: bool
+    w_fwd_frag: Optional[torch.Tensor] = None    # MFMA fragment order (3x3 bf16, 64-multiple K channels): conv_hwr
+    w_dgrad_frag: Optional[torch.Tensor] = None
 
 
 class TrainState:
@@ -204,10 +206,19 @@ class TrainState:
         has_bias = conv.bias is not None
         p = TConv(conv, convT, kh, kw, stride, pad, ca, ca_r, cb, cb_r, cout, cols, cout_pad, k_pad, wf, wd, cop,
                   dg_cols, dg_cout_pad, dg_k, ones, shift, has_bias)
+        # second copies in MFMA fragment order for the register-streamed-weight 3x3 kernel (conv_hwr.hip): the
+        # forward when its K channels (ca + cb, each a 64 multiple) allow it, the data gradient when cop does
+        frag_ok = self.dtype == torch.bfloat16 and not convT and (kh, kw) == (3, 3)
+        jobs = [(2 if convT else 0, wf, cout_pad, k_pad), (3 if convT else 1, wd, dg_cout_pad, dg_k)]
+        if frag_ok and ca % 64 == 0 and cb % 64 == 0 and k_pad == 9 * (ca + cb):
+            p.w_fwd_frag = torch.empty_like(wf)
+            jobs.append((0 | L.HISEG_PACK_FRAG, p.w_fwd_frag, cout_pad, k_pad))
+        if frag_ok and cop % 64 == 0 and dg_k == 9 * cop:
+            p.w_dgrad_frag = torch.empty_like(wd)
+            jobs.append((1 | L.HISEG_PACK_FRAG, p.w_dgrad_frag, dg_cout_pad, dg_k))
         src = w.detach()
         assert src.dtype == torch.float32 and src.is_contiguous()
-        rows = 0
-        for mode, dst, rows, kp in ((2 if convT else 0, wf, cout_pad, k_pad), (3 if convT else 1, wd, dg_cout_pad, dg_k)):
+        for mode, dst, rows, kp in jobs:
             e = L.PackEntry()
             e.src, e.dst, e.dtype, e.mode = src.data_ptr(), dst.data_ptr(), hdtype(self.dtype), mode
             e.Cout, e.Cin_real, e.KH, e.KW = cout, (cin if convT else ca_r + cb_r), kh, kw
@@ -218,9 +229,9 @@ class TrainState:
         self.table = None
         self.convs[id(conv)] = p
         # pack the new layer now (later steps re-pack every layer in one launch at forward start)
-        raw = b"".join(bytes(e) for e in self.entries[-2:])
+        raw = b"".join(bytes(e) for e in self.entries[-len(jobs):])
         tab = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
-        _chk(L.lib().hiseg_pack_weights(tab.data_ptr(), 2, max(rows * 0 + cout_pad * k_pad, dg_cout_pad * dg_k),
+        _chk(L.lib().hiseg_pack_weights(tab.data_ptr(), len(jobs), max(r * kp for _, _, r, kp in jobs),
                                         _stream()), "pack_weights")
         self.cached.setdefault("keep_tables", []).append(tab)
         if has_bias:
@@ -324,6 +335,8 @@ def _desc(S: TrainState, p: TConv, xa: Act, xb: Optional[Act], out: Act, *, act=
     if xb is not None:
         d.srcB, d.b_cstride, d.b_coff, d.Cb = xb.ptr(), xb.cstride, xb.coff, p.cb
     d.weight, d.Cout, d.Cout_pad, d.K_pad = p.w_fwd.data_ptr(), p.gemm_cols, p.cout_pad, p.k_pad
+    if p.w_fwd_frag is not None:
+        d.weight_frag = p.w_fwd_frag.data_ptr()
     d.scale, d.shift = p.ones.data_ptr(), (shift if shift is not None else p.shift).data_ptr()
     d.act, d.act_beta = int(act), L.act_beta(act)
     if residual is not None:
@@ -400,6 +413,8 @@ def conv_bwd(T: Tape, p: TConv, d: L.Conv2dDesc, xa: Act, xb: Optional[Act], dz:
         dg.KH, dg.KW, dg.stride, dg.pad = p.kh, p.kw, 1, p.kh - 1 - p.pad
     dg.srcA, dg.a_cstride, dg.a_coff, dg.Ca, dg.a_up = dz.ptr(), dz.cstride, dz.coff, p.cop, 1
     dg.weight, dg.Cout, dg.Cout_pad, dg.K_pad = p.w_dgrad.data_ptr(), p.dg_cols, p.dg_cout_pad, p.dg_k_pad
+    if p.w_dgrad_frag is not None:
+        dg.weight_frag = p.w_dgrad_frag.data_ptr()
     zeros = S.cached.get(("zeros", p.dg_cout_pad))
     if zeros is None:
         zeros = torch.zeros(max(p.dg_cout_pad, 16), dtype=torch.float32, device=dz.t.device)

@@ -49,7 +49,11 @@ int hiseg_conv2d_wgrad_reduce(const float* ws, int splits, const hiseg_wgrad_map
  * (device memory) packs one f32 parameter in the reference layout into the implicit-GEMM
  * operand of the forward conv (mode 0: conv, 2: convT) or of its data-gradient conv
  * (mode 1: conv -> flipped taps, Cin/Cout swapped; mode 3: convT -> 2x2/s2 conv).
+ * mode | HISEG_PACK_FRAG (modes 0 and 1 of 3x3 layers whose K channel count is a multiple of 64): the same
+ * [rows][K_pad] matrix written in MFMA A-fragment order (hiseg.ops.frag_pack: [rows/16][K/64 channel blocks]
+ * [tap][2][64 lanes][8], the weight_frag operand of hiseg_conv2d_desc).
  * -------------------------------------------------------------------------------------- */
+#define HISEG_PACK_FRAG 8
 typedef struct hiseg_pack_entry {
   const float* src; void* dst; int dtype; int mode;
   int Cout, Cin_real, KH, KW;   /* reference dims (convT: Cin_real = in, Cout = out channels)  */

@@ -779,18 +779,22 @@ def test_conv_hwr_bit_identical_to_halo_kernel(name):
     assert p.weight_frag is not None
     R = ops.Act.from_nchw(torch.randn(N, Cout, H, W, device=DEV, generator=g), dt) if res else None
     y82 = ops.conv2d(p, xa, residual=R, variant=82).t.clone()
-    y92 = ops.conv2d(p, xa, residual=R, variant=92).t.clone()
+    y86 = ops.conv2d(p, xa, residual=R, variant=86).t.clone()
+    ys = {v: ops.conv2d(p, xa, residual=R, variant=v).t.clone() for v in (92, 93, 94, 95, 96, 97)}
     auto = ops.conv2d(p, xa, residual=R, variant=0).t.clone()
     torch.cuda.synchronize()
-    assert torch.isfinite(y92.float()).all()
-    assert torch.equal(y92, y82)
-    assert torch.equal(auto, y92)   # the automatic choice takes it
+    assert torch.isfinite(ys[92].float()).all()
+    for v in (92, 93, 94, 95):    # ky-major taps: variant 82's accumulation order
+        assert torch.equal(ys[v], y82), v
+    for v in (96, 97):            # kx-major taps with B reuse: variant 86's
+        assert torch.equal(ys[v], y86), v
+    assert torch.equal(auto, ys[97])   # the automatic choice takes variant 97
 
 
 @pytest.mark.parametrize("shape", [(2, 128, 128, 128, 32, 24, False), (3, 64, 64, 128, 21, 13, True),
                                    (2, 192, 64, 256, 9, 23, True)])
 def test_conv_hwr_two_source_bit_identical(shape):
-    """Variant 92 over a two-source concat (EnhancedUNet decoder up ++ skip): bit-identical to variant 82."""
+    """Variants 92 / 97 over a two-source concat (EnhancedUNet decoder up ++ skip): bit-identical to 82 / 86."""
     from hiseg import ops
     N, Ca, Cb, Cout, H, W, res = shape
     dt = torch.bfloat16
@@ -803,8 +807,11 @@ def test_conv_hwr_two_source_bit_identical(shape):
     R = ops.Act.from_nchw(torch.randn(N, Cout, H, W, device=DEV, generator=g), dt) if res else None
     y82 = ops.conv2d(p, xa, xb, residual=R, variant=82).t.clone()
     y92 = ops.conv2d(p, xa, xb, residual=R, variant=92).t.clone()
+    y86 = ops.conv2d(p, xa, xb, residual=R, variant=86).t.clone()
+    y97 = ops.conv2d(p, xa, xb, residual=R, variant=97).t.clone()
     torch.cuda.synchronize()
     assert torch.equal(y92, y82)
+    assert torch.equal(y97, y86)
 
 
 @pytest.mark.parametrize("variant", [86, 89])

@@ -725,7 +725,7 @@ def test_graphed_train_step_equals_eager():
     images = torch.from_numpy(filler.uniform(31, (2, 3, 96, 128))).to(DEV)
     rois = torch.from_numpy(filler.box_rois(32, 2, 2)).to(DEV)
     tgt = torch.from_numpy(filler.ellipse_targets(33, 4, 128, 96)).to(DEV)
-    runs, diag = [], []
+    runs, diag, gnorms = [], [], []
     for graphed in (False, True):
         torch.manual_seed(0)
         m = _model(torch.bfloat16, p_drop_zero=False).to(DEV).train()
@@ -751,6 +751,11 @@ def test_graphed_train_step_equals_eager():
         for _ in range(4):
             losses.append(float(run().detach()))
             norms.append((float(st["opt"].last_norm), st["opt"].step_count, st["opt"].skipped_steps))
+            if not np.isfinite(norms[-1][0]):   # name the parameters whose gradient is not finite
+                bad = [n for n, p in m.named_parameters() if p.grad is not None and not torch.isfinite(p.grad).all()]
+                norms.append(("non-finite grads", bad[:8], len(bad)))
+            if len(losses) == 1:   # per-parameter gradient norms of the first step (after clipping)
+                gnorms.append({n: float(p.grad.float().norm()) for n, p in m.named_parameters() if p.grad is not None})
         torch.cuda.synchronize()
         if graphed:
             assert run.captures == 1
@@ -759,7 +764,17 @@ def test_graphed_train_step_equals_eager():
         diag.append(norms)
     (l0, p0, m0, s0), (l1, p1, m1, s1) = runs
     # diag: per step (pre-clip gradient norm, applied steps, skipped steps) of the eager / graphed runs
-    assert l0 == l1, (l0, l1, diag)
+    if l0 != l1:
+        print("graphed-vs-eager diagnostics:", repr((l0, l1, diag)), flush=True)
+        ge, gg = gnorms
+        c0, c1 = diag[0][0][0], diag[1][0][0]   # pre-clip totals: compare unclipped per-parameter norms
+        s0, s1 = min(1.0, 1.0 / (c0 + 1e-6)), min(1.0, 1.0 / (c1 + 1e-6))
+        rows = sorted(((abs(ge[k] / s0 - gg[k] / s1) / (gg[k] / s1 + 1e-12), k, ge[k] / s0, gg[k] / s1) for k in gg),
+                      reverse=True)
+        print("first-step gradient norms, eager vs graphed (largest relative differences):", flush=True)
+        for r in rows[:25]:
+            print("   %.3e  %-70s %.6e %.6e" % r, flush=True)
+    assert l0 == l1, f"eager {l0} vs graphed {l1}; per step (grad norm, steps, skipped): {diag}"
     assert s0 == s1 == 4
     assert torch.equal(p0, p1) and torch.equal(m0, m1)
     assert l0[-1] != l0[0]
@@ -852,3 +867,23 @@ def test_side_stream_train_step_equals_default_stream():
         assert l == runs[0][0]
         assert s == runs[0][3] == 3
         assert torch.equal(p, runs[0][1]) and torch.equal(v, runs[0][2])
+
+
+@pytest.mark.parametrize("cin,cout,split", [(128, 256, None), (256, 128, None), (128, 128, (64, 64)), (64, 64, None)])
+def test_train_pack_fragment_order_matches_frag_pack(cin, cout, split):
+    """hiseg_pack_weights with HISEG_PACK_FRAG (the training path's weights for conv_hwr.hip): the forward and the
+    data-gradient matrices in MFMA fragment order equal hiseg.ops.frag_pack of the row-major packs, bit for bit."""
+    from hiseg import ops
+    from hiseg import train_engine as TE
+    torch.manual_seed(3)
+    m = nn.Sequential(nn.Conv2d(cin, cout, 3, padding=1)).to(DEV)
+    S = TE.TrainState(m, torch.bfloat16, torch.device(DEV))
+    p = S.conv(m[0], split=split)
+    torch.cuda.synchronize()
+    assert p.w_fwd_frag is not None
+    ref = ops.frag_pack(p.w_fwd.float(), 9, p.ca + p.cb).to(torch.bfloat16)
+    assert torch.equal(p.w_fwd_frag.reshape(-1), ref.reshape(-1))
+    if p.cop % 64 == 0:
+        assert p.w_dgrad_frag is not None
+        refd = ops.frag_pack(p.w_dgrad.float(), 9, p.cop).to(torch.bfloat16)
+        assert torch.equal(p.w_dgrad_frag.reshape(-1), refd.reshape(-1))
