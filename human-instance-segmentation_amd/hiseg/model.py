@@ -17,6 +17,7 @@ import torch.nn as nn
 
 from . import _lib as L
 from . import engine
+from . import export
 from .effunet import EfficientNetUnet
 from .layers import RefinedHierarchicalSegmentationHead, ResidualBlock, make_act_unet, make_norm
 
@@ -36,6 +37,8 @@ class DynamicRoIAlign(nn.Module):
         self.aligned = aligned
 
     def forward(self, input_feature_map: torch.Tensor, rois: torch.Tensor, output_height, output_width):
+        if export.tracing(input_feature_map, rois):
+            return export.traced_roi_align(self, input_feature_map, rois, output_height, output_width)
         return engine.roi_align_nchw(self, input_feature_map, rois, output_height, output_width)
 
 
@@ -71,6 +74,8 @@ class PreTrainedPeopleSegmentationUNet(nn.Module):
             self._freeze_bn = False
         self.register_buffer("norm_mean", torch.tensor(self.mean).view(1, 3, 1, 1))
         self.register_buffer("norm_std", torch.tensor(self.std).view(1, 3, 1, 1))
+        export.record_init(self, in_channels=in_channels, classes=classes, pretrained_weights_path="",
+                           mean=list(self.mean), std=list(self.std), encoder_name=encoder_name)
 
     def train(self, mode: bool = True):
         super().train(mode)
@@ -79,6 +84,8 @@ class PreTrainedPeopleSegmentationUNet(nn.Module):
         return self
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if export.tracing(x):
+            return export.traced_unet_logit(self, x)
         return engine.unet_logits_nchw(self, x)
 
 
@@ -119,6 +126,8 @@ class PreTrainedPeopleSegmentationUNetWrapper(nn.Module):
             self.output_conv.bias.data.zero_()
 
     def forward(self, x: torch.Tensor):
+        if export.tracing(x):
+            return export.traced_unet_wrapper(self, x), []
         return engine.unet_two_channel_nchw(self, x), []
 
 
@@ -170,11 +179,21 @@ class HierarchicalRGBSegmentationModelWithFullImagePretrainedUNet(nn.Module):
             hierarchical_depth=depth)
         # compute precision of the HIP path: f32 (parity with the reference) or bf16 (throughput)
         self.hiseg_dtype = torch.float32
+        export.record_init(self, roi_size=list(self.roi_size), mask_size=list(self.mask_size),
+                           pretrained_weights_path="", use_attention_module=use_attention_module,
+                           use_boundary_refinement=use_boundary_refinement,
+                           use_progressive_upsampling=use_progressive_upsampling, use_subpixel_conv=use_subpixel_conv,
+                           use_contour_detection=use_contour_detection,
+                           use_distance_transform=use_distance_transform, normalization_type=normalization_type,
+                           normalization_groups=normalization_groups, activation_function=activation_function,
+                           activation_beta=activation_beta, **kwargs)
 
     def forward(self, images: torch.Tensor, rois: torch.Tensor) -> Tuple[torch.Tensor, Dict[str, torch.Tensor]]:
         if self.training:  # train-mode BatchNorm / Dropout + hand-written backward (hiseg.train_engine)
             from . import train_engine
             return train_engine.train_forward(self, images, rois)
+        if export.tracing(images, rois):
+            return export.traced_rgb_model(self, images, rois, aux="full")
         return engine.rgb_model_forward(self, images, rois, aux="full")
 
     def infer(self, images: torch.Tensor, rois: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -204,6 +223,8 @@ class RGBHierarchicalExportWrapper(nn.Module):
         for m in (self.model.roi_align_mask, self.model.roi_align_rgb):
             m.spatial_scale = (H, W)
             m.spatial_scale_h, m.spatial_scale_w = H, W
+        if export.tracing(images, rois):
+            return export.traced_export(self, images, rois)
         return engine.export_forward(self.model, images, rois, self.dilation_pixels)
 
 
