@@ -236,17 +236,12 @@ static int launch_typed(const ConvArgs& a, hipStream_t s) {
 
 namespace hiseg {
 int conv_fast_try(const ConvArgs& a, hipStream_t s, int variant);
-#ifdef HISEG_DIAG
-int conv_halo_try(const ConvArgs& a, hipStream_t s, int variant);
-int conv_halo2_try(const ConvArgs& a, hipStream_t s, int variant);
-int conv_halo3_try(const ConvArgs& a, hipStream_t s, int variant);
-int conv_8ph_try(const ConvArgs& a, hipStream_t s, int variant);
-#endif
 int conv_wide_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_hw_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_pw_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_hwr_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_small_try(const ConvArgs& a, hipStream_t s, int variant);
+int conv_rows_try(const ConvArgs& a, hipStream_t s, int variant);
 }
 
 using namespace hiseg;
@@ -264,7 +259,7 @@ extern "C" int hiseg_conv2d_fwd(const hiseg_conv2d_desc* d, hiseg_stream_t strea
 static bool release_variant(int v) {
   return v == -1 || v == 0 || (v >= 1 && v <= 8) || v == 50 || v == 51 || v == 52 || v == 54 || v == 58 ||
          (v >= 60 && v <= 69) || v == 70 || v == 71 || v == 72 || v == 74 || v == 80 || v == 82 || v == 84 || v == 86 ||
-         v == 88 || v == 89 || v == 90 || (v >= 92 && v <= 97);
+         v == 88 || v == 89 || v == 90 || (v >= 92 && v <= 98);
 }
 
 extern "C" int hiseg_conv2d_fwd_variant(const hiseg_conv2d_desc* d, int variant, hiseg_stream_t stream) {
@@ -348,8 +343,10 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
   hipStream_t s = (hipStream_t)stream;
   // Automatic choice (variant 0) = the fastest measured configuration per layer class
   // (tools/conv_bench.py): LDS-DMA ring kernel, 128x128 tiles for Cout >= 128, 64x128 for 64.
-  // Experimental kernels (halo / halo2 / halo3) run only when forced by variant.
-  if (variant == 90) {
+  if (variant == 98) {
+    const int r = conv_rows_try(a, s, variant);
+    if (r != 0) return r < 0 ? r : HISEG_OK;
+  } else if (variant == 90) {
     const int r = conv_pw_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
   } else if (variant >= 92 && variant <= 97) {
@@ -367,20 +364,6 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
   } else if (variant >= 50) {
     const int r = conv_small_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
-#ifdef HISEG_DIAG
-  } else if (variant >= 40) {
-    const int r = conv_8ph_try(a, s, variant);
-    if (r != 0) return r < 0 ? r : HISEG_OK;
-  } else if (variant >= 30) {
-    const int r = conv_halo3_try(a, s, variant);
-    if (r != 0) return r < 0 ? r : HISEG_OK;
-  } else if (variant >= 20) {
-    const int r = conv_halo2_try(a, s, variant);
-    if (r != 0) return r < 0 ? r : HISEG_OK;
-  } else if (variant >= 10 && variant != 18 && variant != 19) {
-    const int r = conv_halo_try(a, s, variant);
-    if (r != 0) return r < 0 ? r : HISEG_OK;
-#endif
   } else if (variant >= 0) {
     int v = variant;
     // 61 = 128x128 ring, 8 waves as 4 (Cout) x 2 (pixel) with 32x64 wave tiles, LDS full-row epilogue;
@@ -404,6 +387,13 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
     // combiner, 0.16 vs 0.24 ms on 128->256; bit-identical)
     if (v == 0 && d->KH == 1 && d->KW == 1) {
       const int r = conv_pw_try(a, s, 90);
+      if (r != 0) return r < 0 ? r : HISEG_OK;
+    }
+    // narrow 3x3 layers (16 / 32 output channels: the full-image UNet's last decoder blocks and head): the
+    // row-streaming kernel (conv_rows.hip, variant 98: weights in registers, input rows streamed through an LDS
+    // ring; bit-identical to conv_small)
+    if (v == 0 && d->KH == 3 && d->KW == 3 && d->Cout_pad <= 32) {
+      const int r = conv_rows_try(a, s, 98);
       if (r != 0) return r < 0 ? r : HISEG_OK;
     }
     // 3x3 layers with weights also packed in MFMA fragment order (hiseg.ops.frag_pack) and 128-multiple Cout: the

@@ -278,6 +278,43 @@ def test_conv_small_kernel_bit_identical(name):
             assert torch.equal(y2, ref2), f"variant {v} out2 differs"
 
 
+# The full-image UNet's narrow decoder layers on the row-streaming kernel (conv_rows.hip, variant 98 and the
+# automatic choice) vs the generic kernel, bit for bit: smp DecoderBlock conv1 over up(x) ++ skip (B0/B1 stem
+# skip 32, B7 64), conv2, the last block's 32 -> 16 / 16 -> 16 and the 16 -> 1 f32 segmentation head; heights
+# spanning several workgroups' row runs (segments crossing strips and images), ragged strip widths.
+# name: (N, Ca, Cb, Cout, H, W, a_up, f32 out)
+ROWS_CASES = {
+    "up2_64+32_to_32": (2, 64, 32, 32, 96, 200, 2, False),
+    "up2_64+64_to_32_b7": (2, 64, 64, 32, 50, 70, 2, False),
+    "32_to_32": (3, 32, 0, 32, 61, 130, 1, False),
+    "up2_32_to_16": (2, 32, 0, 16, 90, 300, 2, False),
+    "16_to_16": (2, 16, 0, 16, 77, 260, 1, False),
+    "16_to_1_f32": (2, 16, 0, 1, 64, 150, 1, True),
+    "16_to_16_tiny": (1, 16, 0, 16, 3, 5, 1, False),
+}
+
+
+@pytest.mark.parametrize("name", list(ROWS_CASES))
+def test_conv_rows_bit_identical(name):
+    from hiseg import ops
+    N, Ca, Cb, Cout, H, W, up, f32o = ROWS_CASES[name]
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(19)
+    xa = ops.Act.from_nchw(torch.randn(N, Ca, H // up, W // up, device=DEV, generator=g), dt)
+    xb = ops.Act.from_nchw(torch.randn(N, Cb, H, W, device=DEV, generator=g), dt) if Cb else None
+    w = torch.randn(Cout, Ca + Cb, 3, 3, device=DEV, generator=g) / ((Ca + Cb) * 9) ** 0.5
+    p = ops.pack_conv(w, torch.randn(Cout, device=DEV, generator=g) * 0.1, None, 0 if f32o else 1, dt, DEV, pad=1,
+                      split=(Ca, Cb) if Cb else None)
+    outs = {}
+    for v in (-1, 50, 98, 0):
+        y = ops.conv2d(p, xa, xb, a_up=up, out_dtype=torch.float32 if f32o else None, variant=v)
+        torch.cuda.synchronize()
+        outs[v] = y.t.clone()
+    assert torch.isfinite(outs[-1].float()).all()
+    for v in (50, 98, 0):
+        assert torch.equal(outs[v], outs[-1]), f"variant {v} differs from the generic kernel"
+
+
 @pytest.mark.parametrize("shape", [(2, 3, 32, 20, 150), (3, 16, 24, 9, 70), (1, 8, 64, 33, 17)])
 def test_conv_small_stride2_bit_identical(shape):
     """The EfficientNet stem form (3x3 / stride 2 / pad 1, timm conv_stem + bn1 + SiLU) on the halo-tiled

@@ -39,6 +39,7 @@ SHAPES = {
     # smp decoder blocks 3/4 (nearest-x2 upsampled src A + skip), B0 at 480x640
     "dec3_up64+32to32_3x3_240x320": (32, 64, 32, 32, 240, 320, 3, False, 2),
     "dec4_up32to16_3x3_480x640": (32, 32, 0, 16, 480, 640, 3, False, 2),
+    "dec3_b7_up64+64to32_3x3_240x320": (8, 64, 64, 32, 240, 320, 3, False, 2),
 }
 
 
@@ -101,6 +102,8 @@ def main():
         shape = SHAPES[name]
         N, Ca, Cb, Cout, H, W, k, res = shape[:8]
         flops = 2.0 * N * H * W * Cout * k * k * (Ca + Cb)
+        up = shape[8] if len(shape) > 8 else 1
+        nbytes = 2.0 * N * (H * W // (up * up) * Ca + H * W * Cb + H * W * Cout * (2 if res else 1))
         p, xa, xb, r, out = make(shape, torch.bfloat16)
         d = desc(p, xa, xb, r, out)
         run(d, -1)
@@ -136,7 +139,8 @@ def main():
         row = {}
         for v in variants:
             ms = min(times[v])
-            row[str(v)] = {"ms": round(ms, 4), "tflops": round(flops / ms / 1e9, 1), "rel_err_vs_generic": ok[v]}
+            row[str(v)] = {"ms": round(ms, 4), "tflops": round(flops / ms / 1e9, 1),
+                           "alg_gbs": round(nbytes / ms / 1e6, 1), "rel_err_vs_generic": ok[v]}
             if v in same:
                 row[str(v)]["bit_equal_ref"] = same[v]
         results[name] = row

@@ -11,6 +11,7 @@ Derivations (MI355X_MICROARCH.md §rocprofv3 PMC slots, §Per-instruction cycle 
                  (s_waitcnt, barrier)
   lds_conflict = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
 Usage: python tools/sq_derive.py gpurun_out/<dir>/pmc_counter_collection.csv [kernel-substring] [--json out.json]
+       (or the rocpd SQLite database rocprofv3 writes by default: gpurun_out/<dir>/<name>_results.db)
 """
 import collections
 import csv
@@ -25,7 +26,14 @@ def main():
         args.remove(out_json)
     path = args[0]
     sub = args[1] if len(args) > 1 else "hiseg"
-    rows = list(csv.DictReader(open(path)))
+    if path.endswith(".db"):
+        import sqlite3
+        cur = sqlite3.connect(path).cursor()
+        cur.execute("select dispatch_id, kernel_name, counter_name, value, start, end from counters_collection")
+        rows = [{"Dispatch_Id": str(r[0]), "Kernel_Name": r[1], "Counter_Name": r[2], "Counter_Value": r[3],
+                 "Start_Timestamp": r[4], "End_Timestamp": r[5]} for r in cur.fetchall()]
+    else:
+        rows = list(csv.DictReader(open(path)))
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     dur = {}
     name = {}
