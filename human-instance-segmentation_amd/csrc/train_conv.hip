@@ -720,7 +720,9 @@ __global__ void __launch_bounds__(256) pack_weights_kernel(const hiseg_pack_entr
       k = (int)(idx - (long long)row * e.K_pad);
     }
     float v = 0.f;
-    if (mode == 0) {            // conv forward: [co][tap*cinp + cp]
+    if (mode == HISEG_PACK_BIAS) {  // bias -> f32 epilogue shift, replicated per ConvTranspose sub-pixel block
+      v = e.src[idx % e.Cout];
+    } else if (mode == 0) {     // conv forward: [co][tap*cinp + cp]
       if (row < e.Cout && k < e.KH * e.KW * cinp) {
         const int tap = k / cinp, ci = real_channel(e, k - tap * cinp);
         if (ci >= 0) v = e.src[((long long)row * e.Cin_real + ci) * e.KH * e.KW + tap];

@@ -84,6 +84,7 @@ class WgradMap(ctypes.Structure):
 
 
 HISEG_PACK_FRAG = 8   # include/hiseg_train.h: pack mode flag, MFMA fragment order
+HISEG_PACK_BIAS = 4   # pack mode: conv bias -> f32 epilogue shift
 
 
 class PackEntry(ctypes.Structure):

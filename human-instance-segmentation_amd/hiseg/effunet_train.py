@@ -108,7 +108,7 @@ def se_train(T: TE.Tape, se: nn.Module, h: Act) -> Act:
                                    gate.data_ptr(), out.ptr(), TE._stream()), "se_train_fwd")
 
     def back():
-        gout, _ = T.grad(out)
+        gout = T.grad_in(out)
         gh, acc = T.grad(h)
         target = gh if not acc else Act.new(h.N, h.H, h.W, C, h.dtype, dev, zero=False)
         ws2 = torch.empty_like(ws)
@@ -219,9 +219,14 @@ def up_conv_bn_relu(T: TE.Tape, conv: nn.Conv2d, bn: nn.BatchNorm2d, x_low: Act,
                     "upsample2x_bwd")
             T.mark(x_low)
         if skip_dx:
-            gs, _ = T.grad(skip)        # zero-initialised when new: add covers both cases
-            TE._chk(lib.hiseg_add_inplace(hdtype(dz.dtype), skip.N * H * W, skip.C, TE.ew(gs),
-                                          TE.ew(full.slice(p.ca, skip.C)), TE._stream()), "add")
+            gs, acc_s = T.grad(skip)
+            if acc_s:
+                TE._chk(lib.hiseg_add_inplace(hdtype(dz.dtype), skip.N * H * W, skip.C, TE.ew(gs),
+                                              TE.ew(full.slice(p.ca, skip.C)), TE._stream()), "add")
+            else:       # first contribution: copy
+                part = TE.ew(full.slice(p.ca, skip.C))
+                TE._chk(lib.hiseg_act_bwd_pre(hdtype(dz.dtype), skip.N * H * W, skip.C, part, part, ACT_NONE, 1.0,
+                                              TE.ew(gs), 0, TE._stream()), "copy")
             T.mark(skip)
         T.keep.extend([ones, zeros, full])
     T.push(back)

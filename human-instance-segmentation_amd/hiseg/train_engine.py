@@ -109,6 +109,10 @@ class FlatParams:
     def prepare_backward(self):
         """Gradient-accumulation semantics of autograd: parameters whose .grad is None (zero_grad
         set_to_none) start from zero; an existing .grad elsewhere is copied into the flat buffer."""
+        if all(p.grad is None for _, p in self.named):   # (zero_grad(set_to_none)): one fill, not one per tensor
+            self.grad.zero_()
+            self.attach_grads()
+            return
         for _, p in self.named:
             g = p.grad
             view = self.grad_view(p)
@@ -218,9 +222,13 @@ class TrainState:
             jobs.append((1 | L.HISEG_PACK_FRAG, p.w_dgrad_frag, dg_cout_pad, dg_k))
         src = w.detach()
         assert src.dtype == torch.float32 and src.is_contiguous()
+        if has_bias:   # the bias into the epilogue shift (ConvTranspose: once per sub-pixel column block)
+            jobs.append((L.HISEG_PACK_BIAS, shift, 1, 4 * cout if convT else cout))
         for mode, dst, rows, kp in jobs:
             e = L.PackEntry()
-            e.src, e.dst, e.dtype, e.mode = src.data_ptr(), dst.data_ptr(), hdtype(self.dtype), mode
+            bias = mode == L.HISEG_PACK_BIAS
+            e.src = conv.bias.detach().data_ptr() if bias else src.data_ptr()
+            e.dst, e.dtype, e.mode = dst.data_ptr(), (L.HISEG_F32 if bias else hdtype(self.dtype)), mode
             e.Cout, e.Cin_real, e.KH, e.KW = cout, (cin if convT else ca_r + cb_r), kh, kw
             e.ca, e.ca_real, e.cb, e.cb_real = ca, ca_r, cb, cb_r
             e.rows, e.K_pad, e.cop, e.total = rows, kp, cop, rows * kp
@@ -234,12 +242,11 @@ class TrainState:
         _chk(L.lib().hiseg_pack_weights(tab.data_ptr(), len(jobs), max(r * kp for _, _, r, kp in jobs),
                                         _stream()), "pack_weights")
         self.cached.setdefault("keep_tables", []).append(tab)
-        if has_bias:
-            _copy_bias(shift, conv.bias.detach(), cout, convT)
         return p
 
     def pack(self):
-        """One launch re-packs every conv's forward and dgrad weights from the current parameters."""
+        """One launch re-packs every conv's forward and dgrad weights and epilogue biases from the current
+        parameters."""
         if not self.entries:
             return
         if self.table is None:
@@ -247,9 +254,6 @@ class TrainState:
             self.table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
         _chk(L.lib().hiseg_pack_weights(self.table.data_ptr(), len(self.entries), self.max_total, _stream()),
              "pack_weights")
-        for p in self.convs.values():
-            if p.has_bias:  # bias into the epilogue shift (ConvTranspose: one bias per output channel, 4 columns)
-                _copy_bias(p.shift, p.conv.bias.detach(), p.cout, p.convT)
 
     def grad(self, p: nn.Parameter) -> torch.Tensor:
         """Gradient slice of p; during a backward also tells the gradient exchange which tape op writes it."""
@@ -268,13 +272,6 @@ class TrainState:
         return self.seed_offset
 
 
-def _copy_bias(shift: torch.Tensor, b: torch.Tensor, n: int, convT: bool):
-    if convT:
-        shift[:4 * n].view(4, n).copy_(b.view(1, n).expand(4, n))
-    else:
-        shift[:n].copy_(b)
-
-
 # ======================================================================================= tape
 class Tape:
     """Backward closures in forward order + the gradient buffers of the recorded activations."""
@@ -291,13 +288,29 @@ class Tape:
         self.ops.append(fn)
 
     def grad(self, a: Act) -> Tuple[Act, bool]:
-        """(gradient buffer of a, whether it already holds a contribution)."""
+        """(gradient buffer of a, whether it already holds a contribution) -- for a backward that WRITES a's
+        gradient: with the flag False it must overwrite every channel < a.C (pad channels are zero-filled
+        here; the rest is not: the zero-fills were ~2 % of the train step)."""
         g = self.grads.get(id(a))
-        if g is None:  # zero-filled: contributions are added, pad channels stay zero
-            g = Act.new(a.N, a.H, a.W, a.C, a.dtype, a.t.device, cpad=a.cstride, zero=True)
+        if g is None:
+            g = Act.new(a.N, a.H, a.W, a.C, a.dtype, a.t.device, cpad=a.cstride)
             self.grads[id(a)] = g
             self.keep.append(a)
         return g, self.written.get(id(a), False)
+
+    def grad_in(self, a: Act) -> Act:
+        """The gradient of a for a backward that READS it (a is that op's output): zeros if nothing wrote it."""
+        g = self.grads.get(id(a))
+        if g is not None and self.written.get(id(a), False):
+            return g
+        if g is None:
+            g = Act.new(a.N, a.H, a.W, a.C, a.dtype, a.t.device, cpad=a.cstride, zero=True)
+            self.grads[id(a)] = g
+            self.keep.append(a)
+        else:
+            g.t.zero_()
+        self.written[id(a)] = True
+        return g
 
     def mark(self, a: Act):
         self.written[id(a)] = True
@@ -437,7 +450,11 @@ def conv_bwd(T: Tape, p: TConv, d: L.Conv2dDesc, xa: Act, xb: Optional[Act], dz:
             g, acc = T.grad(src_act)
             part = tmp.slice(off, c)
             P = src_act.N * src_act.H * src_act.W
-            _chk(lib.hiseg_add_inplace(hdtype(dz.dtype), P, src_act.C, ew(g), ew(part), _stream()), "add")
+            if acc:
+                _chk(lib.hiseg_add_inplace(hdtype(dz.dtype), P, src_act.C, ew(g), ew(part), _stream()), "add")
+            else:       # first contribution: copy
+                _chk(lib.hiseg_act_bwd_pre(hdtype(dz.dtype), P, src_act.C, ew(part), ew(part), ACT_NONE, 1.0, ew(g), 0,
+                                           _stream()), "copy")
             T.mark(src_act)
 
 
@@ -493,7 +510,7 @@ def ln_forward(T: Tape, ln: LayerNorm2d, z: Act, *, act: int, residual: Optional
 def ln_backward(T: Tape, ln: LayerNorm2d, z: Act, y: Act, st: LNState, dz: Act, *, act: int,
                 residual: Optional[Act] = None, drop=None, conv_bias: Optional[torch.Tensor] = None):
     lib, S = L.lib(), T.S
-    gy, _ = T.grad(y)
+    gy = T.grad_in(y)
     d = L.LnBwdDesc()
     d.dtype, d.N, d.HW, d.C = hdtype(z.dtype), z.N, z.H * z.W, z.C
     d.dy, d.dy_cstride, d.dy_coff = gy.ptr(), gy.cstride, gy.coff
@@ -557,7 +574,7 @@ def bn_backward(T: Tape, bn: nn.BatchNorm2d, z: Act, y: Act, st: BNState, dz: Ac
     if isinstance(bn, LayerNorm2d):
         return ln_backward(T, bn, z, y, st, dz, act=act, residual=residual, drop=drop, conv_bias=conv_bias)
     lib, S = L.lib(), T.S
-    gy, _ = T.grad(y)
+    gy = T.grad_in(y)
     C = z.C
     P = z.N * z.H * z.W
     part = torch.empty((lib.hiseg_bn_partials() + 1) * 3 * C, dtype=torch.float32, device=z.t.device)
@@ -621,7 +638,7 @@ def conv_plain(T: Tape, conv: nn.Conv2d, act: int, x: Act, xb: Optional[Act] = N
 
     def back():
         lib = L.lib()
-        gy, _ = T.grad(y)
+        gy = T.grad_in(y)
         P = y.N * y.H * y.W
         if y.dtype != S.dtype or act == ACT_SIGMOID or y.cstride % chunk_elems(S.dtype):
             # f32 / narrow heads: convert (and apply the activation derivative) into a padded compute-dtype buffer
@@ -656,7 +673,7 @@ def _conv_smooth_act(T: Tape, p: TConv, act: int, x: Act, xb: Optional[Act]) -> 
     T.keep.extend([one, zero])
 
     def back():
-        gy, _ = T.grad(y)
+        gy = T.grad_in(y)
         dz = Act.new(z.N, z.H, z.W, z.C, z.dtype, z.t.device, cpad=z.cstride, zero=z.cstride != z.C)
         _chk(lib.hiseg_act_bwd_pre(hdtype(z.dtype), z.N * z.H * z.W, z.C, ew(gy), ew(z), int(act), L.act_beta(act),
                                    ew(dz), 0, _stream()), "act_bwd_pre")
@@ -704,7 +721,7 @@ def maxpool(T: Tape, x: Act) -> Act:
     y = ops.maxpool2x2(x)
 
     def back():
-        gy, _ = T.grad(y)
+        gy = T.grad_in(y)
         gx, acc = T.grad(x)
         _chk(L.lib().hiseg_maxpool2x2_bwd(hdtype(x.dtype), x.ptr(), x.N, x.H, x.W, x.cstride, gy.ptr(), gx.ptr(),
                                           int(acc), _stream()), "maxpool_bwd")
@@ -721,7 +738,7 @@ def gate(T: Tape, a: Act, g: Act) -> Act:
     _chk(lib.hiseg_gate_fwd(hdtype(a.dtype), P, a.C, ew(a), ew(g), ew(out), _stream()), "gate_fwd")
 
     def back():
-        gy, _ = T.grad(out)
+        gy = T.grad_in(out)
         ga, acc = T.grad(a)
         gg, accg = T.grad(g)
         assert not accg, "sigmoid gate consumed twice"
@@ -745,7 +762,7 @@ def conv_sigmoid_gate(T: Tape, conv: nn.Conv2d, x: Act) -> Act:
     y, d = conv_fwd(S, p, x, act=ACT_SIGMOID)
 
     def back():
-        dz, _ = T.grad(y)  # gate_bwd wrote dy * a * g * (1-g) = dL/dz here
+        dz = T.grad_in(y)  # gate_bwd wrote dy * a * g * (1-g) = dL/dz here
         conv_bwd(T, p, d, x, None, dz)
     T.push(back)
     return y
@@ -824,7 +841,7 @@ def spatial_attention(T: Tape, m: nn.Module, x: Act, drop) -> Act:
          "attn_spatial_train_fwd")
 
     def back():
-        gy, _ = T.grad(out)
+        gy = T.grad_in(out)
         gx, acc = T.grad(x)
         ws = torch.empty(lib.hiseg_attn_spatial_ws(x.N, x.H, x.W, k), dtype=torch.float32, device=dev)
         target = gx if not acc else Act.new(x.N, x.H, x.W, x.C, x.dtype, dev, zero=False)
@@ -855,7 +872,7 @@ def channel_attention(T: Tape, m: nn.Module, x: Act, drop) -> Act:
                                           out.ptr(), _stream()), "attn_channel_train_fwd")
 
     def back():
-        gy, _ = T.grad(out)
+        gy = T.grad_in(out)
         gx, acc = T.grad(x)
         target = gx if not acc else Act.new(x.N, x.H, x.W, C, x.dtype, dev, zero=False)
         _chk(lib.hiseg_attn_channel_bwd(hdtype(x.dtype), x.ptr(), x.N, HW, C, w1.data_ptr(), Cr, w2.data_ptr(),
@@ -887,7 +904,7 @@ def _dropout_after(T: Tape, m: nn.Module, y: Act) -> Act:
     T.keep.extend([one, zero])
 
     def back():
-        gy, _ = T.grad(out)
+        gy = T.grad_in(out)
         gx, acc = T.grad(y)
         assert not acc
         d2 = L.BnApplyDesc.from_buffer_copy(d)

@@ -54,6 +54,9 @@ int hiseg_conv2d_wgrad_reduce(const float* ws, int splits, const hiseg_wgrad_map
  * [tap][2][64 lanes][8], the weight_frag operand of hiseg_conv2d_desc).
  * -------------------------------------------------------------------------------------- */
 #define HISEG_PACK_FRAG 8
+/* mode HISEG_PACK_BIAS: dst (f32, total entries) [i] = src[i % Cout] -- a conv bias into its epilogue shift
+ * (ConvTranspose: total = 4 * Cout, one copy per sub-pixel column block); rows = 1, K_pad = total. */
+#define HISEG_PACK_BIAS 4
 typedef struct hiseg_pack_entry {
   const float* src; void* dst; int dtype; int mode;
   int Cout, Cin_real, KH, KW;   /* reference dims (convT: Cin_real = in, Cout = out channels)  */
