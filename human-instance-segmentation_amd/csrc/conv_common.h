@@ -13,6 +13,9 @@ struct ConvArgs {
   int Cin;     // Ca + Cb
   int nK;      // K blocks
   int Hs, Ws;  // src-A grid
+  int kper;    // split-K: K blocks per split (grid.z = splits); nK when unsplit
+  int ins_vec; // in_scale rows 16-B aligned (vector gate loads)
+  float* ws;   // split-K workspace [splits][M][Cout_pad] f32
 };
 
 template <typename T>

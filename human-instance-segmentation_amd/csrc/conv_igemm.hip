@@ -23,7 +23,12 @@
 
 namespace hiseg {
 
-template <typename T, typename TO, int BCO, int BPX, int WCO, int WPX>
+// SPLIT: split-K (grid.z = splits, a.kper K blocks each) for small grids with long K loops -- the SE-gated
+// EfficientNet projections at the deep stages (B7: 2304 -> 384 over 4 x 20 x 20 pixels = 39 tiles of 128 x 128
+// for 36 K blocks: one global round trip per K block on one workgroup per CU).  Each split stores its raw f32
+// tile to the caller's workspace [split][M][Cout_pad]; conv_splitk_reduce_kernel sums the splits in order and
+// applies the epilogue (deterministic; within f32 re-association of the unsplit kernel).
+template <typename T, typename TO, int BCO, int BPX, int WCO, int WPX, bool SPLIT = false>
 __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
   constexpr int KCH = Chunk<T>::N;
   constexpr int BK = 8 * KCH;
@@ -66,10 +71,13 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
       rn[i] = -1; riy[i] = 0; rix[i] = 0;
     }
   }
+  // K range of this workgroup (split-K: blocks [kb0, kb1))
+  const int kb0 = SPLIT ? (int)blockIdx.z * a.kper : 0;
+  const int kb1 = SPLIT ? (kb0 + a.kper < a.nK ? kb0 + a.kper : a.nK) : a.nK;
   // K state of this thread's chunk: k = kb*BK + c*KCH  ->  (ky, kx, ci)
   int ci, ky, kx;
   {
-    const int k = c * KCH;
+    const int k = kb0 * BK + c * KCH;
     const int tap = k / a.Cin;
     ci = k - tap * a.Cin;
     ky = tap / d.KW;
@@ -82,11 +90,19 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
   for (int i = 0; i < W_CH; ++i) rw[i] = make_uint4(0u, 0u, 0u, 0u);
 
+  // SE gate (in_scale) of the gathered chunks: loaded beside the activations, applied when the chunk is stored to
+  // LDS (after the current K block's MFMAs), so the loads' latency overlaps the MFMAs instead of stalling the
+  // gather -- the gate multiply once made every K block of the deep EfficientNet projections wait for its loads
+  // (1.5 us of 3.2 us per block, tools/splitk_bench.py with HISEG_SPLITK sweeps)
+  constexpr int GREG = sizeof(T) == 2 ? 2 : 1;   // float4 gate vectors per chunk
+  float4 rg[A_CH][GREG];
+  bool rgs[A_CH];
   auto gather = [&](int kb) __attribute__((always_inline)) {
     const bool kvalid = ky < d.KH;
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      rgs[i] = false;
       if (rn[i] >= 0 && kvalid) {
         const int iy = riy[i] + ky, ix = rix[i] + kx;
         if (iy >= 0 && iy < d.H && ix >= 0 && ix < d.W) {
@@ -96,12 +112,15 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
             const long long off = (((long long)rn[i] * a.Hs + sy) * a.Ws + sx) * d.a_cstride + d.a_coff + ci;
             v = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(d.srcA) + off);
             if (d.in_scale) {
-              float f[KCH];
-              Chunk<T>::unpack(v, f);
               const float* s = d.in_scale + (long long)rn[i] * d.Ca + ci;
+              rgs[i] = true;
+              if (a.ins_vec) {   // 16-B aligned gate rows: vector loads
 #pragma unroll
-              for (int e = 0; e < KCH; ++e) f[e] *= s[e];
-              v = Chunk<T>::pack(f);
+                for (int e = 0; e < GREG; ++e) rg[i][e] = *reinterpret_cast<const float4*>(s + 4 * e);
+              } else {
+#pragma unroll
+                for (int e = 0; e < GREG; ++e) rg[i][e] = make_float4(s[4 * e], s[4 * e + 1], s[4 * e + 2], s[4 * e + 3]);
+              }
             }
           } else {
             const long long off = (((long long)rn[i] * d.H + iy) * d.W + ix) * d.b_cstride + d.b_coff + (ci - d.Ca);
@@ -140,7 +159,17 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int r = (t >> 3) + 32 * i;
-      if (A_FULL || r < BPX) sm[BCO * 8 + swz(r, c)] = ra[i];
+      uint4 v = ra[i];
+      if (d.in_scale && rgs[i]) {   // the loader's rounding: bf16(x * gate) (f32: exact product)
+        float f[KCH];
+        Chunk<T>::unpack(v, f);
+#pragma unroll
+        for (int e = 0; e < GREG; ++e) {
+          f[4 * e] *= rg[i][e].x; f[4 * e + 1] *= rg[i][e].y; f[4 * e + 2] *= rg[i][e].z; f[4 * e + 3] *= rg[i][e].w;
+        }
+        v = Chunk<T>::pack(f);
+      }
+      if (A_FULL || r < BPX) sm[BCO * 8 + swz(r, c)] = v;
     }
   };
 
@@ -150,14 +179,13 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  gather(0);
+  gather(kb0);
   stage_store(0);
   __syncthreads();
 
-  const int nK = a.nK;
-  for (int kb = 0; kb < nK; ++kb) {
-    const int cur = kb & 1;
-    if (kb + 1 < nK) {
+  for (int kb = kb0; kb < kb1; ++kb) {
+    const int cur = (kb - kb0) & 1;
+    if (kb + 1 < kb1) {
       advance();
       gather(kb + 1);
     }
@@ -188,7 +216,7 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
         }
       }
     }
-    if (kb + 1 < nK) stage_store(cur ^ 1);
+    if (kb + 1 < kb1) stage_store(cur ^ 1);
     __syncthreads();
   }
 
@@ -198,6 +226,16 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
   for (int j = 0; j < TN; ++j) epx[j] = px0 + wpx * TN * 16 + j * 16 + (lane & 15);
 #pragma unroll
   for (int i = 0; i < TM; ++i) eco[i] = co0 + wco * TM * 16 + i * 16 + (lane >> 4) * 4;
+  if constexpr (SPLIT) {
+    float* ws = a.ws + (long long)blockIdx.z * a.M * d.Cout_pad;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        if (epx[j] < a.M && eco[i] < d.Cout_pad)
+          *reinterpret_cast<floatx4*>(ws + (long long)epx[j] * d.Cout_pad + eco[i]) = acc[i][j];
+    return;
+  }
   if (TileEpi<T, TO, TM, TN>::ok(d)) {
     TileEpi<T, TO, TM, TN> ep;
     ep.prefetch(d, a.M, epx, eco);
@@ -213,23 +251,100 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
   }
 }
 
+// Split-K reduction: one thread per (pixel, 4-column quad); the splits are summed in order 0..S-1, then the
+// conv epilogue (scale / shift, residual, activation, mul, dual store) of the unsplit kernel.
+template <typename T, typename TO>
+__global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvArgs a, int splits) {
+  const hiseg_conv2d_desc& d = a.d;
+  const int nq = d.Cout_pad >> 2;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)a.M * nq) return;
+  const int px = (int)(i / nq), co = (int)(i - (long long)px * nq) * 4;
+  const long long plane = (long long)a.M * d.Cout_pad;
+  const float* p = a.ws + (long long)px * d.Cout_pad + co;
+  floatx4 acc = *reinterpret_cast<const floatx4*>(p);
+  for (int z = 1; z < splits; ++z) acc += *reinterpret_cast<const floatx4*>(p + z * plane);
+  conv_epilogue<T, TO>(a, px, co, acc);
+}
+
 template <typename T, typename TO, int BCO, int BPX, int WCO, int WPX>
-static int launch_cfg(const ConvArgs& a, hipStream_t s) {
-  dim3 grid((a.M + BPX - 1) / BPX, (a.d.Cout_pad + BCO - 1) / BCO);
+static int launch_cfg(const ConvArgs& a, hipStream_t s, int splits) {
+  dim3 grid((a.M + BPX - 1) / BPX, (a.d.Cout_pad + BCO - 1) / BCO, splits > 1 ? splits : 1);
   const size_t lds = 2u * (BCO + BPX) * 8u * 16u;
+  if (splits > 1) {
+    hipLaunchKernelGGL((conv_igemm_kernel<T, TO, BCO, BPX, WCO, WPX, true>), grid, dim3(256), lds, s, a);
+    const int r = hiseg_check_launch("conv_igemm_splitk");
+    if (r) return r;
+    const long long n = (long long)a.M * (a.d.Cout_pad >> 2);
+    hipLaunchKernelGGL((conv_splitk_reduce_kernel<T, TO>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, splits);
+    return hiseg_check_launch("conv_splitk_reduce");
+  }
   hipLaunchKernelGGL((conv_igemm_kernel<T, TO, BCO, BPX, WCO, WPX>), grid, dim3(256), lds, s, a);
   return hiseg_check_launch("conv_igemm");
 }
 
 // Tile choice: the widest Cout tile whose overhang past Cout_pad adds <= 1/6 to the MFMA work.
-template <typename T, typename TO>
-static int launch_typed(const ConvArgs& a, hipStream_t s) {
-  const int cp = a.d.Cout_pad;
+static int igemm_bco(int cp) {
   auto fits = [&](int bco) { return ((cp + bco - 1) / bco) * bco * 6 <= cp * 7; };
-  if (cp >= 96 && fits(128)) return launch_cfg<T, TO, 128, 128, 2, 2>(a, s);
-  if (cp >= 48 && fits(64)) return launch_cfg<T, TO, 64, 128, 2, 2>(a, s);
-  if (fits(32)) return launch_cfg<T, TO, 32, 256, 1, 4>(a, s);
-  return launch_cfg<T, TO, 16, 256, 1, 4>(a, s);
+  if (cp >= 96 && fits(128)) return 128;
+  if (cp >= 48 && fits(64)) return 64;
+  if (fits(32)) return 32;
+  return 16;
+}
+
+// split-K tiles: 128 x 128, or 64 x 128 -- never the narrow 32 / 16 x 256 tiles, whose eight gathered chunks per
+// thread made a gated split workgroup several times slower (960 -> 160 over 4 x 40 x 40: 57 us)
+static int splitk_bco(int cp) { return cp >= 96 && igemm_bco(cp) == 128 ? 128 : 64; }
+
+template <typename T, typename TO>
+static int launch_typed(const ConvArgs& a, hipStream_t s, int splits = 1) {
+  if (splits > 1) {
+    if (splitk_bco(a.d.Cout_pad) == 128) return launch_cfg<T, TO, 128, 128, 2, 2>(a, s, splits);
+    return launch_cfg<T, TO, 64, 128, 2, 2>(a, s, splits);
+  }
+  switch (igemm_bco(a.d.Cout_pad)) {
+    case 128: return launch_cfg<T, TO, 128, 128, 2, 2>(a, s, splits);
+    case 64: return launch_cfg<T, TO, 64, 128, 2, 2>(a, s, splits);
+    case 32: return launch_cfg<T, TO, 32, 256, 1, 4>(a, s, splits);
+    default: return launch_cfg<T, TO, 16, 256, 1, 4>(a, s, splits);
+  }
+}
+
+static int cu_count_igemm() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+
+// Split-K plan of the generic kernel for a bf16 1x1 layer whose tile grid leaves most CUs idle while its K loop
+// is long: splits (>= 2) so that tiles x splits fills two workgroups per CU with >= 3 K blocks per split, or 1
+// (no split).  The workspace it needs: splits x M x Cout_pad f32.
+static int splitk_plan(const ConvArgs& a) {
+  const hiseg_conv2d_desc& d = a.d;
+  if (d.dtype != HISEG_BF16 || d.KH != 1 || d.KW != 1 || d.convT || a.nK < 6) return 1;
+  // ungated layers take the LDS-DMA ring kernel (conv_fast.hip), which keeps more K blocks in flight: only long
+  // K loops split there (the 384 -> 2304 expansion over 4 x 20 x 20 pixels: 17 us unsplit, 31 us split in two)
+  if (d.in_scale == nullptr && a.nK < 24) return 1;
+  const int bco = splitk_bco(d.Cout_pad), bpx = 128;
+  const long long tiles = (long long)((a.M + bpx - 1) / bpx) * ((d.Cout_pad + bco - 1) / bco);
+  // HISEG_SPLITK=S forces S splits on every layer the split applies to (A/B timing only)
+  static const int forced = [] { const char* e = getenv("HISEG_SPLITK"); return e ? atoi(e) : 0; }();
+  if (forced > 0) return forced < a.nK ? forced : a.nK;
+  const int cus = cu_count_igemm();
+  if (tiles >= cus) return 1;
+  long long sp = (2LL * cus + tiles - 1) / tiles;
+  const int smax = a.nK / 3;
+  if (sp > smax) sp = smax;
+  if (sp > 16) sp = 16;
+  return sp >= 2 ? (int)sp : 1;
+}
+
+static long long splitk_bytes(const ConvArgs& a, int splits) {
+  return splits > 1 ? (long long)splits * a.M * a.d.Cout_pad * 4 : 0;
 }
 
 }  // namespace hiseg
@@ -242,6 +357,7 @@ int conv_pw_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_hwr_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_small_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_rows_try(const ConvArgs& a, hipStream_t s, int variant);
+bool conv_pw_applies(const ConvArgs& a);
 }
 
 using namespace hiseg;
@@ -259,7 +375,23 @@ extern "C" int hiseg_conv2d_fwd(const hiseg_conv2d_desc* d, hiseg_stream_t strea
 static bool release_variant(int v) {
   return v == -1 || v == 0 || (v >= 1 && v <= 8) || v == 50 || v == 51 || v == 52 || v == 54 || v == 58 ||
          (v >= 60 && v <= 69) || v == 70 || v == 71 || v == 72 || v == 74 || v == 80 || v == 82 || v == 84 || v == 86 ||
-         v == 88 || v == 89 || v == 90 || (v >= 92 && v <= 98);
+         v == 88 || v == 89 || v == 90 || (v >= 92 && v <= 99);
+}
+
+// Workspace bytes the automatic choice uses for this layer (split-K generic kernel), 0 when it needs none.
+extern "C" long long hiseg_conv2d_workspace_bytes(const hiseg_conv2d_desc* d) {
+  if (d == nullptr || d->dtype != HISEG_BF16 || d->KH != 1 || d->KW != 1 || d->convT || d->N <= 0) return 0;
+  const long long M = (long long)d->N * d->Ho * d->Wo;
+  if (M >= (1ll << 31) || d->K_pad % 64) return 0;
+  ConvArgs a;
+  a.d = *d;
+  a.M = (int)M;
+  a.Cin = d->Ca + d->Cb;
+  a.nK = d->K_pad / 64;
+  a.Hs = d->H / (d->a_up > 0 ? d->a_up : 1);
+  a.Ws = d->W / (d->a_up > 0 ? d->a_up : 1);
+  if (conv_pw_applies(a)) return 0;
+  return splitk_bytes(a, splitk_plan(a));
 }
 
 extern "C" int hiseg_conv2d_fwd_variant(const hiseg_conv2d_desc* d, int variant, hiseg_stream_t stream) {
@@ -343,6 +475,20 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
   hipStream_t s = (hipStream_t)stream;
   // Automatic choice (variant 0) = the fastest measured configuration per layer class
   // (tools/conv_bench.py): LDS-DMA ring kernel, 128x128 tiles for Cout >= 128, 64x128 for 64.
+  a.ins_vec = d->in_scale != nullptr && ((uintptr_t)d->in_scale & 15) == 0 && (d->Ca & 3) == 0;
+  a.ws = static_cast<float*>(d->workspace);
+  a.kper = a.nK;
+  if (variant == 99 || variant == 0) {
+    // split-K generic kernel for small-grid, long-K 1x1 layers (variant 99 forces it when the plan splits)
+    const int sp = splitk_plan(a);
+    if (sp > 1 && d->workspace != nullptr && d->workspace_bytes >= splitk_bytes(a, sp) &&
+        !(variant == 0 && conv_pw_applies(a))) {
+      a.kper = (a.nK + sp - 1) / sp;
+      const int spl = (a.nK + a.kper - 1) / a.kper;
+      return d->out_dtype == HISEG_BF16 ? launch_typed<bf16_t, bf16_t>(a, s, spl) : launch_typed<bf16_t, float>(a, s, spl);
+    }
+    HISEG_REQUIRE(variant == 0, HISEG_ERR_BAD_ARG, "conv2d: variant 99 (split-K) does not apply to this layer / workspace");
+  }
   if (variant == 98) {
     const int r = conv_rows_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;

@@ -27,7 +27,7 @@
 // pixel (n, 2y + dy, 2x + dx), channel co; a 512-column layer runs as two column tiles.
 //
 // Built twice (Makefile): this file (HISEG_PW_PART 1: RB 16, and conv_pw_try) and conv_pw_n.hip
-// (HISEG_PW_PART 2: RB 1, 2, 4, 8).
+// (HISEG_PW_PART 2: RB 1, 2, 4, 8; up to 10 k-steps at RB <= 4).
 #include "conv_common.h"
 
 #ifndef HISEG_PW_PART
@@ -305,6 +305,9 @@ template <int RB>
 static int launch_pw_n1(const ConvArgs& a, hipStream_t s, int nks_max, int nks) {
   if (nks_max == 2) return launch_pw_n2<RB, 2>(a, s, nks);
   if (nks_max == 4) return launch_pw_n2<RB, 4>(a, s, nks);
+  if constexpr (RB <= 4) {
+    if (nks_max == 10) return launch_pw_n2<RB, 10>(a, s, nks);
+  }
   return launch_pw_n2<RB, 8>(a, s, nks);
 }
 int launch_pw_narrow(const ConvArgs& a, hipStream_t s, int rb, int nks_max, int nks) {
@@ -344,57 +347,70 @@ static int launch_pw_k(const ConvArgs& a, hipStream_t s, int nks) {
   }
 }
 
-// Returns 1 if launched, 0 if the layer does not qualify (caller falls back), <0 on error.  variant 90.
-int conv_pw_try(const ConvArgs& a, hipStream_t s, int variant) {
+// The pointwise kernel's plan for a layer: false when it does not qualify (caller falls back).
+static bool pw_plan(const ConvArgs& a, int& rb, int& nks, int& nks_max) {
   const hiseg_conv2d_desc& d = a.d;
-  if (variant != 90) return 0;
-  if (d.dtype != HISEG_BF16 || d.out_dtype != HISEG_BF16) return 0;
-  if (d.KH != 1 || d.KW != 1 || d.stride != 1 || d.pad != 0 || d.a_up != 1) return 0;
-  if (d.out2) return 0;
-  if (d.residual && d.mul) return 0;
-  if (d.Ca % 8 || d.Cb % 8 || d.Cout % 4) return 0;
-  if (d.convT && (d.Cout / 4) % 4) return 0;
-  if (d.convT && d.residual) return 0;
-  const int nks = (a.Cin + 31) / 32;
-  if (d.K_pad < nks * 32 || nks > 9) return 0;
+  if (d.dtype != HISEG_BF16 || d.out_dtype != HISEG_BF16) return false;
+  if (d.KH != 1 || d.KW != 1 || d.stride != 1 || d.pad != 0 || d.a_up != 1) return false;
+  if (d.out2) return false;
+  if (d.residual && d.mul) return false;
+  if (d.Ca % 8 || d.Cb % 8 || d.Cout % 4) return false;
+  if (d.convT && (d.Cout / 4) % 4) return false;
+  if (d.convT && d.residual) return false;
+  nks = (a.Cin + 31) / 32;
+  if (d.K_pad < nks * 32 || nks > 10) return false;
   // HISEG_PW_EFF=0 restores the round-2 v5 coverage (256-multiple columns, 4 / 8 / 9 k-steps of whole 32-channel
   // slices, no SE gate) for same-box A/B timing
   static const bool eff = [] { const char* e = getenv("HISEG_PW_EFF"); return !(e && atoi(e) == 0); }();
-  if (!eff && (d.Cout_pad % 256 || d.Ca % 32 || d.in_scale || (nks != 4 && nks != 8 && nks != 9))) return 0;
-  const bool comb = nks == 9;
+  if (!eff && (d.Cout_pad % 256 || d.Ca % 32 || d.in_scale || (nks != 4 && nks != 8 && nks != 9))) return false;
+  // 9 k-steps at 256-column tiles: the 256 + 8 combiner only; 9..10 k-steps at narrow tiles: a single source of
+  // up to 320 channels (the B7 encoder's 288-channel SE-gated projections)
+  rb = 16;
+  if (d.Cout_pad <= 128) rb = d.Cout_pad <= 16 ? 1 : d.Cout_pad <= 32 ? 2 : d.Cout_pad <= 64 ? 4 : 8;
+  const bool comb = rb == 16 && nks == 9;
+  if ((rb == 16 && nks > 9) || (rb > 4 && nks > 8)) return false;   // (registers: 2 x 10 B fragment sets)
   if (comb ? (d.Ca != 256 || d.Cb > 32 || d.convT || d.residual || d.mul || d.in_scale ||
               (d.act != HISEG_ACT_NONE && d.act != HISEG_ACT_RELU))
            : d.Cb != 0)
-    return 0;
-  // column tile: 16 RB columns, RB the smallest power of two covering Cout_pad (at most 16; wider layers take
-  // ceil(Cout_pad / 256) tiles of 256, the last one ragged)
-  int rb = 16;
-  if (d.Cout_pad <= 128) rb = d.Cout_pad <= 16 ? 1 : d.Cout_pad <= 32 ? 2 : d.Cout_pad <= 64 ? 4 : 8;
+    return false;
   if (rb == 16) {
     // the head's forms (ReLU / sigmoid / none; residual, mul, ConvTranspose) and the EfficientNet expansion
     // (SiLU); no SE gate at 256-column tiles
-    if (d.in_scale) return 0;
+    if (d.in_scale) return false;
     if (d.act == HISEG_ACT_SIGMOID ? (d.convT || d.residual)
                                    : (d.act != HISEG_ACT_NONE && d.act != HISEG_ACT_RELU &&
                                       !(d.act == HISEG_ACT_SILU && !d.convT && !d.residual && !d.mul)))
-      return 0;
-    if (d.mul && (d.act == HISEG_ACT_RELU || d.convT || ((d.m_cstride | d.m_coff) & 3))) return 0;
+      return false;
+    if (d.mul && (d.act == HISEG_ACT_RELU || d.convT || ((d.m_cstride | d.m_coff) & 3))) return false;
   } else {
     // narrow tiles: plain or residual epilogue with any elementwise activation, optional SE gate
-    if (d.convT || d.mul || d.act == HISEG_ACT_SWISH || comb) return 0;
-    if (d.in_scale && (((uintptr_t)d.in_scale & 15) || (long long)d.N * d.Ca * 4 > 64 * 1024)) return 0;
+    if (d.convT || d.mul || d.act == HISEG_ACT_SWISH) return false;
+    if (d.in_scale && (((uintptr_t)d.in_scale & 15) || (long long)d.N * d.Ca * 4 > 64 * 1024)) return false;
   }
   const long long out_px = (long long)a.M * (d.convT ? 4 : 1);
   const long long lim = 0x7fffffffll;
   if ((long long)a.M * d.a_cstride * 2 >= lim || (d.Cb && (long long)a.M * d.b_cstride * 2 >= lim) ||
       out_px * d.o_cstride * 2 >= lim || (d.residual && out_px * d.r_cstride * 2 >= lim) ||
       (d.mul && out_px * d.m_cstride * 2 >= lim))
-    return 0;
-  if ((d.a_cstride | d.a_coff) & 7) return 0;
-  if (d.Cb && ((d.b_cstride | d.b_coff) & 7)) return 0;
-  if (((d.o_cstride | d.o_coff) & 3) || (d.residual && ((d.r_cstride | d.r_coff) & 3))) return 0;
-  if (((uintptr_t)d.out | (uintptr_t)d.residual | (uintptr_t)d.mul) & 7) return 0;
-  const int nks_max = comb ? 9 : nks <= 2 ? 2 : nks <= 4 ? 4 : 8;
+    return false;
+  if ((d.a_cstride | d.a_coff) & 7) return false;
+  if (d.Cb && ((d.b_cstride | d.b_coff) & 7)) return false;
+  if (((d.o_cstride | d.o_coff) & 3) || (d.residual && ((d.r_cstride | d.r_coff) & 3))) return false;
+  if (((uintptr_t)d.out | (uintptr_t)d.residual | (uintptr_t)d.mul) & 7) return false;
+  nks_max = comb ? 9 : nks <= 2 ? 2 : nks <= 4 ? 4 : nks <= 8 ? 8 : 10;
+  return true;
+}
+
+bool conv_pw_applies(const ConvArgs& a) {
+  int rb, nks, nks_max;
+  return pw_plan(a, rb, nks, nks_max);
+}
+
+// Returns 1 if launched, 0 if the layer does not qualify (caller falls back), <0 on error.  variant 90.
+int conv_pw_try(const ConvArgs& a, hipStream_t s, int variant) {
+  if (variant != 90) return 0;
+  int rb, nks, nks_max;
+  if (!pw_plan(a, rb, nks, nks_max)) return 0;
   int r;
   if (rb < 16) {
     r = launch_pw_narrow(a, s, rb, nks_max, nks);

@@ -75,6 +75,7 @@ class Conv2dDesc(ctypes.Structure):
         ("convT", c_int),
         ("weight_frag", c_void_p),
         ("act_beta", c_float),
+        ("workspace", c_void_p), ("workspace_bytes", ctypes.c_longlong),
     ]
 
 
@@ -192,6 +193,7 @@ def _declare(lib):
         "hiseg_roi_align_fwd": ([ctypes.POINTER(RoiAlignDesc), P], c_int),
         "hiseg_conv2d_fwd": ([ctypes.POINTER(Conv2dDesc), P], c_int),
         "hiseg_conv2d_fwd_variant": ([ctypes.POINTER(Conv2dDesc), c_int, P], c_int),
+        "hiseg_conv2d_workspace_bytes": ([ctypes.POINTER(Conv2dDesc)], c_ll),
         "hiseg_maxpool2x2_fwd": ([c_int, P, c_int, c_int, c_int, c_int, P, P], c_int),
         "hiseg_attn_spatial_fwd": ([c_int, P, c_int, c_int, c_int, c_int, P, c_int, P, P, P, P], c_int),
         "hiseg_gap_splits": ([c_int], c_int),

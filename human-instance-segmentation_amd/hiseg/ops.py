@@ -314,9 +314,17 @@ def conv2d(p: ConvPlan, xa: Act, xb: Optional[Act] = None, out: Optional[Act] = 
     d.convT = int(p.convT)
     if p.weight_frag is not None:
         d.weight_frag = p.weight_frag.data_ptr()
+    ws = None
+    if p.kh * p.kw == 1 and p.k_pad >= 384 and dt == torch.bfloat16 and not p.convT:
+        # small-grid, long-K 1x1 layers (the EfficientNet's deep SE-gated projections) split their K loop over
+        # workgroups into this stream-ordered workspace (hiseg_conv2d_workspace_bytes: 0 when the layer does not)
+        nbytes = L.lib().hiseg_conv2d_workspace_bytes(ctypes.byref(d))
+        if nbytes > 0:
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=xa.t.device)
+            d.workspace, d.workspace_bytes = ws.data_ptr(), nbytes
     if RECORD is not None:
         dc = L.Conv2dDesc.from_buffer_copy(d)
-        keep = [t for t in (xa, xb, out, residual, mul, out2) if t is not None]
+        keep = [t for t in (xa, xb, out, residual, mul, out2, ws) if t is not None]
         flops = 2.0 * d.N * d.Ho * d.Wo * p.gemm_cols * p.kh * p.kw * (xa.C + (xb.C if xb is not None else 0))
         RECORD.append((dc, keep, p, flops))
     if PROBE is not None:

@@ -128,10 +128,17 @@ typedef struct hiseg_conv2d_desc {
    * kernel that streams weights straight into registers; null disables that kernel. */
   const void* weight_frag;
   float act_beta;           /* Swish beta (act == HISEG_ACT_SWISH); ignored otherwise        */
+  /* Optional caller workspace (device memory, stream-ordered like the operands): the automatic
+   * choice splits the K loop of a small-grid 1x1 layer over workgroups when it holds at least
+   * hiseg_conv2d_workspace_bytes(d) bytes; null keeps every layer unsplit. */
+  void* workspace; long long workspace_bytes;
 } hiseg_conv2d_desc;
 int hiseg_conv2d_fwd(const hiseg_conv2d_desc* d, hiseg_stream_t stream);
+/* Workspace bytes hiseg_conv2d_fwd's automatic choice would use for this layer (0: none). */
+long long hiseg_conv2d_workspace_bytes(const hiseg_conv2d_desc* d);
 /* Tuning/test entry: variant -1 forces the generic kernel, 0 = automatic choice (as
- * hiseg_conv2d_fwd), k > 0 selects pipelined-kernel configuration k when the layer qualifies. */
+ * hiseg_conv2d_fwd), k > 0 selects pipelined-kernel configuration k when the layer qualifies
+ * (99: the split-K generic kernel; it needs the workspace and fails when the layer does not split). */
 int hiseg_conv2d_fwd_variant(const hiseg_conv2d_desc* d, int variant, hiseg_stream_t stream);
 
 /* MaxPool2d(2) on NHWC (hierarchical_segmentation_unet.py:331-332,391).

@@ -72,7 +72,12 @@ def test_release_library_refuses_diagnostic_conv_variants():
     d.weight, d.Cout, d.Cout_pad, d.K_pad = fake, 256, 256, 9 * 256
     d.scale, d.shift, d.act = fake, fake, 0
     d.out, d.o_cstride, d.o_coff = fake, 256, 0
-    for v in (9, 10, 18, 19, 20, 30, 40, 41, 44, 59, 73, 75, 76, 77, 79, 99, -5):
+    for v in (9, 10, 18, 19, 20, 30, 40, 41, 44, 59, 73, 75, 76, 77, 79, 100, -5):
         st = L.lib().hiseg_conv2d_fwd_variant(ctypes.byref(d), v, None)
         assert st == -1, v   # HISEG_ERR_BAD_ARG
         assert b"not a release variant" in L.lib().hiseg_last_error_string(), v
+    # the split-K variant (99) is a release variant, refused before any launch where it does not apply (3x3, no
+    # workspace)
+    assert L.lib().hiseg_conv2d_fwd_variant(ctypes.byref(d), 99, None) == -1
+    assert b"split-K" in L.lib().hiseg_last_error_string()
+    assert L.lib().hiseg_conv2d_workspace_bytes(ctypes.byref(d)) == 0

@@ -353,6 +353,10 @@ PW_EFF_CASES = {
     "ds_32_16_ins": (2, 32, 16, 9, 70, 0, True, False),
     "head_8_64_relu": (2, 8, 64, 6, 9, 1, False, False),
     "head_64_128_relu_res": (2, 64, 128, 9, 7, 1, False, True),
+    # 9-10 k-steps at narrow tiles (round 3): the B7 encoder's 288-channel SE-gated projections
+    "proj_288_48_ins_res": (2, 288, 48, 9, 13, 0, True, True),
+    "proj_320_32_ins": (3, 320, 32, 7, 9, 0, True, False),
+    "proj_264_16_ins_tail": (2, 264, 16, 5, 5, 0, True, False),
 }
 
 
@@ -377,6 +381,71 @@ def test_conv_pointwise_efficientnet_bit_identical(name):
     assert torch.isfinite(outs[-1].float()).all()
     for v in (0, 90):
         assert torch.equal(outs[v], outs[-1]), f"variant {v} differs from the generic kernel"
+
+
+# Split-K generic kernel (round 3): small-grid, long-K 1x1 layers -- the deep SE-gated EfficientNet projections of
+# the B7 teacher / B0 student in distillation (N, Ca, Cout, H, W, act, in_scale, residual)
+SPLITK_CASES = {
+    "b7_2304_384_ins_res": (4, 2304, 384, 20, 20, 0, True, True),
+    "b7_3840_640_ins": (4, 3840, 640, 20, 20, 0, True, False),
+    "b7_1344_224_ins_res": (4, 1344, 224, 40, 40, 0, True, True),
+    "b0_1152_192_ins_res": (2, 1152, 192, 20, 20, 0, True, True),
+    "b7_960_160_ins": (4, 960, 160, 40, 40, 0, True, False),
+    "plain_1536_96_relu_ragged": (3, 1536, 96, 7, 9, 1, False, False),
+}
+
+
+@pytest.mark.parametrize("name", list(SPLITK_CASES))
+def test_conv_splitk_within_reassociation(name):
+    """The split-K generic kernel (variant 99, and the automatic choice that picks it with the workspace ops.conv2d
+    supplies) against the unsplit generic kernel and a float64 reference of the same bf16 operands (the SE gate
+    applied and rounded to bf16 as the loader does): f32 re-association only, so the bf16 outputs agree with the
+    generic kernel's up to one rounding step, and the error against float64 is no larger than the generic kernel's
+    own (+ one bf16 ulp).  Deterministic run to run."""
+    from hiseg import ops
+    from hiseg import _lib as L
+    import ctypes
+    N, Ca, Cout, H, W, act, ins, res = SPLITK_CASES[name]
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(17)
+    x = torch.randn(N, Ca, H, W, device=DEV, generator=g)
+    xa = ops.Act.from_nchw(x, dt)
+    w = torch.randn(Cout, Ca, 1, 1, device=DEV, generator=g) / Ca ** 0.5
+    bn = torch.nn.BatchNorm2d(Cout).to(DEV).eval()
+    filler.fill_module(bn)
+    p = ops.pack_conv(w, None, bn, act, dt, DEV, pad=0)
+    gate = torch.rand(N, p.ca, device=DEV, generator=g) if ins else None
+    R = ops.Act.from_nchw(torch.randn(N, Cout, H, W, device=DEV, generator=g), dt) if res else None
+    # the library plans a split for this layer
+    d = L.Conv2dDesc()
+    d.dtype = d.out_dtype = 1
+    d.N, d.H, d.W, d.Ho, d.Wo, d.KH, d.KW, d.stride = N, H, W, H, W, 1, 1, 1
+    d.Ca, d.Cout, d.Cout_pad, d.K_pad = p.ca, p.gemm_cols, p.cout_pad, p.k_pad
+    d.srcA = d.weight = d.scale = d.shift = d.out = 1
+    d.in_scale = 16 if ins else None
+    assert L.lib().hiseg_conv2d_workspace_bytes(ctypes.byref(d)) > 0
+    outs = {}
+    for v in (-1, 99, 0, "again"):
+        y = ops.conv2d(p, xa, residual=R, in_scale=gate, variant=0 if v == "again" else v)
+        torch.cuda.synchronize()
+        outs[v] = y.to_nchw().float()
+    assert torch.equal(outs[0], outs[99]) and torch.equal(outs[0], outs["again"])
+    xq = xa.to_nchw().float().double()
+    if ins:
+        xq = (xq.float() * gate[:, :Ca, None, None]).to(dt).double()
+    wq = p.weight[:Cout, :Ca].float().double()
+    z = torch.einsum("nchw,oc->nohw", xq, wq) * p.scale[:Cout].double()[:, None, None] + p.shift[:Cout].double()[:, None, None]
+    if res:
+        z = z + R.to_nchw().double()
+    if act == 1:
+        z = torch.relu(z)
+    e_gen = (outs[-1].double() - z).abs().max().item()
+    e_spl = (outs[99].double() - z).abs().max().item()
+    ulp = z.abs().max().item() * 2.0 ** -8
+    assert e_spl <= e_gen + ulp, (e_spl, e_gen, ulp)
+    diff = (outs[99] - outs[-1]).abs()
+    assert (diff <= outs[-1].abs() * 2.0 ** -7 + 1e-6).all()
+    assert (diff == 0).float().mean().item() > 0.9
 
 
 # ------------------------------------------------------------------------------------------ misc kernels

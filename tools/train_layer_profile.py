@@ -47,8 +47,43 @@ def wgrad_family(d, want_bias):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--leg", default="train", choices=["train", "distill"])
     args = ap.parse_args()
     dev = torch.device("cuda:0")
+    if args.leg == "distill":
+        step = distill_step(dev)
+    else:
+        step = train_step(dev)
+    profile(step, args.warmup)
+
+
+def distill_step(dev):
+    """bench.py's C5 distillation step (B7 teacher eval + B0 student decoder-only phase, 4 x 640x640)."""
+    import filler
+    import hiseg
+    model, loss_fn = hiseg.create_unet_distillation_model("timm-efficientnet-b0", "timm-efficientnet-b7",
+                                                          teacher_checkpoint="absent.pth", device="cpu",
+                                                          progressive_unfreeze=True)
+    filler.fill_module(model.student, seed=11)
+    filler.fill_module(model.teacher, seed=12)
+    hiseg.set_compute_dtype(model, torch.bfloat16)
+    model = model.to(dev).train()
+    loss_fn.temperature = 4.0
+    x = torch.randn(4, 3, 640, 640, generator=torch.Generator().manual_seed(100)).to(dev)
+    m = (torch.rand(4, 1, 640, 640, generator=torch.Generator().manual_seed(101)) > 0.5).float().to(dev)
+    opt = hiseg.FusedAdamW(model.student, lr=1e-4, weight_decay=1e-4, max_grad_norm=1.0,
+                           params=model.student.get_decoder_parameters())
+
+    def step():
+        s, t = model(x)
+        loss, _ = loss_fn(s, t, m)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    return step
+
+
+def train_step(dev):
     import filler
     import hiseg
     model = bench.build_model(dev, torch.bfloat16).train()
@@ -67,8 +102,11 @@ def main():
         opt.zero_grad()
         loss.backward()
         opt.step()
+    return step
 
-    for _ in range(args.warmup):
+
+def profile(step, warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize()
 
@@ -124,7 +162,7 @@ def main():
         print(f"{g[1]:8.3f} ms {g[0]:3d}x {g[1] / g[0] * 1e3:8.1f}us  {n} {k}")
         out.append({"call": n, "key": k, "count": g[0], "ms": g[1]})
     os.makedirs("gpurun_out", exist_ok=True)
-    with open("gpurun_out/train_layer_profile.json", "w") as f:
+    with open(os.environ.get("HISEG_PROFILE_OUT", "gpurun_out/train_layer_profile.json"), "w") as f:
         json.dump({"step_ms": step_ms, "rows": out}, f, indent=1)
 
 
