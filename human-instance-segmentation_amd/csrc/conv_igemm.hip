@@ -310,37 +310,26 @@ static int launch_typed(const ConvArgs& a, hipStream_t s, int splits = 1) {
   }
 }
 
-static int cu_count_igemm() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-  }
-  return n;
-}
-
-// Split-K plan of the generic kernel for a bf16 1x1 layer whose tile grid leaves most CUs idle while its K loop
-// is long: splits (>= 2) so that tiles x splits fills two workgroups per CU with >= 3 K blocks per split, or 1
-// (no split).  The workspace it needs: splits x M x Cout_pad f32.
+// Split-K plan of the generic kernel for a bf16 1x1 layer with a long K loop over a small image: splits (>= 2) or 1
+// (no split).  The plan depends on the layer and the per-image grid only, never on the batch: an output element's
+// f32 summation order (K blocks within a split, then the splits in order) is then the same whether its image is
+// computed alone or in a batch, which keeps the exported masks batch-invariant bit for bit
+// (test_c2_shape_bf16_properties_and_oracle).  Images of <= 1600 pixels (the EfficientNet's stride-16 / 32
+// stages at 640 x 640 and 480 x 640), >= 6 K blocks: nK / 4 splits, 2..8.  The workspace it needs: splits x M x
+// Cout_pad f32.
 static int splitk_plan(const ConvArgs& a) {
   const hiseg_conv2d_desc& d = a.d;
   if (d.dtype != HISEG_BF16 || d.KH != 1 || d.KW != 1 || d.convT || a.nK < 6) return 1;
   // ungated layers take the LDS-DMA ring kernel (conv_fast.hip), which keeps more K blocks in flight: only long
   // K loops split there (the 384 -> 2304 expansion over 4 x 20 x 20 pixels: 17 us unsplit, 31 us split in two)
   if (d.in_scale == nullptr && a.nK < 24) return 1;
-  const int bco = splitk_bco(d.Cout_pad), bpx = 128;
-  const long long tiles = (long long)((a.M + bpx - 1) / bpx) * ((d.Cout_pad + bco - 1) / bco);
   // HISEG_SPLITK=S forces S splits on every layer the split applies to (A/B timing only)
   static const int forced = [] { const char* e = getenv("HISEG_SPLITK"); return e ? atoi(e) : 0; }();
   if (forced > 0) return forced < a.nK ? forced : a.nK;
-  const int cus = cu_count_igemm();
-  if (tiles >= cus) return 1;
-  long long sp = (2LL * cus + tiles - 1) / tiles;
-  const int smax = a.nK / 3;
-  if (sp > smax) sp = smax;
-  if (sp > 16) sp = 16;
-  return sp >= 2 ? (int)sp : 1;
+  if ((long long)d.Ho * d.Wo > 1600) return 1;
+  int sp = a.nK / 4;
+  if (sp > 8) sp = 8;
+  return sp >= 2 ? sp : 2;
 }
 
 static long long splitk_bytes(const ConvArgs& a, int splits) {

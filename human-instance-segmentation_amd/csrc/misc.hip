@@ -155,9 +155,18 @@ __global__ void __launch_bounds__(256) gap_reduce_kernel(const float* partial, i
   __shared__ float red[256];
   const int n = blockIdx.x, t = threadIdx.x;
   const int c = blockIdx.y * 64 + (t & 63), sg = t >> 6;
-  float a = 0.f;
-  if (c < C)
-    for (int sp = sg; sp < splits; sp += 4) a += partial[((long long)n * splits + sp) * C + c];
+  // eight independent partial sums per thread (eight loads in flight: the depthwise producers write up to 512
+  // tile partials per image), combined in a fixed order
+  float a8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    const float* base = partial + (long long)n * splits * C + c;
+    int sp = sg;
+    for (; sp + 28 < splits; sp += 32)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a8[u] += base[(long long)(sp + 4 * u) * C];
+    for (int u = 0; sp < splits; sp += 4, ++u) a8[u & 7] += base[(long long)sp * C];
+  }
+  const float a = ((a8[0] + a8[1]) + (a8[2] + a8[3])) + ((a8[4] + a8[5]) + (a8[6] + a8[7]));
   red[t] = a;
   __syncthreads();
   if (sg == 0 && c < C) sums[(long long)n * C + c] = red[t] + red[t + 64] + red[t + 128] + red[t + 192];
@@ -697,7 +706,9 @@ extern "C" int hiseg_attn_spatial_fwd(int dtype, const void* x, int N, int H, in
 }
 
 extern "C" int hiseg_gap_splits(int HW) {
-  int s = HW / 512;
+  // >= 32 pixels per split (was 512: the B0 student's SE pools over 4 x 20 x 20 ran as 4 blocks, one 400-pixel
+  // dependent load chain per thread, 52 us)
+  int s = HW / 32;
   if (s < 1) s = 1;
   if (s > 64) s = 64;
   return s;
@@ -733,12 +744,13 @@ extern "C" int hiseg_channel_scale_fwd(int dtype, const void* x, int N, int HW, 
 }
 
 extern "C" int hiseg_dw_gap_tiles(int N, int Ho, int Wo) {
-  // strip ranges of >= 16 strips (a thread of dwconv_q_kernel keeps its weights in registers across them), at
-  // most 2048 / N per image
+  // strip ranges of >= 2 strips, at most 2048 / N per image.  (Ranges of >= 16 strips, which amortised a thread's
+  // register-held weights, left the deep low-resolution layers with ~120 blocks: the B7's k5 2304-channel
+  // depthwise conv over 4 x 20 x 20 ran at 0.3 TB/s, tools/train_layer_profile.py --leg distill.)
   const int strips = Ho * ((Wo + kDwXS - 1) / kDwXS);
   int t = 2048 / (N > 0 ? N : 1);
   if (t < 1) t = 1;
-  int by_len = strips / 16;
+  int by_len = strips / 2;
   if (by_len < 1) by_len = 1;
   return t < by_len ? t : by_len;
 }

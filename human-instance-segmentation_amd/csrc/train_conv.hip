@@ -21,22 +21,14 @@
 
 #include "conv_common.h"
 #include "hiseg_train.h"
+#include "wgrad_common.h"
 
 namespace hiseg {
+int wgrad_wide_bc(const hiseg_conv2d_desc* d, int Cg, int Kg, int Cin, int M, int dy_cs, int dy_coff);
+int wgrad_wide_try(const WgradArgs& a, hipStream_t s);
+}
 
-struct WgradArgs {
-  hiseg_conv2d_desc d;  // forward descriptor (input side + geometry)
-  const void* dy; int dy_cs, dy_coff;
-  int M;          // GEMM rows of the forward conv (output pixels; input pixels for convT)
-  int Cin;        // Ca + Cb (padded)
-  int Ktot;       // KH*KW*Cin
-  int want_bias;
-  int Cg, Kg;
-  int splits, blocks_per_split;  // pixel blocks per split
-  float* ws;
-  int x_tile_src;  // transposed-read kernel: 1 = one X source per K tile (two sources too far apart for one
-                   // buffer resource; the layer's tiles never mix them), 0 = per-lane source over one resource
-};
+namespace hiseg {
 
 // KCH x KCH transpose of 16-B chunks: in[i] = chunk of pixel i (KCH channels), out[e] = chunk of
 // channel e (KCH pixels).
@@ -556,13 +548,15 @@ static int wgrad_geometry(const hiseg_conv2d_desc* d, int want_bias, int* Cg, in
   *M = (int)Mll;
   const int PB = 8 * kch;
   const int nblocks = (*M + PB - 1) / PB;
-  const int BK = *Kg >= 128 ? 128 : 64;
-  const int BC = *Cg >= 128 ? 128 : *Cg >= 64 ? 64 : *Cg >= 32 ? 32 : 16;
+  // the wide tile (wgrad_wide.hip: 256 x 256 / 256 x 128, one workgroup per CU): about 256 workgroups, one round
+  const int wbc = wgrad_wide_bc(d, *Cg, *Kg, *Cin, *M, -1, 0);
+  const int BK = wbc ? 256 : *Kg >= 128 ? 128 : 64;
+  const int BC = wbc ? wbc : *Cg >= 128 ? 128 : *Cg >= 64 ? 64 : *Cg >= 32 ? 32 : 16;
   const long long tiles = (long long)((*Kg + BK - 1) / BK) * ((*Cg + BC - 1) / BC);
   // about 1024 workgroups but never past it: the wgrad kernels run two workgroups per CU, so 1024 = two full
   // rounds on 256 CUs, and rounding up (36 tiles x 29 splits = 1044) added a third, nearly empty round that cost
   // a third of the layer's time
-  int sp = (int)(1024 / tiles);
+  int sp = (int)((wbc ? 256 : 1024) / tiles);
   if (sp > nblocks) sp = nblocks;
   if (sp < 1) sp = 1;
   *bps = (nblocks + sp - 1) / sp;
@@ -596,6 +590,8 @@ extern "C" int hiseg_conv2d_wgrad(const hiseg_conv2d_desc* fwd, const void* dy, 
   a.splits = splits;
   a.ws = ws;
   hipStream_t s = (hipStream_t)stream;
+  const int rw = wgrad_wide_try(a, s);
+  if (rw != 0) return rw < 0 ? rw : HISEG_OK;
   const int rt = wgrad_tr_try(a, s);
   if (rt != 0) return rt < 0 ? rt : HISEG_OK;
   return fwd->dtype == HISEG_BF16 ? wgrad_typed<bf16_t>(a, s) : wgrad_typed<float>(a, s);

@@ -1,0 +1,313 @@
+// Wide-tile weight gradient on CDNA4 MFMA (gfx950, bf16): the ROI head's 128- and 256-channel 3x3 layers
+// (refinement.py:31-55 ResidualBlock and the mask-grid blocks, trained by train_advanced.py:680-762).
+//
+// GEMM (include/hiseg_train.h, hiseg_conv2d_wgrad):  D[k][j] = sum_p X[p][k] * dY[p][j], contracted over pixels.
+// train_conv.hip's conv_wgrad_tr_kernel runs it on 128 x 128 workgroup tiles with 64 x 64 wave tiles, two
+// workgroups per CU: per 64-pixel stage every workgroup moves 32 KiB from L2 into LDS for 128 MFMAs per SIMD,
+// 128 B/clk per CU at two workgroups -- twice an XCD's L2 share per CU -- and each MFMA needs 512 B of
+// transposed LDS reads.  It held 0.28-0.30 of the bf16 peak on the 256-channel class (1.24 ms per launch vs
+// 0.65 ms for the forward conv of the same FLOPs, profiles/r3_*).
+//
+// Here one 256-thread workgroup per CU computes a 256 (K) x 256 (C) tile (NW = 4; the kernel is written for
+// BC = 128 and NW = 8 too, both measured slower): each wave a 128 x 128 quarter held in AGPRs (64 16x16
+// accumulators), the operands of a 64-pixel stage as 128-column
+// transposed-read images (the T10 (b) swizzle of conv_wgrad_tr_kernel: two for X, BC / 128 for dY) filled by
+// LDS-DMA, a two-stage ring with one barrier per stage.  Per MFMA the L2 -> LDS traffic is a quarter of the
+// 128 x 128 tile's and the LDS reads half (128 x 128 wave tiles), wave K-half wk reads X image wk only.
+// Split-K over pixel blocks with f32 partial tiles, reduced by wgrad_reduce_kernel exactly as before; the
+// per-lane source addressing (two sources, upsampled source A, GEMM-bias column, halo taps through
+// out-of-range offsets) is conv_wgrad_tr_kernel's.  Results equal it up to f32 re-association (the same
+// pixel partition into splits is not guaranteed: the split count follows this tile's grid).
+#include <cstdlib>
+
+#include "hiseg_train.h"
+#include "wgrad_common.h"
+
+namespace hiseg {
+
+typedef short ww_v4s_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) ww_v4s_t ww_lds_v4s_t;
+typedef __attribute__((address_space(3))) void ww_lds_void_t;
+typedef unsigned ww_v4u_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) ww_v4u_t ww_lds_v4u_t;
+
+__device__ __forceinline__ unsigned ww_swz(int row, int ch) {
+  return 256u * (unsigned)row + 16u * (unsigned)(ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+__device__ __forceinline__ void ww_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned lds_addr, unsigned voff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :: "s"(lds_addr), "v"(voff), "s"(rsrc) : "memory");
+}
+
+__device__ __forceinline__ ww_v4s_t ww_tr(unsigned byte_addr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((ww_lds_v4s_t*)(uintptr_t)byte_addr);
+}
+
+template <int BC, int NW>
+__global__ void __launch_bounds__(NW * 64, 1) conv_wgrad_wide_kernel(WgradArgs a) {
+  constexpr int BK = 256, PB = 64;
+  constexpr int NXH = 2, NYH = BC / 128;   // 128-column images per stage
+  constexpr int NI = 16 / NW;              // DMA instructions per image per wave (4 rows each, 64 rows)
+  constexpr int WCN = NW / 2;              // waves along C
+  constexpr int WCOLS = BC / WCN;          // a wave's C columns
+  constexpr int TM = 8, TN = WCOLS / 16;   // wave tile 128 (K) x WCOLS (C)
+  constexpr int IMG = PB * 256;
+  constexpr int STAGE = (NXH + NYH) * IMG;
+  static_assert((BC == 128 || BC == 256) && (NW == 4 || NW == 8) && TN >= 1, "tile");
+  extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+  const hiseg_conv2d_desc& d = a.d;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wk = w / WCN, wc = w % WCN;
+  // XCD-major bijective remap (conv_wgrad_tr_kernel's): the K / C tiles of one pixel split run on one XCD
+  const int nkt = (a.Kg + BK - 1) / BK, nct = (a.Cg + BC - 1) / BC;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = orig & 7, loc = orig >> 3;
+  const int wgi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int k0 = (wgi % nkt) * BK, j0 = ((wgi / nkt) % nct) * BC, split = wgi / (nkt * nct);
+  const int pb_begin = split * a.blocks_per_split;
+  const int nblocks = (a.M + PB - 1) / PB;
+  int pb_end = pb_begin + a.blocks_per_split;
+  if (pb_end > nblocks) pb_end = nblocks;
+  const int nit = pb_end > pb_begin ? pb_end - pb_begin : 0;
+
+  // one buffer resource over both X sources from the lower address (the launcher checked the span)
+  const char* const pa = reinterpret_cast<const char*>(d.srcA);
+  const char* const pb = d.Cb ? reinterpret_cast<const char*>(d.srcB) : pa;
+  const char* const xbase = pa < pb ? pa : pb;
+  const unsigned dA = (unsigned)(pa - xbase), dB = (unsigned)(pb - xbase);
+  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(xbase), (short)0, 0x7fffffff,
+                                                                       0x00020000);
+  const __amdgpu_buffer_rsrc_t rY = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.dy), (short)0, 0x7fffffff,
+                                                                       0x00020000);
+  const unsigned OOB = 0x80000000u;
+
+  // per-lane DMA state: instruction i of an image fills rows 4(w + 4i) .. +3; this lane row (lane >> 4), slot
+  // lane & 15.  Packed to keep the 256-column tile's state in registers: xo = channel offset (-1: zero column),
+  // xk = ky | kx << 4 | upsampling shift << 8 | source B << 9; yo = dY channel offset (-1: zero) | sub-pixel q << 28
+  int xo[NXH][NI], xk[NXH][NI], yo[NYH][NI];
+  int pn[NI], py[NI], px[NI], pp[NI];
+  unsigned bias_lanes = 0;   // bit NI h + i: this lane's chunk of X image h, instruction i is the GEMM-bias column's
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int r = 4 * (w + NW * i) + (lane >> 4);
+    const int c = (lane & 15) ^ (((r & 3) << 2) | ((r >> 2) & 3));
+#pragma unroll
+    for (int h = 0; h < NXH; ++h) {
+      const int k = k0 + 128 * h + 8 * c;
+      const int tap = k / a.Cin;
+      const int ci = k - tap * a.Cin;
+      const bool la = d.Cb == 0 || ci < d.Ca;
+      xo[h][i] = k < a.Ktot ? (la ? d.a_coff + ci : d.b_coff + ci - d.Ca) : -1;
+      const int kyv = tap / d.KW, kxv = tap - kyv * d.KW;
+      xk[h][i] = kyv | (kxv << 4) | ((la && d.a_up == 2) ? 1 << 8 : 0) | (la ? 0 : 1 << 9);
+      if (a.want_bias && k == a.Ktot) bias_lanes |= 1u << (NI * h + i);
+    }
+#pragma unroll
+    for (int hh = 0; hh < NYH; ++hh) {
+      const int j = j0 + 128 * hh + 8 * c;
+      if (d.convT) {
+        const int C = d.Cout >> 2, q = j / C;
+        yo[hh][i] = j < d.Cout ? (a.dy_coff + (j - q * C)) | (q << 28) : -1;
+      } else {
+        yo[hh][i] = j < d.Cout ? a.dy_coff + j : -1;
+      }
+    }
+    const int p = pb_begin * PB + r;
+    pp[i] = p;
+    px[i] = p % d.Wo;
+    const int tt = p / d.Wo;
+    py[i] = tt % d.Ho;
+    pn[i] = tt / d.Ho;
+  }
+  const int adv_x = PB % d.Wo, adv_y = PB / d.Wo;
+  const unsigned lds_base = (unsigned)(uintptr_t)(ww_lds_void_t*)smem;
+
+  // DMA of a stage in 2 NI parts (part p: row block i = p / 2 of the X images if p is even, of the dY images if odd;
+  // the odd part advances the row block's pixels), interleaved with the previous stage's MFMA rows so the DMA
+  // issue (about 100 cycles per 1-KiB piece) hides under them
+  auto issue_part = [&](int s, int p) __attribute__((always_inline)) {
+    const unsigned sb = lds_base + (unsigned)(s * STAGE);
+    const int i = p >> 1;
+    const unsigned row_base = 256u * (unsigned)(4 * (w + NW * i));
+    if ((p & 1) == 0) {
+#pragma unroll
+      for (int h = 0; h < NXH; ++h) {
+        const int kk = xk[h][i];
+        const int iy = py[i] * d.stride - d.pad + (kk & 15);
+        const int ix = px[i] * d.stride - d.pad + ((kk >> 4) & 15);
+        const bool okx = xo[h][i] >= 0 && pp[i] < a.M && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+        const int sh = (kk >> 8) & 1, Hs = d.H >> sh, Ws = d.W >> sh;
+        const bool fb = (kk >> 9) & 1;
+        const unsigned offx = okx ? (fb ? dB : dA) + (unsigned)((((pn[i] * Hs + (iy >> sh)) * Ws + (ix >> sh)) *
+                                                                  (fb ? d.b_cstride : d.a_cstride) + xo[h][i]) * 2)
+                                  : OOB;
+        ww_dma16(rX, sb + (unsigned)(h * IMG) + row_base, offx);
+      }
+    } else {
+#pragma unroll
+      for (int hh = 0; hh < NYH; ++hh) {
+        const int yv = yo[hh][i];
+        const bool oky = yv >= 0 && pp[i] < a.M;
+        int yp = pp[i];
+        if (d.convT) {
+          const int qq = (yv >> 28) & 3;
+          yp = (pn[i] * (2 * d.Ho) + 2 * py[i] + (qq >> 1)) * (2 * d.Wo) + 2 * px[i] + (qq & 1);
+        }
+        const unsigned offy = oky ? (unsigned)((yp * a.dy_cs + (yv & 0x0fffffff)) * 2) : OOB;
+        ww_dma16(rY, sb + (unsigned)((NXH + hh) * IMG) + row_base, offy);
+      }
+      pp[i] += PB;
+      px[i] += adv_x;
+      py[i] += adv_y;
+      if (px[i] >= d.Wo) { px[i] -= d.Wo; ++py[i]; }
+      while (py[i] >= d.Ho) { py[i] -= d.Ho; ++pn[i]; }
+    }
+  };
+  auto issue = [&](int s) __attribute__((always_inline)) {
+#pragma unroll
+    for (int p = 0; p < 2 * NI; ++p) issue_part(s, p);
+  };
+
+  floatx4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment reads: group g = lane >> 4 takes pixel rows 8g..8g+7 of a 32-pixel k-step; lane 4q+p of the group
+  // addresses row q, columns 4p..4p+3 of its 16-column block
+  const int g = lane >> 4, q = (lane & 15) >> 2, pq = lane & 3;
+  // this wave's X image (K half wk) and dY image / column base
+  const int yimg = (wc * WCOLS) / 128;
+  const int ych0 = ((wc * WCOLS) % 128) / 8;
+
+  if (nit > 0) issue(0);
+  for (int it = 0; it < nit; ++it) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (bias_lanes) {   // the GEMM-bias column: X = 1 in every row, written over the landed DMA zeros
+      const unsigned sb = lds_base + (unsigned)((it & 1) * STAGE);
+#pragma unroll
+      for (int h = 0; h < NXH; ++h)
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+          if (bias_lanes & (1u << (NI * h + i)))
+            *reinterpret_cast<ww_lds_v4u_t*>(
+                (uintptr_t)(sb + (unsigned)(h * IMG) + 256u * (unsigned)(4 * (w + NW * i)) + 16u * (unsigned)lane)) =
+                ww_v4u_t{0x3f80u, 0u, 0u, 0u};
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // stage it landed everywhere; every wave left stage it-1's buffer
+    asm volatile("" ::: "memory");
+    const bool more = it + 1 < nit;
+
+    const unsigned sX = lds_base + (unsigned)((it & 1) * STAGE) + (unsigned)(wk * IMG);
+    const unsigned sY = lds_base + (unsigned)((it & 1) * STAGE) + (unsigned)((NXH + yimg) * IMG);
+    // k-step 0 fragments, then per A row i: its MFMAs, after which af[i] takes row i of k-step 1 (the reads land
+    // under the remaining rows' MFMAs); k-step 1's B fragments after the last row
+    bf16x8_t af[TM], bfr[TN];
+    auto rdA = [&](int ks, int i) __attribute__((always_inline)) -> bf16x8_t {
+      const int r0 = ks * 32 + 8 * g + q, ch = 2 * i + (pq >> 1);
+      const ww_v4s_t lo = ww_tr(sX + ww_swz(r0, ch) + 8u * (pq & 1));
+      const ww_v4s_t hi = ww_tr(sX + ww_swz(r0 + 4, ch) + 8u * (pq & 1));
+      return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+    auto rdB = [&](int ks, int j) __attribute__((always_inline)) -> bf16x8_t {
+      const int r0 = ks * 32 + 8 * g + q, ch = ych0 + 2 * j + (pq >> 1);
+      const ww_v4s_t lo = ww_tr(sY + ww_swz(r0, ch) + 8u * (pq & 1));
+      const ww_v4s_t hi = ww_tr(sY + ww_swz(r0 + 4, ch) + 8u * (pq & 1));
+      return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    };
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfr[j] = rdB(0, j);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = rdA(0, i);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (ks == 0) af[i] = rdA(1, i);
+        if (ks == 0 && more && i < 2 * NI) issue_part((it + 1) & 1, i);
+      }
+      if (ks == 0) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bfr[j] = rdB(1, j);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  float* ws = a.ws + (long long)split * a.Cg * a.Kg;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int k = k0 + wk * 128 + i * 16 + (lane >> 4) * 4;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int jj = j0 + wc * WCOLS + j * 16 + (lane & 15);
+      if (k < a.Kg && jj < a.Cg) *reinterpret_cast<floatx4*>(ws + (long long)jj * a.Kg + k) = acc[i][j];
+    }
+  }
+}
+
+// HISEG_WGRAD_WIDE=0 keeps every layer on conv_wgrad_tr_kernel (A/B timing only)
+static bool wide_mode() {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("HISEG_WGRAD_WIDE");
+    mode = e ? atoi(e) : 1;
+  }
+  return mode != 0;
+}
+
+// The wide tile for a layer: 256 or 128 (C tile), 0 when it does not apply.  bf16, 128-multiple GEMM columns
+// (no ConvTranspose), the transposed-read kernel's alignment rules, every X source within one 2^31-byte buffer
+// resource, and a K extent of at least two 128-column images.
+int wgrad_wide_bc(const hiseg_conv2d_desc* d, int Cg, int Kg, int Cin, int M, int dy_cs, int dy_coff) {
+  if (!wide_mode() || d->dtype != HISEG_BF16 || d->convT) return 0;
+  if (Cg % 128 || Kg < 256) return 0;
+  if (d->Ca % 8 || Cin % 8 || d->a_cstride % 8 || d->a_coff % 8) return 0;
+  if (d->Cb && (d->b_cstride % 8 || d->b_coff % 8)) return 0;
+  if (dy_cs >= 0 && (dy_cs % 8 || dy_coff % 8)) return 0;
+  const long long span_a = (long long)d->N * d->H * d->W * d->a_cstride * 2;
+  const long long span_b = d->Cb ? (long long)d->N * d->H * d->W * d->b_cstride * 2 : 0;
+  if (span_a >= 0x7fffffffll || span_b >= 0x7fffffffll) return 0;
+  if (dy_cs >= 0 && ((long long)M * dy_cs + dy_coff + Cg) * 2 >= 0x7fffffffll) return 0;
+  if (d->Cb) {
+    const long long pa = (long long)(uintptr_t)d->srcA, pb = (long long)(uintptr_t)d->srcB;
+    const long long lo = pa < pb ? pa : pb;
+    if (pa - lo + span_a >= 0x7fffffffll || pb - lo + span_b >= 0x7fffffffll) return 0;
+  }
+  return Cg % 256 == 0 ? 256 : 0;   // (the 256 x 128 tile measured slower than the 128 x 128 kernel)
+}
+
+template <int BC, int NW>
+static int wide_launch(const WgradArgs& a, hipStream_t s) {
+  constexpr size_t lds = (size_t)2 * (2 + BC / 128) * 64 * 256;
+  auto kern = conv_wgrad_wide_kernel<BC, NW>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  const int nwg = ((a.Kg + 255) / 256) * ((a.Cg + BC - 1) / BC) * a.splits;
+  hipLaunchKernelGGL(kern, dim3(nwg), dim3(NW * 64), lds, s, a);
+  return hiseg_check_launch("conv_wgrad_wide");
+}
+
+// 1 = launched, 0 = the layer does not take the wide tile
+int wgrad_wide_try(const WgradArgs& a, hipStream_t s) {
+  const int bc = wgrad_wide_bc(&a.d, a.Cg, a.Kg, a.Cin, a.M, a.dy_cs, a.dy_coff);
+  if (bc == 0) return 0;
+  // four waves, one per SIMD, 128 x 128 wave tiles in AGPRs.  (Eight waves at two per SIMD with 128 x 64 wave tiles
+  // spill 76 B per lane and ran 1.74 ms on the 256-channel class; this form 1.19 ms, conv_wgrad_tr_kernel 1.31 ms,
+  // same box, tools/wgrad_bench.py.)
+  const int r = wide_launch<256, 4>(a, s);
+  return r < 0 ? r : 1;
+}
+
+}  // namespace hiseg

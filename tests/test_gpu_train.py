@@ -120,6 +120,47 @@ def test_conv_backward_matches_autograd(case, dt):
         assert err(dt)(grad_nchw(T, xb), xr.grad[:, split[0]:]) < tol(dt)
 
 
+WIDE_WGRAD_CASES = [  # (cin, cout, k, H, W, N, bias, two-source split): 128-multiple GEMM columns (wgrad_wide.hip)
+    (256, 256, 3, 16, 12, 2, False, None),
+    (256, 256, 3, 32, 24, 4, False, None),        # many pixel splits
+    (128, 128, 3, 9, 7, 2, True, None),           # ragged K tile (1152 + bias column), C tile 128
+    (256, 128, 3, 12, 10, 2, False, None),
+    (128, 256, 3, 12, 10, 3, True, None),
+    (258, 256, 1, 8, 6, 2, True, (256, 2)),       # two sources + bias in one K tile
+    (256, 128, 3, 10, 8, 2, False, (128, 128)),   # decoder concat: two 128-channel sources
+]
+
+
+@pytest.mark.parametrize("case", WIDE_WGRAD_CASES)
+def test_wgrad_wide_matches_f64_of_bf16_operands(case):
+    """bf16 weight gradients of the 128-multiple-column layers (the wide-tile kernel) against float64 autograd of
+    the same bf16-rounded operands: the kernel's only error is its f32 accumulation, so 1e-4 of the max holds."""
+    from hiseg.ops import Act
+    cin, cout, k, H, W, N, bias, split = case
+    dt = torch.bfloat16
+    conv = nn.Conv2d(cin, cout, k, padding=k // 2, bias=bias)
+    filler.fill_module(conv, seed=17)
+    TE, S, T = engine(_Holder(c=conv), dt)
+    x = torch.from_numpy(filler.normal(11, (N, cin, H, W))).to(DEV)
+    if split is None:
+        xa, xb = Act.from_nchw(x, dt), None
+    else:
+        xa, xb = Act.from_nchw(x[:, :split[0]], dt), Act.from_nchw(x[:, split[0]:], dt)
+    y = TE.conv_plain(T, conv, TE.ACT_NONE, xa, xb, split=split)
+    g = torch.from_numpy(filler.normal(12, (N, cout, H, W))).to(DEV)
+    inject(T, y, g, dt)
+    S.flat.prepare_backward()
+    T.run_backward()
+    xr = x.to(dt).double().requires_grad_(True)
+    wr = conv.weight.detach().to(dt).double().requires_grad_(True)
+    br = torch.zeros(cout, dtype=torch.float64, device=DEV, requires_grad=True) if bias else None
+    yr = F.conv2d(xr, wr, br, padding=k // 2)
+    (yr * g.to(dt).double()).sum().backward()
+    assert rel(conv.weight.grad, wr.grad) < 1e-4
+    if bias:
+        assert rel(conv.bias.grad, br.grad) < 1e-4
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("cio", [(256, 128), (128, 64), (64, 32)])
 def test_convT_backward_matches_autograd(dt, cio):

@@ -133,6 +133,13 @@ def profile(step, warmup):
             elif _n == "hiseg_conv2d_wgrad":
                 d = a[0]._obj
                 key = f"{wgrad_family(d, a[4])} {conv_key(d)}{' bias' if a[4] else ''}"
+            elif _n in ("hiseg_dwconv_gap_fwd", "hiseg_dwconv_fwd"):
+                # (dtype, in, N, H, W, C, K, stride, ...): algorithmic bytes = input + output activations (bf16)
+                N, H, W, C, K, st = a[2], a[3], a[4], a[5], a[6], a[7]
+                Ho, Wo = (H + 2 * (K // 2) - K) // st + 1, (W + 2 * (K // 2) - K) // st + 1
+                key = f"k{K} s{st} C{C} {N}x{H}x{W} MB {2 * N * C * (H * W + Ho * Wo) / 1e6:.1f}"
+            elif _n in ("hiseg_bn_stats",):
+                key = f"P{a[2]} C{a[3]} MB {2 * a[2] * a[3] / 1e6:.1f}"
             rec.append((_n, key, e0, e1))
             return r
         setattr(lib, name, wrap)
