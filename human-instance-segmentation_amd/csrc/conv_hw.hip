@@ -111,10 +111,14 @@ __global__ void __launch_bounds__(256, 1) conv_hw_kernel(ConvArgs a) {
     const bool ok = hr < kHaloRows && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
     const bool fb = 32 * sl >= d.Ca;
     const int cs = fb ? d.b_cstride : d.a_cstride, coff = fb ? d.b_coff + 32 * sl - d.Ca : d.a_coff + 32 * sl;
-    return ok ? (unsigned)((((n * d.H + iy) * d.W + ix) * cs + coff + (slot ^ hhswz(hr)) * 8) * 2) : OOB;
+    // src A of an smp decoder conv1 is the nearest-x2 upsampled low-resolution map: halo pixel (iy, ix) reads
+    // source pixel (iy / 2, ix / 2) of the (H / 2, W / 2) grid
+    const int ush = (!fb && d.a_up == 2) ? 1 : 0;
+    const int sy = iy >> ush, sx = ix >> ush, sH = d.H >> ush, sW = d.W >> ush;
+    return ok ? (unsigned)((((n * sH + sy) * sW + sx) * cs + coff + (slot ^ hhswz(hr)) * 8) * 2) : OOB;
   };
   const int nrec_w = d.Cout_pad * d.K_pad * 2;
-  const int nrec_a = d.N * d.H * d.W * d.a_cstride * 2;
+  const int nrec_a = d.N * (d.H / d.a_up) * (d.W / d.a_up) * d.a_cstride * 2;
   const int nrec_b = d.Cb ? d.N * d.H * d.W * d.b_cstride * 2 : 0;
   const int nsl = a.Cin >> 5;          // 32-channel slices
   const int nS = 9 * nsl;
@@ -429,9 +433,11 @@ int launch_hw64(const ConvArgs& a, hipStream_t s, bool reuse);
 int conv_hw_try(const ConvArgs& a, hipStream_t s, int variant) {
   const hiseg_conv2d_desc& d = a.d;
   if (d.dtype != HISEG_BF16 || d.out_dtype != HISEG_BF16) return 0;
-  if (d.a_up != 1 || d.in_scale != nullptr || d.convT || d.mul != nullptr || d.out2 != nullptr) return 0;
+  if (d.in_scale != nullptr || d.convT || d.mul != nullptr || d.out2 != nullptr) return 0;
   if (d.KH != 3 || d.KW != 3 || d.stride != 1 || d.pad != 1 || d.Ho != d.H || d.Wo != d.W) return 0;
   if (d.act != HISEG_ACT_NONE && d.act != HISEG_ACT_RELU) return 0;
+  // src A nearest-x2 upsampled (smp decoder conv1): even grid (conv2d_impl checks)
+  if (d.a_up != 1 && d.a_up != 2) return 0;
   // two sources (concat): each whole 32-channel slice from one of them
   if (d.Ca % 32 != 0 || d.Cb % 32 != 0 || d.Ca < 64 || d.K_pad != 9 * (d.Ca + d.Cb)) return 0;
   if ((d.a_cstride | d.a_coff) & 7) return 0;
@@ -443,7 +449,7 @@ int conv_hw_try(const ConvArgs& a, hipStream_t s, int variant) {
   if (((d.Cout & cmul) && !narrow) || ((d.o_cstride | d.o_coff) & 7) || (d.residual && ((d.r_cstride | d.r_coff) & 7)))
     return 0;
   if ((((uintptr_t)d.scale | (uintptr_t)d.shift | (uintptr_t)d.out | (uintptr_t)d.residual) & 15)) return 0;
-  const long long span_a = (long long)d.N * d.H * d.W * d.a_cstride * 2;
+  const long long span_a = (long long)d.N * (d.H / d.a_up) * (d.W / d.a_up) * d.a_cstride * 2;
   const long long span_b = d.Cb ? (long long)d.N * d.H * d.W * d.b_cstride * 2 : 0;
   const long long span_w = (long long)d.Cout_pad * d.K_pad * 2;
   const long long span_r = d.residual ? (long long)a.M * d.r_cstride * 2 : 0;

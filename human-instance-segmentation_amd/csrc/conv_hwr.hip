@@ -22,8 +22,6 @@ namespace hiseg {
 
 typedef unsigned hr_u4 __attribute__((ext_vector_type(4)));
 
-constexpr int kHrHaloRows = 324;          // 18 x 18
-constexpr int kHrHaloBytes = 24 * 1024;   // 24 pieces of 16 rows x 64 B (rows 324..383 unused)
 
 __device__ __forceinline__ int hr_hswz(int r) { return ((r >> 2) & 1) << 1; }   // halo rows (any start)
 
@@ -37,19 +35,31 @@ typedef __attribute__((address_space(3))) void hr_lds_void;
 // SCH (schedule of a K step): bit 1 -- s_setprio 1 around the MFMA groups (the co-resident workgroup's wave yields
 // its issue slots to them); bit 2 -- B-fragment reuse across ky (below).  Bit 0 is unused (an earlier interleaving
 // of the B reads between the last group's MFMAs measured slower: the variant numbers stay for the A/B record).
-template <int ACT, bool RES, int SCH>
-__global__ void __launch_bounds__(256, 2) conv_hwr_kernel(ConvArgs a) {
-  constexpr int BCO = 128, TM = 4, TN = 8;
+// UP: src A is the nearest-x2 upsampled low-resolution map of an smp decoder conv1 (halo pixel (iy, ix) reads
+// source pixel (iy / 2, ix / 2)); a template flag so the dominant class's code is untouched.
+// WCO x TWB: waves along Cout (BCO = 64 WCO) x 16-column pixel blocks of the tile (TW = 16 TWB): (2, 1) is the
+// 128-Cout x 16 x 16 workgroup of four waves; (1, 2) a 64-Cout x 16 x 32 workgroup of four waves (the 64-channel
+// layers: every wave keeps the 64 x 128 wave tile); (2, 2) 128 Cout x 16 x 32 with eight waves.  The per-element
+// accumulation order is the same for every configuration: results are bit-identical across them.
+template <int ACT, bool RES, int SCH, bool UP = false, int WCO = 2, int TWB = 1>
+__global__ void __launch_bounds__(WCO * TWB * 128, (WCO * TWB > 2) ? 1 : 2) conv_hwr_kernel(ConvArgs a) {
+  constexpr int BCO = 64 * WCO, TM = 4, TN = 8;
+  constexpr int TW = 16 * TWB, NPW = 2 * TWB, NW = WCO * NPW, HWD = TW + 2;
+  constexpr int NHR = 18 * HWD;                          // halo rows (pixels) of a slice
+  constexpr int PPW = ((NHR + 15) / 16 + NW - 1) / NW;   // halo pieces (16 rows, 1 KiB) per wave per slice
+  constexpr int HB = PPW * NW * 1024;                    // bytes of one halo buffer
+  constexpr int NPX = 16 * TW;                           // output pixels of the tile
+  static_assert(PPW <= 12 && (WCO == 1 || WCO == 2) && (TWB == 1 || TWB == 2), "configuration");
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   const hiseg_conv2d_desc& d = a.d;
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wco = w >> 1, wpx = w & 1;
+  const int wco = w / NPW, wpx = w % NPW;   // pixel wave: tile rows 8 (wpx & 1) .. + 7, columns 16 (wpx >> 1) .. + 15
 
   // ---- XCD-major bijective remap; Cout tiles fastest (the tiles of one pixel block share its halo in L2)
   const int nco = d.Cout_pad / BCO;
-  const int ntx = (d.W + 15) >> 4, nty = (d.H + 15) >> 4;
+  const int ntx = (d.W + TW - 1) / TW, nty = (d.H + 15) >> 4;
   const int nwg = gridDim.x;
   const int orig = blockIdx.x;
   const int q8 = nwg >> 3, r8 = nwg & 7, xcd = orig & 7, loc = orig >> 3;
@@ -60,15 +70,16 @@ __global__ void __launch_bounds__(256, 2) conv_hwr_kernel(ConvArgs a) {
   tl /= ntx;
   const int ty = tl % nty;
   const int n = tl / nty;
-  const int y0 = ty * 16, x0 = tx * 16;
+  const int y0 = ty * 16, x0 = tx * TW;
 
   const unsigned OOB = 0x80000000u;   // >= num_records: loads return zeros
   const int nsl = a.Cin >> 5;         // 32-channel slices (even: Cin % 64 == 0)
   const int ncb = a.Cin >> 6;
   const __amdgpu_buffer_rsrc_t rF = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(d.weight_frag), (short)0, d.Cout_pad * 9 * a.Cin * 2, 0x00020000);
+  constexpr int USH = UP ? 1 : 0;
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<void*>(d.srcA), (short)0, d.N * d.H * d.W * d.a_cstride * 2, 0x00020000);
+      const_cast<void*>(d.srcA), (short)0, d.N * (d.H >> USH) * (d.W >> USH) * d.a_cstride * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(d.Cb ? d.srcB : d.srcA), (short)0, d.Cb ? d.N * d.H * d.W * d.b_cstride * 2 : 0, 0x00020000);
 
@@ -97,26 +108,33 @@ __global__ void __launch_bounds__(256, 2) conv_hwr_kernel(ConvArgs a) {
   auto halo_dma = [&](int p, int sl, int buf) __attribute__((always_inline)) {
     int ln = lane;
     asm volatile("" : "+v"(ln));
-    const int hr = 16 * (4 * p + w) + (ln >> 2);
-    const int hy = hr / 18, hx = hr - 18 * hy;
+    const int hr = 16 * (NW * p + w) + (ln >> 2);
+    const int hy = hr / HWD, hx = hr - HWD * hy;
     const int iy = y0 + hy - 1, ix = x0 + hx - 1;
-    const bool ok = hr < kHrHaloRows && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+    const bool ok = hr < NHR && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
     const int chunk = (ln & 3) ^ (((hx >> 2) & 1) << 1);
     const bool fb = 32 * sl >= d.Ca;
     const int cs = fb ? d.b_cstride : d.a_cstride, coff = fb ? d.b_coff + 32 * sl - d.Ca : d.a_coff + 32 * sl;
-    const unsigned off = ok ? (unsigned)((((n * d.H + iy) * d.W + ix) * cs + coff + chunk * 8) * 2) : OOB;
-    hr_dma16(fb ? rB : rA, lds_base + (unsigned)(buf * kHrHaloBytes + 1024 * (4 * p + w)), off);
+    unsigned off;
+    if constexpr (UP) {
+      const int ush = fb ? 0 : 1;
+      off = ok ? (unsigned)((((n * (d.H >> ush) + (iy >> ush)) * (d.W >> ush) + (ix >> ush)) * cs + coff + chunk * 8) * 2)
+               : OOB;
+    } else {
+      off = ok ? (unsigned)((((n * d.H + iy) * d.W + ix) * cs + coff + chunk * 8) * 2) : OOB;
+    }
+    hr_dma16(fb ? rB : rA, lds_base + (unsigned)(buf * HB + 1024 * (NW * p + w)), off);
   };
   char* lds_c = reinterpret_cast<char*>(smem);
   // B fragment: pixel (tile row wpx*8 + j, column lane % 16) at tap (ky, kx), channels 8 (lane / 16) .. + 7:
   // halo row (wpx * 8 + j + ky, lane % 16 + kx)
   auto bsw = [&](int ln, int kx) __attribute__((always_inline)) -> int {
-    const int hx = (ln & 15) + kx;
-    return (wpx * TN * 18 + hx) * 64 + (((ln >> 4) ^ (((hx >> 2) & 1) << 1)) << 4);
+    const int hx = (ln & 15) + kx + 16 * (wpx >> 1);
+    return ((wpx & 1) * TN * HWD + hx) * 64 + (((ln >> 4) ^ (((hx >> 2) & 1) << 1)) << 4);
   };
   auto rdB = [&](int ln, int buf, int tap, int j) __attribute__((always_inline)) -> hr_u4 {
     const int ky = tap / 3, kx = tap - 3 * (tap / 3);
-    return *reinterpret_cast<const hr_u4*>(lds_c + bsw(ln, kx) + buf * kHrHaloBytes + (j + ky) * 18 * 64);
+    return *reinterpret_cast<const hr_u4*>(lds_c + bsw(ln, kx) + buf * HB + (j + ky) * HWD * 64);
   };
 
   floatx4 acc[TM][TN];
@@ -129,9 +147,9 @@ __global__ void __launch_bounds__(256, 2) conv_hwr_kernel(ConvArgs a) {
   constexpr int NBMAX = TN + 2;
   hr_u4 af[TM], bf[NBMAX];
 #pragma unroll
-  for (int p = 0; p < 6; ++p) halo_dma(p, 0, 0);
+  for (int p = 0; p < PPW; ++p) halo_dma(p, 0, 0);
   load_a(af, 0, 0);
-  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // the 6 halo pieces (older than the 4 A loads)
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // the halo pieces (older than the 4 A loads)
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < ((SCH & 4) ? TN + 2 : TN); ++k) bf[k] = rdB(lane, 0, 0, k);
@@ -183,8 +201,11 @@ __global__ void __launch_bounds__(256, 2) conv_hwr_kernel(ConvArgs a) {
       }
     }
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (st < 6) {
-      if (more) halo_dma(st, sl + 1, buf ^ 1);
+    if constexpr (st < 6) {   // pieces st, st + 6 of slice sl + 1's halo
+      if (more) {
+#pragma unroll
+        for (int p = st; p < PPW; p += 6) halo_dma(p, sl + 1, buf ^ 1);
+      }
     }
     if constexpr (st == 8) {
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -218,21 +239,21 @@ __global__ void __launch_bounds__(256, 2) conv_hwr_kernel(ConvArgs a) {
   constexpr int SWM = CPR - 1;
   char* tile = reinterpret_cast<char*>(smem);
   auto px_of = [&](int r) __attribute__((always_inline)) -> int {
-    const int y = y0 + (r >> 4), x = x0 + (r & 15);
+    const int y = y0 + r / TW, x = x0 + r % TW;
     return (y < d.Ho && x < d.Wo) ? (n * d.Ho + y) * d.Wo + x : -1;
   };
   if constexpr (RES) {
     const int nrec_r = a.M * d.r_cstride * 2;
     const __amdgpu_buffer_rsrc_t rR = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(d.residual), (short)0, nrec_r,
                                                                        0x00020000);
-    constexpr int NRI = 256 / (RPI * 4);
+    constexpr int NRI = NPX / (RPI * NW);
     const int c = lane % CPR;
 #pragma unroll
     for (int k = 0; k < NRI; ++k) {
-      const int r = RPI * (w + 4 * k) + lane / CPR;
+      const int r = RPI * (w + NW * k) + lane / CPR;
       const int px = px_of(r);
       const unsigned off = px >= 0 ? (unsigned)((px * d.r_cstride + d.r_coff + co0 + ((c ^ (r & SWM)) * 8)) * 2) : OOB;
-      hr_dma16(rR, lds_base + (unsigned)(RPI * (w + 4 * k) * EROWB), off);
+      hr_dma16(rR, lds_base + (unsigned)(RPI * (w + NW * k) * EROWB), off);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -250,7 +271,7 @@ __global__ void __launch_bounds__(256, 2) conv_hwr_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int cl = wco * TM * 16 + i * 16 + (lane >> 4) * 4;
-      const int r = wpx * TN * 16 + j * 16 + (lane & 15);
+      const int r = ((wpx & 1) * TN + j) * TW + 16 * (wpx >> 1) + (lane & 15);
       char* q = tile + r * EROWB + ((((cl >> 3) ^ (r & SWM)) << 4) | ((cl & 4) << 1));
       const floatx4 ac = acc[i][j];
       float v[4];
@@ -268,10 +289,10 @@ __global__ void __launch_bounds__(256, 2) conv_hwr_kernel(ConvArgs a) {
       *reinterpret_cast<uint2*>(q) = o;
     }
   __syncthreads();
-  constexpr int NST = CPR;   // 256 rows x CPR chunks over 256 threads
+  constexpr int NST = NPX * CPR / (NW * 64);   // NPX rows x CPR chunks over the workgroup's threads
 #pragma unroll 4
   for (int k = 0; k < NST; ++k) {
-    const int idx = t + 256 * k;
+    const int idx = t + NW * 64 * k;
     const int r = idx / CPR, c = idx % CPR;
     const int px = px_of(r), co = co0 + 8 * c;
     const uint4 v = *reinterpret_cast<const uint4*>(tile + r * EROWB + ((c ^ (r & SWM)) << 4));
@@ -280,57 +301,81 @@ __global__ void __launch_bounds__(256, 2) conv_hwr_kernel(ConvArgs a) {
   }
 }
 
-template <int ACT, bool RES, int SCH>
+template <int ACT, bool RES, int SCH, bool UP = false, int WCO = 2, int TWB = 1>
 static int launch_hwr(const ConvArgs& a, hipStream_t s) {
   const hiseg_conv2d_desc& d = a.d;
-  const int tiles = d.N * ((d.H + 15) / 16) * ((d.W + 15) / 16);
-  const int nco = d.Cout_pad / 128;
-  const size_t lds = (size_t)256 * 128 * 2;   // >= 2 halo buffers (48 KiB)
-  auto kern = conv_hwr_kernel<ACT, RES, SCH>;
+  constexpr int BCO = 64 * WCO, TW = 16 * TWB, NW = WCO * 2 * TWB;
+  constexpr int PPW = ((18 * (TW + 2) + 15) / 16 + NW - 1) / NW;
+  constexpr size_t halo2 = (size_t)2 * PPW * NW * 1024, epi = (size_t)16 * TW * BCO * 2;
+  const int tiles = d.N * ((d.H + 15) / 16) * ((d.W + TW - 1) / TW);
+  const int nco = d.Cout_pad / BCO;
+  const size_t lds = halo2 > epi ? halo2 : epi;
+  auto kern = conv_hwr_kernel<ACT, RES, SCH, UP, WCO, TWB>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL(kern, dim3(tiles * nco), dim3(256), lds, s, a);
+  hipLaunchKernelGGL(kern, dim3(tiles * nco), dim3(NW * 64), lds, s, a);
   return hiseg_check_launch("conv_hwr");
 }
 
 template <int SCH>
 static int launch_hwr_sch(const ConvArgs& a, hipStream_t s) {
   const hiseg_conv2d_desc& d = a.d;
+  if constexpr (SCH == 6) {
+    if (d.a_up == 2) return launch_hwr<HISEG_ACT_RELU, false, 6, true>(a, s);   // (conv_hwr_try checked the form)
+  }
   const bool res = d.residual != nullptr, relu = d.act == HISEG_ACT_RELU;
   return res ? (relu ? launch_hwr<HISEG_ACT_RELU, true, SCH>(a, s) : launch_hwr<HISEG_ACT_NONE, true, SCH>(a, s))
              : (relu ? launch_hwr<HISEG_ACT_RELU, false, SCH>(a, s) : launch_hwr<HISEG_ACT_NONE, false, SCH>(a, s));
 }
 
+// the 16 x 32-pixel configurations (SCH 6): ReLU / none, residual or not, upsampled src A (decoder conv1 form)
+template <int WCO>
+static int launch_hwr_wide(const ConvArgs& a, hipStream_t s) {
+  const hiseg_conv2d_desc& d = a.d;
+  if (d.a_up == 2) return launch_hwr<HISEG_ACT_RELU, false, 6, true, WCO, 2>(a, s);
+  const bool res = d.residual != nullptr, relu = d.act == HISEG_ACT_RELU;
+  return res ? (relu ? launch_hwr<HISEG_ACT_RELU, true, 6, false, WCO, 2>(a, s)
+                     : launch_hwr<HISEG_ACT_NONE, true, 6, false, WCO, 2>(a, s))
+             : (relu ? launch_hwr<HISEG_ACT_RELU, false, 6, false, WCO, 2>(a, s)
+                     : launch_hwr<HISEG_ACT_NONE, false, 6, false, WCO, 2>(a, s));
+}
+
 // 1 = launched, 0 = the layer does not qualify (caller falls back), <0 on error.  Variants 92..95 = SCH 0..3,
-// 96 = SCH 4 (B reuse across ky), 97 = SCH 6 (reuse + priority).
+// 96 = SCH 4 (B reuse across ky), 97 = SCH 6 (reuse + priority); 100 = SCH 6 on 64-Cout x 16 x 32-pixel tiles
+// (64-multiple Cout), 101 = SCH 6 on 128-Cout x 16 x 32-pixel tiles with eight waves.
 int conv_hwr_try(const ConvArgs& a, hipStream_t s, int variant) {
   const hiseg_conv2d_desc& d = a.d;
-  if (variant < 92 || variant > 97 || d.weight_frag == nullptr) return 0;
+  if (!((variant >= 92 && variant <= 97) || variant == 100 || variant == 101) || d.weight_frag == nullptr) return 0;
   if (d.dtype != HISEG_BF16 || d.out_dtype != HISEG_BF16) return 0;
-  if (d.a_up != 1 || d.in_scale != nullptr || d.convT || d.mul != nullptr || d.out2 != nullptr) return 0;
+  if ((d.a_up != 1 && d.a_up != 2) || d.in_scale != nullptr || d.convT || d.mul != nullptr || d.out2 != nullptr)
+    return 0;
   if (d.KH != 3 || d.KW != 3 || d.stride != 1 || d.pad != 1 || d.Ho != d.H || d.Wo != d.W) return 0;
   if (d.act != HISEG_ACT_NONE && d.act != HISEG_ACT_RELU) return 0;
   if (d.Ca % 32 != 0 || d.Cb % 32 != 0 || (d.Ca + d.Cb) % 64 != 0 || d.Ca < 64 || d.K_pad != 9 * (d.Ca + d.Cb))
     return 0;
   if ((d.a_cstride | d.a_coff) & 7) return 0;
   if (d.Cb && (d.srcB == nullptr || ((d.b_cstride | d.b_coff) & 7))) return 0;
-  if ((d.Cout & 127) || d.Cout_pad != d.Cout || ((d.o_cstride | d.o_coff) & 7) ||
+  if ((d.Cout & (variant == 100 ? 63 : 127)) || d.Cout_pad != d.Cout || ((d.o_cstride | d.o_coff) & 7) ||
       (d.residual && ((d.r_cstride | d.r_coff) & 7)))
     return 0;
   if ((((uintptr_t)d.scale | (uintptr_t)d.shift | (uintptr_t)d.out | (uintptr_t)d.residual |
         (uintptr_t)d.weight_frag) & 15))
     return 0;
-  const long long span_a = (long long)d.N * d.H * d.W * d.a_cstride * 2;
+  const long long span_a = (long long)d.N * (d.H / d.a_up) * (d.W / d.a_up) * d.a_cstride * 2;
   const long long span_b = d.Cb ? (long long)d.N * d.H * d.W * d.b_cstride * 2 : 0;
   const long long span_w = (long long)d.Cout_pad * d.K_pad * 2;
   const long long span_r = d.residual ? (long long)a.M * d.r_cstride * 2 : 0;
   if (span_a >= 0x7fffffffll || span_b >= 0x7fffffffll || span_w >= 0x7fffffffll || span_r >= 0x7fffffffll) return 0;
   if ((long long)d.N * d.H * d.W >= (1ll << 29)) return 0;   // halo source pixel packed with its chunk in 31 bits
+  // upsampled src A: the smp decoder conv1 form only (ReLU, no residual), automatic schedule (variant 97)
+  if (d.a_up == 2 && (variant < 97 || d.residual || d.act != HISEG_ACT_RELU)) return 0;
   int r;
   switch (variant) {
+    case 100: r = launch_hwr_wide<1>(a, s); break;
+    case 101: r = launch_hwr_wide<2>(a, s); break;
     case 92: r = launch_hwr_sch<0>(a, s); break;
     case 93: r = launch_hwr_sch<1>(a, s); break;
     case 94: r = launch_hwr_sch<2>(a, s); break;

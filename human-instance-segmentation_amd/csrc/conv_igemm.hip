@@ -364,7 +364,7 @@ extern "C" int hiseg_conv2d_fwd(const hiseg_conv2d_desc* d, hiseg_stream_t strea
 static bool release_variant(int v) {
   return v == -1 || v == 0 || (v >= 1 && v <= 8) || v == 50 || v == 51 || v == 52 || v == 54 || v == 58 ||
          (v >= 60 && v <= 69) || v == 70 || v == 71 || v == 72 || v == 74 || v == 80 || v == 82 || v == 84 || v == 86 ||
-         v == 88 || v == 89 || v == 90 || (v >= 92 && v <= 99);
+         v == 88 || v == 89 || v == 90 || (v >= 92 && v <= 101);
 }
 
 // Workspace bytes the automatic choice uses for this layer (split-K generic kernel), 0 when it needs none.
@@ -484,7 +484,7 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
   } else if (variant == 90) {
     const int r = conv_pw_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
-  } else if (variant >= 92 && variant <= 97) {
+  } else if ((variant >= 92 && variant <= 97) || variant == 100 || variant == 101) {
     const int r = conv_hwr_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
   } else if (variant >= 80 && variant < 90) {
@@ -538,6 +538,12 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
     // on 128->256; bit-identical to variant 86)
     if (v == 0 && !four_waves && halo && d->weight_frag != nullptr && d->Cout % 128 == 0) {
       const int r = conv_hwr_try(a, s, 97);
+      if (r != 0) return r < 0 ? r : HISEG_OK;
+    }
+    // 64-multiple Cout (the EnhancedUNet's 64-channel layers, the smp decoder's 64-channel block): the same kernel on
+    // 64-Cout x 16 x 32-pixel tiles (variant 100)
+    if (v == 0 && !four_waves && halo && d->weight_frag != nullptr && d->Cout % 64 == 0) {
+      const int r = conv_hwr_try(a, s, 100);
       if (r != 0) return r < 0 ? r : HISEG_OK;
     }
     if (v == 0 && !four_waves && halo) {

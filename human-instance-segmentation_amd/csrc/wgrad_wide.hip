@@ -44,17 +44,20 @@ __device__ __forceinline__ ww_v4s_t ww_tr(unsigned byte_addr) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((ww_lds_v4s_t*)(uintptr_t)byte_addr);
 }
 
-template <int BC, int NW>
+template <int BC, int NW, int PB, int STAGES>
 __global__ void __launch_bounds__(NW * 64, 1) conv_wgrad_wide_kernel(WgradArgs a) {
-  constexpr int BK = 256, PB = 64;
+  constexpr int BK = 256;
+  constexpr int KS = PB / 32;              // 32-pixel k-steps per stage
   constexpr int NXH = 2, NYH = BC / 128;   // 128-column images per stage
-  constexpr int NI = 16 / NW;              // DMA instructions per image per wave (4 rows each, 64 rows)
+  constexpr int NI = PB / (4 * NW);        // DMA instructions per image per wave (4 rows each, PB rows)
+  constexpr int NLW = NI * (NXH + NYH);    // DMA instructions per wave per stage
   constexpr int WCN = NW / 2;              // waves along C
   constexpr int WCOLS = BC / WCN;          // a wave's C columns
   constexpr int TM = 8, TN = WCOLS / 16;   // wave tile 128 (K) x WCOLS (C)
   constexpr int IMG = PB * 256;
   constexpr int STAGE = (NXH + NYH) * IMG;
-  static_assert((BC == 128 || BC == 256) && (NW == 4 || NW == 8) && TN >= 1, "tile");
+  static_assert((BC == 128 || BC == 256) && (NW == 4 || NW == 8) && TN >= 1 && NI >= 1 && (KS == 1 || KS == 2) &&
+                STAGES >= 2, "tile");
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   const hiseg_conv2d_desc& d = a.d;
   const int t = threadIdx.x, lane = t & 63;
@@ -66,9 +69,10 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_wgrad_wide_kernel(WgradArgs a
   const int q8 = nwg >> 3, r8 = nwg & 7, xcd = orig & 7, loc = orig >> 3;
   const int wgi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
   const int k0 = (wgi % nkt) * BK, j0 = ((wgi / nkt) % nct) * BC, split = wgi / (nkt * nct);
-  const int pb_begin = split * a.blocks_per_split;
+  // blocks_per_split counts 64-pixel blocks (wgrad_geometry); stages of PB pixels
+  const int pb_begin = split * a.blocks_per_split * (64 / PB);
   const int nblocks = (a.M + PB - 1) / PB;
-  int pb_end = pb_begin + a.blocks_per_split;
+  int pb_end = pb_begin + a.blocks_per_split * (64 / PB);
   if (pb_end > nblocks) pb_end = nblocks;
   const int nit = pb_end > pb_begin ? pb_end - pb_begin : 0;
 
@@ -183,11 +187,15 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_wgrad_wide_kernel(WgradArgs a
   const int yimg = (wc * WCOLS) / 128;
   const int ych0 = ((wc * WCOLS) % 128) / 8;
 
-  if (nit > 0) issue(0);
+#pragma unroll
+  for (int s0 = 0; s0 < STAGES - 1; ++s0)
+    if (s0 < nit) issue(s0);
   for (int it = 0; it < nit; ++it) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int cur = it % STAGES;
+    if (STAGES > 2 && it + STAGES - 2 < nit) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NLW * (STAGES - 2)) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (bias_lanes) {   // the GEMM-bias column: X = 1 in every row, written over the landed DMA zeros
-      const unsigned sb = lds_base + (unsigned)((it & 1) * STAGE);
+      const unsigned sb = lds_base + (unsigned)(cur * STAGE);
 #pragma unroll
       for (int h = 0; h < NXH; ++h)
 #pragma unroll
@@ -200,10 +208,11 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_wgrad_wide_kernel(WgradArgs a
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();   // stage it landed everywhere; every wave left stage it-1's buffer
     asm volatile("" ::: "memory");
-    const bool more = it + 1 < nit;
+    const int nxt = it + STAGES - 1;   // the stage whose DMA this iteration issues (into stage it-1's buffer)
+    const bool more = nxt < nit;
 
-    const unsigned sX = lds_base + (unsigned)((it & 1) * STAGE) + (unsigned)(wk * IMG);
-    const unsigned sY = lds_base + (unsigned)((it & 1) * STAGE) + (unsigned)((NXH + yimg) * IMG);
+    const unsigned sX = lds_base + (unsigned)(cur * STAGE) + (unsigned)(wk * IMG);
+    const unsigned sY = lds_base + (unsigned)(cur * STAGE) + (unsigned)((NXH + yimg) * IMG);
     // k-step 0 fragments, then per A row i: its MFMAs, after which af[i] takes row i of k-step 1 (the reads land
     // under the remaining rows' MFMAs); k-step 1's B fragments after the last row
     bf16x8_t af[TM], bfr[TN];
@@ -224,17 +233,17 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_wgrad_wide_kernel(WgradArgs a
 #pragma unroll
     for (int i = 0; i < TM; ++i) af[i] = rdA(0, i);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < KS; ++ks) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
-        if (ks == 0) af[i] = rdA(1, i);
-        if (ks == 0 && more && i < 2 * NI) issue_part((it + 1) & 1, i);
+        if (ks + 1 < KS) af[i] = rdA(1, i);
+        if (ks == 0 && more && i < 2 * NI) issue_part(nxt % STAGES, i);
       }
-      if (ks == 0) {
+      if (ks + 1 < KS) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) bfr[j] = rdB(1, j);
       }
@@ -285,10 +294,10 @@ int wgrad_wide_bc(const hiseg_conv2d_desc* d, int Cg, int Kg, int Cin, int M, in
   return Cg % 256 == 0 ? 256 : 0;   // (the 256 x 128 tile measured slower than the 128 x 128 kernel)
 }
 
-template <int BC, int NW>
+template <int BC, int NW, int PB, int STAGES>
 static int wide_launch(const WgradArgs& a, hipStream_t s) {
-  constexpr size_t lds = (size_t)2 * (2 + BC / 128) * 64 * 256;
-  auto kern = conv_wgrad_wide_kernel<BC, NW>;
+  constexpr size_t lds = (size_t)STAGES * (2 + BC / 128) * PB * 256;
+  auto kern = conv_wgrad_wide_kernel<BC, NW, PB, STAGES>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -306,7 +315,9 @@ int wgrad_wide_try(const WgradArgs& a, hipStream_t s) {
   // four waves, one per SIMD, 128 x 128 wave tiles in AGPRs.  (Eight waves at two per SIMD with 128 x 64 wave tiles
   // spill 76 B per lane and ran 1.74 ms on the 256-channel class; this form 1.19 ms, conv_wgrad_tr_kernel 1.31 ms,
   // same box, tools/wgrad_bench.py.)
-  const int r = wide_launch<256, 4>(a, s);
+  // (32-pixel stages in a 4-deep ring, the same kernel at <256, 4, 32, 4>: 1.229 vs 1.212 ms, same box -- the
+  // DMA lookahead is not what holds it at ~0.31 of peak)
+  const int r = wide_launch<256, 4, 64, 2>(a, s);
   return r < 0 ? r : 1;
 }
 

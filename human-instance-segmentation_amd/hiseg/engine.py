@@ -27,7 +27,7 @@ from . import _lib as L
 from . import ops
 from .effunet import DepthwiseSeparableConv, InvertedResidual
 from .layers import LayerNorm2d, Swish
-from .ops import Act
+from .ops import Act, round_up
 
 ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_SILU = L.ACT_NONE, L.ACT_RELU, L.ACT_SIGMOID, L.ACT_SILU
 ACT_GELU, ACT_SWISH = L.ACT_GELU, L.ACT_SWISH
@@ -336,17 +336,24 @@ def _dw_se(E: Ctx, conv: nn.Conv2d, bn, se: nn.Module, x: Act) -> Tuple[Act, tor
                               E.f32(se.conv_expand.bias), ACT_SILU)
 
 
-def mbconv(E: Ctx, blk: nn.Module, x: Act) -> Act:
+def mbconv(E: Ctx, blk: nn.Module, x: Act, out_cpad: Optional[int] = None) -> Act:
     """timm DepthwiseSeparableConv / InvertedResidual (eval): the SE pool is fused into the depthwise conv,
-    the SE gate is applied inside the projection conv's loader (in_scale), the skip add in its epilogue."""
+    the SE gate is applied inside the projection conv's loader (in_scale), the skip add in its epilogue.
+    ``out_cpad``: channel stride of the block output (zero pad channels)."""
     if isinstance(blk, DepthwiseSeparableConv):
         h, g = _dw_se(E, blk.conv_dw, blk.bn1, blk.se, x)
-        return ops.conv2d(E.conv(blk.conv_pw, blk.bn2), h, in_scale=g, residual=x if blk.has_skip else None)
+        return ops.conv2d(E.conv(blk.conv_pw, blk.bn2), h, in_scale=g, residual=x if blk.has_skip else None,
+                          out_cpad=out_cpad)
     if isinstance(blk, InvertedResidual):
         h = ops.conv2d(E.conv(blk.conv_pw, blk.bn1, ACT_SILU), x)
         h, g = _dw_se(E, blk.conv_dw, blk.bn2, blk.se, h)
-        return ops.conv2d(E.conv(blk.conv_pwl, blk.bn3), h, in_scale=g, residual=x if blk.has_skip else None)
+        return ops.conv2d(E.conv(blk.conv_pwl, blk.bn3), h, in_scale=g, residual=x if blk.has_skip else None,
+                          out_cpad=out_cpad)
     raise TypeError(type(blk))
+
+
+def _block_out_channels(blk: nn.Module) -> int:
+    return (blk.conv_pw if isinstance(blk, DepthwiseSeparableConv) else blk.conv_pwl).out_channels
 
 
 def unet_logit(E: Ctx, pre: nn.Module, images: torch.Tensor) -> torch.Tensor:
@@ -365,15 +372,23 @@ def effunet_forward(E: Ctx, net: nn.Module, x: Act) -> torch.Tensor:
     x = ops.conv2d(E.conv(enc.conv_stem, enc.bn1, ACT_SILU), x)
     feats = [x]
     for si, stage in enumerate(enc.blocks):
-        for blk in stage:
-            x = mbconv(E, blk, x)
+        for bi, blk in enumerate(stage):
+            # the skip features of decoder blocks 0-2 (stage 2 / 3 / 5 outputs: 24 / 40 / 112 channels for B0-B1,
+            # 48 / 80 / 224 for B7) are stored with a 64-multiple channel stride, zero pad channels, so those
+            # blocks' conv1 (upsampled x ++ skip) takes the halo-tiled kernels instead of the generic one; the next
+            # stage reads the padded map through its channel stride
+            cpad = None
+            if E.dtype == torch.bfloat16 and si + 1 in (2, 3, 5) and bi == len(stage) - 1:
+                c = _block_out_channels(blk)
+                cpad = round_up(c, 64) if c % 64 else None
+            x = mbconv(E, blk, x, out_cpad=cpad)
         if si + 1 in (2, 3, 5, 7):
             feats.append(x)
     skips = feats[-2::-1]
     x = feats[-1]
     for i, blk in enumerate(net.decoder.blocks):
         skip = skips[i] if i < len(skips) else None
-        split = (x.C, skip.C) if skip is not None else None
+        split = (x.C, skip.C, skip.cstride) if skip is not None else None
         x = ops.conv2d(E.conv(blk.conv1[0], blk.conv1[1], ACT_RELU, split=split), x, skip, a_up=2)
         x = ops.conv2d(E.conv(blk.conv2[0], blk.conv2[1], ACT_RELU), x)
     u = Act.new(B, H, W, 1, torch.float32, E.device, cpad=1, zero=False)

@@ -191,14 +191,18 @@ def pack_conv(weight: torch.Tensor, bias: Optional[torch.Tensor], bn: Optional[t
     """Pack an nn.Conv2d weight [Cout, Cin, kh, kw] (+ eval BN + bias) for the implicit GEMM.
 
     ``split`` = (ca_real, cb_real) partitions the input channels into the two loader sources
-    (each padded to whole chunks); default: all channels from source A.
+    (each padded to whole chunks); default: all channels from source A.  A third entry pads source B's
+    channels further (zero weights) to that count -- a skip feature stored with a 64-multiple channel
+    stride so the decoder conv takes the halo-tiled kernels (engine.effunet_forward).
     """
     ce = chunk_elems(dtype)
     w = weight.detach().float()
     cout, cin, kh, kw = w.shape
-    ca_r, cb_r = split if split is not None else (cin, 0)
+    ca_r, cb_r = split[:2] if split is not None else (cin, 0)
     assert ca_r + cb_r == cin
     ca, cb = round_up(ca_r, ce), round_up(cb_r, ce)
+    if split is not None and len(split) > 2:
+        cb = max(cb, int(split[2]))
     wk = torch.zeros(cout, kh, kw, ca + cb, dtype=torch.float32, device=w.device)
     wt = w.permute(0, 2, 3, 1)
     wk[..., :ca_r] = wt[..., :ca_r]
@@ -272,8 +276,9 @@ def fold_affine(cout: int, bias: Optional[torch.Tensor], bn, device):
 def conv2d(p: ConvPlan, xa: Act, xb: Optional[Act] = None, out: Optional[Act] = None, *, a_up: int = 1,
            residual: Optional[Act] = None, mul: Optional[Act] = None, out2: Optional[Act] = None,
            in_scale: Optional[torch.Tensor] = None, out_dtype: Optional[torch.dtype] = None,
-           variant: int = 0) -> Act:
-    """hiseg_conv2d_fwd.  Returns the output Act (allocated when ``out`` is None).
+           variant: int = 0, out_cpad: Optional[int] = None) -> Act:
+    """hiseg_conv2d_fwd.  Returns the output Act (allocated when ``out`` is None; ``out_cpad``: its channel
+    stride, the pad channels zero).
 
     ``variant`` != 0 forces a kernel variant (hiseg_conv2d_fwd_variant; -1 = generic kernel).
     """
@@ -289,7 +294,8 @@ def conv2d(p: ConvPlan, xa: Act, xb: Optional[Act] = None, out: Optional[Act] = 
         Wo = (W + 2 * p.pad - p.kw) // p.stride + 1
         oH, oW = Ho, Wo
     if out is None:
-        out = Act.new(xa.N, oH, oW, p.cout, out_dtype or dt, xa.t.device)
+        out = Act.new(xa.N, oH, oW, p.cout, out_dtype or dt, xa.t.device, cpad=out_cpad,
+                      zero=None if out_cpad is None else out_cpad != p.cout)
     assert (out.N, out.H, out.W) == (xa.N, oH, oW), ((out.N, out.H, out.W), (xa.N, oH, oW))
     assert xa.C <= p.ca and (xb is None or xb.C <= p.cb)
     d = L.Conv2dDesc()

@@ -897,6 +897,40 @@ def test_conv_hwr_bit_identical_to_halo_kernel(name):
     assert torch.equal(auto, ys[97])   # the automatic choice takes variant 97
 
 
+@pytest.mark.parametrize("shape", [(2, 64, 0, 64, 64, 48, True), (3, 64, 0, 64, 21, 37, False), (2, 128, 0, 64, 16, 33, True),
+                                   (2, 64, 64, 64, 20, 31, False), (2, 256, 0, 128, 18, 40, True),
+                                   (2, 128, 128, 256, 9, 23, False), (1, 256, 0, 256, 64, 48, True)])
+def test_conv_hwr_wide_tile_bit_identical(shape):
+    """Variants 100 (64-Cout x 16 x 32-pixel tiles, four waves) and 101 (128-Cout x 16 x 32, eight waves): the same
+    per-element accumulation order as variant 97 / conv_hw's 86 and 89 (channel-major slices, kx-major taps) -- bit
+    for bit, ragged pixel tiles, residual, two sources; the automatic choice on 64-channel layers takes 100."""
+    from hiseg import ops
+    N, Ca, Cb, Cout, H, W, res = shape
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(29)
+    xa = ops.Act.from_nchw(torch.randn(N, Ca, H, W, device=DEV, generator=g), dt)
+    xb = ops.Act.from_nchw(torch.randn(N, Cb, H, W, device=DEV, generator=g), dt) if Cb else None
+    w = torch.randn(Cout, Ca + Cb, 3, 3, device=DEV, generator=g) / ((Ca + Cb) * 9) ** 0.5
+    p = ops.pack_conv(w, torch.randn(Cout, device=DEV, generator=g) * 0.1, None, 1, dt, DEV, pad=1,
+                      split=(Ca, Cb) if Cb else None)
+    assert p.weight_frag is not None
+    R = ops.Act.from_nchw(torch.randn(N, Cout, H, W, device=DEV, generator=g), dt) if res else None
+    y100 = ops.conv2d(p, xa, xb, residual=R, variant=100).t.clone()
+    ref = ops.conv2d(p, xa, xb, residual=R, variant=89).t.clone()
+    auto = ops.conv2d(p, xa, xb, residual=R, variant=0).t.clone()
+    if Cout % 128 == 0:
+        y97 = ops.conv2d(p, xa, xb, residual=R, variant=97).t.clone()
+        y101 = ops.conv2d(p, xa, xb, residual=R, variant=101).t.clone()
+    torch.cuda.synchronize()
+    assert torch.isfinite(y100.float()).all()
+    assert torch.equal(y100, ref)
+    if Cout % 128 == 0:
+        assert torch.equal(y97, ref) and torch.equal(y101, ref)
+        assert torch.equal(auto, y97)
+    else:
+        assert torch.equal(auto, y100)
+
+
 @pytest.mark.parametrize("shape", [(2, 128, 128, 128, 32, 24, False), (3, 64, 64, 128, 21, 13, True),
                                    (2, 192, 64, 256, 9, 23, True)])
 def test_conv_hwr_two_source_bit_identical(shape):
@@ -944,6 +978,47 @@ def test_conv_halo_two_source_within_bf16(shape, variant):
     assert torch.isfinite(y).all()
     assert ((y - ref).abs().max() / ref.abs().max()).item() < 8e-3
     assert ((auto - ref).abs().max() / ref.abs().max()).item() < 8e-3
+
+
+@pytest.mark.parametrize("shape", [(2, 320, 112, 128, 256, 12, 16, 97), (2, 256, 40, 64, 128, 10, 14, 97),
+                                   (2, 128, 24, 64, 64, 16, 20, 89), (1, 640, 224, 256, 256, 8, 8, 97),
+                                   (3, 128, 64, 64, 128, 6, 22, 86)])
+def test_conv_halo_upsampled_decoder_within_bf16(shape):
+    """smp decoder conv1 on the halo-tiled kernels (round 3): src A nearest-x2 upsampled from (H/2, W/2), src B the
+    encoder skip stored with a 64-multiple channel stride and zero pad channels (engine.effunet_forward).  The
+    forced halo variant and the automatic choice against the generic kernel on the same padded operands, and the
+    generic kernel on the padded operands against the unpadded layout (zero channels add exact zeros)."""
+    from hiseg import ops
+    N, Ca, Cb, Cbp, Cout, H, W, variant = shape
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(23)
+    xa = ops.Act.from_nchw(torch.randn(N, Ca, H // 2, W // 2, device=DEV, generator=g), dt)
+    skip = torch.randn(N, Cb, H, W, device=DEV, generator=g)
+    xb = ops.Act.from_nchw(skip, dt)
+    xbp = ops.Act.new(N, H, W, Cb, dt, DEV, cpad=Cbp, zero=True)
+    xbp.t.view(-1, Cbp)[:, :Cb].copy_(xb.t.view(-1, xb.cstride)[:, :Cb])
+    w = torch.randn(Cout, Ca + Cb, 3, 3, device=DEV, generator=g) / ((Ca + Cb) * 9) ** 0.5
+    bias = torch.randn(Cout, device=DEV, generator=g) * 0.1
+    p = ops.pack_conv(w, bias, None, 1, dt, DEV, pad=1, split=(Ca, Cb, Cbp))
+    p0 = ops.pack_conv(w, bias, None, 1, dt, DEV, pad=1, split=(Ca, Cb))
+    assert p.cb == Cbp
+    ref0 = ops.conv2d(p0, xa, xb, a_up=2, variant=-1).to_nchw().float()
+    ref = ops.conv2d(p, xa, xbp, a_up=2, variant=-1).to_nchw().float()
+    y = ops.conv2d(p, xa, xbp, a_up=2, variant=variant).to_nchw().float()
+    auto = ops.conv2d(p, xa, xbp, a_up=2, variant=0).to_nchw().float()
+    torch.cuda.synchronize()
+    assert torch.isfinite(y).all()
+    scale = ref.abs().max()
+    assert ((ref - ref0).abs().max() / scale).item() < 8e-3
+    assert ((y - ref).abs().max() / scale).item() < 8e-3
+    assert ((auto - ref).abs().max() / scale).item() < 8e-3
+    # the ReLU output against float64 of the same bf16 operands
+    up = torch.nn.functional.interpolate(xa.to_nchw().double(), scale_factor=2, mode="nearest")
+    xin = torch.cat([up, xb.to_nchw().double()], 1)
+    z = torch.relu(torch.nn.functional.conv2d(xin, p0.weight[:Cout, :9 * (p0.ca + p0.cb)].float().double()
+                                              .view(Cout, 3, 3, p0.ca + p0.cb).permute(0, 3, 1, 2)[:, :Ca + Cb],
+                                              bias.double(), padding=1))
+    assert ((y.double() - z).abs().max() / z.abs().max()).item() < 1e-2
 
 
 @pytest.mark.parametrize("name", list(VARIANT_CASES))

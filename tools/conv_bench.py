@@ -40,6 +40,10 @@ SHAPES = {
     "dec3_up64+32to32_3x3_240x320": (32, 64, 32, 32, 240, 320, 3, False, 2),
     "dec4_up32to16_3x3_480x640": (32, 32, 0, 16, 480, 640, 3, False, 2),
     "dec3_b7_up64+64to32_3x3_240x320": (8, 64, 64, 32, 240, 320, 3, False, 2),
+    # smp decoder blocks 0-2 with 64-multiple padded skips (round 3), B0 at 480x640 x 32 images
+    "dec0_up320+128to256_3x3_30x40": (32, 320, 128, 256, 30, 40, 3, False, 2),
+    "dec1_up256+64to128_3x3_60x80": (32, 256, 64, 128, 60, 80, 3, False, 2),
+    "dec2_up128+64to64_3x3_120x160": (32, 128, 64, 64, 120, 160, 3, False, 2),
 }
 
 

@@ -1,6 +1,7 @@
 """Average duration of bench.py's dominant launch class from a rocprofv3 kernel trace (developer tool).
 
-The dominant class is the 256->256 3x3 conv at the 64x48 ROI grid over 256 ROIs.  Round 2: the wide-tile
+The dominant class is the 256->256 3x3 conv at the 64x48 ROI grid over 256 ROIs.  Round 3: conv_hwr_kernel
+(6144 workgroups of 256, default); round 2: conv_hw_kernel<128> (--hw), before it the wide-tile
 kernel conv_wide_kernel<256, 4, ...> with 3072 pixel tiles x 1 Cout tile (grid 786 432 threads: 256-thread
 workgroups); round 1: conv_fast_kernel<128, 128, ...>, 12288 workgroups of 512 (--r1).  The kernel-stats
 summary averages every launch of a kernel (all layer shapes); this filters the trace to the class bench.py's
@@ -21,8 +22,10 @@ import sys
 R1 = "--r1" in sys.argv
 WIDE = "--wide" in sys.argv    # round 2 v1: conv_wide_kernel<256, 4>
 GRID = 12288 * 512 if R1 else (3072 * 256 if WIDE else 6144 * 256)
+HW = "--hw" in sys.argv        # round 2 v2-v12: conv_hw_kernel<128, ...>; default (round 3): conv_hwr_kernel
 PREFIX = ("void hiseg::conv_fast_kernel<128, 128" if R1 else
-          "void hiseg::conv_wide_kernel<256, 4" if WIDE else "void hiseg::conv_hw_kernel<128")
+          "void hiseg::conv_wide_kernel<256, 4" if WIDE else
+          "void hiseg::conv_hw_kernel<128" if HW else "void hiseg::conv_hwr_kernel<")
 allrows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 cut_t = next((int(r["Start_Timestamp"]) for r in allrows if "bn_stats" in r["Kernel_Name"]), None)
 rows = [r for r in allrows

@@ -5,7 +5,7 @@ keeps the launches before the first train-mode BatchNorm kernel (bn_stats) and, 
 those that start in the last T ms before that cut (the timed steps), then groups them by kernel name and
 grid size and prints total / average time, the share of the summed kernel time and the busy wall span.
 --dominant N keeps the window from the first to the last of the N latest dominant-class launches
-(conv_hw_kernel<128> over 6144 workgroups: 9 per inference step).
+(conv_hwr_kernel / round-2 conv_hw_kernel<128> over 6144 workgroups: 9 per inference step).
 Usage: python tools/phase_stats.py gpurun_out/<dir>/trace_kernel_trace.csv [--last-ms 250 | --dominant 45] [--top 40]
 """
 import csv
@@ -24,7 +24,7 @@ def main():
     rows = [r for r in rows if int(r["Start_Timestamp"]) < cut]
     if "--dominant" in sys.argv:   # window spanned by the last N launches of the dominant class (timed steps)
         nd = int(sys.argv[sys.argv.index("--dominant") + 1])
-        dom = [r for r in rows if r["Kernel_Name"].startswith("void hiseg::conv_hw_kernel<128")
+        dom = [r for r in rows if r["Kernel_Name"].startswith(("void hiseg::conv_hwr_kernel<", "void hiseg::conv_hw_kernel<128"))
                and int(r["Grid_Size_X"]) == 6144 * 256][-nd:]
         t0, t1 = int(dom[0]["Start_Timestamp"]), int(dom[-1]["End_Timestamp"])
         rows = [r for r in rows if t0 <= int(r["Start_Timestamp"]) <= t1]

@@ -47,14 +47,37 @@ def wgrad_family(d, want_bias):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--leg", default="train", choices=["train", "distill"])
+    ap.add_argument("--leg", default="train", choices=["train", "distill", "unet", "head"])
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     if args.leg == "distill":
         step = distill_step(dev)
+    elif args.leg in ("unet", "head"):
+        step = infer_phase(dev, args.leg)
     else:
         step = train_step(dev)
     profile(step, args.warmup)
+
+
+def infer_phase(dev, leg):
+    """One phase of bench.py's C2 inference step (engine.export_unet_phase / export_head_phase), no grad."""
+    import hiseg
+    from hiseg import engine
+    model = bench.build_model(dev, torch.bfloat16)
+    wrapper = hiseg.RGBHierarchicalExportWrapper(model)
+    images, rois = bench.synthetic_batch(dev, 0)
+    for m in (model.roi_align_mask, model.roi_align_rgb):
+        m.spatial_scale_h, m.spatial_scale_w = bench.H, bench.W
+    with torch.no_grad():
+        u, _ = engine.export_unet_phase(model, images)
+
+    def step():
+        with torch.no_grad():
+            if leg == "unet":
+                engine.export_unet_phase(model, images)
+            else:
+                engine.export_head_phase(model, images, rois, u, wrapper.dilation_pixels)
+    return step
 
 
 def distill_step(dev):
