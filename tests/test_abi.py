@@ -81,3 +81,35 @@ def test_release_library_refuses_diagnostic_conv_variants():
     assert L.lib().hiseg_conv2d_fwd_variant(ctypes.byref(d), 99, None) == -1
     assert b"split-K" in L.lib().hiseg_last_error_string()
     assert L.lib().hiseg_conv2d_workspace_bytes(ctypes.byref(d)) == 0
+
+
+def test_conv_splitk_workspace_plan_is_batch_invariant():
+    """hiseg_conv2d_workspace_bytes (no GPU call): the split-K plan of a small-image, long-K SE-gated 1x1 layer
+    depends on the layer and the per-image grid only -- bytes per image are the same for every batch size, so an
+    image's outputs do not depend on the batch it runs in -- and layers outside the plan need no workspace."""
+    import ctypes
+    from hiseg import _lib as L
+
+    def ws(N, H, W, Ca, Cout, gated=True, k=1):
+        d = L.Conv2dDesc()
+        d.dtype = d.out_dtype = 1
+        d.N, d.H, d.W, d.Ho, d.Wo = N, H, W, H, W
+        d.KH = d.KW = k
+        d.stride, d.pad = 1, k // 2
+        d.Ca, d.a_cstride, d.a_up = Ca, Ca, 1
+        d.Cout, d.Cout_pad = Cout, (Cout + 15) // 16 * 16
+        d.K_pad = (k * k * Ca + 63) // 64 * 64
+        d.srcA = d.weight = d.scale = d.shift = d.out = 1 << 20
+        d.in_scale = (1 << 20) if gated else None
+        return L.lib().hiseg_conv2d_workspace_bytes(ctypes.byref(d))
+
+    for Ca, Cout, H, W in ((2304, 384, 20, 20), (960, 160, 40, 40), (1152, 192, 15, 20), (3840, 640, 20, 20)):
+        nK = (Ca + 63) // 64
+        sp = min(8, max(2, nK // 4))
+        per_image = sp * H * W * ((Cout + 15) // 16 * 16) * 4
+        for N in (1, 4, 32):
+            assert ws(N, H, W, Ca, Cout) == N * per_image, (Ca, Cout, N)
+    assert ws(4, 80, 80, 480, 80) == 0           # > 1600 pixels per image: unsplit
+    assert ws(4, 20, 20, 384, 2304, gated=False) == 0   # ungated, short K: the LDS-DMA ring kernel
+    assert ws(4, 20, 20, 288, 48) == 0           # the 10-k-step pointwise kernel takes it
+    assert ws(4, 20, 20, 2304, 384, k=3) == 0    # 3x3: never split
