@@ -439,13 +439,15 @@ int conv_hw_try(const ConvArgs& a, hipStream_t s, int variant) {
   // src A nearest-x2 upsampled (smp decoder conv1): even grid (conv2d_impl checks)
   if (d.a_up != 1 && d.a_up != 2) return 0;
   // two sources (concat): each whole 32-channel slice from one of them
-  if (d.Ca % 32 != 0 || d.Cb % 32 != 0 || d.Ca < 64 || d.K_pad != 9 * (d.Ca + d.Cb)) return 0;
+  // (K_pad is only the packed weight rows' stride: a 32-multiple Cin padded to a 64-multiple K is fine)
+  if (d.Ca % 32 != 0 || d.Cb % 32 != 0 || d.Ca < 64 || d.K_pad < 9 * (d.Ca + d.Cb)) return 0;
   if ((d.a_cstride | d.a_coff) & 7) return 0;
   if (d.Cb && (d.srcB == nullptr || ((d.b_cstride | d.b_coff) & 7))) return 0;
-  // BCO 64 also takes 16 / 32 / 48 output columns as one partial tile: weight rows past Cout_pad read zeros
-  // (exact num_records), columns past Cout are neither scaled from real tables nor stored
+  // BCO 64 also takes a partial last tile of 16 / 32 / 48 output columns (16..48 columns alone, or the B7-ultra
+  // head's 96 / 160-channel layers): weight rows past Cout_pad read zeros (exact num_records), columns past Cout
+  // are neither scaled from real tables nor stored
   const int cmul = variant >= 88 ? 63 : 127;
-  const bool narrow = variant >= 88 && d.Cout < 64 && d.Cout % 16 == 0;
+  const bool narrow = variant >= 88 && d.Cout % 16 == 0;
   if (((d.Cout & cmul) && !narrow) || ((d.o_cstride | d.o_coff) & 7) || (d.residual && ((d.r_cstride | d.r_coff) & 7)))
     return 0;
   if ((((uintptr_t)d.scale | (uintptr_t)d.shift | (uintptr_t)d.out | (uintptr_t)d.residual) & 15)) return 0;

@@ -347,6 +347,7 @@ int conv_hwr_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_small_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_rows_try(const ConvArgs& a, hipStream_t s, int variant);
 bool conv_pw_applies(const ConvArgs& a);
+bool conv_rows_form(const ConvArgs& a);
 }
 
 using namespace hiseg;
@@ -530,6 +531,13 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
     if (v == 0 && d->KH == 3 && d->KW == 3 && d->Cout_pad <= 32) {
       const int r = conv_rows_try(a, s, 98);
       if (r != 0) return r < 0 ? r : HISEG_OK;
+      // conv_rows also declines a layer of its form when the two sources lie too far apart in memory for one buffer
+      // resource: such a layer takes conv_small, whose accumulation order is conv_rows' (bit-identical), so that
+      // the numerics never depend on where the allocator placed the operands
+      if (conv_rows_form(a)) {
+        const int r2 = conv_small_try(a, s, 0);
+        if (r2 != 0) return r2 < 0 ? r2 : HISEG_OK;
+      }
     }
     // 3x3 layers with weights also packed in MFMA fragment order (hiseg.ops.frag_pack) and 128-multiple Cout: the
     // register-streamed-weight halo kernel (conv_hwr.hip: one barrier per 32-channel slice) in its B-reuse,
@@ -547,6 +555,7 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
       if (r != 0) return r < 0 ? r : HISEG_OK;
     }
     if (v == 0 && !four_waves && halo) {
+      // (BCO 64 for every Cout that is not a 128 multiple: full 64 tiles plus a partial last tile)
       const int r = conv_hw_try(a, s, d->Cout % 128 ? 89 : 86);
       if (r != 0) return r < 0 ? r : HISEG_OK;
     }

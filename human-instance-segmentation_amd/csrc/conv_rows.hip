@@ -351,6 +351,18 @@ static int dispatch_rows(const ConvArgs& a, hipStream_t s, int ch, int ncb, int 
 }
 
 // Returns 1 if launched, 0 if the layer does not qualify, <0 on error.  variant: 0 / 98 (the same kernel).
+// The layer forms conv_rows computes, address constraints aside (conv2d_impl sends such a layer to conv_small when
+// conv_rows declines it for its sources' placement only).
+bool conv_rows_form(const ConvArgs& a) {
+  const hiseg_conv2d_desc& d = a.d;
+  if (d.dtype != HISEG_BF16 || d.convT || d.stride != 1 || d.KH != 3 || d.KW != 3 || d.pad != 1) return false;
+  if (d.Ho != d.H || d.Wo != d.W) return false;
+  if (d.residual || d.mul || d.out2 || d.in_scale) return false;
+  if (d.act != HISEG_ACT_NONE && d.act != HISEG_ACT_RELU) return false;
+  const int ncb = d.Cout_pad / 16;
+  return (ncb == 1 || ncb == 2) && a.Cin % 8 == 0 && d.Ca % 8 == 0;
+}
+
 int conv_rows_try(const ConvArgs& a, hipStream_t s, int variant) {
   const hiseg_conv2d_desc& d = a.d;
   (void)variant;

@@ -24,7 +24,6 @@
 #include "wgrad_common.h"
 
 namespace hiseg {
-int wgrad_wide_bc(const hiseg_conv2d_desc* d, int Cg, int Kg, int Cin, int M, int dy_cs, int dy_coff);
 int wgrad_wide_try(const WgradArgs& a, hipStream_t s);
 }
 
@@ -548,15 +547,17 @@ static int wgrad_geometry(const hiseg_conv2d_desc* d, int want_bias, int* Cg, in
   *M = (int)Mll;
   const int PB = 8 * kch;
   const int nblocks = (*M + PB - 1) / PB;
-  // the wide tile (wgrad_wide.hip: 256 x 256 / 256 x 128, one workgroup per CU): about 256 workgroups, one round
-  const int wbc = wgrad_wide_bc(d, *Cg, *Kg, *Cin, *M, -1, 0);
-  const int BK = wbc ? 256 : *Kg >= 128 ? 128 : 64;
-  const int BC = wbc ? wbc : *Cg >= 128 ? 128 : *Cg >= 64 ? 64 : *Cg >= 32 ? 32 : 16;
+  // The pixel partition into splits follows the 128-column tiles for every kernel (the wide 256 x 256 tile of
+  // wgrad_wide.hip included): an element's f32 accumulation order -- the 64-pixel blocks of its split, then the
+  // splits in order -- is then the same whichever kernel runs it, and the kernel choice depends on where the
+  // allocator placed two-source operands (one buffer resource must span both), which must never change the result.
+  const int BK = *Kg >= 128 ? 128 : 64;
+  const int BC = *Cg >= 128 ? 128 : *Cg >= 64 ? 64 : *Cg >= 32 ? 32 : 16;
   const long long tiles = (long long)((*Kg + BK - 1) / BK) * ((*Cg + BC - 1) / BC);
   // about 1024 workgroups but never past it: the wgrad kernels run two workgroups per CU, so 1024 = two full
   // rounds on 256 CUs, and rounding up (36 tiles x 29 splits = 1044) added a third, nearly empty round that cost
-  // a third of the layer's time
-  int sp = (int)((wbc ? 256 : 1024) / tiles);
+  // a third of the layer's time (the wide kernel, one workgroup per CU, gets a quarter of them per round)
+  int sp = (int)(1024 / tiles);
   if (sp > nblocks) sp = nblocks;
   if (sp < 1) sp = 1;
   *bps = (nblocks + sp - 1) / sp;

@@ -956,7 +956,11 @@ def test_conv_hwr_two_source_bit_identical(shape):
 
 @pytest.mark.parametrize("variant", [86, 89])
 @pytest.mark.parametrize("shape", [(3, 64, 64, 64, 64, 48, True), (2, 128, 128, 128, 32, 24, False),
-                                   (2, 64, 32, 64, 21, 13, True), (2, 96, 64, 128, 9, 23, False)])
+                                   (2, 64, 32, 64, 21, 13, True), (2, 96, 64, 128, 9, 23, False),
+                                   # B7-ultra head widths (round 3): 96-channel input (K padded past 9 x Cin),
+                                   # 96 / 160 outputs (partial last 64-column tile)
+                                   (2, 96, 0, 96, 20, 17, True), (2, 96, 96, 96, 12, 9, False),
+                                   (2, 192, 0, 160, 10, 21, True)])
 def test_conv_halo_two_source_within_bf16(shape, variant):
     """The halo-tiled kernel over a two-source concat (EnhancedUNet decoder: up ++ skip, hierarchical_segmentation_unet.py
     decoders) -- each 32-channel slice read from its own source -- vs the generic kernel within bf16 rounding."""
@@ -967,9 +971,10 @@ def test_conv_halo_two_source_within_bf16(shape, variant):
     dt = torch.bfloat16
     g = torch.Generator(device=DEV).manual_seed(19)
     xa = ops.Act.from_nchw(torch.randn(N, Ca, H, W, device=DEV, generator=g), dt)
-    xb = ops.Act.from_nchw(torch.randn(N, Cb, H, W, device=DEV, generator=g), dt)
+    xb = ops.Act.from_nchw(torch.randn(N, Cb, H, W, device=DEV, generator=g), dt) if Cb else None
     w = torch.randn(Cout, Ca + Cb, 3, 3, device=DEV, generator=g) / ((Ca + Cb) * 9) ** 0.5
-    p = ops.pack_conv(w, torch.randn(Cout, device=DEV, generator=g) * 0.1, None, 1, dt, DEV, pad=1, split=(Ca, Cb))
+    p = ops.pack_conv(w, torch.randn(Cout, device=DEV, generator=g) * 0.1, None, 1, dt, DEV, pad=1,
+                      split=(Ca, Cb) if Cb else None)
     R = ops.Act.from_nchw(torch.randn(N, Cout, H, W, device=DEV, generator=g), dt) if res else None
     ref = ops.conv2d(p, xa, xb, residual=R, variant=-1).to_nchw().float()
     y = ops.conv2d(p, xa, xb, residual=R, variant=variant).to_nchw().float()

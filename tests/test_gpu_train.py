@@ -928,3 +928,52 @@ def test_train_pack_fragment_order_matches_frag_pack(cin, cout, split):
         assert p.w_dgrad_frag is not None
         refd = ops.frag_pack(p.w_dgrad.float(), 9, p.cop).to(torch.bfloat16)
         assert torch.equal(p.w_dgrad_frag.reshape(-1), refd.reshape(-1))
+
+
+def _placed(big, off_elems, x_nchw, dt):
+    """An NHWC Act over big[off_elems:] (bf16) holding x: its address is chosen by the caller."""
+    from hiseg.ops import Act
+    a = Act.from_nchw(x_nchw, dt)
+    n = a.t.numel()
+    t = big[off_elems:off_elems + n]
+    t.copy_(a.t)
+    return Act(t, a.N, a.H, a.W, a.C, a.cstride, a.coff)
+
+
+@pytest.mark.parametrize("case", [(64, 32, 3, 12, 16, 2, 2, 32), (128, 128, 3, 8, 6, 2, 1, 128),
+                                  (256, 8, 1, 8, 6, 2, 1, 256), (64, 64, 3, 10, 9, 2, 1, 64)])
+def test_two_source_results_do_not_depend_on_operand_placement(case):
+    """Kernels that address both sources of a concat through one buffer resource decline layers whose sources lie
+    more than 2 GiB apart; the kernel then chosen must give bit-identical results (conv_rows -> conv_small; the
+    weight gradient's pixel splits follow one geometry for every kernel).  Same layer, the sources 64 MiB apart
+    vs 3 GiB apart inside one allocation: forward outputs and weight / bias gradients bit-identical."""
+    from hiseg.ops import Act
+    ca, cb, k, H, W, N, up, cout = case
+    dt = torch.bfloat16
+    big = torch.zeros((3 << 30) + (64 << 20), dtype=torch.uint8, device=DEV).view(dt)
+    x = torch.from_numpy(filler.normal(61, (N, ca, H // up, W // up))).to(DEV)
+    s_ = torch.from_numpy(filler.normal(62, (N, cb, H, W))).to(DEV)
+    g = torch.from_numpy(filler.normal(63, (N, cout, H, W))).to(DEV)
+    res = []
+    for far in (False, True):
+        conv = nn.Conv2d(ca + cb, cout, k, padding=k // 2, bias=True)
+        filler.fill_module(conv, seed=64)
+        TE, S, T = engine(_Holder(c=conv), dt)
+        xa = _placed(big, 0, x, dt)
+        xb = _placed(big, ((3 << 30) if far else (64 << 20)) // 2, s_, dt)
+        assert abs(xb.ptr() - xa.ptr()) >= (3 << 30) if far else abs(xb.ptr() - xa.ptr()) < (1 << 30)
+        if up == 1:
+            y = TE.conv_plain(T, conv, TE.ACT_NONE, xa, xb, split=(ca, cb))
+            inject(T, y, g, dt)
+            S.flat.prepare_backward()
+            T.run_backward()
+            torch.cuda.synchronize()
+            res.append((y.t.clone(), conv.weight.grad.clone(), conv.bias.grad.clone()))
+        else:   # the smp decoder's conv1 form (upsampled src A ++ skip): forward through the inference kernels
+            from hiseg import ops
+            p = ops.pack_conv(conv.weight, conv.bias, None, 1, dt, DEV, pad=1, split=(ca, cb))
+            yy = ops.conv2d(p, xa, xb, a_up=2)
+            torch.cuda.synchronize()
+            res.append((yy.t.clone(),))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
