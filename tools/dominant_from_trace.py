@@ -40,7 +40,8 @@ if "--last" in sys.argv:
     d = d[-int(sys.argv[sys.argv.index("--last") + 1]):]
 d = sorted(d)
 name = ("conv_fast_kernel<128,128,4,2,2,lds-epilogue> grid 12288 x 512" if R1 else
-        "conv_wide_kernel<256,4> grid 3072 x 256" if WIDE else "conv_hw_kernel<128> grid 6144 x 256")
+        "conv_wide_kernel<256,4> grid 3072 x 256" if WIDE else
+        "conv_hw_kernel<128> grid 6144 x 256" if HW else "conv_hwr_kernel<ACT, RES, 6> grid 6144 x 256")
 print(json.dumps({"kernel": name + " (256->256 3x3 @64x48 x256 ROIs)",
                   "launches": len(d), "same_grid_launches": len(d_all), "cluster_cut_ms": round(cut, 4), "avg_ms": round(sum(d) / len(d), 4), "median_ms": round(d[len(d) // 2], 4),
                   "min_ms": round(d[0], 4), "max_ms": round(d[-1], 4),
