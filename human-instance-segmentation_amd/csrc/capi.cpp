@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include "hiseg.h"
 
 static thread_local char g_err[512] = "";
@@ -20,6 +21,20 @@ int hiseg_check_launch(const char* what) {
     return HISEG_ERR_LAUNCH;
   }
   return HISEG_OK;
+}
+
+// Diagnostic: HISEG_LOG_PLACEMENT=1 reports every kernel choice that depended on where two operands lie in memory.
+void hiseg_note_placement(const char* what, const hiseg_conv2d_desc* d) {
+  static const bool on = getenv("HISEG_LOG_PLACEMENT") != nullptr;
+  if (on)
+    fprintf(stderr, "[hiseg placement] %s: A %p (%d ch) B %p (%d ch) -> %d, %dx%d taps, N %d %dx%d, convT %d up %d\n",
+            what, d->srcA, d->Ca, d->srcB, d->Cb, d->Cout, d->KH, d->KW, d->N, d->H, d->W, d->convT, d->a_up);
+}
+
+// Diagnostic: HISEG_PLACEMENT_FAR=1 makes every two-source layer take the path of sources lying far apart.
+bool hiseg_force_far() {
+  static const bool on = getenv("HISEG_PLACEMENT_FAR") != nullptr;
+  return on;
 }
 
 extern "C" int hiseg_version(void) { return 100; }

@@ -115,6 +115,9 @@ template <> struct Chunk<bf16_t> {
 // Host-side error plumbing (defined in capi.cpp).
 void hiseg_set_error(const char* fmt, ...);
 int hiseg_check_launch(const char* what);
+struct hiseg_conv2d_desc;
+void hiseg_note_placement(const char* what, const hiseg_conv2d_desc* d);
+bool hiseg_force_far();
 
 static inline bool al16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 

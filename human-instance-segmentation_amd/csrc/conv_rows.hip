@@ -391,7 +391,10 @@ int conv_rows_try(const ConvArgs& a, hipStream_t s, int variant) {
   const long long span_b = d.Cb ? (long long)d.N * d.H * d.W * d.b_cstride * 2 : 0;
   const long long pa = (long long)(uintptr_t)d.srcA, pb = d.Cb ? (long long)(uintptr_t)d.srcB : pa;
   const long long lo = pa < pb ? pa : pb;
-  if (pa - lo + span_a >= 0x7fffffffll || pb - lo + span_b >= 0x7fffffffll) return 0;
+  if (pa - lo + span_a >= 0x7fffffffll || pb - lo + span_b >= 0x7fffffffll || hiseg_force_far()) {
+    hiseg_note_placement("conv_rows declined (sources far apart)", &d);
+    return 0;
+  }
   const unsigned dA = (unsigned)(pa - lo), dB = (unsigned)(pb - lo);
   // HISEG_ROWS_PER_WG=n: fixed rows per workgroup instead of whole rounds (A/B timing only)
   static const int rpw = [] { const char* e = getenv("HISEG_ROWS_PER_WG"); const int v = e ? atoi(e) : 0; return v > 0 ? v : 0; }();

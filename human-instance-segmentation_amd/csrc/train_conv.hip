@@ -500,8 +500,11 @@ static int wgrad_tr_try(const WgradArgs& a, hipStream_t s) {
   if (d.Cb) {   // both sources within 2^31 bytes of the lower one (one X resource), else one source per K tile
     const long long pa = (long long)(uintptr_t)d.srcA, pb = (long long)(uintptr_t)d.srcB;
     const long long lo = pa < pb ? pa : pb;
-    if (pa - lo + span_a >= 0x7fffffffll || pb - lo + span_b >= 0x7fffffffll) {
+    if (pa - lo + span_a >= 0x7fffffffll || pb - lo + span_b >= 0x7fffffffll || hiseg_force_far()) {
       // A ends on a 128-column tile boundary and (with more than one tap) so does each tap
+      hiseg_note_placement(d.Ca % 128 == 0 && (d.KH * d.KW == 1 || d.Cb % 128 == 0)
+                               ? "wgrad_tr: one source per tile (sources far apart)"
+                               : "wgrad_tr declined -> register-transpose kernel (sources far apart)", &d);
       if (!(d.Ca % 128 == 0 && (d.KH * d.KW == 1 || d.Cb % 128 == 0))) return 0;
       b.x_tile_src = 1;
     }

@@ -289,7 +289,10 @@ int wgrad_wide_bc(const hiseg_conv2d_desc* d, int Cg, int Kg, int Cin, int M, in
   if (d->Cb) {
     const long long pa = (long long)(uintptr_t)d->srcA, pb = (long long)(uintptr_t)d->srcB;
     const long long lo = pa < pb ? pa : pb;
-    if (pa - lo + span_a >= 0x7fffffffll || pb - lo + span_b >= 0x7fffffffll) return 0;
+    if (pa - lo + span_a >= 0x7fffffffll || pb - lo + span_b >= 0x7fffffffll || hiseg_force_far()) {
+      if (dy_cs >= 0) hiseg_note_placement("wgrad_wide declined (sources far apart)", d);
+      return 0;
+    }
   }
   return Cg % 256 == 0 ? 256 : 0;   // (the 256 x 128 tile measured slower than the 128 x 128 kernel)
 }

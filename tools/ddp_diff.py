@@ -21,12 +21,16 @@ DEV = "cuda"
 LOSSES = []
 
 
-def poison(seed):
+def poison(seed, big=False):
     """Fill most of the caching allocator's free memory with random values, then free it again: an uninitialised
-    read then changes the result from run to run."""
+    read then changes the result from run to run.  big: also 0.5-3 GiB segments (the full GPU suite leaves such
+    segments cached, and a run's tensors are then carved out of them)."""
     g = torch.Generator(device=DEV).manual_seed(seed)
     held = []
-    for n in [256 << 10] * 1000 + [(2 << 20) * k for k in (1, 2, 4, 8, 16, 32, 64)] * 4:
+    sizes = [256 << 10] * 1000 + [(2 << 20) * k for k in (1, 2, 4, 8, 16, 32, 64)] * 4
+    if big:
+        sizes += [512 << 20, 1 << 30, 2 << 30, 3 << 30]
+    for n in sizes:
         t = torch.empty(n // 4, dtype=torch.float32, device=DEV)
         t.uniform_(-1e3, 1e3, generator=g)
         held.append(t)
