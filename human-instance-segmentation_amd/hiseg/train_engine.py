@@ -697,13 +697,18 @@ def residual_block(T: Tape, blk: nn.Module, x: Act, drop=None) -> Act:
 
 
 def dropout_mask(T: Tape, m: nn.Module, N: int, C: int, device) -> Optional[torch.Tensor]:
-    """Dropout2d mask [N, C] (0 or 1/(1-p)), or None when the module is a no-op."""
+    """Dropout2d mask [N, C] (0 or 1/(1-p)), or None when the module is a no-op.  The tape keeps the mask: a
+    backward reaches it through descriptors holding its raw address (_dropout_after's copy of the forward
+    descriptor), and a mask freed after the forward let the caching allocator hand its block to the next small
+    tensor -- the backward then scaled by whatever that tensor held (a different loss from the first update on,
+    depending on the allocator's history)."""
     p = float(getattr(m, "p", 0.0))
     if p <= 0.0:
         return None
     out = torch.empty(N * C, dtype=torch.float32, device=device)
     _chk(L.lib().hiseg_dropout2d_mask_dev(N, C, p, T.S.seed_base.data_ptr(), T.S.next_seed(), out.data_ptr(),
                                           _stream()), "dropout2d_mask")
+    T.keep.append(out)
     return out
 
 
