@@ -154,16 +154,17 @@ def train_bench(device, dtype, rank, world, dist, steps, warmup, preset=None, ba
         state["opt"].step()
         return loss
 
-    # One HIP graph per step on one GPU (hiseg.GraphedStep; every per-step state lives on the device): the eager
-    # C3 / C4 steps take 28 / 33 ms of Python enqueue for 38 / 41 ms of GPU work (tools/host_bound.py --train), so
-    # any host contention made them host-bound (C3 53-70 ms in full bench runs vs 38 ms alone); replayed, the
-    # step costs one launch.  Same GPU time as eager on a quiet host (profiles/r3_graph_vs_eager.txt).  Data-parallel
-    # legs stay eager (the bucketed all-reduce on the comm stream is not captured).  --eager-train: eager always.
-    run = step
-    if world == 1 and graph_train:
-        run = hiseg.GraphedStep(step, lambda: state["opt"])
+    # One HIP graph per step (hiseg.GraphedStep; every per-step state lives on the device): the eager C3 / C4 steps
+    # take 28 / 33 ms of Python enqueue for 38 / 41 ms of GPU work (tools/host_bound.py --train), so any host
+    # contention made them host-bound (C3 53-70 ms in full bench runs vs 38 ms alone); replayed, the step costs one
+    # launch.  Same GPU time as eager on a quiet host (profiles/r3_graph_vs_eager.txt).  Data-parallel legs over RCCL
+    # are captured with their bucketed all-reduces (graphs.py); a gloo group cannot be captured and stays eager.
+    # --eager-train: eager always.
+    graphable = graph_train and (world == 1 or _backend(dist) == "nccl")
+    runner = {"run": hiseg.GraphedStep(step, lambda: state["opt"]) if graphable else step}
 
     def timed():
+        run = runner["run"]
         for _ in range(max(warmup, 3 if run is not step else 1)):
             loss = run()
         torch.cuda.synchronize()
@@ -200,6 +201,8 @@ def train_bench(device, dtype, rank, world, dist, steps, warmup, preset=None, ba
         HD.sync_loss_class_weights(loss_fn)   # class weights from the counts of the whole (all-rank) batch
         # the local leg left per-rank optimizer moments / loss EMA: start the DDP leg from rank 0's
         HD.broadcast_training_state(state["opt"], loss_fn)
+        if graphable:   # a new graph: the exchange (and the loss's count all-reduce) must be in it
+            runner["run"] = hiseg.GraphedStep(step, lambda: state["opt"])
     prof = None
     if world == 1:   # per-call profile of one eager step (before any graph capture: its pool would skew it)
         step()
@@ -223,7 +226,8 @@ def train_bench(device, dtype, rank, world, dist, steps, warmup, preset=None, ba
            "config": {"workload": workload, "global_batch": int(images.shape[0]) * world,
                       "roi_samples_per_step": n_samples * world,
                       "parallelism": f"dp{world} (DDP, bucketed RCCL grad all-reduce)" if world > 1 else "dp1",
-                      "schedule": "eager" if run is step else "one HIP graph per step (hiseg.GraphedStep)"}}
+                      "schedule": "eager" if runner["run"] is step else
+                      ("one HIP graph per step (hiseg.GraphedStep)" + (", all-reduces captured" if world > 1 else ""))}}
     pipe = out["pipeline_tflops"] / world
     out["pipeline_frac"] = round(pipe / PEAK_BF16_TFLOPS, 4)
     if prof is not None:
@@ -234,6 +238,10 @@ def train_bench(device, dtype, rank, world, dist, steps, warmup, preset=None, ba
         out["ddp_over_local"] = round(sps / local, 4)   # 1.0 = the gradient exchange is fully hidden
     del model
     return out
+
+
+def _backend(dist):
+    return dist.get_backend() if dist else None
 
 
 def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=640, graph=True):
@@ -276,7 +284,8 @@ def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=6
         step()
         step()
         prof = call_profile(step)
-    run = hiseg.GraphedStep(step, lambda: state["opt"]) if (graph and world == 1) else step
+    graphable = graph and (world == 1 or _backend(dist) == "nccl")
+    run = hiseg.GraphedStep(step, lambda: state["opt"]) if graphable else step
     for _ in range(max(warmup, 3 if run is not step else 1)):
         loss = run()
     torch.cuda.synchronize()

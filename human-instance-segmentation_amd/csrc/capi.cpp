@@ -3,6 +3,8 @@
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
+#include <atomic>
 #include "hiseg.h"
 
 static thread_local char g_err[512] = "";
@@ -23,8 +25,12 @@ int hiseg_check_launch(const char* what) {
   return HISEG_OK;
 }
 
-// Diagnostic: HISEG_LOG_PLACEMENT=1 reports every kernel choice that depended on where two operands lie in memory.
+static std::atomic<long long> g_place_declined{0}, g_place_far{0};
+
+// Diagnostic: HISEG_LOG_PLACEMENT=1 reports every kernel choice that depended on where two operands lie in memory;
+// hiseg_placement_stats counts them ("... declined ..." notes: a fallback kernel took the layer).
 void hiseg_note_placement(const char* what, const hiseg_conv2d_desc* d) {
+  (strstr(what, "declined") ? g_place_declined : g_place_far).fetch_add(1);
   static const bool on = getenv("HISEG_LOG_PLACEMENT") != nullptr;
   if (on)
     fprintf(stderr, "[hiseg placement] %s: A %p (%d ch) B %p (%d ch) -> %d, %dx%d taps, N %d %dx%d, convT %d up %d\n",
@@ -35,6 +41,16 @@ void hiseg_note_placement(const char* what, const hiseg_conv2d_desc* d) {
 bool hiseg_force_far() {
   static const bool on = getenv("HISEG_PLACEMENT_FAR") != nullptr;
   return on;
+}
+
+extern "C" int hiseg_placement_stats(long long* declined, long long* far, int reset) {
+  if (declined) *declined = g_place_declined.load();
+  if (far) *far = g_place_far.load();
+  if (reset) {
+    g_place_declined = 0;
+    g_place_far = 0;
+  }
+  return HISEG_OK;
 }
 
 extern "C" int hiseg_version(void) { return 100; }

@@ -348,6 +348,7 @@ static int launch_pw_k(const ConvArgs& a, hipStream_t s, int nks) {
 }
 
 // The pointwise kernel's plan for a layer: false when it does not qualify (caller falls back).
+static constexpr long long kPwGateBytes = 64 * 1024;   // LDS bytes for an SE gate [N][Ca] f32
 static bool pw_plan(const ConvArgs& a, int& rb, int& nks, int& nks_max) {
   const hiseg_conv2d_desc& d = a.d;
   if (d.dtype != HISEG_BF16 || d.out_dtype != HISEG_BF16) return false;
@@ -385,7 +386,7 @@ static bool pw_plan(const ConvArgs& a, int& rb, int& nks, int& nks_max) {
   } else {
     // narrow tiles: plain or residual epilogue with any elementwise activation, optional SE gate
     if (d.convT || d.mul || d.act == HISEG_ACT_SWISH) return false;
-    if (d.in_scale && (((uintptr_t)d.in_scale & 15) || (long long)d.N * d.Ca * 4 > 64 * 1024)) return false;
+    if (d.in_scale && (((uintptr_t)d.in_scale & 15) || (long long)d.N * d.Ca * 4 > kPwGateBytes)) return false;
   }
   const long long out_px = (long long)a.M * (d.convT ? 4 : 1);
   const long long lim = 0x7fffffffll;
@@ -404,6 +405,22 @@ static bool pw_plan(const ConvArgs& a, int& rb, int& nks, int& nks_max) {
 bool conv_pw_applies(const ConvArgs& a) {
   int rb, nks, nks_max;
   return pw_plan(a, rb, nks, nks_max);
+}
+
+// SE-gated layers stage the gate of every image of the launch in LDS ([N][Ca] f32, kPwGateBytes at most), so the
+// plan depends on the batch.  The images a pointwise launch may take for this layer when the gate alone makes it
+// decline (0: the layer does not qualify anyway or fits as it is): conv2d_impl then runs it in image ranges of that
+// many, so a pixel's kernel -- and its accumulation order -- never depends on the batch it comes in.
+int conv_pw_gate_images(const ConvArgs& a) {
+  const hiseg_conv2d_desc& d = a.d;
+  if (!d.in_scale || d.Ca <= 0 || (long long)d.N * d.Ca * 4 <= kPwGateBytes) return 0;
+  const int per = (int)(kPwGateBytes / (4ll * d.Ca));
+  if (per < 1) return 0;
+  ConvArgs one = a;
+  one.d.N = per;
+  one.M = per * d.Ho * d.Wo;
+  int rb, nks, nks_max;
+  return pw_plan(one, rb, nks, nks_max) ? per : 0;
 }
 
 // Returns 1 if launched, 0 if the layer does not qualify (caller falls back), <0 on error.  variant 90.

@@ -46,6 +46,28 @@ __device__ __forceinline__ void rows_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned
                :: "s"(lds_addr), "v"(voff), "s"(rsrc) : "memory");
 }
 
+// Two-resource form (sources far apart): the lanes of source A load through rsrc_a, those of source B through
+// rsrc_b, into the same LDS slots -- two instructions under complementary exec masks (both non-empty: mixed groups
+// only; the caller handles single-source groups), exec restored inside the asm block.
+__device__ __forceinline__ void rows_dma16_ab(__amdgpu_buffer_rsrc_t rsrc_a, __amdgpu_buffer_rsrc_t rsrc_b,
+                                              unsigned lds_addr, unsigned voff, unsigned long long mask_a,
+                                              unsigned long long mask_b) {
+  unsigned long long saved;
+  asm volatile("s_mov_b32 m0, %[lds]\n\t"
+               "s_and_saveexec_b64 %[sv], %[ma]\n\t"
+               "s_nop 0\n\t"
+               "buffer_load_dwordx4 %[off], %[ra], 0 offen lds\n\t"
+               "s_mov_b64 exec, %[sv]\n\t"
+               "s_and_b64 exec, exec, %[mb]\n\t"
+               "s_nop 0\n\t"
+               "buffer_load_dwordx4 %[off], %[rb], 0 offen lds\n\t"
+               "s_mov_b64 exec, %[sv]"
+               : [sv] "=&s"(saved)
+               : [lds] "s"(lds_addr), [off] "v"(voff), [ra] "s"(rsrc_a), [rb] "s"(rsrc_b), [ma] "s"(mask_a),
+                 [mb] "s"(mask_b)
+               : "memory", "scc");
+}
+
 __device__ uint4 g_conv_rows_sink[64];            // the stores of dead lanes / halo steps (never read)
 
 template <typename TO>
@@ -65,14 +87,16 @@ __device__ __forceinline__ void rows_store(void* p, const float (&v)[4], bool ve
 // CH: input channels / 8.  NCB: 16-channel output blocks (1 or 2; TW = 128 / NCB pixels per strip).
 // P (even): rows in flight ahead of the computed pair.  OCC: workgroups per CU the launch bounds allow.
 // Output forms: bf16 with Cout % 4 == 0, f32 with Cout % 4 == 0 (vec4) or Cout == 1 (the head).
-template <int CH, int NCB, typename TO, int P, int OCC, int ACT>
+// TWO: the concat's two sources through one buffer resource each (their allocations lie too far apart for one
+// 32-bit offset range): every DMA group becomes two counted instructions (same slots, same arithmetic after).
+template <int CH, int NCB, typename TO, int P, int OCC, int ACT, bool TWO>
 __global__ void __launch_bounds__(512, 2 * OCC) conv_rows_kernel(ConvArgs a, int nstrip, long long ntask, int nwg,
                                                                  unsigned dA, unsigned dB) {
   constexpr int TW = 128 / NCB;
   using G = RowsGeom<CH, TW>;
   constexpr int CIN = G::CIN, NKC = G::NKC, HP = G::HP, ROWS = G::ROWS, NDMA = G::NDMA, NJ = G::NJ;
   constexpr int RB = P + 4;
-  constexpr int WAIT = (P / 2 - 1) * 2 * (NJ + 1);
+  constexpr int WAIT = (P / 2 - 1) * 2 * ((TWO ? 2 : 1) * NJ + 1);
   static_assert(P % 2 == 0 && WAIT <= 63, "P even; vmcnt field");
   extern __shared__ __attribute__((aligned(16))) uint4 ring[];   // RB rows, then a 64-slot DMA sink
   // descriptor fields as scalars (a reference into the kernel arguments inside the lambdas below would be
@@ -137,9 +161,12 @@ __global__ void __launch_bounds__(512, 2 * OCC) conv_rows_kernel(ConvArgs a, int
   // DMA: instruction j = w + 8 i of a row fills slots 64 j .. 64 j + 63; this lane's slot 64 j + lane holds
   // chunk c of pixel pix (or nothing: past the row -> an out-of-range offset, the DMA writes zeros).  Every wave
   // issues NJ per row; j >= NDMA goes to the sink slots.
-  const char* const base = reinterpret_cast<const char*>(a.d.Cb && a.d.srcB < a.d.srcA ? a.d.srcB : a.d.srcA);
+  const char* const base = TWO ? reinterpret_cast<const char*>(a.d.srcA)
+                               : reinterpret_cast<const char*>(a.d.Cb && a.d.srcB < a.d.srcA ? a.d.srcB : a.d.srcA);
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), (short)0,
                                                                         0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsrc_b = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(TWO ? a.d.srcB : a.d.srcA), (short)0, 0x7fffffff, 0x00020000);
   const unsigned OOB = 0x80000000u;
   const int up = a.d.a_up == 2 ? 1 : 0;
   int jpix[NJ], jcoff[NJ];
@@ -155,6 +182,13 @@ __global__ void __launch_bounds__(512, 2 * OCC) conv_rows_kernel(ConvArgs a, int
     jA[i] = ci < Ca;
     jcoff[i] = jA[i] ? aco + ci : bco + (ci - Ca);
     jpix[i] = (slot < G::NSLOT && pix < HP && w + 8 * i < NDMA) ? pix : -(1 << 20);
+  }
+  // TWO: per DMA group, the lanes reading source A / B (wave-uniform masks)
+  unsigned long long mA[NJ], mB[NJ];
+#pragma unroll
+  for (int i = 0; i < NJ; ++i) {
+    mA[i] = TWO ? __builtin_amdgcn_ballot_w64(jA[i]) : ~0ull;
+    mB[i] = TWO ? ~mA[i] : 0ull;
   }
   const unsigned lds_base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)ring;
   const unsigned lds_sink = lds_base + 16u * (unsigned)(RB * ROWS);
@@ -178,7 +212,20 @@ __global__ void __launch_bounds__(512, 2 * OCC) conv_rows_kernel(ConvArgs a, int
     for (int i = 0; i < NJ; ++i) {
       const unsigned off = rok && jok[i] ? jcol[i] + (jA[i] ? rowA : rowB) : OOB;
       const bool real = live && w + 8 * i < NDMA;  // (wave-uniform)
-      rows_dma16(rsrc, real ? slotb + 1024u * (unsigned)(w + 8 * i) : lds_sink, off);
+      const unsigned dst = real ? slotb + 1024u * (unsigned)(w + 8 * i) : lds_sink;
+      if constexpr (TWO) {                     // exactly two counted instructions per group, whatever its sources
+        if (mB[i] == 0ull) {
+          rows_dma16(rsrc, dst, off);
+          rows_dma16(rsrc, lds_sink, OOB);
+        } else if (mA[i] == 0ull) {
+          rows_dma16(rsrc_b, dst, off);
+          rows_dma16(rsrc, lds_sink, OOB);
+        } else {
+          rows_dma16_ab(rsrc, rsrc_b, dst, off, mA[i], mB[i]);
+        }
+      } else {
+        rows_dma16(rsrc, dst, off);
+      }
     }
   };
 
@@ -289,7 +336,7 @@ __global__ void __launch_bounds__(512, 2 * OCC) conv_rows_kernel(ConvArgs a, int
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int CH, int NCB, typename TO, int P, int OCC, int ACT>
+template <int CH, int NCB, typename TO, int P, int OCC, int ACT, bool TWO>
 static int launch_rows_act(const ConvArgs& a, hipStream_t s, int rows_per_wg, unsigned dA, unsigned dB) {
   const hiseg_conv2d_desc& d = a.d;
   constexpr int TW = 128 / NCB;
@@ -316,7 +363,7 @@ static int launch_rows_act(const ConvArgs& a, hipStream_t s, int rows_per_wg, un
     if (nwg > cap) nwg = cap;
   }
   if (nwg > (1ll << 30)) nwg = 1ll << 30;
-  auto kern = conv_rows_kernel<CH, NCB, TO, P, OCC, ACT>;
+  auto kern = conv_rows_kernel<CH, NCB, TO, P, OCC, ACT, TWO>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -328,24 +375,28 @@ static int launch_rows_act(const ConvArgs& a, hipStream_t s, int rows_per_wg, un
 }
 
 template <int CH, int NCB, typename TO, int P, int OCC>
-static int launch_rows(const ConvArgs& a, hipStream_t s, int rows_per_wg, unsigned dA, unsigned dB) {
-  return a.d.act == HISEG_ACT_RELU ? launch_rows_act<CH, NCB, TO, P, OCC, HISEG_ACT_RELU>(a, s, rows_per_wg, dA, dB)
-                                   : launch_rows_act<CH, NCB, TO, P, OCC, HISEG_ACT_NONE>(a, s, rows_per_wg, dA, dB);
+static int launch_rows(const ConvArgs& a, hipStream_t s, int rows_per_wg, unsigned dA, unsigned dB, bool two) {
+  if (two)
+    return a.d.act == HISEG_ACT_RELU ? launch_rows_act<CH, NCB, TO, P, OCC, HISEG_ACT_RELU, true>(a, s, rows_per_wg, dA, dB)
+                                     : launch_rows_act<CH, NCB, TO, P, OCC, HISEG_ACT_NONE, true>(a, s, rows_per_wg, dA, dB);
+  return a.d.act == HISEG_ACT_RELU ? launch_rows_act<CH, NCB, TO, P, OCC, HISEG_ACT_RELU, false>(a, s, rows_per_wg, dA, dB)
+                                   : launch_rows_act<CH, NCB, TO, P, OCC, HISEG_ACT_NONE, false>(a, s, rows_per_wg, dA, dB);
 }
 
 template <typename TO>
-static int dispatch_rows(const ConvArgs& a, hipStream_t s, int ch, int ncb, int rpw, unsigned dA, unsigned dB) {
+static int dispatch_rows(const ConvArgs& a, hipStream_t s, int ch, int ncb, int rpw, unsigned dA, unsigned dB,
+                         bool two) {
   if (ncb == 2) {
     switch (ch) {
-      case 4: return launch_rows<4, 2, TO, 8, 2>(a, s, rpw, dA, dB);
-      case 12: return launch_rows<12, 2, TO, 6, 1>(a, s, rpw, dA, dB);
-      case 16: return launch_rows<16, 2, TO, 4, 1>(a, s, rpw, dA, dB);
+      case 4: return launch_rows<4, 2, TO, 8, 2>(a, s, rpw, dA, dB, two);
+      case 12: return launch_rows<12, 2, TO, 6, 1>(a, s, rpw, dA, dB, two);
+      case 16: return launch_rows<16, 2, TO, 4, 1>(a, s, rpw, dA, dB, two);
       default: return 0;
     }
   }
   switch (ch) {
-    case 2: return launch_rows<2, 1, TO, 8, 2>(a, s, rpw, dA, dB);
-    case 4: return launch_rows<4, 1, TO, 4, 2>(a, s, rpw, dA, dB);
+    case 2: return launch_rows<2, 1, TO, 8, 2>(a, s, rpw, dA, dB, two);
+    case 4: return launch_rows<4, 1, TO, 4, 2>(a, s, rpw, dA, dB, two);
     default: return 0;
   }
 }
@@ -386,20 +437,21 @@ int conv_rows_try(const ConvArgs& a, hipStream_t s, int variant) {
   if (d.K_pad < nkc * 32) return 0;
   // the DMA moves 16-B chunks: every source's channel stride / offset in 8-channel units
   if ((d.a_cstride | d.a_coff) % 8 != 0 || (d.Cb && ((d.b_cstride | d.b_coff) % 8 != 0))) return 0;
-  // one buffer resource from the lower source: both sources within 2^31 bytes of it
+  // one buffer resource from the lower source when both sources lie within 2^31 bytes of it; otherwise one
+  // resource per source (the TWO form: two DMA instructions per group) -- the same kernel and arithmetic either
+  // way, so the layer's speed and bits do not depend on where the allocator placed its sources
   const long long span_a = (long long)d.N * a.Hs * a.Ws * d.a_cstride * 2;
   const long long span_b = d.Cb ? (long long)d.N * d.H * d.W * d.b_cstride * 2 : 0;
+  if (span_a >= 0x7fffffffll || span_b >= 0x7fffffffll) return 0;   // (conv2d_impl's image ranges prevent it)
   const long long pa = (long long)(uintptr_t)d.srcA, pb = d.Cb ? (long long)(uintptr_t)d.srcB : pa;
   const long long lo = pa < pb ? pa : pb;
-  if (pa - lo + span_a >= 0x7fffffffll || pb - lo + span_b >= 0x7fffffffll || hiseg_force_far()) {
-    hiseg_note_placement("conv_rows declined (sources far apart)", &d);
-    return 0;
-  }
-  const unsigned dA = (unsigned)(pa - lo), dB = (unsigned)(pb - lo);
+  const bool two = d.Cb && (pa - lo + span_a >= 0x7fffffffll || pb - lo + span_b >= 0x7fffffffll || hiseg_force_far());
+  if (two) hiseg_note_placement("conv_rows: sources far apart, one buffer resource each", &d);
+  const unsigned dA = two ? 0u : (unsigned)(pa - lo), dB = two ? 0u : (unsigned)(pb - lo);
   // HISEG_ROWS_PER_WG=n: fixed rows per workgroup instead of whole rounds (A/B timing only)
   static const int rpw = [] { const char* e = getenv("HISEG_ROWS_PER_WG"); const int v = e ? atoi(e) : 0; return v > 0 ? v : 0; }();
-  return d.out_dtype == HISEG_BF16 ? dispatch_rows<bf16_t>(a, s, ch, ncb, rpw, dA, dB)
-                                   : dispatch_rows<float>(a, s, ch, ncb, rpw, dA, dB);
+  return d.out_dtype == HISEG_BF16 ? dispatch_rows<bf16_t>(a, s, ch, ncb, rpw, dA, dB, two)
+                                   : dispatch_rows<float>(a, s, ch, ncb, rpw, dA, dB, two);
 }
 
 }  // namespace hiseg

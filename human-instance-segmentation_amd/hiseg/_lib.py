@@ -7,6 +7,7 @@ package's GPU path raises immediately.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 
@@ -42,8 +43,68 @@ c_float = ctypes.c_float
 c_void_p = ctypes.c_void_p
 c_ll = ctypes.c_longlong
 
+# Strict pointer mode (tests set HISEG_STRICT_PTRS=1): a descriptor pointer field may only be assigned a tensor /
+# activation view (held by the descriptor) or None -- a raw integer address raises, so no descriptor can point at
+# memory nothing keeps alive.
+STRICT_PTRS = os.environ.get("HISEG_STRICT_PTRS", "0") == "1"
 
-class RoiAlignDesc(ctypes.Structure):
+
+class Desc(ctypes.Structure):
+    """A C-ABI descriptor that owns what it points at.
+
+    Assigning a ``torch.Tensor`` or an activation view (anything with ``.t`` and ``.ptr()``, hiseg.ops.Act) to a
+    pointer field stores its device address AND keeps the object alive for as long as the descriptor lives.  The
+    training tape's backward closures capture descriptors built in the forward (the conv epilogue operands, a
+    Dropout2d mask, the upsample/combine head's buffers) and launch kernels through them later; a tensor whose
+    only reference was its address inside such a descriptor could be released after the forward and its block
+    handed to another tensor by the caching allocator (round 3: fg_gate's Dropout2d mask).  Holding by
+    construction makes that impossible; ``copy()`` carries the holds over to the copy."""
+
+    _ptr_fields = frozenset()
+
+    def __init_subclass__(cls, **kw):
+        super().__init_subclass__(**kw)
+        cls._ptr_fields = frozenset(n for n, t in cls.__dict__.get("_fields_", ()) if t is c_void_p)
+
+    def __setattr__(self, name, value):
+        if name in self._ptr_fields and value is not None and not isinstance(value, int):
+            t = getattr(value, "t", value)
+            if not isinstance(t, torch.Tensor):
+                raise TypeError(f"{type(self).__name__}.{name}: expected a tensor / activation view, got {type(value)}")
+            self.__dict__.setdefault("_held", {})[name] = value
+            value = t.data_ptr()
+        elif name in self._ptr_fields:
+            if STRICT_PTRS and value:
+                raise TypeError(f"{type(self).__name__}.{name}: raw address assigned (strict pointer mode): pass the "
+                                "tensor so the descriptor keeps it alive")
+            held = self.__dict__.get("_held")
+            if held is not None:
+                held.pop(name, None)
+        super().__setattr__(name, value)
+
+    def held(self):
+        """{field: object} of the pointer fields this descriptor keeps alive."""
+        return dict(self.__dict__.get("_held", {}))
+
+    def copy(self):
+        c = type(self).from_buffer_copy(self)
+        c.__dict__["_held"] = dict(self.__dict__.get("_held", {}))
+        return c
+
+
+@contextlib.contextmanager
+def raw_pointers():
+    """Allow raw integer addresses in descriptor pointer fields (tests that probe the C ABI's argument checks
+    with descriptors that are never launched)."""
+    global STRICT_PTRS
+    old, STRICT_PTRS = STRICT_PTRS, False
+    try:
+        yield
+    finally:
+        STRICT_PTRS = old
+
+
+class RoiAlignDesc(Desc):
     _fields_ = [
         ("feat", c_void_p), ("B", c_int), ("C", c_int), ("H", c_int), ("W", c_int),
         ("rois", c_void_p), ("N", c_int),
@@ -56,7 +117,7 @@ class RoiAlignDesc(ctypes.Structure):
     ]
 
 
-class Conv2dDesc(ctypes.Structure):
+class Conv2dDesc(Desc):
     _fields_ = [
         ("dtype", c_int), ("out_dtype", c_int),
         ("N", c_int), ("H", c_int), ("W", c_int),
@@ -79,7 +140,7 @@ class Conv2dDesc(ctypes.Structure):
     ]
 
 
-class WgradMap(ctypes.Structure):
+class WgradMap(Desc):
     _fields_ = [(n, c_int) for n in ("Cout", "KH", "KW", "ca", "ca_real", "cb", "cb_real", "convT", "Cg", "Kg",
                                      "want_bias")]
 
@@ -88,14 +149,14 @@ HISEG_PACK_FRAG = 8   # include/hiseg_train.h: pack mode flag, MFMA fragment ord
 HISEG_PACK_BIAS = 4   # pack mode: conv bias -> f32 epilogue shift
 
 
-class PackEntry(ctypes.Structure):
+class PackEntry(Desc):
     _fields_ = [("src", c_void_p), ("dst", c_void_p), ("dtype", c_int), ("mode", c_int),
                 ("Cout", c_int), ("Cin_real", c_int), ("KH", c_int), ("KW", c_int),
                 ("ca", c_int), ("ca_real", c_int), ("cb", c_int), ("cb_real", c_int),
                 ("rows", c_int), ("K_pad", c_int), ("cop", c_int), ("total", c_int)]
 
 
-class BnApplyDesc(ctypes.Structure):
+class BnApplyDesc(Desc):
     _fields_ = [("dtype", c_int), ("P", c_ll), ("HW", c_int), ("C", c_int),
                 ("z", c_void_p), ("z_cstride", c_int), ("z_coff", c_int),
                 ("scale", c_void_p), ("shift", c_void_p),
@@ -105,7 +166,7 @@ class BnApplyDesc(ctypes.Structure):
                 ("act_beta", c_float), ("per_sample", c_int)]
 
 
-class BnBwdDesc(ctypes.Structure):
+class BnBwdDesc(Desc):
     _fields_ = [("dtype", c_int), ("P", c_ll), ("HW", c_int), ("C", c_int),
                 ("dy", c_void_p), ("dy_cstride", c_int), ("dy_coff", c_int),
                 ("y", c_void_p), ("y_cstride", c_int), ("y_coff", c_int),
@@ -120,7 +181,7 @@ class BnBwdDesc(ctypes.Structure):
                 ("act_beta", c_float), ("residual", c_void_p), ("r_cstride", c_int), ("r_coff", c_int)]
 
 
-class LnBwdDesc(ctypes.Structure):
+class LnBwdDesc(Desc):
     _fields_ = [("dtype", c_int), ("N", c_int), ("HW", c_int), ("C", c_int),
                 ("dy", c_void_p), ("dy_cstride", c_int), ("dy_coff", c_int),
                 ("z", c_void_p), ("z_cstride", c_int), ("z_coff", c_int),
@@ -134,11 +195,11 @@ class LnBwdDesc(ctypes.Structure):
                 ("ws", c_void_p)]
 
 
-class EwView(ctypes.Structure):
+class EwView(Desc):
     _fields_ = [("p", c_void_p), ("cstride", c_int), ("coff", c_int)]
 
 
-class UbfDesc(ctypes.Structure):
+class UbfDesc(Desc):
     _fields_ = [("dtype", c_int), ("low", c_void_p), ("N", c_int), ("h", c_int), ("w", c_int),
                 ("ut_w", c_void_p), ("ut_b", c_void_p), ("gamma", c_void_p), ("beta", c_void_p),
                 ("mean", c_void_p), ("invstd", c_void_p), ("scale", c_void_p), ("shift", c_void_p),
@@ -148,7 +209,7 @@ class UbfDesc(ctypes.Structure):
                 ("act", c_int), ("act_beta", c_float), ("layernorm", c_int)]
 
 
-class UbfGrads(ctypes.Structure):
+class UbfGrads(Desc):
     _fields_ = [(n, c_void_p) for n in ("dut_w", "dut_b", "dgamma", "dbeta", "du1_w", "du1_b")]
 
 
@@ -293,6 +354,7 @@ def _declare(lib):
                                       P, c_int, P, P], c_int),
         "hiseg_adamw_max_segments": ([], c_int),
         "hiseg_debug_fill_lds": ([ctypes.c_uint, c_int, P], c_int),
+        "hiseg_placement_stats": ([ctypes.POINTER(c_ll), ctypes.POINTER(c_ll), c_int], c_int),
         "hiseg_adamw_step_segmented": ([P, P, P, P, c_ll, c_float, c_float, c_float, c_float, c_float, c_float,
                                         c_float, P, c_float, P, P, c_int, P, c_int, P, P], c_int),
     }
@@ -335,6 +397,13 @@ def check(status: int, what: str) -> None:
     if status != 0:
         msg = lib().hiseg_last_error_string().decode(errors="replace")
         raise HisegError(f"{what} failed with status {status}: {msg}")
+
+
+def placement_stats(reset: bool = False):
+    """(declined, far): placement-dependent kernel choices since the last reset (include/hiseg.h)."""
+    a, b = c_ll(), c_ll()
+    check(lib().hiseg_placement_stats(ctypes.byref(a), ctypes.byref(b), int(reset)), "placement_stats")
+    return a.value, b.value
 
 
 def stream_ptr(device=None) -> int:

@@ -157,7 +157,20 @@ def broadcast_training_state(optimizer=None, loss_fn: Optional[nn.Module] = None
         raise RuntimeError("hiseg.distributed: torch.distributed is not initialised")
     with torch.no_grad():
         if optimizer is not None and getattr(optimizer, "exp_avg", None) is not None:
-            for t in (optimizer.exp_avg, optimizer.exp_avg_sq, optimizer._seg_start, optimizer._steps):
+            # the flat layouts must match; the step-count segment table may not (ranks with different unfreeze
+            # histories): broadcast the source's sizes first and re-size this rank's table to them
+            o = optimizer
+            meta = torch.tensor([o.exp_avg.numel(), o._nseg], dtype=torch.int64, device=o.exp_avg.device)
+            dist.broadcast(meta, src, group=process_group)
+            numel, nseg = (int(v) for v in meta.tolist())
+            if numel != o.exp_avg.numel():
+                raise RuntimeError(f"broadcast_training_state: this rank's optimizer covers {o.exp_avg.numel()} "
+                                   f"parameters, rank {src}'s {numel}: the flat layouts differ")
+            if nseg != o._nseg:
+                o._seg_start = torch.empty(nseg + 1, dtype=o._seg_start.dtype, device=o._seg_start.device)
+                o._steps = torch.empty(2 * nseg, dtype=o._steps.dtype, device=o._steps.device)
+                o._nseg = nseg
+            for t in (o.exp_avg, o.exp_avg_sq, o._seg_start, o._steps):
                 dist.broadcast(t, src, group=process_group)
         st = getattr(loss_fn, "_state", None) if loss_fn is not None else None
         if st is not None:

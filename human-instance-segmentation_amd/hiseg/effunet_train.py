@@ -71,7 +71,6 @@ def dw_bn_silu(T: TE.Tape, conv: nn.Conv2d, bn: nn.BatchNorm2d, x: Act, need_dx:
     TE._chk(lib.hiseg_dw_train_fwd(hdtype(x.dtype), x.ptr(), x.N, x.H, x.W, c, k, st, conv.weight.data_ptr(), z.ptr(),
                                    Ho, Wo, TE._stream()), "dw_train_fwd")
     y, bst = TE.bn_forward(T, bn, z, act=ACT_SILU)
-    T.keep.append(x)
 
     def back():
         dz = Act.new(z.N, z.H, z.W, c, z.dtype, dev, zero=False)
@@ -188,8 +187,7 @@ def up_conv_bn_relu(T: TE.Tape, conv: nn.Conv2d, bn: nn.BatchNorm2d, x_low: Act,
     d = TE._desc(S, p, x_low, skip, z)
     d.H, d.W, d.Ho, d.Wo, d.a_up = H, W, H, W, 2
     TE._chk(lib.hiseg_conv2d_fwd(ctypes.byref(d), TE._stream()), "conv2d(decoder)")
-    y, st = TE.bn_forward(T, bn, z, act=ACT_RELU)
-    T.keep.extend([x_low, skip])   # the weight gradient re-reads both sources through d's raw pointers
+    y, st = TE.bn_forward(T, bn, z, act=ACT_RELU)   # d holds x_low and skip for the weight gradient
 
     def back():
         dz = Act.new(z.N, z.H, z.W, z.C, z.dtype, dev, cpad=z.cstride, zero=z.cstride != z.C)
@@ -203,14 +201,14 @@ def up_conv_bn_relu(T: TE.Tape, conv: nn.Conv2d, bn: nn.BatchNorm2d, x_low: Act,
         dg.dtype = dg.out_dtype = hdtype(dz.dtype)
         dg.N, dg.H, dg.W, dg.Ho, dg.Wo = dz.N, H, W, H, W
         dg.KH, dg.KW, dg.stride, dg.pad = p.kh, p.kw, 1, p.kh - 1 - p.pad
-        dg.srcA, dg.a_cstride, dg.a_coff, dg.Ca, dg.a_up = dz.ptr(), dz.cstride, dz.coff, p.cop, 1
+        dg.srcA, dg.a_cstride, dg.a_coff, dg.Ca, dg.a_up = dz, dz.cstride, dz.coff, p.cop, 1
         # rows 0..ca-1 of the packed dgrad weights are the upsampled source's input channels, ca.. the skip's
-        dg.weight, dg.Cout, dg.Cout_pad, dg.K_pad = p.w_dgrad.data_ptr(), nout, round_up(nout, 16), p.dg_k_pad
+        dg.weight, dg.Cout, dg.Cout_pad, dg.K_pad = p.w_dgrad, nout, round_up(nout, 16), p.dg_k_pad
         ones = torch.ones(round_up(nout, 16), dtype=torch.float32, device=dev)
         zeros = torch.zeros_like(ones)
-        dg.scale, dg.shift, dg.act = ones.data_ptr(), zeros.data_ptr(), ACT_NONE
+        dg.scale, dg.shift, dg.act = ones, zeros, ACT_NONE
         full = Act.new(z.N, H, W, nout, dz.dtype, dev, cpad=nout, zero=False)
-        dg.out, dg.o_cstride, dg.o_coff = full.ptr(), full.cstride, 0
+        dg.out, dg.o_cstride, dg.o_coff = full, full.cstride, 0
         TE._chk(TE._dgrad_launch(dg), "conv2d(decoder dgrad)")
         if need_dx:
             gx, acc = T.grad(x_low)
@@ -228,7 +226,6 @@ def up_conv_bn_relu(T: TE.Tape, conv: nn.Conv2d, bn: nn.BatchNorm2d, x_low: Act,
                 TE._chk(lib.hiseg_act_bwd_pre(hdtype(dz.dtype), skip.N * H * W, skip.C, part, part, ACT_NONE, 1.0,
                                               TE.ew(gs), 0, TE._stream()), "copy")
             T.mark(skip)
-        T.keep.extend([ones, zeros, full])
     T.push(back)
     return y
 
@@ -273,7 +270,6 @@ class _StudentFunction(torch.autograd.Function):
         gt = g.contiguous().float()
         T.grads[id(u)] = Act(gt.view(-1), u.N, u.H, u.W, 1, 1, 0)
         T.mark(u)
-        T.keep.append(gt)
         T.run_backward()
         return (None, None) + tuple(None for _ in range(len(ctx.needs_input_grad) - 2))
 

@@ -76,15 +76,22 @@ def _state(module: torch.nn.Module, skip: str = "") -> List[Tensor]:
 
 
 # ------------------------------------------------------------------------------------ skeletons (real kernels)
-_SKELETONS: Dict[str, torch.nn.Module] = {}
+# spec key -> (skeleton module, its lock).  One skeleton serves every exported program of that architecture; the
+# engine's plan cache on it (packed weights, folded BN tables: engine.Ctx, root.__dict__['_hiseg_plans']) is keyed
+# by the (address, version) of the state tensors, which the plans themselves do not hold.  So the skeleton holds the
+# state set it last ran with, and a call with another state set (a different exported program, or the same one
+# reloaded) drops the plans first: addresses of a released program cannot come back under the same version and
+# make another program's weights run.  The lock covers swap-in + run: two threads on one skeleton would otherwise
+# overwrite each other's parameters mid-forward.
+_SKELETONS: Dict[str, Tuple[torch.nn.Module, threading.Lock]] = {}
 _SKELETON_LOCK = threading.Lock()
 
 
-def _skeleton(spec: dict) -> torch.nn.Module:
+def _skeleton(spec: dict) -> Tuple[torch.nn.Module, threading.Lock]:
     key = json.dumps({k: spec[k] for k in ("cls", "init", "dtype")}, sort_keys=True)
     with _SKELETON_LOCK:
-        m = _SKELETONS.get(key)
-        if m is None:
+        ent = _SKELETONS.get(key)
+        if ent is None:
             from . import model as M
             cls = {c.__name__: c for c in (M.PreTrainedPeopleSegmentationUNet,
                                            M.HierarchicalRGBSegmentationModelWithFullImagePretrainedUNet)}[spec["cls"]]
@@ -93,18 +100,24 @@ def _skeleton(spec: dict) -> torch.nn.Module:
             m = m.to_empty(device="cpu").eval()   # storage is replaced by the op's state tensors on every call
             for mm in m.modules():
                 mm.hiseg_dtype = _DTYPES[spec["dtype"]]
-            _SKELETONS[key] = m
-    return m
+            ent = _SKELETONS[key] = (m, threading.Lock())
+    return ent
 
 
 def _run_on(spec: dict, state: Sequence[Tensor], skip: str, fn):
-    m = _skeleton(spec)
+    m, lock = _skeleton(spec)
     names = [k for k in m.state_dict().keys() if not (skip and k.startswith(skip))]
     if len(names) != len(state):
         raise ValueError(f"hiseg export op: {len(state)} state tensors for a {spec['cls']} with {len(names)}")
     from torch.nn.utils.stateless import _reparametrize_module
-    with _reparametrize_module(m, dict(zip(names, state))):
-        return fn(m)
+    ident = tuple(t.data_ptr() for t in state)
+    with lock:
+        if m.__dict__.get("_hiseg_state_ident") != ident:   # another program's weights: no plan carries over
+            m.__dict__.pop("_hiseg_plans", None)
+            m.__dict__["_hiseg_state_ident"] = ident
+            m.__dict__["_hiseg_state_held"] = list(state)   # keeps these addresses from being reused meanwhile
+        with _reparametrize_module(m, dict(zip(names, state))):
+            return fn(m)
 
 
 def _shape(template, env: dict):

@@ -17,6 +17,13 @@ model's flat parameters and its conv packing table.  Anything that re-allocates 
 trainable set or compute dtype -- changes GraphedStep's fingerprint of that state; the next call then
 drops the graph, runs ``eager`` steps again (the re-binding and re-packing happen there, for real) and
 captures anew.
+
+Data parallel (hiseg.distributed over RCCL): the bucketed gradient all-reduces are enqueued on the
+communication stream during the backward and joined back before the optimizer, so stream capture records
+them into the same graph (the RCCL kernels become graph nodes; the communicator was created by the eager
+steps).  The first eager step of a GradBucketSync learns its launch schedule, the second uses it, the
+capture records it.  Enabling the exchange after a capture changes the fingerprint (re-capture).  gloo
+process groups cannot be captured (host-side reduction): keep such steps eager.
 """
 from __future__ import annotations
 
@@ -70,6 +77,9 @@ class GraphedStep:
                 S = m.__dict__.get("_hiseg_train")
                 if S is not None:
                     fp += [id(m), id(S), id(S.flat), S.dtype, ptr(S.table), len(S.entries)]
+                sync = m.__dict__.get("_hiseg_grad_sync")
+                if sync is not None:   # a gradient exchange enabled after the capture must be captured too
+                    fp += [id(sync), ptr(sync.state.flat.grad) if sync.state is not None else None]
         return tuple(fp)
 
     def __call__(self):

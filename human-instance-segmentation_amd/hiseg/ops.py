@@ -111,19 +111,19 @@ def roi_align(feat: torch.Tensor, rois: torch.Tensor, oh: int, ow: int, scale_h:
     assert rois.dim() == 2 and rois.shape[1] == 5
     B, C, H, W = feat.shape
     d = L.RoiAlignDesc()
-    d.feat, d.B, d.C, d.H, d.W = feat.data_ptr(), B, C, H, W
-    d.rois, d.N = rois.data_ptr(), rois.shape[0]
+    d.feat, d.B, d.C, d.H, d.W = feat, B, C, H, W
+    d.rois, d.N = rois, rois.shape[0]
     d.oh, d.ow = int(oh), int(ow)
     d.scale_h, d.scale_w = float(scale_h), float(scale_w)
     d.aligned = int(bool(aligned))
     if aff_w is not None:
-        d.aff_w, d.aff_b, d.n_aff = aff_w.data_ptr(), _ptr(aff_b), aff_w.numel()
+        d.aff_w, d.aff_b, d.n_aff = aff_w, (aff_b), aff_w.numel()
     if nchw_out is not None:
         assert nchw_out.dtype == torch.float32 and nchw_out.is_contiguous()
-        d.out, d.out_dtype, d.o_nchw = nchw_out.data_ptr(), L.HISEG_F32, 1
+        d.out, d.out_dtype, d.o_nchw = nchw_out, L.HISEG_F32, 1
         d.o_cstride = 1
     else:
-        d.out, d.out_dtype, d.o_cstride, d.o_coff = out.ptr(), hdtype(out.dtype), out.cstride, out.coff
+        d.out, d.out_dtype, d.o_cstride, d.o_coff = out, hdtype(out.dtype), out.cstride, out.coff
         d.zero_to = zero_to
     L.check(L.lib().hiseg_roi_align_fwd(ctypes.byref(d), L.stream_ptr()), "roi_align")
 
@@ -302,24 +302,24 @@ def conv2d(p: ConvPlan, xa: Act, xb: Optional[Act] = None, out: Optional[Act] = 
     d.dtype, d.out_dtype = hdtype(dt), hdtype(out.dtype)
     d.N, d.H, d.W, d.Ho, d.Wo = xa.N, H, W, Ho, Wo
     d.KH, d.KW, d.stride, d.pad = p.kh, p.kw, p.stride, p.pad
-    d.srcA, d.a_cstride, d.a_coff, d.Ca, d.a_up = xa.ptr(), xa.cstride, xa.coff, p.ca, a_up
+    d.srcA, d.a_cstride, d.a_coff, d.Ca, d.a_up = xa, xa.cstride, xa.coff, p.ca, a_up
     if xb is not None:
-        d.srcB, d.b_cstride, d.b_coff, d.Cb = xb.ptr(), xb.cstride, xb.coff, p.cb
+        d.srcB, d.b_cstride, d.b_coff, d.Cb = xb, xb.cstride, xb.coff, p.cb
     if in_scale is not None:
-        d.in_scale = in_scale.data_ptr()
-    d.weight, d.Cout, d.Cout_pad, d.K_pad = p.weight.data_ptr(), p.gemm_cols, p.cout_pad, p.k_pad
-    d.scale, d.shift, d.act, d.act_beta = p.scale.data_ptr(), p.shift.data_ptr(), int(p.act), L.act_beta(p.act)
+        d.in_scale = in_scale
+    d.weight, d.Cout, d.Cout_pad, d.K_pad = p.weight, p.gemm_cols, p.cout_pad, p.k_pad
+    d.scale, d.shift, d.act, d.act_beta = p.scale, p.shift, int(p.act), L.act_beta(p.act)
     if residual is not None:
-        d.residual, d.r_cstride, d.r_coff = residual.ptr(), residual.cstride, residual.coff
+        d.residual, d.r_cstride, d.r_coff = residual, residual.cstride, residual.coff
     if mul is not None:
-        d.mul, d.m_cstride, d.m_coff = mul.ptr(), mul.cstride, mul.coff
-    d.out, d.o_cstride, d.o_coff = out.ptr(), out.cstride, out.coff
+        d.mul, d.m_cstride, d.m_coff = mul, mul.cstride, mul.coff
+    d.out, d.o_cstride, d.o_coff = out, out.cstride, out.coff
     if out2 is not None:
         assert out2.dtype == dt
-        d.out2, d.o2_cstride, d.o2_coff = out2.ptr(), out2.cstride, out2.coff
+        d.out2, d.o2_cstride, d.o2_coff = out2, out2.cstride, out2.coff
     d.convT = int(p.convT)
     if p.weight_frag is not None:
-        d.weight_frag = p.weight_frag.data_ptr()
+        d.weight_frag = p.weight_frag
     ws = None
     if p.kh * p.kw == 1 and p.k_pad >= 384 and dt == torch.bfloat16 and not p.convT:
         # small-grid, long-K 1x1 layers (the EfficientNet's deep SE-gated projections) split their K loop over
@@ -327,9 +327,9 @@ def conv2d(p: ConvPlan, xa: Act, xb: Optional[Act] = None, out: Optional[Act] = 
         nbytes = L.lib().hiseg_conv2d_workspace_bytes(ctypes.byref(d))
         if nbytes > 0:
             ws = torch.empty(nbytes, dtype=torch.uint8, device=xa.t.device)
-            d.workspace, d.workspace_bytes = ws.data_ptr(), nbytes
+            d.workspace, d.workspace_bytes = ws, nbytes
     if RECORD is not None:
-        dc = L.Conv2dDesc.from_buffer_copy(d)
+        dc = d.copy()
         keep = [t for t in (xa, xb, out, residual, mul, out2, ws) if t is not None]
         flops = 2.0 * d.N * d.Ho * d.Wo * p.gemm_cols * p.kh * p.kw * (xa.C + (xb.C if xb is not None else 0))
         RECORD.append((dc, keep, p, flops))
@@ -475,12 +475,12 @@ def layernorm2d(z: Act, weight: torch.Tensor, bias: torch.Tensor, eps: float, ac
     y = out if out is not None else Act.new(N, z.H, z.W, C, z.dtype, dev, cpad=z.cstride)
     d = L.BnApplyDesc()
     d.dtype, d.P, d.HW, d.C = hdtype(z.dtype), N * HW, HW, C
-    d.z, d.z_cstride, d.z_coff = z.ptr(), z.cstride, z.coff
-    d.scale, d.shift, d.per_sample = scale.data_ptr(), shift.data_ptr(), 1
+    d.z, d.z_cstride, d.z_coff = z, z.cstride, z.coff
+    d.scale, d.shift, d.per_sample = scale, shift, 1
     if residual is not None:
-        d.residual, d.r_cstride, d.r_coff = residual.ptr(), residual.cstride, residual.coff
+        d.residual, d.r_cstride, d.r_coff = residual, residual.cstride, residual.coff
     d.act, d.act_beta = int(act), L.act_beta(act)
-    d.y, d.y_cstride, d.y_coff = y.ptr(), y.cstride, y.coff
+    d.y, d.y_cstride, d.y_coff = y, y.cstride, y.coff
     L.check(lib.hiseg_bn_apply(ctypes.byref(d), L.stream_ptr()), "ln_apply")
     return y
 

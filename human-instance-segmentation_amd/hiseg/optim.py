@@ -341,7 +341,7 @@ class FusedAdamW(torch.optim.Optimizer):
         for every parameter whose moments this optimiser keeps."""
         f = self._flat
         plist = self.param_groups[0]["params"]
-        key = (id(f), len(plist))
+        key = (id(f), tuple(id(p) for p in plist))   # the list can change in place (parameters swapped)
         if self._slot_list is not None and self._slot_list[0] == key:
             return self._slot_list[1]
         b, e = self._range

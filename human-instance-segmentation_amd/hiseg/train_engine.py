@@ -61,7 +61,7 @@ def _ptr(t):
 def ew(a: Optional[Act]) -> L.EwView:
     v = L.EwView()
     if a is not None:
-        v.p, v.cstride, v.coff = a.t.data_ptr(), a.cstride, a.coff
+        v.p, v.cstride, v.coff = a.t, a.cstride, a.coff
     return v
 
 
@@ -227,8 +227,8 @@ class TrainState:
         for mode, dst, rows, kp in jobs:
             e = L.PackEntry()
             bias = mode == L.HISEG_PACK_BIAS
-            e.src = conv.bias.detach().data_ptr() if bias else src.data_ptr()
-            e.dst, e.dtype, e.mode = dst.data_ptr(), (L.HISEG_F32 if bias else hdtype(self.dtype)), mode
+            e.src = conv.bias.detach() if bias else src
+            e.dst, e.dtype, e.mode = dst, (L.HISEG_F32 if bias else hdtype(self.dtype)), mode
             e.Cout, e.Cin_real, e.KH, e.KW = cout, (cin if convT else ca_r + cb_r), kh, kw
             e.ca, e.ca_real, e.cb, e.cb_real = ca, ca_r, cb, cb_r
             e.rows, e.K_pad, e.cop, e.total = rows, kp, cop, rows * kp
@@ -344,21 +344,21 @@ def _desc(S: TrainState, p: TConv, xa: Act, xb: Optional[Act], out: Act, *, act=
     d.N, d.H, d.W = xa.N, H, W
     d.Ho, d.Wo = (H, W) if p.convT else ((H + 2 * p.pad - p.kh) // p.stride + 1, (W + 2 * p.pad - p.kw) // p.stride + 1)
     d.KH, d.KW, d.stride, d.pad = (1, 1, 1, 0) if p.convT else (p.kh, p.kw, p.stride, p.pad)
-    d.srcA, d.a_cstride, d.a_coff, d.Ca, d.a_up = xa.ptr(), xa.cstride, xa.coff, p.ca, 1
+    d.srcA, d.a_cstride, d.a_coff, d.Ca, d.a_up = xa, xa.cstride, xa.coff, p.ca, 1
     if xb is not None:
-        d.srcB, d.b_cstride, d.b_coff, d.Cb = xb.ptr(), xb.cstride, xb.coff, p.cb
-    d.weight, d.Cout, d.Cout_pad, d.K_pad = p.w_fwd.data_ptr(), p.gemm_cols, p.cout_pad, p.k_pad
+        d.srcB, d.b_cstride, d.b_coff, d.Cb = xb, xb.cstride, xb.coff, p.cb
+    d.weight, d.Cout, d.Cout_pad, d.K_pad = p.w_fwd, p.gemm_cols, p.cout_pad, p.k_pad
     if p.w_fwd_frag is not None:
-        d.weight_frag = p.w_fwd_frag.data_ptr()
-    d.scale, d.shift = p.ones.data_ptr(), (shift if shift is not None else p.shift).data_ptr()
+        d.weight_frag = p.w_fwd_frag
+    d.scale, d.shift = p.ones, (shift if shift is not None else p.shift)
     d.act, d.act_beta = int(act), L.act_beta(act)
     if residual is not None:
-        d.residual, d.r_cstride, d.r_coff = residual.ptr(), residual.cstride, residual.coff
+        d.residual, d.r_cstride, d.r_coff = residual, residual.cstride, residual.coff
     if mul is not None:
-        d.mul, d.m_cstride, d.m_coff = mul.ptr(), mul.cstride, mul.coff
-    d.out, d.o_cstride, d.o_coff = out.ptr(), out.cstride, out.coff
+        d.mul, d.m_cstride, d.m_coff = mul, mul.cstride, mul.coff
+    d.out, d.o_cstride, d.o_coff = out, out.cstride, out.coff
     if out2 is not None:
-        d.out2, d.o2_cstride, d.o2_coff = out2.ptr(), out2.cstride, out2.coff
+        d.out2, d.o2_cstride, d.o2_coff = out2, out2.cstride, out2.coff
     d.convT = int(p.convT)
     return d
 
@@ -386,7 +386,7 @@ def conv_wgrad(T: Tape, p: TConv, d: L.Conv2dDesc, dz: Act, bias_from_gemm: bool
     accumulated into the flat gradient."""
     S, lib = T.S, L.lib()
     want_bias = int(p.has_bias and bias_from_gemm)
-    wd = L.Conv2dDesc.from_buffer_copy(d)
+    wd = d.copy()
     ce = chunk_elems(S.dtype)
     if wd.Cout % ce:            # 1-/2-channel heads: the gradient buffer is padded with zeros
         wd.Cout = round_up(wd.Cout, ce)
@@ -424,27 +424,27 @@ def conv_bwd(T: Tape, p: TConv, d: L.Conv2dDesc, xa: Act, xb: Optional[Act], dz:
     else:
         dg.N, dg.H, dg.W, dg.Ho, dg.Wo = dz.N, dz.H, dz.W, xa.H, xa.W
         dg.KH, dg.KW, dg.stride, dg.pad = p.kh, p.kw, 1, p.kh - 1 - p.pad
-    dg.srcA, dg.a_cstride, dg.a_coff, dg.Ca, dg.a_up = dz.ptr(), dz.cstride, dz.coff, p.cop, 1
-    dg.weight, dg.Cout, dg.Cout_pad, dg.K_pad = p.w_dgrad.data_ptr(), p.dg_cols, p.dg_cout_pad, p.dg_k_pad
+    dg.srcA, dg.a_cstride, dg.a_coff, dg.Ca, dg.a_up = dz, dz.cstride, dz.coff, p.cop, 1
+    dg.weight, dg.Cout, dg.Cout_pad, dg.K_pad = p.w_dgrad, p.dg_cols, p.dg_cout_pad, p.dg_k_pad
     if p.w_dgrad_frag is not None:
-        dg.weight_frag = p.w_dgrad_frag.data_ptr()
+        dg.weight_frag = p.w_dgrad_frag
     zeros = S.cached.get(("zeros", p.dg_cout_pad))
     if zeros is None:
         zeros = torch.zeros(max(p.dg_cout_pad, 16), dtype=torch.float32, device=dz.t.device)
         ones = torch.ones(max(p.dg_cout_pad, 16), dtype=torch.float32, device=dz.t.device)
         S.cached[("zeros", p.dg_cout_pad)] = zeros
         S.cached[("ones", p.dg_cout_pad)] = ones
-    dg.scale, dg.shift, dg.act = S.cached[("ones", p.dg_cout_pad)].data_ptr(), zeros.data_ptr(), ACT_NONE
+    dg.scale, dg.shift, dg.act = S.cached[("ones", p.dg_cout_pad)], zeros, ACT_NONE
     if xb is None:
         gx, acc = T.grad(xa)
         if acc:
-            dg.residual, dg.r_cstride, dg.r_coff = gx.ptr(), gx.cstride, gx.coff
-        dg.out, dg.o_cstride, dg.o_coff = gx.ptr(), gx.cstride, gx.coff
+            dg.residual, dg.r_cstride, dg.r_coff = gx, gx.cstride, gx.coff
+        dg.out, dg.o_cstride, dg.o_coff = gx, gx.cstride, gx.coff
         _chk(_dgrad_launch(dg), "conv2d(dgrad)")
         T.mark(xa)
     else:
         tmp = Act.new(xa.N, xa.H, xa.W, p.ca + p.cb, dz.dtype, dz.t.device, cpad=p.ca + p.cb, zero=False)
-        dg.out, dg.o_cstride, dg.o_coff = tmp.ptr(), tmp.cstride, 0
+        dg.out, dg.o_cstride, dg.o_coff = tmp, tmp.cstride, 0
         _chk(_dgrad_launch(dg), "conv2d(dgrad)")
         for src_act, off, c in ((xa, 0, p.ca), (xb, p.ca, p.cb)):
             g, acc = T.grad(src_act)
@@ -496,13 +496,13 @@ def ln_forward(T: Tape, ln: LayerNorm2d, z: Act, *, act: int, residual: Optional
     y = out if out is not None else Act.new(N, z.H, z.W, C, z.dtype, z.t.device, cpad=z.cstride)
     d = L.BnApplyDesc()
     d.dtype, d.P, d.HW, d.C = hdtype(z.dtype), N * HW, HW, C
-    d.z, d.z_cstride, d.z_coff = z.ptr(), z.cstride, z.coff
-    d.scale, d.shift, d.per_sample = st.scale.data_ptr(), st.shift.data_ptr(), 1
+    d.z, d.z_cstride, d.z_coff = z, z.cstride, z.coff
+    d.scale, d.shift, d.per_sample = st.scale, st.shift, 1
     if residual is not None:
-        d.residual, d.r_cstride, d.r_coff = residual.ptr(), residual.cstride, residual.coff
+        d.residual, d.r_cstride, d.r_coff = residual, residual.cstride, residual.coff
     d.act, d.act_beta = int(act), L.act_beta(act)
-    d.chan_mul = _ptr(drop)
-    d.y, d.y_cstride, d.y_coff = y.ptr(), y.cstride, y.coff
+    d.chan_mul = (drop)
+    d.y, d.y_cstride, d.y_coff = y, y.cstride, y.coff
     _chk(lib.hiseg_bn_apply(ctypes.byref(d), _stream()), "ln_apply")
     return y, st
 
@@ -513,22 +513,22 @@ def ln_backward(T: Tape, ln: LayerNorm2d, z: Act, y: Act, st: LNState, dz: Act, 
     gy = T.grad_in(y)
     d = L.LnBwdDesc()
     d.dtype, d.N, d.HW, d.C = hdtype(z.dtype), z.N, z.H * z.W, z.C
-    d.dy, d.dy_cstride, d.dy_coff = gy.ptr(), gy.cstride, gy.coff
-    d.z, d.z_cstride, d.z_coff = z.ptr(), z.cstride, z.coff
-    d.chan_mul, d.act, d.act_beta = _ptr(drop), int(act), L.act_beta(act)
-    d.mean, d.invstd, d.scale, d.shift = st.mean.data_ptr(), st.invstd.data_ptr(), st.scale.data_ptr(), \
-        st.shift.data_ptr()
-    d.gamma = ln.weight.data_ptr()
-    d.dgamma = _ptr(S.grad(ln.weight)) if ln.weight.requires_grad else None
-    d.dbeta = _ptr(S.grad(ln.bias)) if ln.bias.requires_grad else None
-    d.dconv_bias = _ptr(conv_bias)
+    d.dy, d.dy_cstride, d.dy_coff = gy, gy.cstride, gy.coff
+    d.z, d.z_cstride, d.z_coff = z, z.cstride, z.coff
+    d.chan_mul, d.act, d.act_beta = (drop), int(act), L.act_beta(act)
+    d.mean, d.invstd, d.scale, d.shift = st.mean, st.invstd, st.scale, \
+        st.shift
+    d.gamma = ln.weight
+    d.dgamma = (S.grad(ln.weight)) if ln.weight.requires_grad else None
+    d.dbeta = (S.grad(ln.bias)) if ln.bias.requires_grad else None
+    d.dconv_bias = (conv_bias)
     d.accumulate_params = 1
-    d.dz, d.dz_cstride, d.dz_coff = dz.ptr(), dz.cstride, dz.coff
-    d.ws = st.ws.data_ptr()
+    d.dz, d.dz_cstride, d.dz_coff = dz, dz.cstride, dz.coff
+    d.ws = st.ws
     if residual is not None:
         gr, acc = T.grad(residual)
-        d.residual, d.r_cstride, d.r_coff = residual.ptr(), residual.cstride, residual.coff
-        d.dres, d.dres_cstride, d.dres_coff, d.dres_accumulate = gr.ptr(), gr.cstride, gr.coff, int(acc)
+        d.residual, d.r_cstride, d.r_coff = residual, residual.cstride, residual.coff
+        d.dres, d.dres_cstride, d.dres_coff, d.dres_accumulate = gr, gr.cstride, gr.coff, int(acc)
     _chk(lib.hiseg_ln_bwd(ctypes.byref(d), _stream()), "ln_bwd")
     if residual is not None:
         T.mark(residual)
@@ -558,13 +558,13 @@ def bn_forward(T: Tape, bn: nn.BatchNorm2d, z: Act, *, act: int, residual: Optio
     y = out if out is not None else Act.new(z.N, z.H, z.W, C, z.dtype, z.t.device, cpad=z.cstride)
     d = L.BnApplyDesc()
     d.dtype, d.P, d.HW, d.C = hdtype(z.dtype), P, z.H * z.W, C
-    d.z, d.z_cstride, d.z_coff = z.ptr(), z.cstride, z.coff
-    d.scale, d.shift = st.scale.data_ptr(), st.shift.data_ptr()
+    d.z, d.z_cstride, d.z_coff = z, z.cstride, z.coff
+    d.scale, d.shift = st.scale, st.shift
     if residual is not None:
-        d.residual, d.r_cstride, d.r_coff = residual.ptr(), residual.cstride, residual.coff
+        d.residual, d.r_cstride, d.r_coff = residual, residual.cstride, residual.coff
     d.act, d.act_beta = int(act), L.act_beta(act)
-    d.chan_mul = _ptr(drop)
-    d.y, d.y_cstride, d.y_coff = y.ptr(), y.cstride, y.coff
+    d.chan_mul = (drop)
+    d.y, d.y_cstride, d.y_coff = y, y.cstride, y.coff
     _chk(lib.hiseg_bn_apply(ctypes.byref(d), _stream()), "bn_apply")
     return y, st
 
@@ -580,27 +580,27 @@ def bn_backward(T: Tape, bn: nn.BatchNorm2d, z: Act, y: Act, st: BNState, dz: Ac
     part = torch.empty((lib.hiseg_bn_partials() + 1) * 3 * C, dtype=torch.float32, device=z.t.device)
     d = L.BnBwdDesc()
     d.dtype, d.P, d.HW, d.C = hdtype(z.dtype), P, z.H * z.W, C
-    d.dy, d.dy_cstride, d.dy_coff = gy.ptr(), gy.cstride, gy.coff
-    d.y, d.y_cstride, d.y_coff = y.ptr(), y.cstride, y.coff
-    d.z, d.z_cstride, d.z_coff = z.ptr(), z.cstride, z.coff
-    d.chan_mul, d.act, d.act_beta = _ptr(drop), int(act), L.act_beta(act)
-    d.mean, d.invstd, d.gamma, d.beta = st.mean.data_ptr(), st.invstd.data_ptr(), _ptr(bn.weight), _ptr(bn.bias)
-    d.partial = part.data_ptr()
-    d.dgamma = _ptr(S.grad(bn.weight)) if bn.weight is not None and bn.weight.requires_grad else None
-    d.dbeta = _ptr(S.grad(bn.bias)) if bn.bias is not None and bn.bias.requires_grad else None
-    d.dconv_bias = _ptr(conv_bias)
+    d.dy, d.dy_cstride, d.dy_coff = gy, gy.cstride, gy.coff
+    d.y, d.y_cstride, d.y_coff = y, y.cstride, y.coff
+    d.z, d.z_cstride, d.z_coff = z, z.cstride, z.coff
+    d.chan_mul, d.act, d.act_beta = (drop), int(act), L.act_beta(act)
+    d.mean, d.invstd, d.gamma, d.beta = st.mean, st.invstd, (bn.weight), (bn.bias)
+    d.partial = part
+    d.dgamma = (S.grad(bn.weight)) if bn.weight is not None and bn.weight.requires_grad else None
+    d.dbeta = (S.grad(bn.bias)) if bn.bias is not None and bn.bias.requires_grad else None
+    d.dconv_bias = (conv_bias)
     d.accumulate_params = 1
-    d.dz, d.dz_cstride, d.dz_coff = dz.ptr(), dz.cstride, dz.coff
+    d.dz, d.dz_cstride, d.dz_coff = dz, dz.cstride, dz.coff
     if residual is not None:
         gr, acc = T.grad(residual)
-        d.dres, d.dres_cstride, d.dres_coff, d.dres_accumulate = gr.ptr(), gr.cstride, gr.coff, int(acc)
+        d.dres, d.dres_cstride, d.dres_coff, d.dres_accumulate = gr, gr.cstride, gr.coff, int(acc)
     elif act == ACT_RELU:   # ReLU mask recomputed from z with the forward's folded affine: y is not re-read
-        d.fwd_scale, d.fwd_shift = st.scale.data_ptr(), st.shift.data_ptr()
+        d.fwd_scale, d.fwd_shift = st.scale, st.shift
     if int(act) in (ACT_GELU, ACT_SWISH) or (int(act) == ACT_SILU and residual is not None):
         # derivative at the forward's own pre-activation z*scale + shift (+ residual)
-        d.fwd_scale, d.fwd_shift = st.scale.data_ptr(), st.shift.data_ptr()
+        d.fwd_scale, d.fwd_shift = st.scale, st.shift
         if residual is not None:
-            d.residual, d.r_cstride, d.r_coff = residual.ptr(), residual.cstride, residual.coff
+            d.residual, d.r_cstride, d.r_coff = residual, residual.cstride, residual.coff
     _chk(lib.hiseg_bn_bwd(ctypes.byref(d), _stream()), "bn_bwd")
     if residual is not None:
         T.mark(residual)
@@ -666,11 +666,10 @@ def _conv_smooth_act(T: Tape, p: TConv, act: int, x: Act, xb: Optional[Act]) -> 
     zero = torch.zeros(z.C, dtype=torch.float32, device=z.t.device)
     a = L.BnApplyDesc()
     a.dtype, a.P, a.HW, a.C = hdtype(z.dtype), z.N * z.H * z.W, z.H * z.W, z.C
-    a.z, a.z_cstride, a.z_coff = z.ptr(), z.cstride, z.coff
-    a.scale, a.shift, a.act, a.act_beta = one.data_ptr(), zero.data_ptr(), int(act), L.act_beta(act)
-    a.y, a.y_cstride, a.y_coff = y.ptr(), y.cstride, y.coff
+    a.z, a.z_cstride, a.z_coff = z, z.cstride, z.coff
+    a.scale, a.shift, a.act, a.act_beta = one, zero, int(act), L.act_beta(act)
+    a.y, a.y_cstride, a.y_coff = y, y.cstride, y.coff
     _chk(lib.hiseg_bn_apply(ctypes.byref(a), _stream()), "act_apply")
-    T.keep.extend([one, zero])
 
     def back():
         gy = T.grad_in(y)
@@ -697,18 +696,17 @@ def residual_block(T: Tape, blk: nn.Module, x: Act, drop=None) -> Act:
 
 
 def dropout_mask(T: Tape, m: nn.Module, N: int, C: int, device) -> Optional[torch.Tensor]:
-    """Dropout2d mask [N, C] (0 or 1/(1-p)), or None when the module is a no-op.  The tape keeps the mask: a
-    backward reaches it through descriptors holding its raw address (_dropout_after's copy of the forward
-    descriptor), and a mask freed after the forward let the caching allocator hand its block to the next small
-    tensor -- the backward then scaled by whatever that tensor held (a different loss from the first update on,
-    depending on the allocator's history)."""
+    """Dropout2d mask [N, C] (0 or 1/(1-p)), or None when the module is a no-op.  A backward reaches the mask
+    through a descriptor built in the forward (_dropout_after's BnApplyDesc) or a closure variable; both keep it
+    alive (hiseg._lib.Desc holds every tensor assigned to a pointer field).  Round 3's flake was this mask held
+    only as a raw address: freed after the forward, its block went to the next small tensor and the backward
+    scaled by whatever that tensor held."""
     p = float(getattr(m, "p", 0.0))
     if p <= 0.0:
         return None
     out = torch.empty(N * C, dtype=torch.float32, device=device)
     _chk(L.lib().hiseg_dropout2d_mask_dev(N, C, p, T.S.seed_base.data_ptr(), T.S.next_seed(), out.data_ptr(),
                                           _stream()), "dropout2d_mask")
-    T.keep.append(out)
     return out
 
 
@@ -902,19 +900,18 @@ def _dropout_after(T: Tape, m: nn.Module, y: Act) -> Act:
     zero = torch.zeros(y.C, dtype=torch.float32, device=y.t.device)
     d = L.BnApplyDesc()
     d.dtype, d.P, d.HW, d.C = hdtype(y.dtype), y.N * y.H * y.W, y.H * y.W, y.C
-    d.z, d.z_cstride, d.z_coff = y.ptr(), y.cstride, y.coff
-    d.scale, d.shift, d.act, d.chan_mul = one.data_ptr(), zero.data_ptr(), ACT_NONE, drop.data_ptr()
-    d.y, d.y_cstride, d.y_coff = out.ptr(), out.cstride, out.coff
+    d.z, d.z_cstride, d.z_coff = y, y.cstride, y.coff
+    d.scale, d.shift, d.act, d.chan_mul = one, zero, ACT_NONE, drop
+    d.y, d.y_cstride, d.y_coff = out, out.cstride, out.coff
     _chk(lib.hiseg_bn_apply(ctypes.byref(d), _stream()), "dropout2d")
-    T.keep.extend([one, zero])
 
     def back():
         gy = T.grad_in(out)
         gx, acc = T.grad(y)
         assert not acc
-        d2 = L.BnApplyDesc.from_buffer_copy(d)
-        d2.z, d2.z_cstride, d2.z_coff = gy.ptr(), gy.cstride, gy.coff
-        d2.y, d2.y_cstride, d2.y_coff = gx.ptr(), gx.cstride, gx.coff
+        d2 = d.copy()
+        d2.z, d2.z_cstride, d2.z_coff = gy, gy.cstride, gy.coff
+        d2.y, d2.y_cstride, d2.y_coff = gx, gx.cstride, gx.coff
         _chk(lib.hiseg_bn_apply(ctypes.byref(d2), _stream()), "dropout2d_bwd")
         T.mark(y)
     T.push(back)
@@ -969,14 +966,14 @@ def hier_head_train(T: Tape, head: nn.Module, feat: Act):
         bst.shift = torch.empty_like(bst.scale)
     ud = L.UbfDesc()
     ud.dtype = hdtype(S.dtype)
-    ud.low, ud.N, ud.h, ud.w = low.ptr(), N, h, w
-    ud.ut_w, ud.ut_b = up[0].weight.data_ptr(), up[0].bias.data_ptr()
-    ud.gamma, ud.beta = ubn.weight.data_ptr(), ubn.bias.data_ptr()
-    ud.mean, ud.invstd, ud.scale, ud.shift = bst.mean.data_ptr(), bst.invstd.data_ptr(), bst.scale.data_ptr(), \
-        bst.shift.data_ptr()
-    ud.u1_w, ud.u1_b = up[3].weight.data_ptr(), up[3].bias.data_ptr()
-    ud.tfeat, ud.Ct, ud.t_w, ud.t_b = t.ptr(), t.C, last.weight.data_ptr(), last.bias.data_ptr()
-    ud.logits, ud.bgfg, ud.tn = logits.data_ptr(), bgfg.data_ptr(), tn.data_ptr()
+    ud.low, ud.N, ud.h, ud.w = low, N, h, w
+    ud.ut_w, ud.ut_b = up[0].weight, up[0].bias
+    ud.gamma, ud.beta = ubn.weight, ubn.bias
+    ud.mean, ud.invstd, ud.scale, ud.shift = bst.mean, bst.invstd, bst.scale, \
+        bst.shift
+    ud.u1_w, ud.u1_b = up[3].weight, up[3].bias
+    ud.tfeat, ud.Ct, ud.t_w, ud.t_b = t, t.C, last.weight, last.bias
+    ud.logits, ud.bgfg, ud.tn = logits, bgfg, tn
     ud.act, ud.act_beta, ud.layernorm = int(uact), L.act_beta(uact), int(uln)
     ws = torch.empty(lib.hiseg_ubf_ws(N), dtype=torch.float32, device=dev)
     if uln:
@@ -989,7 +986,6 @@ def hier_head_train(T: Tape, head: nn.Module, feat: Act):
                                      ubn.running_mean.data_ptr(), ubn.running_var.data_ptr(), ws.data_ptr(),
                                      _stream()), "ubf_train_fwd")
         torch.autograd.graph.increment_version([ubn.running_mean, ubn.running_var])
-    T.keep.extend([bst, ws])
     aux = {"bg_fg_logits": bgfg, "target_nontarget_logits": tn}
 
     def back():
@@ -1000,9 +996,9 @@ def hier_head_train(T: Tape, head: nn.Module, feat: Act):
         glow, acc = T.grad(low)
         assert not acc
         gr = L.UbfGrads()
-        gr.dut_w, gr.dut_b = S.grad(up[0].weight).data_ptr(), S.grad(up[0].bias).data_ptr()
-        gr.dgamma, gr.dbeta = S.grad(ubn.weight).data_ptr(), S.grad(ubn.bias).data_ptr()
-        gr.du1_w, gr.du1_b = S.grad(up[3].weight).data_ptr(), S.grad(up[3].bias).data_ptr()
+        gr.dut_w, gr.dut_b = S.grad(up[0].weight), S.grad(up[0].bias)
+        gr.dgamma, gr.dbeta = S.grad(ubn.weight), S.grad(ubn.bias)
+        gr.du1_w, gr.du1_b = S.grad(up[3].weight), S.grad(up[3].bias)
         _chk(lib.hiseg_ubf_train_bwd(ctypes.byref(ud), dl.data_ptr(), _ptr(T.ctx.get("dbgfg")),
                                      _ptr(T.ctx.get("dtn")), db.data_ptr(), dtn.data_ptr(), glow.ptr(),
                                      ws.data_ptr(), ctypes.byref(gr), _stream()), "ubf_train_bwd")
@@ -1088,12 +1084,12 @@ def roi_path_train(model: nn.Module, S: TrainState, T: Tape, images: torch.Tenso
         if not acc or not oc.weight.requires_grad:
             return
         d = L.RoiAlignDesc()
-        d.feat, d.B, d.C, d.H, d.W = u.data_ptr(), u.shape[0], 1, u.shape[2], u.shape[3]
-        d.rois, d.N = rois.data_ptr(), N
+        d.feat, d.B, d.C, d.H, d.W = u, u.shape[0], 1, u.shape[2], u.shape[3]
+        d.rois, d.N = rois, N
         d.oh, d.ow = rh, rw
         d.scale_h, d.scale_w = float(ma.spatial_scale_h), float(ma.spatial_scale_w)
         d.aligned = int(bool(ma.aligned))
-        d.aff_w, d.aff_b, d.n_aff = oc.weight.data_ptr(), oc.bias.data_ptr(), 2
+        d.aff_w, d.aff_b, d.n_aff = oc.weight, oc.bias, 2
         ws = torch.empty(lib.hiseg_roi_align_ws(N), dtype=torch.float32, device=dev)
         _chk(lib.hiseg_roi_align_bwd_affine(ctypes.byref(d), g.ptr(), hdtype(g.dtype), g.cstride, g.coff,
                                             ws.data_ptr(), S.grad(oc.weight).data_ptr(), S.grad(oc.bias).data_ptr(),

@@ -50,6 +50,10 @@ int hiseg_built_for_gfx950(void);
  * times the CU count of them -- so that a kernel which reads LDS it did not write in its own dispatch (stale data
  * left by an earlier kernel: LDS is not cleared between dispatches) sees the pattern (e.g. a NaN). */
 int hiseg_debug_fill_lds(unsigned pattern, int rounds, hiseg_stream_t stream);
+/* Test utility: counts of the kernel choices that depended on where a layer's two sources lie in memory, since the
+ * last reset -- `declined`: a kernel refused the layer for its placement (another kernel took it); `far`: a kernel
+ * took it through one buffer resource per source.  Either pointer may be NULL; reset != 0 zeroes both after reading. */
+int hiseg_placement_stats(long long* declined, long long* far, int reset);
 
 /* A HIP stream whose kernels run only on the CUs whose bits are set in mask[0..nwords) (hipExtStreamCreateWithCUMask),
  * for the serving schedule's full-image UNet stream (hiseg.StreamPipelinedExport(cu_mask=...)); destroy with

@@ -102,6 +102,8 @@ def roi_align_torch(feat: torch.Tensor, rois: torch.Tensor, oh: int, ow: int, sc
 
 # ---------------------------------------------------------------------------------------- loss
 def _ce(logits, target, weight=None, reduction="mean"):
+    if weight is not None:   # (float64 oracle runs: the class weights follow the logits' dtype)
+        weight = weight.to(logits.dtype)
     return F.cross_entropy(logits, target, weight=weight, reduction=reduction)
 
 

@@ -3,6 +3,10 @@ import sys
 
 import pytest
 
+# Descriptor pointer fields take tensors (held by the descriptor) or None, never raw addresses
+# (hiseg._lib.Desc): the suite runs in strict mode, rank processes it spawns inherit it.
+os.environ.setdefault("HISEG_STRICT_PTRS", "1")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "human-instance-segmentation_amd")
 GOLDEN = os.path.join(ROOT, "tests", "golden")

@@ -68,10 +68,11 @@ def test_release_library_refuses_diagnostic_conv_variants():
     d.N, d.H, d.W, d.Ho, d.Wo = 1, 16, 16, 16, 16
     d.KH, d.KW, d.stride, d.pad = 3, 3, 1, 1
     fake = 1 << 20
-    d.srcA, d.a_cstride, d.a_coff, d.Ca, d.a_up = fake, 256, 0, 256, 1
-    d.weight, d.Cout, d.Cout_pad, d.K_pad = fake, 256, 256, 9 * 256
-    d.scale, d.shift, d.act = fake, fake, 0
-    d.out, d.o_cstride, d.o_coff = fake, 256, 0
+    with L.raw_pointers():   # never launched: the library refuses the variant first
+        d.srcA, d.a_cstride, d.a_coff, d.Ca, d.a_up = fake, 256, 0, 256, 1
+        d.weight, d.Cout, d.Cout_pad, d.K_pad = fake, 256, 256, 9 * 256
+        d.scale, d.shift, d.act = fake, fake, 0
+        d.out, d.o_cstride, d.o_coff = fake, 256, 0
     for v in (9, 10, 18, 19, 20, 30, 40, 41, 44, 59, 73, 75, 76, 77, 79, 102, -5):
         st = L.lib().hiseg_conv2d_fwd_variant(ctypes.byref(d), v, None)
         assert st == -1, v   # HISEG_ERR_BAD_ARG
@@ -99,8 +100,9 @@ def test_conv_splitk_workspace_plan_is_batch_invariant():
         d.Ca, d.a_cstride, d.a_up = Ca, Ca, 1
         d.Cout, d.Cout_pad = Cout, (Cout + 15) // 16 * 16
         d.K_pad = (k * k * Ca + 63) // 64 * 64
-        d.srcA = d.weight = d.scale = d.shift = d.out = 1 << 20
-        d.in_scale = (1 << 20) if gated else None
+        with L.raw_pointers():   # planning only, never launched
+            d.srcA = d.weight = d.scale = d.shift = d.out = 1 << 20
+            d.in_scale = (1 << 20) if gated else None
         return L.lib().hiseg_conv2d_workspace_bytes(ctypes.byref(d))
 
     for Ca, Cout, H, W in ((2304, 384, 20, 20), (960, 160, 40, 40), (1152, 192, 15, 20), (3840, 640, 20, 20)):

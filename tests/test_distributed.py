@@ -153,13 +153,19 @@ def _state_worker(rank, world, port, q):
         dist.init_process_group("gloo", rank=rank, world_size=world)
         import types
         from hiseg import distributed as HD
-        opt = types.SimpleNamespace(   # FusedAdamW's device state (moments, segment bounds, step counts)
-            exp_avg=torch.full((6,), float(rank + 1)), exp_avg_sq=torch.full((6,), 10.0 * (rank + 1)),
-            _seg_start=torch.tensor([0, 2, 6]), _steps=torch.tensor([3 + rank, 5 + rank, 3 + rank, 5 + rank],
-                                                                     dtype=torch.int32))
+        # FusedAdamW's device state (moments, segment bounds, step counts); rank 1 has a different segment count
+        # (another unfreeze history): it adopts rank 0's table size
+        if rank == 0:
+            seg, steps, nseg = torch.tensor([0, 2, 6]), torch.tensor([3, 5, 3, 5], dtype=torch.int32), 2
+        else:
+            seg, steps, nseg = torch.tensor([0, 1, 4, 6]), torch.tensor([1, 2, 3, 1, 2, 3], dtype=torch.int32), 3
+        opt = types.SimpleNamespace(exp_avg=torch.full((6,), float(rank + 1)),
+                                    exp_avg_sq=torch.full((6,), 10.0 * (rank + 1)),
+                                    _seg_start=seg, _steps=steps, _nseg=nseg)
         loss = types.SimpleNamespace(_state=torch.arange(8, dtype=torch.float64) * (rank + 1))
         HD.broadcast_training_state(opt, loss)
-        q.put((rank, [opt.exp_avg.tolist(), opt.exp_avg_sq.tolist(), opt._steps.tolist(), loss._state.tolist()]))
+        q.put((rank, [opt.exp_avg.tolist(), opt.exp_avg_sq.tolist(), opt._steps.tolist(), loss._state.tolist(),
+                      opt._seg_start.tolist(), opt._nseg]))
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover
         q.put((rank, repr(e)))
@@ -179,4 +185,4 @@ def test_broadcast_training_state_gloo_world2():
         p.join(timeout=60)
     for rank, res in out:
         assert not isinstance(res, str), res
-        assert res == [[1.0] * 6, [10.0] * 6, [3, 5, 3, 5], [float(i) for i in range(8)]]
+        assert res == [[1.0] * 6, [10.0] * 6, [3, 5, 3, 5], [float(i) for i in range(8)], [0, 2, 6], 2]

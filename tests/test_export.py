@@ -121,12 +121,30 @@ def test_skeleton_rebuilds_the_module_from_its_spec():
     m = _model(use_contour_detection=False)
     hiseg.set_compute_dtype(m, torch.bfloat16)
     sp = json.loads(X._head_spec(m, "full"))
-    sk = X._skeleton(sp)
+    sk, _ = X._skeleton(sp)
     assert type(sk) is type(m) and sk.hiseg_dtype == torch.bfloat16
     assert list(sk.state_dict().keys()) == list(m.state_dict().keys())
     assert all(a.shape == b.shape for a, b in zip(sk.state_dict().values(), m.state_dict().values()))
     assert [n for n, _ in sp["outs"]] == [n for n, _ in X.rgb_out_templates(m, "full")]
     assert "contours" not in dict(sp["outs"])
+
+
+def test_skeleton_plans_do_not_carry_over_between_state_sets():
+    """one skeleton serves every exported program of an architecture; its engine plan cache must not
+    survive a change of state set (a plan is keyed by the state tensors' addresses + versions, which a released
+    program's tensors could hand to the next one).  Same state set: plans kept; another set: dropped, and the
+    skeleton holds the set it runs with."""
+    import json
+    m = _model(use_contour_detection=False)
+    sp = json.loads(X._head_spec(m, "full"))
+    state_a = X._state(m, X.UNET_PREFIX)
+    state_b = [t.detach().clone() for t in state_a]
+    sk, _ = X._skeleton(sp)
+    X._run_on(sp, state_a, X.UNET_PREFIX, lambda k: k.__dict__.__setitem__("_hiseg_plans", {"marker": 1}))
+    assert X._run_on(sp, state_a, X.UNET_PREFIX, lambda k: k.__dict__.get("_hiseg_plans")) == {"marker": 1}
+    assert X._run_on(sp, state_b, X.UNET_PREFIX, lambda k: k.__dict__.get("_hiseg_plans")) is None
+    held = sk.__dict__["_hiseg_state_held"]
+    assert len(held) == len(state_b) and all(a is b for a, b in zip(held, state_b))
 
 
 # ------------------------------------------------------------------------------------ ONNX lowerings

@@ -1,0 +1,326 @@
+"""Data-parallel training on the GPU (hiseg.distributed), VERDICT r3 item 1.
+
+(a) World size 2 on the one-GPU box: two rank processes share cuda:0 and exchange over gloo (which takes
+device tensors: it stages them through host memory), so the whole eager DDP path -- first-step schedule
+recording, bucketed all-reduces launched on the communication stream while the tape's backward still runs,
+the loss's class-count exchange -- executes against live HIP kernels.  The bar: after each of 3 steps every
+rank's post-exchange gradient equals, bit for bit, the mean of the two half-batch gradients one process
+computes with the summed class counts (per-rank BatchNorm, as the reference has no SyncBN), and the
+parameters after the optimizer step are identical on both ranks and to that single-process trajectory.
+Cases: the C4 B7-ultra ROI model at a small image size (1 ROI per image, train_advanced.py:680-762) and the
+C5 B7 -> B0 distillation step (train_distillation_staged.py:256-366).
+
+(b) World size 1 over RCCL: hiseg.GraphedStep captures the step WITH its bucketed all-reduces on the
+communication stream; the replayed steps are bit-identical to eager ones.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import filler
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+STEPS = 3
+C4_IMG = (2, 96, 128)      # images per rank, H, W (UNet input: multiples of 32)
+C5_IMG = (2, 64, 96)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+# ------------------------------------------------------------------------------------------ C4 ROI model
+def _c4_model():
+    import hiseg
+    from helpers import configs, hiseg_kwargs
+    m = hiseg.create_rgb_hierarchical_model(**hiseg_kwargs(dict(configs()["b7"]["model_kwargs"])))
+    filler.fill_module(m)
+    for mod in m.modules():     # parity mode: no Dropout2d (each process would draw its own masks)
+        if isinstance(mod, (torch.nn.Dropout, torch.nn.Dropout2d)):
+            mod.p = 0.0
+    hiseg.set_compute_dtype(m, torch.bfloat16)
+    m = m.to(DEV).train()
+    _, H, W = C4_IMG
+    for mm in (m.roi_align_mask, m.roi_align_rgb):
+        mm.spatial_scale_h, mm.spatial_scale_w = H, W
+    return m
+
+
+def _c4_batch(world):
+    """The whole batch: world x n images, one ROI each (dataset.py:74-80), 3-class targets at the mask size."""
+    from helpers import configs
+    n, H, W = C4_IMG
+    B = world * n
+    images = torch.from_numpy(filler.uniform(401, (B, 3, H, W)))
+    rois = torch.from_numpy(filler.box_rois(402, B, 1))
+    mh, mw = configs()["b7"]["model_kwargs"]["mask_size"]
+    tgt = torch.from_numpy(filler.ellipse_targets(403, B, mh, mw))
+    return images, rois, tgt
+
+
+def _c4_half(batch, r):
+    """Rank r's shard: its images, their ROIs with the batch index re-based, their targets."""
+    images, rois, tgt = batch
+    n = C4_IMG[0]
+    sl = slice(r * n, (r + 1) * n)
+    rr = rois[sl].clone()
+    rr[:, 0] -= r * n
+    return images[sl].to(DEV), rr.to(DEV), tgt[sl].to(DEV)
+
+
+def _loss():
+    import hiseg
+    return hiseg.RefinedHierarchicalLoss(use_boundary_aware_loss=True, use_contour_detection=True,
+                                         use_distance_transform=True, boundary_aware_weight=0.1,
+                                         contour_loss_weight=0.1, distance_loss_weight=0.1)
+
+
+def _opt(m):
+    import hiseg
+    return hiseg.FusedAdamW(m, lr=5e-4, weight_decay=0.01, max_grad_norm=1.0)
+
+
+# ------------------------------------------------------------------------------------------ C5 distillation
+def _c5_model():
+    import hiseg
+    model, loss_fn = hiseg.create_unet_distillation_model("timm-efficientnet-b0", "timm-efficientnet-b7",
+                                                          teacher_checkpoint="absent.pth", device="cpu",
+                                                          progressive_unfreeze=True)
+    filler.fill_module(model.student, seed=11)
+    filler.fill_module(model.teacher, seed=12)
+    hiseg.set_compute_dtype(model, torch.bfloat16)
+    model = model.to(DEV).train()
+    loss_fn.temperature = 4.0
+    return model, loss_fn
+
+
+def _c5_batch(world):
+    from oracle import distill as OD
+    n, H, W = C5_IMG
+    x = torch.from_numpy(filler.normal(411, (world * n, 3, H, W)))
+    _, _, m = OD.np_inputs(412, world * n, H, W)
+    return x, m
+
+
+def _c5_opt(model):
+    import hiseg
+    return hiseg.FusedAdamW(model.student, lr=1e-3, weight_decay=1e-4, max_grad_norm=1.0,
+                            params=model.student.get_decoder_parameters())
+
+
+# ------------------------------------------------------------------------------------------ rank processes
+def _rank_worker(rank, world, port, case, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from hiseg import distributed as HD
+        grads, params = [], []
+        if case == "c4":
+            m = _c4_model()
+            sync = HD.enable_grad_sync(m, bucket_mb=16.0)
+            loss_fn = HD.sync_loss_class_weights(_loss())
+            images, rois, tgt = _c4_half(_c4_batch(world), rank)
+            opt = None
+            for _ in range(STEPS):
+                logits, aux = m(images, rois)
+                loss, _ = loss_fn(logits, tgt, aux)
+                opt = opt or _opt(m)
+                opt.zero_grad()
+                loss.backward()
+                torch.cuda.synchronize()
+                S = m.__dict__["_hiseg_train"]
+                grads.append(S.flat.grad.cpu().clone())
+                opt.step()
+                torch.cuda.synchronize()
+                params.append(S.flat.data.cpu().clone())
+        else:
+            model, loss_fn = _c5_model()
+            sync = HD.enable_grad_sync(model.student, bucket_mb=2.0)
+            x, msk = _c5_batch(world)
+            n = C5_IMG[0]
+            x, msk = x[rank * n:(rank + 1) * n].to(DEV), msk[rank * n:(rank + 1) * n].to(DEV)
+            opt = None
+            for _ in range(STEPS):
+                s, t = model(x)
+                loss, _ = loss_fn(s, t, msk)
+                opt = opt or _c5_opt(model)
+                opt.zero_grad()
+                loss.backward()
+                torch.cuda.synchronize()
+                S = model.student.__dict__["_hiseg_train"]
+                grads.append(S.flat.grad.cpu().clone())
+                opt.step()
+                torch.cuda.synchronize()
+                params.append(S.flat.data.cpu().clone())
+        q.put((rank, grads, params, len(sync.buckets), sorted(k for k in sync.launch_after if k >= 0)))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - surfaced by the parent
+        import traceback
+        q.put((rank, traceback.format_exc() + repr(e), None, None, None))
+
+
+def _run_ranks(case, world=2):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_worker, args=(r, world, port, case, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        out = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r, g, *_ in out:
+        assert not isinstance(g, str), f"rank {r}: {g}"
+    return out
+
+
+def _counts_of(loss, tgt):
+    """The 4 class pixel counts one rank contributes (hiseg_loss_fwd_begin, what its count_sync all-reduces)."""
+    import ctypes
+    from hiseg import _lib as L
+    n, H, W = tgt.shape
+    cfg, _ = loss._cfg(H, W, True, True)
+    ws = torch.empty(int(L.lib().hiseg_loss_ws(n, H, W)), dtype=torch.float32, device=DEV)
+    c = torch.empty(4, dtype=torch.float64, device=DEV)
+    L.check(L.lib().hiseg_loss_fwd_begin(ctypes.byref(cfg), n, H, W, tgt.contiguous().data_ptr(), ws.data_ptr(),
+                                         c.data_ptr(), L.stream_ptr()), "loss_fwd_begin")
+    return c
+
+
+def _check(out, ref_grads, ref_params):
+    (_, g0, p0, nb, sched), (_, g1, p1, _, _) = out
+    assert nb > 1 and sched, "the exchange should run in several buckets, some launched during the backward"
+    for step in range(STEPS):
+        assert torch.isfinite(ref_grads[step]).all()
+        assert torch.equal(g0[step], g1[step]), f"step {step}: the ranks' averaged gradients differ"
+        d = (g0[step] - ref_grads[step]).abs().max().item()
+        assert torch.equal(g0[step], ref_grads[step]), f"step {step}: gradient differs from the half-batch mean by {d}"
+        assert torch.equal(p0[step], p1[step]), f"step {step}: parameters differ across ranks"
+        assert torch.equal(p0[step], ref_params[step]), f"step {step}: parameters differ from the single process"
+    assert not torch.equal(p0[0], p0[-1])
+
+
+def test_ddp_world2_c4_b7_ultra_equals_half_batch_mean():
+    """C4 (B7-ultra ROI model, 1 ROI per image) at world size 2 over gloo on one GPU vs the single-process mean
+    of the two half-batch gradients (class counts summed over the halves, sync_loss_class_weights)."""
+    world = 2
+    out = _run_ranks("c4", world)
+    m = _c4_model()
+    losses = [_loss(), _loss()]   # one loss per rank: each carries its own (identical) EMA state
+    batch = _c4_batch(world)
+    halves = [_c4_half(batch, r) for r in range(world)]
+    for r in range(world):
+        other = halves[1 - r][2]
+        losses[r].count_sync = lambda c, t=other, l=losses[r]: c.add_(_counts_of(l, t))
+    opt, ref_grads, ref_params = None, [], []
+    S = None
+    for _ in range(STEPS):
+        gs = []
+        for r in range(world):
+            images, rois, tgt = halves[r]
+            logits, aux = m(images, rois)
+            loss, _ = losses[r](logits, tgt, aux)
+            opt = opt or _opt(m)
+            opt.zero_grad()
+            loss.backward()
+            S = m.__dict__["_hiseg_train"]
+            gs.append(S.flat.grad.clone())
+        mean = (gs[0] + gs[1]) * (1.0 / world)
+        S.flat.grad.copy_(mean)
+        ref_grads.append(mean.cpu())
+        opt.step()
+        torch.cuda.synchronize()
+        ref_params.append(S.flat.data.cpu().clone())
+    _check(out, ref_grads, ref_params)
+
+
+def test_ddp_world2_c5_distillation_equals_half_batch_mean():
+    """C5 distillation (B7 teacher, B0 student decoder-only phase, decoder AdamW with clipping) at world size 2
+    over gloo on one GPU vs the single-process mean of the two half-batch student gradients."""
+    world = 2
+    out = _run_ranks("c5", world)
+    model, loss_fn = _c5_model()
+    x, msk = _c5_batch(world)
+    n = C5_IMG[0]
+    opt, ref_grads, ref_params, S = None, [], [], None
+    for _ in range(STEPS):
+        gs = []
+        for r in range(world):
+            s, t = model(x[r * n:(r + 1) * n].to(DEV))
+            loss, _ = loss_fn(s, t, msk[r * n:(r + 1) * n].to(DEV))
+            opt = opt or _c5_opt(model)
+            opt.zero_grad()
+            loss.backward()
+            S = model.student.__dict__["_hiseg_train"]
+            gs.append(S.flat.grad.clone())
+        mean = (gs[0] + gs[1]) * (1.0 / world)
+        S.flat.grad.copy_(mean)
+        ref_grads.append(mean.cpu())
+        opt.step()
+        torch.cuda.synchronize()
+        ref_params.append(S.flat.data.cpu().clone())
+    _check(out, ref_grads, ref_params)
+
+
+# ------------------------------------------------------------------------------------------ (b) graph capture
+def test_graphed_ddp_step_rccl_world1_equals_eager():
+    """GraphedStep over a data-parallel B0 train step (RCCL, world size 1): the bucketed all-reduces on the
+    communication stream and the class-count all-reduce are captured with the kernels; 5 replayed steps give the
+    losses, parameters and optimizer moments of 5 eager steps bit for bit."""
+    import hiseg
+    from hiseg import distributed as HD
+    from test_gpu_train import _model
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ["MASTER_PORT"] = str(_free_port())
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device(DEV, 0))
+    try:
+        images = torch.from_numpy(filler.uniform(421, (2, 3, 96, 128))).to(DEV)
+        rois = torch.from_numpy(filler.box_rois(422, 2, 2)).to(DEV)
+        tgt = torch.from_numpy(filler.ellipse_targets(423, 4, 128, 96)).to(DEV)
+        runs = []
+        for graphed in (False, True):
+            torch.manual_seed(0)
+            m = _model(torch.bfloat16, p_drop_zero=False).to(DEV).train()
+            for mm in (m.roi_align_mask, m.roi_align_rgb):
+                mm.spatial_scale_h, mm.spatial_scale_w = 96, 128
+            sync = HD.enable_grad_sync(m, bucket_mb=1.0)
+            loss_fn = HD.sync_loss_class_weights(_loss())
+            st = {"opt": None}
+
+            def step():
+                logits, aux = m(images, rois)
+                loss, _ = loss_fn(logits, tgt, aux)
+                st["opt"] = st["opt"] or _opt(m)
+                st["opt"].zero_grad()
+                loss.backward()
+                st["opt"].step()
+                return loss
+            run = hiseg.GraphedStep(step, lambda: st["opt"]) if graphed else step
+            losses = [float(run().detach()) for _ in range(5)]
+            torch.cuda.synchronize()
+            if graphed:
+                assert run.captures == 1
+            assert len(sync.buckets) > 3 and any(k >= 0 for k in sync.launch_after)
+            params = torch.cat([p.detach().float().reshape(-1) for p in m.parameters()]).cpu()
+            runs.append((losses, params, st["opt"].exp_avg.cpu(), st["opt"].step_count))
+        (l0, p0, m0, s0), (l1, p1, m1, s1) = runs
+        assert l0 == l1, (l0, l1)
+        assert s0 == s1 == 5
+        assert torch.equal(p0, p1) and torch.equal(m0, m1)
+    finally:
+        dist.destroy_process_group()

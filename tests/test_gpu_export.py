@@ -96,3 +96,27 @@ def test_exported_roi_align_and_unet_wrapper_equal_eager():
     want, _ = m.pretrained_unet(images)
     torch.cuda.synchronize()
     assert torch.equal(got, want)
+
+
+def test_two_exported_programs_same_architecture_different_weights():
+    """export program A, run it, drop it; export program B (same architecture, other weights), run it --
+    B's outputs are B's eager outputs, not A's packed weights reused through the shared skeleton's plan cache."""
+    import gc
+    images, rois = _inputs(2, 2)
+    outs = []
+    for seed in (0, 1):
+        m = hiseg.create_rgb_hierarchical_model(**hiseg_kwargs(b0_kwargs()))
+        filler.fill_module(m, seed=100 + seed)
+        hiseg.set_compute_dtype(m, torch.bfloat16)
+        wrapper = hiseg.RGBHierarchicalExportWrapper(m.to(DEV).eval()).eval()
+        ep = torch.export.export(wrapper, (images, rois), dynamic_shapes=_dyn())
+        with torch.no_grad():
+            want = wrapper(images, rois)
+            got = ep.module()(images, rois)
+        torch.cuda.synchronize()
+        for g, w in zip(got, want):
+            assert torch.equal(g, w), seed
+        outs.append([t.clone() for t in got])
+        del ep, wrapper, m, got, want
+        gc.collect()
+    assert not torch.equal(outs[0][1], outs[1][1])

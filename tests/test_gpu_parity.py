@@ -383,6 +383,33 @@ def test_conv_pointwise_efficientnet_bit_identical(name):
         assert torch.equal(outs[v], outs[-1]), f"variant {v} differs from the generic kernel"
 
 
+@pytest.mark.parametrize("Ca,Cout,N", [(240, 40, 80), (288, 48, 60), (96, 24, 200)])
+def test_conv_gated_pointwise_batch_invariant_above_gate_bound(Ca, Cout, N):
+    """the pointwise kernel stages an SE-gated layer's gate [N][Ca] in 64 KiB of LDS, so its plan depended
+    on the batch (N * Ca * 4 > 64 KiB declined it).  conv2d_impl now runs such a layer in image ranges the gate fits
+    (conv_pw_gate_images): a batch above the bound gives every image the bits it gets alone or in a small batch."""
+    from hiseg import ops
+    dt = torch.bfloat16
+    H, W = 10, 12
+    assert N * Ca * 4 > 64 * 1024
+    g = torch.Generator(device=DEV).manual_seed(23)
+    x = torch.randn(N, Ca, H, W, device=DEV, generator=g)
+    w = torch.randn(Cout, Ca, 1, 1, device=DEV, generator=g) / Ca ** 0.5
+    bn = torch.nn.BatchNorm2d(Cout).to(DEV).eval()
+    filler.fill_module(bn)
+    p = ops.pack_conv(w, None, bn, 0, dt, DEV, pad=0)
+    gate = torch.rand(N, p.ca, device=DEV, generator=g)
+    r = torch.randn(N, Cout, H, W, device=DEV, generator=g)
+    y = ops.conv2d(p, ops.Act.from_nchw(x, dt), residual=ops.Act.from_nchw(r, dt), in_scale=gate).to_nchw()
+    for lo, hi in ((0, 1), (N - 3, N), (N // 2, N // 2 + 7)):
+        ys = ops.conv2d(p, ops.Act.from_nchw(x[lo:hi].contiguous(), dt), residual=ops.Act.from_nchw(r[lo:hi].contiguous(), dt),
+                        in_scale=gate[lo:hi].contiguous()).to_nchw()
+        torch.cuda.synchronize()
+        assert torch.equal(ys, y[lo:hi]), (lo, hi)
+    yg = ops.conv2d(p, ops.Act.from_nchw(x, dt), residual=ops.Act.from_nchw(r, dt), in_scale=gate, variant=-1).to_nchw()
+    assert torch.equal(yg, y)
+
+
 # Split-K generic kernel (round 3): small-grid, long-K 1x1 layers -- the deep SE-gated EfficientNet projections of
 # the B7 teacher / B0 student in distillation (N, Ca, Cout, H, W, act, in_scale, residual)
 SPLITK_CASES = {
@@ -421,8 +448,9 @@ def test_conv_splitk_within_reassociation(name):
     d.dtype = d.out_dtype = 1
     d.N, d.H, d.W, d.Ho, d.Wo, d.KH, d.KW, d.stride = N, H, W, H, W, 1, 1, 1
     d.Ca, d.Cout, d.Cout_pad, d.K_pad = p.ca, p.gemm_cols, p.cout_pad, p.k_pad
-    d.srcA = d.weight = d.scale = d.shift = d.out = 1
-    d.in_scale = 16 if ins else None
+    with L.raw_pointers():   # planning only, never launched
+        d.srcA = d.weight = d.scale = d.shift = d.out = 1
+        d.in_scale = 16 if ins else None
     assert L.lib().hiseg_conv2d_workspace_bytes(ctypes.byref(d)) > 0
     outs = {}
     for v in (-1, 99, 0, "again"):

@@ -954,8 +954,10 @@ def test_two_source_results_do_not_depend_on_operand_placement(case):
     x = torch.from_numpy(filler.normal(61, (N, ca, H // up, W // up))).to(DEV)
     s_ = torch.from_numpy(filler.normal(62, (N, cb, H, W))).to(DEV)
     g = torch.from_numpy(filler.normal(63, (N, cout, H, W))).to(DEV)
+    from hiseg import _lib as L
     res = []
     for far in (False, True):
+        L.placement_stats(reset=True)
         conv = nn.Conv2d(ca + cb, cout, k, padding=k // 2, bias=True)
         filler.fill_module(conv, seed=64)
         TE, S, T = engine(_Holder(c=conv), dt)
@@ -975,6 +977,11 @@ def test_two_source_results_do_not_depend_on_operand_placement(case):
             yy = ops.conv2d(p, xa, xb, a_up=2)
             torch.cuda.synchronize()
             res.append((yy.t.clone(),))
+            # the row-streaming kernel takes the layer wherever its sources lie (one buffer
+            # resource per source when far apart), never a placement fallback
+            declined, far_taken = L.placement_stats(reset=True)
+            assert declined == 0, "a kernel declined the decoder conv1 for its sources' placement"
+            assert far_taken == (1 if far else 0)
     for a, b in zip(*res):
         assert torch.equal(a, b)
 
