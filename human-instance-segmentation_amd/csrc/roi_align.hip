@@ -14,6 +14,12 @@
 #include "common.h"
 #include "hiseg_head_train.h"
 
+// hipcc contracts a*b+c into an FMA by default (-ffp-contract=fast-honor-pragmas), and __fmul_rn / __fadd_rn are
+// plain operators in this header set: without this pragma the sample coordinate x1 + g*(x2-x1) and the bilinear sum
+// were fused, one rounding fewer than torch's CPU ops, which moved the taps' weights by an ulp (1e-5 relative on
+// the ROI patches, amplified ~100x by train-mode BatchNorm).
+#pragma clang fp contract(off)
+
 namespace hiseg {
 
 __device__ __forceinline__ float fmul(float a, float b) { return __fmul_rn(a, b); }

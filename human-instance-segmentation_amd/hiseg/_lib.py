@@ -68,7 +68,8 @@ class Desc(ctypes.Structure):
 
     def __setattr__(self, name, value):
         if name in self._ptr_fields and value is not None and not isinstance(value, int):
-            t = getattr(value, "t", value)
+            # (torch.Tensor has a .t method: test for a tensor before looking for an activation view's .t)
+            t = value if isinstance(value, torch.Tensor) else getattr(value, "t", None)
             if not isinstance(t, torch.Tensor):
                 raise TypeError(f"{type(self).__name__}.{name}: expected a tensor / activation view, got {type(value)}")
             self.__dict__.setdefault("_held", {})[name] = value

@@ -115,3 +115,33 @@ def test_conv_splitk_workspace_plan_is_batch_invariant():
     assert ws(4, 20, 20, 384, 2304, gated=False) == 0   # ungated, short K: the LDS-DMA ring kernel
     assert ws(4, 20, 20, 288, 48) == 0           # the 10-k-step pointwise kernel takes it
     assert ws(4, 20, 20, 2304, 384, k=3) == 0    # 3x3: never split
+
+
+def test_descriptor_holds_plain_tensors_and_activation_views():
+    """A pointer field assigned a torch.Tensor stores its address and keeps it alive (torch.Tensor has a .t method,
+    which must not be mistaken for an activation view's .t); an object that is neither raises; strict mode refuses
+    raw addresses."""
+    import pytest
+    import torch
+    from hiseg import _lib as L
+
+    class View:
+        def __init__(self, t):
+            self.t = t
+
+    d = L.Conv2dDesc()
+    w = torch.zeros(8)
+    d.weight = w
+    assert d.weight == w.data_ptr() and d.held()["weight"] is w
+    v = View(torch.zeros(4))
+    d.out = v
+    assert d.out == v.t.data_ptr() and d.held()["out"] is v
+    c = d.copy()
+    assert c.held()["weight"] is w and c.weight == w.data_ptr()
+    d.weight = None
+    assert "weight" not in d.held()
+    with pytest.raises(TypeError):
+        d.scale = "not a tensor"
+    if L.STRICT_PTRS:
+        with pytest.raises(TypeError):
+            d.shift = 1 << 20

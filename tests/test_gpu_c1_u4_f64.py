@@ -77,8 +77,9 @@ def test_u4_train_mode_keeps_the_frozen_unet_in_eval():
     sd = O.np_state(model)
     model = model.to(DEV)
     model.train()
-    unet = model.pretrained_unet.model
-    assert model.training and model.pretrained_unet.training
+    # unet.py:1892-1899: PreTrainedPeopleSegmentationUNet itself follows train(); its smp net (.model) stays in eval
+    assert model.training and model.pretrained_unet.training and model.pretrained_unet.model.training
+    unet = model.pretrained_unet.model.model
     assert not unet.training and not any(m.training for m in unet.modules())
     bufs = {k: v.detach().clone() for k, v in unet.state_dict().items() if "running" in k or "num_batches" in k}
     assert bufs
@@ -120,7 +121,8 @@ def test_f32_train_step_against_float64_oracle():
         lg, aux = OT.forward_train(sd, images.to(dt), rois, u.to(dt), cfg, (96, 128))
         loss, _ = OT.RefinedHierarchicalLoss()(lg, tgt, aux)
         loss.backward()
-        ref[dt] = (lg.detach(), float(loss), {k: v.grad for k, v in sd.items() if v.requires_grad and v.grad is not None})
+        ref[dt] = (lg.detach(), float(loss), {k: v.grad for k, v in sd.items() if v.requires_grad and v.grad is not None},
+                   {k: v.detach() for k, v in aux.items() if torch.is_tensor(v)})
     mm = m.to(DEV).train()
     for x in (mm.roi_align_mask, mm.roi_align_rgb):
         x.spatial_scale_h, x.spatial_scale_w = 96, 128
@@ -131,8 +133,11 @@ def test_f32_train_step_against_float64_oracle():
     loss, _ = loss_fn(logits, tgt.to(DEV), aux)
     loss.backward()
     torch.cuda.synchronize()
-    l64, loss64, g64 = ref[torch.float64]
-    l32, loss32, g32 = ref[torch.float32]
+    l64, loss64, g64, a64 = ref[torch.float64]
+    l32, loss32, g32, a32 = ref[torch.float32]
+    # where along the forward the f32 error enters: every intermediate both sides expose, vs float64
+    stages = "\n".join(f"  {_rel(aux[k].detach().float().cpu(), a64[k]):.3e}  {_rel(a32[k], a64[k]):.3e}  aux[{k}]"
+                        for k in a64 if k in aux and torch.is_tensor(aux[k]) and tuple(aux[k].shape) == tuple(a64[k].shape))
     e_log_h, e_log_o = _rel(logits.detach().cpu(), l64), _rel(l32, l64)
     e_loss_h, e_loss_o = abs(loss.item() - loss64) / abs(loss64), abs(loss32 - loss64) / abs(loss64)
     scale = statistics.median(float(g.norm()) for g in g64.values())
@@ -150,7 +155,8 @@ def test_f32_train_step_against_float64_oracle():
     table = "\n".join(f"  {h:.3e}  {o:.3e}  {k}" for h, o, k in sorted(rows, reverse=True)[:30])
     summary = (f"vs float64 -- logits: hiseg f32 {e_log_h:.3e}, oracle f32 {e_log_o:.3e}; loss {e_loss_h:.3e} / "
                f"{e_loss_o:.3e}; gradients ({len(rows)} tensors) median {med_h:.3e} / {med_o:.3e}, p90 {p90_h:.3e} / "
-               f"{p90_o:.3e}\n  hiseg      oracle-f32  tensor (largest hiseg errors)\n{table}")
+               f"{p90_o:.3e}\n  hiseg      oracle-f32  forward stage\n{stages}\n"
+               f"  hiseg      oracle-f32  tensor (largest hiseg errors)\n{table}")
     print(summary)
     assert e_log_h < max(2 * e_log_o, 1e-6), summary
     assert e_loss_h < max(2 * e_loss_o, 1e-6), summary

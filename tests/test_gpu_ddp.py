@@ -118,7 +118,7 @@ def _c5_opt(model):
 
 
 # ------------------------------------------------------------------------------------------ rank processes
-def _rank_worker(rank, world, port, case, q):
+def _rank_worker(rank, world, port, case, q, outdir):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         torch.cuda.set_device(0)
@@ -162,29 +162,36 @@ def _rank_worker(rank, world, port, case, q):
                 opt.step()
                 torch.cuda.synchronize()
                 params.append(S.flat.data.cpu().clone())
-        q.put((rank, grads, params, len(sync.buckets), sorted(k for k in sync.launch_after if k >= 0)))
+        # results go through a file (hundreds of MB: not through the queue's shared-memory handles, which die
+        # with this process, nor a possibly small /dev/shm)
+        path = os.path.join(outdir, f"rank{rank}.pt")
+        torch.save({"grads": torch.stack(grads), "params": torch.stack(params)}, path)
+        q.put((rank, path, len(sync.buckets), sorted(k for k in sync.launch_after if k >= 0)))
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover - surfaced by the parent
         import traceback
-        q.put((rank, traceback.format_exc() + repr(e), None, None, None))
+        q.put((rank, "ERROR " + traceback.format_exc() + repr(e), None, None))
 
 
-def _run_ranks(case, world=2):
+def _run_ranks(case, outdir, world=2):
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_rank_worker, args=(r, world, port, case, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank_worker, args=(r, world, port, case, q, str(outdir))) for r in range(world)]
     for p in procs:
         p.start()
     try:
-        out = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+        got = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
     finally:
         for p in procs:
             p.join(timeout=60)
             if p.is_alive():
                 p.kill()
-    for r, g, *_ in out:
-        assert not isinstance(g, str), f"rank {r}: {g}"
+    out = []
+    for r, path, nb, sched in got:
+        assert not path.startswith("ERROR"), f"rank {r}: {path}"
+        res = torch.load(path, weights_only=True)
+        out.append((r, res["grads"], res["params"], nb, sched))
     return out
 
 
@@ -205,7 +212,8 @@ def _check(out, ref_grads, ref_params):
     (_, g0, p0, nb, sched), (_, g1, p1, _, _) = out
     assert nb > 1 and sched, "the exchange should run in several buckets, some launched during the backward"
     for step in range(STEPS):
-        assert torch.isfinite(ref_grads[step]).all()
+        fin = [bool(torch.isfinite(x[step]).all()) for x in (g0, g1)] + [bool(torch.isfinite(ref_grads[step]).all())]
+        assert all(fin), f"step {step}: finite gradients (rank 0, rank 1, single process) = {fin}"
         assert torch.equal(g0[step], g1[step]), f"step {step}: the ranks' averaged gradients differ"
         d = (g0[step] - ref_grads[step]).abs().max().item()
         assert torch.equal(g0[step], ref_grads[step]), f"step {step}: gradient differs from the half-batch mean by {d}"
@@ -214,11 +222,11 @@ def _check(out, ref_grads, ref_params):
     assert not torch.equal(p0[0], p0[-1])
 
 
-def test_ddp_world2_c4_b7_ultra_equals_half_batch_mean():
+def test_ddp_world2_c4_b7_ultra_equals_half_batch_mean(tmp_path):
     """C4 (B7-ultra ROI model, 1 ROI per image) at world size 2 over gloo on one GPU vs the single-process mean
     of the two half-batch gradients (class counts summed over the halves, sync_loss_class_weights)."""
     world = 2
-    out = _run_ranks("c4", world)
+    out = _run_ranks("c4", tmp_path, world)
     m = _c4_model()
     losses = [_loss(), _loss()]   # one loss per rank: each carries its own (identical) EMA state
     batch = _c4_batch(world)
@@ -239,6 +247,9 @@ def test_ddp_world2_c4_b7_ultra_equals_half_batch_mean():
             loss.backward()
             S = m.__dict__["_hiseg_train"]
             gs.append(S.flat.grad.clone())
+            assert torch.isfinite(logits).all() and torch.isfinite(loss), f"half {r}: non-finite logits / loss {loss}"
+            bad = [n for n, pp in m.named_parameters() if pp.grad is not None and not torch.isfinite(pp.grad).all()]
+            assert not bad, f"half {r} step {len(ref_grads)}: loss {float(loss)}, non-finite gradients of {bad[:8]}"
         mean = (gs[0] + gs[1]) * (1.0 / world)
         S.flat.grad.copy_(mean)
         ref_grads.append(mean.cpu())
@@ -248,11 +259,11 @@ def test_ddp_world2_c4_b7_ultra_equals_half_batch_mean():
     _check(out, ref_grads, ref_params)
 
 
-def test_ddp_world2_c5_distillation_equals_half_batch_mean():
+def test_ddp_world2_c5_distillation_equals_half_batch_mean(tmp_path):
     """C5 distillation (B7 teacher, B0 student decoder-only phase, decoder AdamW with clipping) at world size 2
     over gloo on one GPU vs the single-process mean of the two half-batch student gradients."""
     world = 2
-    out = _run_ranks("c5", world)
+    out = _run_ranks("c5", tmp_path, world)
     model, loss_fn = _c5_model()
     x, msk = _c5_batch(world)
     n = C5_IMG[0]
@@ -322,5 +333,11 @@ def test_graphed_ddp_step_rccl_world1_equals_eager():
         assert l0 == l1, (l0, l1)
         assert s0 == s1 == 5
         assert torch.equal(p0, p1) and torch.equal(m0, m1)
+    except BaseException:
+        import sys
+        import traceback
+        traceback.print_exc()   # before the process group is torn down (an abort there would hide it)
+        sys.stderr.flush()
+        raise
     finally:
         dist.destroy_process_group()
