@@ -328,7 +328,8 @@ static int launch_pw_k(const ConvArgs& a, hipStream_t s, int nks) {
     return act == R ? launch_pw<NKS, 0, R, false, 16, false>(a, s, nks) : launch_pw<NKS, 0, N, false, 16, false>(a, s, nks);
   } else {
     if (nks != NKS) {   // a k-step count below the register tile: plain epilogue (EfficientNet expansions)
-      if (d.convT || d.residual || d.mul) return 0;
+      HISEG_REQUIRE(!(d.convT || d.residual || d.mul), HISEG_ERR_BAD_ARG,
+                    "conv_pw: residual / mul / ConvTranspose forms need 2, 4 or 8 k-steps (pw_plan declines them)");
       return act == R ? launch_pw<-NKS, 0, R, false, 16, false>(a, s, nks)
            : act == S ? launch_pw<-NKS, 0, S, false, 16, false>(a, s, nks)
            : act == SI ? launch_pw<-NKS, 0, SI, false, 16, false>(a, s, nks)
@@ -399,6 +400,10 @@ static bool pw_plan(const ConvArgs& a, int& rb, int& nks, int& nks_max) {
   if (((d.o_cstride | d.o_coff) & 3) || (d.residual && ((d.r_cstride | d.r_coff) & 3))) return false;
   if (((uintptr_t)d.out | (uintptr_t)d.residual | (uintptr_t)d.mul) & 7) return false;
   nks_max = comb ? 9 : nks <= 2 ? 2 : nks <= 4 ? 4 : nks <= 8 ? 8 : 10;
+  // 256-column tiles at a k-step count below the register tile exist for the plain epilogue only (launch_pw_k):
+  // the residual / mul / ConvTranspose forms need exactly 2, 4 or 8 k-steps (ConvTranspose 144 -> 72 and 192 -> 96,
+  // the B1 / B7 EnhancedUNet up-convolutions, have 5 / 6 and take the LDS-DMA ring kernel)
+  if (rb == 16 && !comb && nks != nks_max && (d.convT || d.residual || d.mul)) return false;
   return true;
 }
 

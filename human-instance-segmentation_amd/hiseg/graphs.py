@@ -99,7 +99,9 @@ class GraphedStep:
             torch.cuda.synchronize()
             before = self._fingerprint()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            # thread-local capture: RCCL's watchdog thread polls the events of earlier collectives while the step
+            # is being captured, which the default (global) mode turns into a capture error in that thread
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 self.out = self.fn()
             self.fp = self._fingerprint()
             if self.fp != before:
