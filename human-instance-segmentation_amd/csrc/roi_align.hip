@@ -22,9 +22,11 @@
 
 namespace hiseg {
 
-__device__ __forceinline__ float fmul(float a, float b) { return __fmul_rn(a, b); }
-__device__ __forceinline__ float fadd(float a, float b) { return __fadd_rn(a, b); }
-__device__ __forceinline__ float fsub(float a, float b) { return __fsub_rn(a, b); }
+// plain operators under the pragma above: the header's __fmul_rn / __fadd_rn carry the contractable flag of the
+// header's own code, and after inlining the backend fused them (x2*sw - x1, x1 + g*len, (n+1)*s - 0.5)
+__device__ __forceinline__ float fmul(float a, float b) { return a * b; }
+__device__ __forceinline__ float fadd(float a, float b) { return a + b; }
+__device__ __forceinline__ float fsub(float a, float b) { return a - b; }
 
 __device__ __forceinline__ float linspace01(int idx, int steps) {
   if (steps == 1) return 0.f;

@@ -13,14 +13,17 @@ for p in (os.path.join(ROOT, "human-instance-segmentation_amd"), os.path.join(RO
           os.path.join(ROOT, "tests")):
     sys.path.insert(0, p)
 
+import torch  # noqa: E402
+
 from hiseg import _lib as L  # noqa: E402
+import test_gpu_churn  # noqa: E402
 import test_gpu_train  # noqa: E402
 
 
 def bare_address(self, name, value):
     """Desc.__setattr__ without the hold: the pre-round-4 behaviour (only the address is kept)."""
     if name in self._ptr_fields and value is not None and not isinstance(value, int):
-        value = getattr(value, "t", value).data_ptr()
+        value = (value if isinstance(value, torch.Tensor) else value.t).data_ptr()
     ctypes.Structure.__setattr__(self, name, value)
 
 
@@ -34,13 +37,17 @@ def run(label, fn):
         return False
 
 
-ok_with = run("with the holds (product)", test_gpu_train.test_train_step_independent_of_allocator_churn_between_forward_and_backward)
+TESTS = [("B0 step", test_gpu_train.test_train_step_independent_of_allocator_churn_between_forward_and_backward),
+         ("C3 step", test_gpu_churn.test_c3_train_step_independent_of_allocator_churn),
+         ("C5 distillation step", test_gpu_churn.test_c5_distillation_step_independent_of_allocator_churn)]
+ok_with = {name: run(f"{name}, with the holds (product)", fn) for name, fn in TESTS}
 L.STRICT_PTRS = False
 L.Desc.__setattr__ = bare_address
-ok_without = run("control, holds undone", test_gpu_train.test_train_step_independent_of_allocator_churn_between_forward_and_backward)
-if ok_with and not ok_without:
-    print("control: the churn test catches the released-mask bug and passes with the fix")
-elif ok_with:
-    print("control: the churn test did NOT catch the bug (passes without the holds)")
-else:
-    print("control: the churn test fails with the holds in place")
+ok_without = {name: run(f"{name}, control: holds undone", fn) for name, fn in TESTS}
+for name, _ in TESTS:
+    if ok_with[name] and not ok_without[name]:
+        print(f"control {name}: the churn test catches a released buffer without the holds and passes with them")
+    elif ok_with[name]:
+        print(f"control {name}: the churn test passes without the holds too (nothing it exercises depends on them)")
+    else:
+        print(f"control {name}: the churn test FAILS with the holds in place")

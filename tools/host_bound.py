@@ -48,8 +48,9 @@ def train(preset, steps, graphed=False, ddp=False):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29541")
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
-        HD.enable_grad_sync(model)
-        HD.sync_loss_class_weights(loss_fn)
+        HD.enable_grad_sync(model, bucket_mb=float(os.environ.get("HB_BUCKET_MB", "25")))
+        if os.environ.get("HB_NO_COUNT_SYNC") != "1":
+            HD.sync_loss_class_weights(loss_fn)
 
     def step():
         logits, aux = model(images, rois)
@@ -70,8 +71,25 @@ def train(preset, steps, graphed=False, ddp=False):
         t1 = time.perf_counter()
         torch.cuda.synchronize()
         t2 = time.perf_counter()
-        print(f"train {preset}{' graphed' if graphed else ''}{' ddp(rccl world 1)' if ddp else ''}: enqueue {1e3 * (t1 - t0) / steps:.2f} ms/step, wall {1e3 * (t2 - t0) / steps:.2f} ms/step",
+        caps = f", captures {run.captures} after {run.calls} calls" if graphed else ""
+        print(f"train {preset}{' graphed' if graphed else ''}{' ddp(rccl world 1)' if ddp else ''}: enqueue {1e3 * (t1 - t0) / steps:.2f} ms/step, wall {1e3 * (t2 - t0) / steps:.2f} ms/step{caps}",
               flush=True)
+    if graphed and run.graph is not None:   # the replay call alone
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            run.graph.replay()
+        t1 = time.perf_counter()
+        torch.cuda.synchronize()
+        print(f"   graph.replay() alone: {1e3 * (t1 - t0) / steps:.2f} ms/call enqueue", flush=True)
+        ts = []
+        for _ in range(5):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            run.graph.replay()
+            ts.append(time.perf_counter() - t0)
+        torch.cuda.synchronize()
+        print(f"   graph.replay() on an idle GPU: {1e3 * sorted(ts)[2]:.2f} ms", flush=True)
 
 
 def main():
