@@ -376,17 +376,64 @@ def _onnx_custom(name):
     return fn
 
 
-def register_onnx_symbolics(opset: int = 17) -> None:
-    """Register the TorchScript-exporter lowering of every hiseg op (opset >= 16 for GridSample)."""
+def _spec_of(spec):
+    from torch.onnx import symbolic_helper as sh
+    return json.loads(spec if isinstance(spec, str) else sh._maybe_get_const(spec, "s"))
+
+
+def _named_state(sp: dict, state_values: Sequence, skip: str) -> Dict[str, object]:
+    """state_dict name -> graph value of an op's state inputs (the skeleton of the spec gives the names)."""
+    m, _ = _skeleton(sp)
+    names = [k for k in m.state_dict().keys() if not (skip and k.startswith(skip))]
+    if len(names) != len(state_values):
+        raise ValueError(f"ONNX lowering: {len(state_values)} state inputs for a {sp['cls']} with {len(names)}")
+    return dict(zip(names, state_values))
+
+
+def onnx_unet_logit(g, images, state_values: Sequence, spec: dict):
+    """hiseg::unet_logit in standard operators (onnx_graph.emit_unet_logit)."""
+    from . import onnx_graph
+    m, _ = _skeleton(spec)
+    return onnx_graph.emit_unet_logit(g, m, _named_state(spec, state_values, ""), images)
+
+
+def onnx_rgb_head(g, images, u, rois, state_values: Sequence, spec: dict) -> list:
+    """hiseg::rgb_head in standard operators: the outputs named in the spec, in order (onnx_graph.emit_rgb_head)."""
+    from . import onnx_graph
+    m, _ = _skeleton(spec)
+    return onnx_graph.emit_rgb_head(g, m, _named_state(spec, state_values, UNET_PREFIX), images, u, rois,
+                                    spec["scale_hw"], [n for n, _ in spec["outs"]])
+
+
+def _sym_unet_logit(g, images, state, spec):
+    from torch.onnx import symbolic_helper as sh
+    return onnx_unet_logit(g, images, sh._unpack_list(state), _spec_of(spec))
+
+
+def _sym_rgb_head(g, images, u, rois, state, spec):
+    from torch.onnx import symbolic_helper as sh
+    outs = onnx_rgb_head(g, images, u, rois, sh._unpack_list(state), _spec_of(spec))
+    return g.op("prim::ListConstruct", *outs)
+
+
+def register_onnx_symbolics(opset: int = 17, custom_domain: bool = False) -> None:
+    """Register the TorchScript-exporter lowering of every hiseg op (opset >= 16 for GridSample).  The composite
+    UNet and head ops lower to standard operators (onnx_graph.py); ``custom_domain=True`` keeps them as single nodes
+    of the ``hiseg`` domain instead (a runtime with a libhiseg custom-op library)."""
     from torch.onnx import symbolic_helper as sh
     reg = torch.onnx.register_custom_op_symbolic
     reg("hiseg::dynamic_roi_align", sh.parse_args("v", "v", "i", "i", "f", "f", "b")(_onnx_roi_align), opset)
     reg("hiseg::output_conv", sh.parse_args("v", "v", "v")(_onnx_output_conv), opset)
     reg("hiseg::binary_masks", sh.parse_args("v", "v", "v")(_onnx_binary_masks), opset)
     reg("hiseg::instance_masks", sh.parse_args("v", "i")(_onnx_instance_masks), opset)
-    reg("hiseg::unet_logit", _onnx_custom("PretrainedPeopleSegmentationUNet"), opset)
-    reg("hiseg::rgb_head", _onnx_custom("RGBHierarchicalHead"), opset)
+    if custom_domain:
+        reg("hiseg::unet_logit", _onnx_custom("PretrainedPeopleSegmentationUNet"), opset)
+        reg("hiseg::rgb_head", _onnx_custom("RGBHierarchicalHead"), opset)
+    else:
+        reg("hiseg::unet_logit", _sym_unet_logit, opset)
+        reg("hiseg::rgb_head", _sym_rgb_head, opset)
 
 
 ONNX_LOWERINGS = {"dynamic_roi_align": _onnx_roi_align, "output_conv": _onnx_output_conv,
-                  "binary_masks": _onnx_binary_masks, "instance_masks": _onnx_instance_masks}
+                  "binary_masks": _onnx_binary_masks, "instance_masks": _onnx_instance_masks,
+                  "unet_logit": onnx_unet_logit, "rgb_head": onnx_rgb_head}

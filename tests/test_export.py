@@ -196,15 +196,55 @@ class EagerOnnx:
         return F.grid_sample(x, grid, mode=mode_s, padding_mode=padding_mode_s, align_corners=bool(align_corners_i))
 
     @staticmethod
-    def _Conv(x, w, b, kernel_shape_i):
-        return F.conv2d(x, w, b)
+    def _Conv(x, w, b=None, kernel_shape_i=None, strides_i=(1, 1), pads_i=(0, 0, 0, 0), group_i=1, dilations_i=(1, 1)):
+        assert pads_i[0] == pads_i[2] and pads_i[1] == pads_i[3]
+        return F.conv2d(x, w, b, stride=tuple(strides_i), padding=(pads_i[0], pads_i[1]), groups=group_i,
+                        dilation=tuple(dilations_i))
+
+    @staticmethod
+    def _ConvTranspose(x, w, b, kernel_shape_i, strides_i, pads_i):
+        return F.conv_transpose2d(x, w, b, stride=tuple(strides_i))
+
+    @staticmethod
+    def _BatchNormalization(x, scale, bias, mean, var, epsilon_f):
+        return F.batch_norm(x, mean, var, scale, bias, False, 0.0, epsilon_f)
+
+    _Relu = staticmethod(torch.relu)
+    _Sigmoid = staticmethod(torch.sigmoid)
+    _Erf = staticmethod(torch.erf)
+    _Sqrt = staticmethod(torch.sqrt)
+
+    @staticmethod
+    def _GlobalAveragePool(x):
+        return x.mean(dim=(2, 3), keepdim=True)
+
+    @staticmethod
+    def _ReduceMean(x, axes_i, keepdims_i):
+        return x.mean(dim=tuple(axes_i), keepdim=bool(keepdims_i))
+
+    @staticmethod
+    def _ReduceMax(x, axes_i=None, keepdims_i=1):
+        if axes_i is None:
+            return x.amax() if not keepdims_i else x.amax(dim=tuple(range(x.dim())), keepdim=True)
+        return x.amax(dim=tuple(axes_i), keepdim=bool(keepdims_i))
+
+    @staticmethod
+    def _Resize(x, roi, scales, sizes=None, mode_s="nearest", coordinate_transformation_mode_s="half_pixel",
+                nearest_mode_s="round_prefer_floor"):
+        if mode_s == "nearest":
+            assert coordinate_transformation_mode_s == "asymmetric" and nearest_mode_s == "floor"
+            return F.interpolate(x, scale_factor=tuple(float(v) for v in scales[2:]), mode="nearest")
+        assert mode_s == "linear" and coordinate_transformation_mode_s == "pytorch_half_pixel"
+        return F.interpolate(x, size=tuple(int(v) for v in sizes[2:]), mode="bilinear", align_corners=False)
 
     @staticmethod
     def _Softmax(x, axis_i):
         return torch.softmax(x, dim=axis_i)
 
     @staticmethod
-    def _Slice(x, starts, ends, axes, steps=None):
+    def _Slice(x, starts, ends, axes=None, steps=None):
+        if axes is None:
+            axes = torch.arange(len(starts))
         idx = [slice(None)] * x.dim()
         for s, e, a in zip(starts.tolist(), ends.tolist(), axes.tolist()):
             idx[a] = slice(s, e)
@@ -251,3 +291,97 @@ def test_onnx_instance_masks_lowering_matches_oracle(dilation):
 
 def test_onnx_symbolics_register():
     X.register_onnx_symbolics(17)
+
+
+# ------------------------------------------------------------------------------------ standard-op UNet / head
+def _filled_model(overrides=None, name="b0"):
+    import hiseg
+    from helpers import configs, hiseg_kwargs
+    kw = hiseg_kwargs(dict(configs()[name]["model_kwargs"]))
+    kw.update(overrides or {})
+    return filler.fill_module(hiseg.create_rgb_hierarchical_model(**kw)).eval(), kw
+
+
+def _rel(a, b):
+    return ((a.double() - b.double()).abs().max() / b.double().abs().max().clamp_min(1e-12)).item()
+
+
+@pytest.mark.parametrize("name", ["b0", "b1"])
+def test_onnx_unet_logit_lowering_matches_oracle(name):
+    """hiseg::unet_logit in standard ONNX operators (onnx_graph.emit_unet_logit: /255 guard, normalisation,
+    EfficientNet encoder with SE, nearest x2 decoder, head) against the oracle's smp-UNet restatement, both the
+    [0, 1] and the 8-bit input branch of normalize_input (unet.py:1885-1890)."""
+    import json
+    from oracle import rgb_model as O
+    model, _ = _filled_model(name=name)
+    pre = model.pretrained_unet.model
+    sd = O.np_state(model)
+    images = torch.from_numpy(filler.uniform(61, (2, 3, 64, 96)))
+    for x in (images, images * 255.0):
+        got = X.onnx_unet_logit(EagerOnnx(), x, X._state(pre), json.loads(X._spec(pre)))
+        with torch.no_grad():
+            want = O.pretrained_unet_logits(sd, x, name)
+        assert got.shape == want.shape == (2, 1, 64, 96)
+        assert _rel(got, want) < 1e-4
+
+
+@pytest.mark.parametrize("case", ["b0", "b0_layernorm_gelu_noattn", "b1"])
+def test_onnx_rgb_head_lowering_matches_oracle(case):
+    """hiseg::rgb_head in standard ONNX operators (onnx_graph.emit_rgb_head: output conv, GridSample RoIAligns, RGB
+    stack, combiner, refined head with every aux output) against the oracle, f32, 1e-4."""
+    import json
+    from oracle import rgb_model as O
+    if case == "b0_layernorm_gelu_noattn":
+        model, kw = _filled_model({"normalization_type": "layernorm2d", "activation_function": "gelu",
+                                   "use_attention_module": False})
+    else:
+        model, kw = _filled_model(name=case)
+    variant = "b1" if case == "b1" else "b0"
+    sd = O.np_state(model)
+    H, W = 64, 96
+    for m in (model.roi_align_mask, model.roi_align_rgb):
+        m.spatial_scale_h, m.spatial_scale_w = H, W
+    images = torch.from_numpy(filler.uniform(62, (2, 3, H, W)))
+    rois = torch.from_numpy(filler.box_rois(63, 2, 2))
+    with torch.no_grad():
+        u = O.pretrained_unet_logits(sd, images, variant)
+        want, want_aux = O.rgb_model_from_unet(sd, images, rois, u, O.cfg_from_kwargs(kw), (H, W))
+    spec = json.loads(X._head_spec(model, "full"))
+    outs = X.onnx_rgb_head(EagerOnnx(), images, u, rois, X._state(model, X.UNET_PREFIX), spec)
+    got = dict(zip([n for n, _ in spec["outs"]], outs))
+    assert _rel(got["logits"], want) < 1e-4
+    for k, v in want_aux.items():
+        assert got[k].shape == v.shape, k
+        assert _rel(got[k], v) < 1e-4, k
+
+
+def test_onnx_symbolics_register_custom_domain_option():
+    X.register_onnx_symbolics(17, custom_domain=True)
+    X.register_onnx_symbolics(17)
+
+
+def test_onnx_exported_contract_composition_matches_oracle():
+    """The whole exported contract as the ONNX graph composes it (traced_export: unet_logit -> rgb_head(aux none) ->
+    instance_masks with dilation 1, binary_masks), every node standard: instance masks equal the oracle's, binary
+    masks at 1e-5 (export_onnx_advanced.py:353-420)."""
+    import json
+    from oracle import rgb_model as O
+    model, kw = _filled_model()
+    sd = O.np_state(model)
+    H, W = 64, 96
+    for m in (model.roi_align_mask, model.roi_align_rgb):
+        m.spatial_scale_h, m.spatial_scale_w = H, W
+    images = torch.from_numpy(filler.uniform(64, (2, 3, H, W)))
+    rois = torch.from_numpy(filler.box_rois(65, 2, 3))
+    g = EagerOnnx()
+    pre, oc = model.pretrained_unet.model, model.pretrained_unet.output_conv
+    u = X.onnx_unet_logit(g, images, X._state(pre), json.loads(X._spec(pre)))
+    spec = json.loads(X._head_spec(model, "none"))
+    logits = X.onnx_rgb_head(g, images, u, rois, X._state(model, X.UNET_PREFIX), spec)[0]
+    inst = X._onnx_instance_masks(g, logits, 1)
+    binary = X._onnx_binary_masks(g, u, oc.weight.detach(), oc.bias.detach())
+    with torch.no_grad():
+        ref, _, ref_u = O.rgb_model(sd, images, rois, O.cfg_from_kwargs(kw), (H, W), "b0")
+    ref_inst = O.instance_masks(ref, 1)
+    assert (inst != ref_inst).float().mean().item() < 1e-3   # argmax ties at 1e-6 logit differences only
+    assert (binary - O.binary_masks(sd, ref_u)).abs().max().item() < 1e-5
