@@ -344,6 +344,7 @@ int conv_wide_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_hw_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_pw_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_hwr_try(const ConvArgs& a, hipStream_t s, int variant);
+int conv_hwt_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_small_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_rows_try(const ConvArgs& a, hipStream_t s, int variant);
 bool conv_pw_applies(const ConvArgs& a);
@@ -366,7 +367,7 @@ extern "C" int hiseg_conv2d_fwd(const hiseg_conv2d_desc* d, hiseg_stream_t strea
 static bool release_variant(int v) {
   return v == -1 || v == 0 || (v >= 1 && v <= 8) || v == 50 || v == 51 || v == 52 || v == 54 || v == 58 ||
          (v >= 60 && v <= 69) || v == 70 || v == 71 || v == 72 || v == 74 || v == 80 || v == 82 || v == 84 || v == 86 ||
-         v == 88 || v == 89 || v == 90 || (v >= 92 && v <= 101);
+         v == 88 || v == 89 || v == 90 || (v >= 92 && v <= 101) || v == 103;
 }
 
 // Workspace bytes the automatic choice uses for this layer (split-K generic kernel), 0 when it needs none.
@@ -504,6 +505,9 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
     if (r != 0) return r < 0 ? r : HISEG_OK;
   } else if ((variant >= 92 && variant <= 97) || variant == 100 || variant == 101) {
     const int r = conv_hwr_try(a, s, variant);
+    if (r != 0) return r < 0 ? r : HISEG_OK;
+  } else if (variant == 103) {
+    const int r = conv_hwt_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
   } else if (variant >= 80 && variant < 90) {
     const int r = conv_hw_try(a, s, variant);

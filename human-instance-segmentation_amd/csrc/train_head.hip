@@ -837,6 +837,11 @@ using namespace hiseg;
 
 static int chunk_of(int dtype) { return dtype == HISEG_BF16 ? 8 : 4; }
 
+// train_norm.hip: the BatchNorm statistics merge over an explicit split count
+int bn_finalize_splits(const float* partial, int S, int C, long long P, const float* gamma, const float* beta,
+                       float eps, float momentum, float* running_mean, float* running_var, float* mean, float* invstd,
+                       float* scale, float* shift, hipStream_t stream);
+
 extern "C" int hiseg_attn_spatial_train_fwd(int dtype, const void* x, int N, int H, int W, int C, const float* w7, int k,
                                             const float* chan_mul, float* stats, int* argmax, float* att, void* out,
                                             hiseg_stream_t stream) {
@@ -1006,9 +1011,9 @@ extern "C" int hiseg_ubf_train_fwd(const hiseg_ubf_desc* d, float eps, float mom
   } else {
     const int S = hiseg_bn_partials();
     hipLaunchKernelGGL(ubf_stats_kernel, dim3(S), dim3(256), 0, s, u, ws);
-    int r = hiseg_bn_finalize(ws, 32, Pm, d->gamma, d->beta, eps, momentum, running_mean, running_var,
-                              const_cast<float*>(d->mean), const_cast<float*>(d->invstd), const_cast<float*>(d->scale),
-                              const_cast<float*>(d->shift), stream);
+    int r = bn_finalize_splits(ws, S, 32, Pm, d->gamma, d->beta, eps, momentum, running_mean, running_var,
+                               const_cast<float*>(d->mean), const_cast<float*>(d->invstd), const_cast<float*>(d->scale),
+                               const_cast<float*>(d->shift), s);
     if (r) return r;
   }
   DISPATCH_T(d->dtype, hipLaunchKernelGGL(ubf_fwd_kernel<T>, dim3(nb(Pm, 256)), dim3(256), 0, s, u, d->tfeat, d->Ct,

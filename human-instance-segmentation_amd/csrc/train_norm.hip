@@ -1025,11 +1025,21 @@ static dim3 vec_grid(long long P, int C, int dtype) {
 
 static int splits_for(long long P) { return (int)(P < kBnSplits ? (P > 0 ? P : 1) : kBnSplits); }
 
+// Pixel splits of the statistics / backward-reduce passes: >= 32 pixels per split, at most kBnSplits (4 blocks per
+// CU).  The deep low-resolution layers (the distillation student's 4 x 20 x 20 = 1 600-pixel stages) used to take
+// 1 024 one- or two-pixel splits whose merge was most of their BN time.  A function of P alone, so hiseg_bn_stats and
+// hiseg_bn_finalize agree.
+static int stat_splits(long long P) {
+  const long long s = P / 32;
+  return (int)(s < 1 ? 1 : s > kBnSplits ? kBnSplits : s);
+}
+static dim3 fin_grid(int C) { return dim3((unsigned)C); }   // one block per channel
+
 extern "C" int hiseg_bn_stats(int dtype, const void* z, long long P, int C, int cstride, int coff, float* partial,
                               hiseg_stream_t stream) {
   HISEG_REQUIRE(z && partial && P > 0 && C > 0 && cstride >= C, HISEG_ERR_BAD_ARG, "bn_stats: bad arguments");
   HISEG_REQUIRE(dtype == HISEG_F32 || dtype == HISEG_BF16, HISEG_ERR_BAD_DTYPE, "bn_stats: dtype");
-  const int S = kBnSplits;  // fixed count: empty splits write n = 0
+  const int S = stat_splits(P);   // empty splits write n = 0
   if (vec_ok(dtype, C, z, cstride, coff)) {
     const int V = dtype == HISEG_BF16 ? 8 : 4;
     dim3 grid(S, (C / V + 255) / 256);
@@ -1047,8 +1057,17 @@ extern "C" int hiseg_bn_finalize(const float* partial, int C, long long P, const
                                  float eps, float momentum, float* running_mean, float* running_var, float* mean,
                                  float* invstd, float* scale, float* shift, hiseg_stream_t stream) {
   HISEG_REQUIRE(partial && mean && invstd && scale && shift && C > 0, HISEG_ERR_BAD_ARG, "bn_finalize: null");
-  hipLaunchKernelGGL(bn_finalize_par_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, partial, kBnSplits, C,
+  hipLaunchKernelGGL(bn_finalize_par_kernel, fin_grid(C), dim3(256), 0, (hipStream_t)stream, partial, stat_splits(P), C,
                      P, gamma, beta, eps, momentum, running_mean, running_var, mean, invstd, scale, shift);
+  return hiseg_check_launch("bn_finalize");
+}
+
+// The same merge over an explicit split count (the fused upsample_bg_fg statistics, train_head.hip: 1 024 splits).
+int bn_finalize_splits(const float* partial, int S, int C, long long P, const float* gamma, const float* beta,
+                       float eps, float momentum, float* running_mean, float* running_var, float* mean, float* invstd,
+                       float* scale, float* shift, hipStream_t stream) {
+  hipLaunchKernelGGL(bn_finalize_par_kernel, fin_grid(C), dim3(256), 0, stream, partial, S, C, P, gamma, beta, eps,
+                     momentum, running_mean, running_var, mean, invstd, scale, shift);
   return hiseg_check_launch("bn_finalize");
 }
 
@@ -1080,7 +1099,7 @@ extern "C" int hiseg_bn_bwd(const hiseg_bn_bwd_desc* d, hiseg_stream_t stream) {
                 "bn_bwd: a smooth activation after a residual add needs the residual (pre-activation)");
   HISEG_REQUIRE(d->P < (1ll << 31), HISEG_ERR_BAD_SHAPE, "bn_bwd: too many pixels");
   hipStream_t s = (hipStream_t)stream;
-  const int S = kBnSplits;
+  const int S = stat_splits(d->P);
   const int dt = d->dtype, C = d->C;
   if (vec_ok(dt, C, d->dy, d->dy_cstride, d->dy_coff) && vec_ok(dt, C, d->y, d->y_cstride, d->y_coff) &&
       vec_ok(dt, C, d->z, d->z_cstride, d->z_coff) && vec_ok(dt, C, d->dz, d->dz_cstride, d->dz_coff) &&
@@ -1091,7 +1110,7 @@ extern "C" int hiseg_bn_bwd(const hiseg_bn_bwd_desc* d, hiseg_stream_t stream) {
 #define BN_BWD_VEC(M)                                                                                         \
   do {                                                                                                        \
     DISPATCH_T(dt, hipLaunchKernelGGL((bn_bwd_reduce_vec_kernel<T, M>), rgrid, dim3(256), 0, s, *d));         \
-    hipLaunchKernelGGL(bn_bwd_finalize_par_kernel, dim3(C), dim3(256), 0, s, *d, S);                          \
+    hipLaunchKernelGGL(bn_bwd_finalize_par_kernel, fin_grid(C), dim3(256), 0, s, *d, S);                          \
     DISPATCH_T(dt, hipLaunchKernelGGL((bn_bwd_apply_vec_kernel<T, M>), agrid, dim3(256), 0, s, *d, S));       \
   } while (0)
     switch (mode) {
@@ -1104,7 +1123,7 @@ extern "C" int hiseg_bn_bwd(const hiseg_bn_bwd_desc* d, hiseg_stream_t stream) {
     return hiseg_check_launch("bn_bwd");
   }
   DISPATCH_T(d->dtype, hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(S, (d->C + 255) / 256), dim3(256), 0, s, *d));
-  hipLaunchKernelGGL(bn_bwd_finalize_par_kernel, dim3(C), dim3(256), 0, s, *d, S);
+  hipLaunchKernelGGL(bn_bwd_finalize_par_kernel, fin_grid(C), dim3(256), 0, s, *d, S);
   DISPATCH_T(d->dtype, hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(ew_blocks(d->P * d->C)), dim3(256), 0, s, *d, S));
   return hiseg_check_launch("bn_bwd");
 }

@@ -1087,3 +1087,33 @@ def test_conv_automatic_choice_within_bf16(name):
         assert ((y - ref).abs().max() / ref.abs().max()).item() < 8e-3
     else:
         assert torch.equal(y, ref)
+
+
+@pytest.mark.parametrize("shape", [(2, 256, 0, 256, 64, 48, True, True), (3, 128, 0, 128, 37, 21, True, False),
+                                   (2, 128, 0, 256, 33, 17, False, True), (2, 128, 128, 128, 32, 24, False, True),
+                                   (2, 64, 64, 384, 20, 30, True, True), (1, 256, 0, 128, 16, 16, False, False)])
+def test_conv_hwt_bit_identical_to_hwr(shape):
+    """Variant 103 (conv_hwt.hip: one wave per SIMD, 64 x 256 wave tiles, A fragments two K steps ahead, 32 x 16-pixel
+    x 128-Cout workgroup tiles): conv_hwr's per-element accumulation order (channel-major slices, kx-major taps, the
+    same MFMA) -- equal to variant 97 bit for bit: ragged pixel tiles, residual / ReLU / none, two sources, Cout
+    128 / 256 / 384."""
+    from hiseg import ops
+    N, Ca, Cb, Cout, H, W, res, relu = shape
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(31)
+    xa = ops.Act.from_nchw(torch.randn(N, Ca, H, W, device=DEV, generator=g), dt)
+    xb = ops.Act.from_nchw(torch.randn(N, Cb, H, W, device=DEV, generator=g), dt) if Cb else None
+    w = torch.randn(Cout, Ca + Cb, 3, 3, device=DEV, generator=g) / ((Ca + Cb) * 9) ** 0.5
+    p = ops.pack_conv(w, torch.randn(Cout, device=DEV, generator=g) * 0.1, None, int(relu), dt, DEV, pad=1,
+                      split=(Ca, Cb) if Cb else None)
+    assert p.weight_frag is not None
+    R = ops.Act.from_nchw(torch.randn(N, Cout, H, W, device=DEV, generator=g), dt) if res else None
+    outs = {}
+    for v in (97, 103, 0):
+        o = ops.Act.new(N, H, W, Cout, dt, torch.device(DEV))
+        o.t.fill_(float("nan"))
+        outs[v] = ops.conv2d(p, xa, xb, out=o, residual=R, variant=v).t.clone()
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[97].float()).all()
+    assert torch.equal(outs[103], outs[97])
+    assert torch.equal(outs[0], outs[97])
