@@ -183,8 +183,19 @@ __global__ void __launch_bounds__(256) se_hidden_kernel(const float* sums, int H
   if (r >= Cr) return;
   const float inv = 1.f / (float)HW;
   const float* m = sums + (long long)n * C;
-  float s = 0.f;
-  for (int c = lane; c < C; c += 64) s += w1[(long long)r * C + c] * (m[c] * inv);
+  const float* wr = w1 + (long long)r * C;
+  // four independent partial sums (eight loads in flight per lane: the B7's 2304..3840-channel rows are a 36..60-step
+  // dependent chain otherwise), combined in a fixed order
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int c = lane;
+  for (; c + 192 < C; c += 256) {
+    s0 += wr[c] * (m[c] * inv);
+    s1 += wr[c + 64] * (m[c + 64] * inv);
+    s2 += wr[c + 128] * (m[c + 128] * inv);
+    s3 += wr[c + 192] * (m[c + 192] * inv);
+  }
+  for (; c < C; c += 64) s0 += wr[c] * (m[c] * inv);
+  float s = (s0 + s1) + (s2 + s3);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
   if (lane == 0) hid[(long long)n * Cr + r] = apply_act(s + (b1 ? b1[r] : 0.f), act, beta);

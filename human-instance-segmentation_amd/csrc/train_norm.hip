@@ -192,9 +192,9 @@ __global__ void __launch_bounds__(256) bn_stats_vec_kernel(const void* z, long l
 #pragma unroll
   for (int k = 0; k < V; ++k) mean[k] = m2[k] = 0.f;
   if (live) {
-    for (long long p = b + r; p < e; p += R) {
-      float x[V];
-      ldv<T>(z, p * cs + coff + ch * V, x);
+    // four pixels' loads in flight before their Welford updates (the updates are a dependent chain; the loads are
+    // not): the small deep layers give each thread tens of pixels at L2 / HBM latency.  Same update order as one by one.
+    auto upd = [&](const float* x) __attribute__((always_inline)) {
       n += 1.f;
       const float rn = 1.f / n;
 #pragma unroll
@@ -203,6 +203,20 @@ __global__ void __launch_bounds__(256) bn_stats_vec_kernel(const void* z, long l
         mean[k] += d * rn;
         m2[k] += d * (x[k] - mean[k]);
       }
+    };
+    long long p = b + r;
+    for (; p + 3 * R < e; p += 4 * R) {
+      float x0[V], x1[V], x2[V], x3[V];
+      ldv<T>(z, p * cs + coff + ch * V, x0);
+      ldv<T>(z, (p + R) * cs + coff + ch * V, x1);
+      ldv<T>(z, (p + 2 * R) * cs + coff + ch * V, x2);
+      ldv<T>(z, (p + 3 * R) * cs + coff + ch * V, x3);
+      upd(x0); upd(x1); upd(x2); upd(x3);
+    }
+    for (; p < e; p += R) {
+      float x[V];
+      ldv<T>(z, p * cs + coff + ch * V, x);
+      upd(x);
     }
   }
   float* my = sh + t * (2 * V + 1);

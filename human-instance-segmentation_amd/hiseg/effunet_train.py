@@ -260,6 +260,7 @@ class _StudentFunction(torch.autograd.Function):
         xa = Act.from_nchw(x, S.dtype)
         feats = encoder_features(E, T, net.encoder, xa)
         u = decoder_head(T, net, feats, first_trainable_stage(net.encoder))
+        S.flush_counters()
         ctx.tape, ctx.state, ctx.u = T, S, u
         return u.t.view(u.N, 1, u.H, u.W)
 

@@ -172,6 +172,14 @@ class TrainState:
         self.cached: Dict = {}
         self.sync = None          # hiseg.distributed.GradBucketSync (data-parallel gradient exchange)
         self.op_index: Optional[int] = None
+        self.nbt: List[torch.Tensor] = []   # BatchNorm num_batches_tracked counters to advance after this forward
+
+    def flush_counters(self):
+        """Advance every train-mode BatchNorm's num_batches_tracked of this forward by one -- one multi-tensor
+        launch instead of one torch add per layer (~50 per step)."""
+        if self.nbt:
+            torch._foreach_add_(self.nbt, 1)
+            self.nbt = []
 
     # -- plans
     def conv(self, conv: nn.Module, split=None, convT: bool = False) -> TConv:
@@ -548,7 +556,7 @@ def bn_forward(T: Tape, bn: nn.BatchNorm2d, z: Act, *, act: int, residual: Optio
     track = bn.track_running_stats and bn.running_mean is not None
     mom = bn.momentum if bn.momentum is not None else 0.1
     if track and bn.num_batches_tracked is not None:
-        bn.num_batches_tracked.add_(1)
+        T.S.nbt.append(bn.num_batches_tracked)
     _chk(lib.hiseg_bn_finalize(part.data_ptr(), C, P, _ptr(bn.weight), _ptr(bn.bias), float(bn.eps), float(mom),
                                _ptr(bn.running_mean) if track else None, _ptr(bn.running_var) if track else None,
                                st.mean.data_ptr(), st.invstd.data_ptr(), st.scale.data_ptr(), st.shift.data_ptr(),
@@ -981,7 +989,7 @@ def hier_head_train(T: Tape, head: nn.Module, feat: Act):
              "ubf_train_fwd")
     else:
         if ubn.num_batches_tracked is not None:
-            ubn.num_batches_tracked.add_(1)
+            S.nbt.append(ubn.num_batches_tracked)
         _chk(lib.hiseg_ubf_train_fwd(ctypes.byref(ud), float(ubn.eps), float(ubn.momentum or 0.1),
                                      ubn.running_mean.data_ptr(), ubn.running_var.data_ptr(), ws.data_ptr(),
                                      _stream()), "ubf_train_fwd")
@@ -1121,6 +1129,7 @@ class _RoiPathFunction(torch.autograd.Function):
         S.pack()
         u = handle["u"]
         logits, aux = roi_path_train(model, S, T, images, rois, u)
+        S.flush_counters()
         ctx.tape, ctx.state = T, S
         diff = [aux.get(k) for k in DIFF_AUX]
         ctx.diff_present = [t is not None for t in diff]
