@@ -573,10 +573,46 @@ def _conv_flops(d):
     return 2.0 * d.N * d.Ho * d.Wo * d.Cout * d.KH * d.KW * (d.Ca + d.Cb)
 
 
+def _es(dtype_code):
+    return 2 if int(dtype_code) == 1 else 4   # include/hiseg.h: HISEG_BF16 = 1, HISEG_F32 = 0
+
+
+def _hbm_bytes(name, args):
+    """Algorithmic HBM bytes of one call of an element-wise / statistics entry point (every operand read or
+    written once), or None for entry points without a formula here.  SURVEY.md §8d: BN stat / apply, depthwise
+    convs and the SE pools are HBM-bound."""
+    try:
+        if name == "hiseg_bn_stats":            # (dtype, z, P, C, cstride, coff, partial, stream): read z
+            return float(args[2]) * args[3] * _es(args[0])
+        if name == "hiseg_bn_apply":            # read z (+ residual), write y
+            d = args[0]._obj
+            return float(d.P) * d.C * _es(d.dtype) * (2 + (1 if d.residual else 0))
+        if name == "hiseg_bn_bwd":              # read dy, z (+ residual), write dz (+ dres, read when accumulating)
+            d = args[0]._obj
+            n = 3 + (1 if d.residual else 0) + ((1 + (1 if d.dres_accumulate else 0)) if d.dres else 0)
+            return float(d.P) * d.C * _es(d.dtype) * n
+        if name in ("hiseg_dwconv_fwd", "hiseg_dwconv_gap_fwd"):   # (dtype, in, N, H, W, C, K, stride, ..., Ho, Wo)
+            dt, N, H, W, C, Ho, Wo = args[0], args[2], args[3], args[4], args[5], args[13], args[14]
+            return float(N) * (H * W + Ho * Wo) * C * _es(dt)
+    except (AttributeError, IndexError, TypeError):
+        return None
+    return None
+
+
+# kernel classes of the train / distill legs: every C-ABI entry point falls in one; a leg's `roofline` is the
+# class that takes the most GPU time, bounded by MFMA (the conv classes, algorithmic FLOPs) or by HBM (the others,
+# algorithmic bytes)
+_HBM_CLASSES = {"hiseg_bn_stats": "BatchNorm (train)", "hiseg_bn_finalize": "BatchNorm (train)",
+                "hiseg_bn_apply": "BatchNorm (train)", "hiseg_bn_bwd": "BatchNorm (train)",
+                "hiseg_dwconv_fwd": "depthwise conv (+ SE pool)", "hiseg_dwconv_gap_fwd": "depthwise conv (+ SE pool)"}
+
+
 def call_profile(step):
     """One extra (untimed) step with HIP events around every libhiseg C-ABI call on its launch stream:
-    per-entry-point GPU time and the dominant conv kernel class (forward / data-gradient / weight-gradient
-    launches grouped by shape) with its MFMA roofline -- the `roofline` of the train and distill legs."""
+    per-entry-point GPU time; per kernel class (conv forward / data gradient / weight gradient over all layers,
+    train-mode BatchNorm, depthwise + SE pool) the time, the algorithmic FLOPs or bytes and the bound -- the
+    class with the largest share of the step is the leg's `roofline`; the heaviest single conv layer class is
+    reported beside it (`dominant_layer`)."""
     from hiseg import _lib as L
     lib = L.lib()
     real, rec = {}, []
@@ -592,15 +628,18 @@ def call_profile(step):
             e0.record()
             r = _f(*a)
             e1.record()
-            key, flops = None, 0.0
+            key, cls, flops, nbytes = None, _HBM_CLASSES.get(_n), 0.0, None
             if _n in ("hiseg_conv2d_fwd", "hiseg_conv2d_fwd_variant", "hiseg_conv2d_wgrad"):
                 d = a[0]._obj
                 kind = "wgrad" if _n == "hiseg_conv2d_wgrad" else (
                     "dgrad" if sys._getframe(1).f_code.co_name == "_dgrad_launch" else "fwd")
                 key = (f"{kind} {d.KH}x{d.KW}{' T' if d.convT else ''} {d.Ca}+{d.Cb}->{d.Cout} "
                        f"{d.N}x{d.Ho}x{d.Wo}")
+                cls = {"fwd": "conv forward", "dgrad": "conv data gradient", "wgrad": "conv weight gradient"}[kind]
                 flops = _conv_flops(d)
-            rec.append((_n, key, flops, e0, e1))
+            elif cls is not None:
+                nbytes = _hbm_bytes(_n, a)
+            rec.append((_n, key, cls, flops, nbytes, e0, e1))
             return r
         setattr(lib, name, wrap)
     try:
@@ -613,26 +652,54 @@ def call_profile(step):
         for name, fn in real.items():
             setattr(lib, name, fn)
     step_ms = t0.elapsed_time(t1)
-    by_entry, groups = {}, {}
-    for n, k, fl, e0, e1 in rec:
+    by_entry, groups, classes = {}, {}, {}
+    for n, k, cls, fl, nb, e0, e1 in rec:
         ms = e0.elapsed_time(e1)
         by_entry[n] = by_entry.get(n, 0.0) + ms
         if k is not None:
             g = groups.setdefault(k, [0, 0.0, fl])
             g[0] += 1
             g[1] += ms
+        if cls is not None:
+            c = classes.setdefault(cls, {"calls": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0, "bytes_ms": 0.0})
+            c["calls"] += 1
+            c["ms"] += ms
+            c["flops"] += fl
+            if nb is not None:   # bytes only over the calls with a formula (bn_finalize: a few KB, not counted)
+                c["bytes"] += nb
+                c["bytes_ms"] += ms
     conv_ms = sum(g[1] for g in groups.values())
     out = {"step_ms_probed": round(step_ms, 3),
+           "c_abi_calls": len(rec),
            "conv_share": round(conv_ms / step_ms, 4) if step_ms > 0 else None,
            "top_entry_points_ms": {n: round(ms, 3) for n, ms in sorted(by_entry.items(), key=lambda kv: -kv[1])[:6]}}
+    table = {}
+    for cls, c in classes.items():
+        row = {"calls": c["calls"], "ms": round(c["ms"], 3), "share_of_step": round(c["ms"] / step_ms, 4)}
+        if c["flops"] > 0:
+            ach = c["flops"] / (c["ms"] * 1e-3) / 1e12
+            row.update(bound="mfma", achieved=round(ach, 1), peak=PEAK_BF16_TFLOPS, unit="TFLOP/s",
+                       frac=round(ach / PEAK_BF16_TFLOPS, 4))
+        elif c["bytes_ms"] > 0:
+            gbs = c["bytes"] / (c["bytes_ms"] * 1e-3) / 1e9
+            row.update(bound="hbm", achieved=round(gbs, 1), peak=PEAK_HBM_GBS, unit="GB/s",
+                       frac=round(gbs / PEAK_HBM_GBS, 4), bytes=c["bytes"])
+        table[cls] = row
+    out["classes"] = table
+    if table:
+        cls, row = max(table.items(), key=lambda kv: kv[1]["ms"])
+        out["roofline"] = {"bound": row.get("bound"), "achieved": row.get("achieved"), "peak": row.get("peak"),
+                           "unit": row.get("unit"), "frac": row.get("frac"), "traffic": None,
+                           "kernel": f"{cls} (all layers of the step, {row['calls']} C-ABI calls)",
+                           "share_of_step": row["share_of_step"], "avg_launch_ms": round(row["ms"] / row["calls"], 4)}
     if groups:
         key, (cnt, ms, fl) = max(groups.items(), key=lambda kv: kv[1][1])
         avg = ms / cnt
         ach = fl / (avg * 1e-3) / 1e12
-        out["roofline"] = {"bound": "mfma", "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                           "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None, "kernel": key,
-                           "launches_timed": cnt, "avg_launch_ms": round(avg, 4), "flop_per_launch": fl,
-                           "share_of_step": round(ms / step_ms, 4) if step_ms > 0 else None}
+        out["dominant_layer"] = {"bound": "mfma", "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS,
+                                 "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "kernel": key,
+                                 "launches_timed": cnt, "avg_launch_ms": round(avg, 4), "flop_per_launch": fl,
+                                 "share_of_step": round(ms / step_ms, 4) if step_ms > 0 else None}
         all_fl = sum(g[2] * g[0] for g in groups.values())
         out["conv_tflops"] = round(all_fl / (conv_ms * 1e-3) / 1e12, 1) if conv_ms > 0 else None
     return out
@@ -684,6 +751,8 @@ def main():
     ap.add_argument("--no-distill", action="store_true")
     ap.add_argument("--no-presets", action="store_true", help="skip the C3 (B1) / C4 (B7) train lines")
     ap.add_argument("--distill-only", action="store_true", help="only the C5 distillation line (profiling)")
+    ap.add_argument("--leg", choices=["train", "c3", "c4", "distill"], default=None,
+                    help="profiling: run only this train / distillation leg (one JSON object)")
     ap.add_argument("--serial", action="store_true", help="one stream (no UNet/head overlap across steps)")
     ap.add_argument("--eager-train", action="store_true", help="train / distill legs as eager launches (default on one "
                                                                 "GPU: one replayed HIP graph per step)")
@@ -730,6 +799,23 @@ def main():
 
     import hiseg  # noqa: F401
     out = {}
+    if args.leg is not None:   # one leg alone (rocprofv3 PMC passes per leg: tools/pmc_classes.py)
+        steps, g = max(2, args.steps // 2), not args.eager_train
+        if args.leg == "train":
+            out["train"] = train_bench(device, dtype, rank, world, dist, steps, max(2, args.warmup), graph_train=g)
+        elif args.leg == "c3":
+            out["train_c3"] = train_bench(device, dtype, rank, world, dist, steps, 2, preset="b1", batch=32,
+                                          rois_per_img=1, hw=(640, 640), graph_train=g)
+        elif args.leg == "c4":
+            out["train_c4"] = train_bench(device, dtype, rank, world, dist, steps, 2, preset="b7", batch=8,
+                                          rois_per_img=1, hw=(640, 640), graph_train=g)
+        else:
+            out["distill"] = distill_bench(device, dtype, rank, world, dist, steps, 2, graph=g)
+        if rank == 0:
+            print(json.dumps(out))
+        if dist:
+            dist.destroy_process_group()
+        return
     if args.distill_only:
         args.train_only, args.no_train = True, True
         out["distill"] = distill_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2,
