@@ -439,6 +439,116 @@ __global__ void __launch_bounds__(256) dwconv_q_kernel(const void* in, int H, in
   }
 }
 
+// LDS-tiled depthwise conv (bf16; round 4).  dwconv_q_kernel gathers every tap straight from global memory (8-B loads,
+// each input pixel fetched by up to K x ceil(K / 4) threads through L1 / L2): 0.6 TB/s on the distillation step's
+// B7 stages.  Here a block owns an 8 x 16 output tile of one image and 64 channels: the (7 ST + K) x (15 ST + K)
+// input window is loaded once into LDS with 16-B loads (a pixel's 64 channels = 128 contiguous bytes, 8 lanes), then
+// every thread computes 4-channel x 4-column strips from LDS (8-B reads; pixel stride 136 B to spread the banks).
+// Per output the arithmetic is dwconv_q_kernel's exactly -- same taps skipped outside the image, same tap order, same
+// fused multiply-adds and epilogue -- so the outputs are bit-identical to it.  SE pool: one partial per (image, tile)
+// (hiseg_dw_gap_tiles = ceil(Ho / 8) x ceil(Wo / 16), independent of the batch).
+constexpr int kDwTH = 8, kDwTW = 16, kDwCG = 64, kDwPS = kDwCG * 2 + 8;
+template <int KS, int ST>
+__global__ void __launch_bounds__(256) dwconv_t_kernel(const void* in, int H, int W, int C, const float* w,
+                                                       const float* scale, const float* shift, int act, void* out,
+                                                       int Ho, int Wo, float* gap) {
+  constexpr int IH = (kDwTH - 1) * ST + KS, IW = (kDwTW - 1) * ST + KS;
+  constexpr int NIN = (kDwXS - 1) * ST + KS;
+  constexpr int NSTRIP = kDwTH * (kDwTW / kDwXS);   // 32 strips of 4 outputs per channel quad
+  extern __shared__ __attribute__((aligned(16))) char dws[];
+  const int t = threadIdx.x;
+  const int n = blockIdx.y, g0 = blockIdx.z * kDwCG;
+  const int ntx = (Wo + kDwTW - 1) / kDwTW;
+  const int ty = blockIdx.x / ntx, tx = blockIdx.x - ty * ntx;
+  const int oy0 = ty * kDwTH, ox0 = tx * kDwTW;
+  const int iy0 = oy0 * ST - KS / 2, ix0 = ox0 * ST - KS / 2;
+  const int nch = C >> 3;   // 8-channel chunks
+  // ---- input window -> LDS: 8 chunks (128 B) per pixel, zeros outside the image / past C
+  const uint4* src = reinterpret_cast<const uint4*>(in) + (long long)n * H * W * nch;
+  for (int idx = t; idx < IH * IW * 8; idx += 256) {
+    const int pix = idx >> 3, ck = idx & 7;
+    const int hy = pix / IW, hx = pix - hy * IW;
+    const int iy = iy0 + hy, ix = ix0 + hx, ch = (g0 >> 3) + ck;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W && ch < nch) v = src[((long long)iy * W + ix) * nch + ch];
+    *reinterpret_cast<uint4*>(dws + pix * kDwPS + ck * 16) = v;
+  }
+  __syncthreads();
+  // ---- compute: thread = channel quad qd (16 per block) x strips it, it + 16 (two per thread)
+  const int qd = t & 15, it = t >> 4;
+  const int c = g0 + qd * 4;
+  const bool live = c < C;
+  const int cc = live ? c : 0;
+  float wk[KS * KS][4], sc[4], sh[4], gs[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < KS * KS; ++k) {
+    const float4 f = *reinterpret_cast<const float4*>(w + k * C + cc);
+    wk[k][0] = f.x; wk[k][1] = f.y; wk[k][2] = f.z; wk[k][3] = f.w;
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { sc[e] = scale[cc + e]; sh[e] = shift[cc + e]; }
+  const int nq = C >> 2;
+  uint2* dst = reinterpret_cast<uint2*>(out) + (long long)n * Ho * Wo * nq;
+#pragma unroll
+  for (int sj = 0; sj < NSTRIP / 16; ++sj) {
+    const int st = it + 16 * sj;
+    const int ry = st / (kDwTW / kDwXS), rx = (st - ry * (kDwTW / kDwXS)) * kDwXS;
+    const int oy = oy0 + ry, ox = ox0 + rx;
+    if (!live || oy >= Ho) continue;
+    float acc[kDwXS][4];
+#pragma unroll
+    for (int xo = 0; xo < kDwXS; ++xo)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[xo][e] = 0.f;
+#pragma unroll
+    for (int ky = 0; ky < KS; ++ky) {
+      const int iy = oy * ST - KS / 2 + ky;
+      if ((unsigned)iy >= (unsigned)H) continue;
+      const char* row = dws + ((ry * ST + ky) * IW + rx * ST) * kDwPS + qd * 8;
+#pragma unroll
+      for (int j = 0; j < NIN; ++j) {
+        const int ix = ox * ST - KS / 2 + j;
+        if ((unsigned)ix >= (unsigned)W) continue;
+        const uint2 raw = *reinterpret_cast<const uint2*>(row + j * kDwPS);
+        const float v[4] = {__uint_as_float(raw.x << 16), __uint_as_float(raw.x & 0xffff0000u),
+                            __uint_as_float(raw.y << 16), __uint_as_float(raw.y & 0xffff0000u)};
+#pragma unroll
+        for (int xo = 0; xo < kDwXS; ++xo) {
+          const int kx = j - xo * ST;
+          if (kx < 0 || kx >= KS) continue;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[xo][e] += wk[ky * KS + kx][e] * v[e];
+        }
+      }
+    }
+#pragma unroll
+    for (int xo = 0; xo < kDwXS; ++xo) {
+      if (ox + xo >= Wo) break;
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[e] = apply_act(acc[xo][e] * sc[e] + sh[e], act);
+        gs[e] += o[e];
+      }
+      dst[((long long)oy * Wo + ox + xo) * nq + (c >> 2)] = make_uint2(f2bf2(o[0], o[1]), f2bf2(o[2], o[3]));
+    }
+  }
+  if (gap == nullptr) return;
+  __syncthreads();   // the window is no longer read: its LDS takes the 16 x 64 pool partials
+  float* red = reinterpret_cast<float*>(dws);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) red[t * 4 + e] = gs[e];
+  __syncthreads();
+  if (it == 0 && live) {
+    for (int r = 1; r < 16; ++r)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gs[e] += red[(r * 16 + qd) * 4 + e];
+    float* gp = gap + ((long long)n * gridDim.x + blockIdx.x) * C + c;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) gp[e] = gs[e];
+  }
+}
+
 // channel quads per block for dwconv_q_kernel: the fewest z groups whose blocks keep >= 90 % of the 256 threads
 // busy (else the best fill seen)
 static int dw_quads_per_block(int nq) {
@@ -766,6 +876,38 @@ extern "C" int hiseg_dw_gap_tiles(int N, int Ho, int Wo) {
   return t < by_len ? t : by_len;
 }
 
+// Which depthwise kernel takes a layer: the LDS-tiled one for bf16 stride-1 layers of >= 192 channels
+// (tools/dw_bench.py: 1.2-6x the register-gather kernel on the B7 / B0 stages of >= 240 channels; the stride-2
+// windows (76-90 KiB, one block per CU) and the narrow wide-image layers are faster gathered).
+static bool dw_use_tiles(int dtype, int C, int stride) {
+  const char* e = getenv("HISEG_DWCONV_T");   // 0: never (A/B timing, the bit-identity test); read per call
+  return dtype == HISEG_BF16 && stride == 1 && C >= 192 && !(e && atoi(e) == 0);
+}
+
+extern "C" int hiseg_dw_gap_parts(int dtype, int N, int Ho, int Wo, int C, int K, int stride) {
+  // SE-pool partials per image of this layer: one per 8 x 16 output tile for the LDS-tiled kernel (independent of
+  // the batch), else hiseg_dw_gap_tiles' strip ranges
+  (void)K;
+  if (dw_use_tiles(dtype, C, stride)) return ((Ho + kDwTH - 1) / kDwTH) * ((Wo + kDwTW - 1) / kDwTW);
+  return hiseg_dw_gap_tiles(N, Ho, Wo);
+}
+
+static size_t dw_lds(int KS, int ST) {
+  const size_t win = (size_t)((kDwTH - 1) * ST + KS) * ((kDwTW - 1) * ST + KS) * kDwPS;
+  return win > 256 * 4 * sizeof(float) ? win : 256 * 4 * sizeof(float);
+}
+
+// the stride-2 windows exceed the default 64 KiB of dynamic LDS (k5: 19 x 35 pixels = 90 KiB)
+template <int KS, int ST>
+static void dw_t_attr() {
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)dwconv_t_kernel<KS, ST>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)dw_lds(KS, ST));
+    done = true;
+  }
+}
+
 static int dwconv_launch(int dtype, const void* in, int N, int H, int W, int C, int K, int stride, const float* w,
                          const float* scale, const float* shift, int act, void* out, int Ho, int Wo, float* gap,
                          hipStream_t s) {
@@ -785,9 +927,17 @@ static int dwconv_launch(int dtype, const void* in, int N, int H, int W, int C, 
   dim3 gridq(tiles, N, (nq + ctq - 1) / ctq);
   // HISEG_DWCONV_Q=0: the round-2 v5 bf16 kernel (8 channels per thread, weights re-read per strip), A/B only
   static const bool dwq = [] { const char* e = getenv("HISEG_DWCONV_Q"); return !(e && atoi(e) == 0); }();
+  const bool dwt = dw_use_tiles(dtype, C, stride);
+  const int tiles2 = ((Ho + kDwTH - 1) / kDwTH) * ((Wo + kDwTW - 1) / kDwTW);
+  const dim3 gridt(tiles2, N, (C + kDwCG - 1) / kDwCG);
 #define DW_L(KS, ST)                                                                                          \
   do {                                                                                                        \
-    if (dtype == HISEG_BF16 && dwq)                                                                           \
+    if (dtype == HISEG_BF16 && dwt && dwq) {                                                                  \
+      dw_t_attr<KS, ST>();                                                                                    \
+      hipLaunchKernelGGL((dwconv_t_kernel<KS, ST>), gridt, dim3(256), dw_lds(KS, ST), s, in, H, W, C, w,      \
+                         scale, shift, act, out, Ho, Wo, gap);                                                \
+    }                                                                                                         \
+    else if (dtype == HISEG_BF16 && dwq)                                                                      \
       hipLaunchKernelGGL((dwconv_q_kernel<KS, ST>), gridq, dim3(256), 0, s, in, H, W, C, w, scale, shift,     \
                          act, out, Ho, Wo, gap, ctq);                                                         \
     else if (dtype != HISEG_BF16)                                                                             \

@@ -264,6 +264,7 @@ def _declare(lib):
         "hiseg_dwconv_fwd": ([c_int, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, c_int, P,
                               c_int, c_int, P], c_int),
         "hiseg_dw_gap_tiles": ([c_int, c_int, c_int], c_int),
+        "hiseg_dw_gap_parts": ([c_int, c_int, c_int, c_int, c_int, c_int, c_int], c_int),
         "hiseg_dwconv_gap_fwd": ([c_int, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P, c_int, P,
                                   c_int, c_int, P, P], c_int),
         "hiseg_se_gate_partials_fwd": ([P, c_int, c_int, c_int, c_int, P, P, c_int, P, P, c_int, P, P], c_int),

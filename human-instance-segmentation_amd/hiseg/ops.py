@@ -414,7 +414,7 @@ def dwconv_se_gate(x: Act, w: torch.Tensor, scale: torch.Tensor, shift: torch.Te
     Wo = (x.W + 2 * pad - k) // stride + 1
     lib = L.lib()
     out = Act.new(x.N, Ho, Wo, x.C, x.dtype, x.t.device, zero=False)
-    tiles = lib.hiseg_dw_gap_tiles(x.N, Ho, Wo)
+    tiles = lib.hiseg_dw_gap_parts(hdtype(x.dtype), x.N, Ho, Wo, x.C, k, stride)
     partial = torch.empty(x.N * tiles * x.C, dtype=torch.float32, device=x.t.device)
     L.check(lib.hiseg_dwconv_gap_fwd(hdtype(x.dtype), x.ptr(), x.N, x.H, x.W, x.C, k, stride, w.data_ptr(),
                                      scale.data_ptr(), shift.data_ptr(), act, out.ptr(), Ho, Wo, partial.data_ptr(),

@@ -177,10 +177,13 @@ int hiseg_dwconv_fwd(int dtype, const void* in, int N, int H, int W, int C, int 
                      const float* w, const float* scale, const float* shift, int act, void* out,
                      int Ho, int Wo, hiseg_stream_t stream);
 /* The same depthwise conv fused with the SqueezeExcite global average pool that consumes its output
- * (timm MBConv: conv_dw -> bn -> act -> se): gap_partial [N][tiles][C] f32 receives per-tile channel
- * sums of the output (tiles = hiseg_dw_gap_tiles(N, Ho, Wo)); hiseg_se_gate_partials_fwd turns them
- * into the gate [N][C] without re-reading the activation. */
+ * (timm MBConv: conv_dw -> bn -> act -> se): gap_partial [N][parts][C] f32 receives per-tile channel
+ * sums of the output (parts = hiseg_dw_gap_parts(dtype, N, Ho, Wo, C, K, stride): the kernel that takes the
+ * layer fixes it); hiseg_se_gate_partials_fwd turns them into the gate [N][C] without re-reading the
+ * activation.  hiseg_dw_gap_tiles(N, Ho, Wo) is the strip-range count of the register-gather kernel (the
+ * layers hiseg_dw_gap_parts does not give to the LDS-tiled kernel). */
 int hiseg_dw_gap_tiles(int N, int Ho, int Wo);
+int hiseg_dw_gap_parts(int dtype, int N, int Ho, int Wo, int C, int K, int stride);
 int hiseg_dwconv_gap_fwd(int dtype, const void* in, int N, int H, int W, int C, int K, int stride,
                          const float* w, const float* scale, const float* shift, int act, void* out,
                          int Ho, int Wo, float* gap_partial, hiseg_stream_t stream);

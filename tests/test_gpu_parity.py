@@ -1117,3 +1117,41 @@ def test_conv_hwt_bit_identical_to_hwr(shape):
     assert torch.isfinite(outs[97].float()).all()
     assert torch.equal(outs[103], outs[97])
     assert torch.equal(outs[0], outs[97])
+
+
+@pytest.mark.parametrize("shape", [(2, 37, 45, 240, 5, 1), (3, 20, 20, 2304, 5, 1), (2, 33, 47, 144, 3, 2),
+                                   (2, 40, 40, 480, 5, 2), (1, 9, 7, 192, 3, 1), (2, 64, 48, 200, 3, 1)])
+def test_dwconv_lds_tile_bit_identical_to_gather_kernel(shape, monkeypatch):
+    """The LDS-tiled depthwise conv (dwconv_t_kernel: 8 x 16 output tiles x 64 channels, the input window loaded
+    once; bf16 stride-1 layers of >= 192 channels) against the register-gather kernel (dwconv_q_kernel,
+    HISEG_DWCONV_T=0): bit-identical outputs (same taps, order and epilogue) at ragged tiles and partial channel
+    groups, k3 / k5; the fused SE pool and gate within f32 re-association (one partial per tile instead of per strip
+    range), the gate batch-invariant.  Stride-2 layers stay on the gather kernel either way."""
+    from hiseg import ops
+    N, H, W, C, k, stride = shape
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(41)
+    A = ops.Act.from_nchw(torch.randn(N, C, H, W, device=DEV, generator=g), dt)
+    wd = (torch.randn(k * k, C, device=DEV, generator=g) * 0.3).contiguous()
+    sc, sh = torch.rand(C, device=DEV, generator=g) + 0.5, torch.randn(C, device=DEV, generator=g) * 0.1
+    cr = max(1, C // 24)
+    w1, b1 = torch.randn(cr, C, device=DEV, generator=g) * 0.1, torch.randn(cr, device=DEV, generator=g) * 0.1
+    w2, b2 = torch.randn(C, cr, device=DEV, generator=g) * 0.1, torch.randn(C, device=DEV, generator=g) * 0.1
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("HISEG_DWCONV_T", mode)
+        plain = ops.dwconv(A, wd, sc, sh, k, stride, 3).t.clone()
+        h, gate = ops.dwconv_se_gate(A, wd, sc, sh, k, stride, 3, w1, b1, w2, b2, 3)
+        res[mode] = (plain, h.t.clone(), gate.clone())
+    torch.cuda.synchronize()
+    (p1, h1, g1), (p0, h0, g0) = res["1"], res["0"]
+    assert torch.isfinite(p1.float()).all()
+    assert torch.equal(p1, p0) and torch.equal(h1, h0) and torch.equal(p1, h1)
+    assert (g1 - g0).abs().max().item() < 1e-5
+    if stride != 1 or C < 192:
+        return
+    # batch invariance of the pooled gate (tile partials do not depend on the batch): image 0 alone
+    monkeypatch.setenv("HISEG_DWCONV_T", "1")
+    one = ops.Act(A.t[:H * W * A.cstride].clone(), 1, H, W, C, A.cstride, 0)
+    _, g_one = ops.dwconv_se_gate(one, wd, sc, sh, k, stride, 3, w1, b1, w2, b2, 3)
+    assert torch.equal(g_one[0], g1[0])
