@@ -214,6 +214,119 @@ __global__ void __launch_bounds__(256) se_out_kernel(const float* hid, int C, in
   if (lane == 0) gate[(long long)n * C + c] = sigmoidf_(s + (b2 ? b2[c] : 0.f));
 }
 
+// Two-launch SqueezeExcite from the pool partials (the three launches above -- reduce, hidden, out -- were ~20 us per
+// SE block, most of it the hidden kernel's 36..60-step load chain over the B7's long W1 rows and two launch
+// boundaries).  Launch 1, grid (N, ceil(C/64)): each block pools its 64 channels (gap_reduce_kernel's order) and
+// multiplies them into the Cr hidden units' W1 columns -- one thread per hidden unit, its 64 weights as 16 loads in
+// flight -- and writes those Cr partial dot products into the partial rows it alone read (se_hpart_at); launch 2,
+// grid (N, ceil(C/256)): every block sums the ceil(C/64) partial products of each hidden unit (fixed order), applies
+// b1 + act into LDS, and gives each thread one channel's gate.  Deterministic and batch-independent; the caller
+// checks that the hidden partials fit (se2_fits).
+__device__ __forceinline__ long long se_hpart_at(int n, int splits, int C, int cb, int r) {
+  const int w = C - cb * 64 < 64 ? C - cb * 64 : 64;   // the block's channel width: its partial columns
+  return ((long long)n * splits + r / w) * C + cb * 64 + r % w;
+}
+
+template <bool V4>
+__global__ void __launch_bounds__(256) se_pool_w1_kernel(float* partial, int splits, int HW, int C, const float* w1,
+                                                         int Cr) {
+  __shared__ float red[256];
+  __shared__ __attribute__((aligned(16))) float mloc[64];
+  const int n = blockIdx.x, cb = blockIdx.y, t = threadIdx.x;
+  const int c = cb * 64 + (t & 63), sg = t >> 6;
+  float a8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    const float* base = partial + (long long)n * splits * C + c;
+    int sp = sg;
+    for (; sp + 28 < splits; sp += 32)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a8[u] += base[(long long)(sp + 4 * u) * C];
+    for (int u = 0; sp < splits; sp += 4, ++u) a8[u & 7] += base[(long long)sp * C];
+  }
+  red[t] = ((a8[0] + a8[1]) + (a8[2] + a8[3])) + ((a8[4] + a8[5]) + (a8[6] + a8[7]));
+  __syncthreads();   // every read of this block's partial columns is done: they may take the hidden partials
+  if (sg == 0) mloc[t] = c < C ? (red[t] + red[t + 64] + red[t + 128] + red[t + 192]) * (1.f / (float)HW) : 0.f;
+  __syncthreads();
+  const int w = C - cb * 64 < 64 ? C - cb * 64 : 64;
+  for (int r = t; r < Cr; r += 256) {
+    const float* wr = w1 + (long long)r * C + cb * 64;
+    float s = 0.f;
+    if (V4 && w == 64) {
+      float4 q[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) q[j] = reinterpret_cast<const float4*>(wr)[j];
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        s += q[j].x * mloc[4 * j] + q[j].y * mloc[4 * j + 1] + q[j].z * mloc[4 * j + 2] + q[j].w * mloc[4 * j + 3];
+    } else {
+      for (int j = 0; j < w; ++j) s += wr[j] * mloc[j];
+    }
+    partial[se_hpart_at(n, splits, C, cb, r)] = s;
+  }
+}
+
+template <bool V4>
+__global__ void __launch_bounds__(256) se_gate_out_kernel(const float* partial, int splits, int C, const float* b1,
+                                                          int Cr, int act, float beta, const float* w2, const float* b2,
+                                                          float* gate) {
+  extern __shared__ __attribute__((aligned(16))) float hid[];
+  const int n = blockIdx.x, t = threadIdx.x;
+  const int ncb = (C + 63) / 64;
+  for (int r = t; r < Cr; r += 256) {
+    float s = 0.f;
+#pragma unroll 8
+    for (int cb = 0; cb < ncb; ++cb) s += partial[se_hpart_at(n, splits, C, cb, r)];
+    hid[r] = apply_act(s + (b1 ? b1[r] : 0.f), act, beta);
+  }
+  __syncthreads();
+  const int c = blockIdx.y * 256 + t;
+  if (c >= C) return;
+  const float* wr = w2 + (long long)c * Cr;
+  float s = 0.f;
+  if (V4) {
+    int r = 0;
+    for (; r + 32 <= Cr; r += 32) {
+      float4 q[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q[j] = reinterpret_cast<const float4*>(wr + r)[j];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        s += q[j].x * hid[r + 4 * j] + q[j].y * hid[r + 4 * j + 1] + q[j].z * hid[r + 4 * j + 2] +
+             q[j].w * hid[r + 4 * j + 3];
+    }
+    for (; r < Cr; r += 4) {
+      const float4 q = *reinterpret_cast<const float4*>(wr + r);
+      s += q.x * hid[r] + q.y * hid[r + 1] + q.z * hid[r + 2] + q.w * hid[r + 3];
+    }
+  } else {
+    for (int r = 0; r < Cr; ++r) s += wr[r] * hid[r];
+  }
+  gate[(long long)n * C + c] = sigmoidf_(s + (b2 ? b2[c] : 0.f));
+}
+
+// the hidden partials of every channel block fit in the partial columns it read: Cr <= splits x (its width)
+static bool se2_fits(int splits, int C, int Cr) {
+  const int wl = C - ((C + 63) / 64 - 1) * 64;
+  return Cr <= (long long)splits * wl && Cr <= 16384;
+}
+
+static void se_two_launch(float* partial, int splits, int N, int HW, int C, const float* w1, const float* b1, int Cr,
+                          const float* w2, const float* b2, int act, float beta, float* gate, hipStream_t s) {
+  const bool v1 = (reinterpret_cast<uintptr_t>(w1) & 15) == 0 && C % 4 == 0;
+  const bool v2 = (reinterpret_cast<uintptr_t>(w2) & 15) == 0 && Cr % 4 == 0;
+  const dim3 g1(N, (C + 63) / 64), g2(N, (C + 255) / 256);
+  if (v1) hipLaunchKernelGGL(se_pool_w1_kernel<true>, g1, dim3(256), 0, s, partial, splits, HW, C, w1, Cr);
+  else hipLaunchKernelGGL(se_pool_w1_kernel<false>, g1, dim3(256), 0, s, partial, splits, HW, C, w1, Cr);
+  const size_t lds = (size_t)Cr * sizeof(float);
+  if (v2) hipLaunchKernelGGL(se_gate_out_kernel<true>, g2, dim3(256), lds, s, partial, splits, C, b1, Cr, act, beta, w2, b2, gate);
+  else hipLaunchKernelGGL(se_gate_out_kernel<false>, g2, dim3(256), lds, s, partial, splits, C, b1, Cr, act, beta, w2, b2, gate);
+}
+
+static bool se2_enabled() {
+  const char* e = getenv("HISEG_SE2");   // 0: the three-launch path (A/B timing, the equivalence test); read per call
+  return !(e && atoi(e) == 0);
+}
+
 // gate holds the pooled sums on entry and the gate on exit; scratch (>= N * Cr floats) takes the hidden units
 static void se_mlp(const float* w1, const float* b1, int Cr, const float* w2, const float* b2, int act, float beta, int N,
                    int HW, int C, float* scratch, float* gate, hipStream_t s) {
@@ -848,6 +961,10 @@ extern "C" int hiseg_se_gate_fwd(int dtype, const void* x, int N, int HW, int C,
   const size_t lds = nch >= 256 ? 0 : (size_t)(256 / nch) * C * sizeof(float);
   hipStream_t s = (hipStream_t)stream;
   DISPATCH_T(dtype, gap_partial_kernel, dim3(N, splits), dim3(256), lds, s, x, HW, C, splits, partial);
+  if (se2_enabled() && se2_fits(splits, C, Cr)) {
+    se_two_launch(partial, splits, N, HW, C, w1, b1, Cr, w2, b2, act, act_beta, gate, s);
+    return hiseg_check_launch("se_gate");
+  }
   // the pooled sums go through the gate buffer: each se_gate block reads its image's row into LDS before
   // it overwrites that row with the gate
   hipLaunchKernelGGL(gap_reduce_kernel, dim3(N, (C + 63) / 64), dim3(256), 0, s, partial, splits, C, gate);
@@ -976,10 +1093,14 @@ extern "C" int hiseg_se_gate_partials_fwd(float* partial, int splits, int N, int
   HISEG_REQUIRE(partial && w1 && w2 && gate && splits > 0 && N > 0 && HW > 0 && C > 0 && Cr > 0, HISEG_ERR_BAD_ARG,
                 "se_gate_partials: bad args");
   hipStream_t s = (hipStream_t)stream;
+  HISEG_REQUIRE(act != HISEG_ACT_SWISH, HISEG_ERR_BAD_ARG, "se_gate_partials: Swish(beta) is not an EfficientNet act");
+  if (se2_enabled() && se2_fits(splits, C, Cr)) {
+    se_two_launch(partial, splits, N, HW, C, w1, b1, Cr, w2, b2, act, 1.f, gate, s);
+    return hiseg_check_launch("se_gate_partials");
+  }
   // pooled sums through the gate buffer (read into LDS per image before the gate overwrites them)
   HISEG_REQUIRE((long long)splits * C >= Cr, HISEG_ERR_BAD_SHAPE, "se_gate_partials: partial buffer below N * Cr");
   hipLaunchKernelGGL(gap_reduce_kernel, dim3(N, (C + 63) / 64), dim3(256), 0, s, partial, splits, C, gate);
-  HISEG_REQUIRE(act != HISEG_ACT_SWISH, HISEG_ERR_BAD_ARG, "se_gate_partials: Swish(beta) is not an EfficientNet act");
   se_mlp(w1, b1, Cr, w2, b2, act, 1.f, N, HW, C, partial, gate, s);   // partial (consumed) holds the hidden units
   return hiseg_check_launch("se_gate_partials");
 }

@@ -160,7 +160,7 @@ int hiseg_attn_spatial_fwd(int dtype, const void* x, int N, int H, int W, int C,
  * (advanced/attention_modules.py:10-64: no bias, act = the module activation) and the
  * EfficientNet SqueezeExcite of the smp encoder (bias, SiLU).  x NHWC [N, HW, C] (cstride C).
  * w1 f32 [Cr][C], b1 [Cr] or null, w2 [C][Cr], b2 [C] or null.  Writes gate[N][C] (f32).
- * `partial` is workspace of N*splits*C floats (splits = hiseg_gap_splits(HW)). */
+ * `partial` is workspace of N*splits*C floats (splits = hiseg_gap_splits(HW)), consumed. */
 int hiseg_gap_splits(int HW);
 int hiseg_se_gate_fwd(int dtype, const void* x, int N, int HW, int C, const float* w1,
                       const float* b1, int Cr, const float* w2, const float* b2, int act, float act_beta,
@@ -187,7 +187,8 @@ int hiseg_dw_gap_parts(int dtype, int N, int Ho, int Wo, int C, int K, int strid
 int hiseg_dwconv_gap_fwd(int dtype, const void* in, int N, int H, int W, int C, int K, int stride,
                          const float* w, const float* scale, const float* shift, int act, void* out,
                          int Ho, int Wo, float* gap_partial, hiseg_stream_t stream);
-/* partial is consumed: after the pooled sums are read, its first N * Cr floats hold the hidden units. */
+/* partial is consumed: after the pooled sums are read it holds intermediate values (the hidden units' partial
+ * products).  Two launches when every 64-channel block's partial columns can hold Cr values, else three. */
 int hiseg_se_gate_partials_fwd(float* partial, int splits, int N, int HW, int C, const float* w1,
                                const float* b1, int Cr, const float* w2, const float* b2, int act,
                                float* gate, hiseg_stream_t stream);

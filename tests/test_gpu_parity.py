@@ -1155,3 +1155,49 @@ def test_dwconv_lds_tile_bit_identical_to_gather_kernel(shape, monkeypatch):
     one = ops.Act(A.t[:H * W * A.cstride].clone(), 1, H, W, C, A.cstride, 0)
     _, g_one = ops.dwconv_se_gate(one, wd, sc, sh, k, stride, 3, w1, b1, w2, b2, 3)
     assert torch.equal(g_one[0], g1[0])
+
+
+@pytest.mark.parametrize("case", [(4, 20, 20, 3840, 160, 5, 1), (2, 40, 40, 240, 10, 3, 2), (3, 15, 11, 100, 25, 3, 1),
+                                  (2, 9, 7, 1152, 48, 5, 1), (1, 30, 30, 2304, 96, 3, 1)])
+def test_se_two_launch_matches_three_launch_and_f64(case, monkeypatch):
+    """The two-launch SqueezeExcite (se_pool_w1_kernel + se_gate_out_kernel: the pooled channels multiplied into
+    W1 per 64-channel block, hidden partials parked in the partial columns that block alone read) against the
+    three-launch path (HISEG_SE2=0: gap_reduce, se_hidden, se_out) and a float64 restatement, at the B7 / B0 deep
+    shapes, a ragged channel block (C = 100), Cr not a multiple of 4 (scalar W2 rows) and the gather kernel's many
+    partials; batch-invariant (image 0 alone gives the same gate bits); the module-level se_gate as well."""
+    from hiseg import ops
+    N, H, W, C, cr, k, stride = case
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(43)
+    A = ops.Act.from_nchw(torch.randn(N, C, H, W, device=DEV, generator=g), dt)
+    wd = (torch.randn(k * k, C, device=DEV, generator=g) * 0.3).contiguous()
+    sc, sh = torch.rand(C, device=DEV, generator=g) + 0.5, torch.randn(C, device=DEV, generator=g) * 0.1
+    w1, b1 = torch.randn(cr, C, device=DEV, generator=g) * 0.1, torch.randn(cr, device=DEV, generator=g) * 0.1
+    w2, b2 = torch.randn(C, cr, device=DEV, generator=g) * 0.1, torch.randn(C, device=DEV, generator=g) * 0.1
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("HISEG_SE2", mode)
+        h, gate = ops.dwconv_se_gate(A, wd, sc, sh, k, stride, 3, w1, b1, w2, b2, 3)
+        sg = ops.se_gate(A, w1, b1, w2, b2, 3)
+        res[mode] = (h.t.clone(), gate.clone(), sg.clone())
+    torch.cuda.synchronize()
+    (h1, g1, s1), (h0, g0, s0) = res["1"], res["0"]
+    assert torch.equal(h1, h0)
+    assert torch.isfinite(g1).all() and torch.isfinite(s1).all()
+    assert (g1 - g0).abs().max().item() < 2e-6
+    assert (s1 - s0).abs().max().item() < 2e-6
+    # float64 restatement of the gate from the kernel's own depthwise output (the fused pool sums the f32 values
+    # before their bf16 rounding: 1e-3)
+    hm = h.to_nchw().double().mean((2, 3))
+    hid = F.silu(hm @ w1.double().t() + b1.double())
+    ref = torch.sigmoid(hid @ w2.double().t() + b2.double())
+    assert (g1.double() - ref).abs().max().item() < 1e-3
+    xm = A.to_nchw().double().mean((2, 3))
+    ref_s = torch.sigmoid(F.silu(xm @ w1.double().t() + b1.double()) @ w2.double().t() + b2.double())
+    assert (s1.double() - ref_s).abs().max().item() < 1e-5
+    if stride != 1 or C < 192 or N == 1:
+        return
+    monkeypatch.setenv("HISEG_SE2", "1")
+    one = ops.Act(A.t[:H * W * A.cstride].clone(), 1, H, W, C, A.cstride, 0)
+    _, g_one = ops.dwconv_se_gate(one, wd, sc, sh, k, stride, 3, w1, b1, w2, b2, 3)
+    assert torch.equal(g_one[0], g1[0])
