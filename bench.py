@@ -206,7 +206,7 @@ def train_bench(device, dtype, rank, world, dist, steps, warmup, preset=None, ba
     prof = None
     if world == 1:   # per-call profile of one eager step (before any graph capture: its pool would skew it)
         step()
-        prof = call_profile(step)
+        prof = call_profile(step, {None: "train", "b1": "c3", "b7": "c4"}.get(preset))
     elapsed, first, last = timed()
     sps = steps / elapsed
     gflop = GFLOP_PER_TRAIN_ROI if preset is None else GFLOP_PER_TRAIN_SAMPLE[preset]
@@ -283,7 +283,7 @@ def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=6
     if world == 1:   # per-call profile of one eager step, before the graph capture
         step()
         step()
-        prof = call_profile(step)
+        prof = call_profile(step, "distill")
     graphable = graph and (world == 1 or _backend(dist) == "nccl")
     run = hiseg.GraphedStep(step, lambda: state["opt"]) if graphable else step
     for _ in range(max(warmup, 3 if run is not step else 1)):
@@ -607,7 +607,18 @@ _HBM_CLASSES = {"hiseg_bn_stats": "BatchNorm (train)", "hiseg_bn_finalize": "Bat
                 "hiseg_dwconv_fwd": "depthwise conv (+ SE pool)", "hiseg_dwconv_gap_fwd": "depthwise conv (+ SE pool)"}
 
 
-def call_profile(step):
+def load_class_traffic(leg):
+    """Measured HBM bytes per step of each kernel class of one leg (tools/pmc_classes.py over two rocprofv3 PMC passes
+    of `bench.py --leg <leg> --eager-train`, FETCH_SIZE / WRITE_SIZE, gfx950-corrected) from roofline_traffic.json's
+    "train_legs"; {} when absent."""
+    try:
+        with open(os.path.join(ROOT, "roofline_traffic.json")) as f:
+            return json.load(f).get("train_legs", {}).get(leg, {})
+    except (OSError, ValueError):
+        return {}
+
+
+def call_profile(step, leg=None):
     """One extra (untimed) step with HIP events around every libhiseg C-ABI call on its launch stream:
     per-entry-point GPU time; per kernel class (conv forward / data gradient / weight gradient over all layers,
     train-mode BatchNorm, depthwise + SE pool) the time, the algorithmic FLOPs or bytes and the bound -- the
@@ -684,14 +695,22 @@ def call_profile(step):
             gbs = c["bytes"] / (c["bytes_ms"] * 1e-3) / 1e9
             row.update(bound="hbm", achieved=round(gbs, 1), peak=PEAK_HBM_GBS, unit="GB/s",
                        frac=round(gbs / PEAK_HBM_GBS, 4), bytes=c["bytes"])
+        meas = load_class_traffic(leg).get(cls) if leg else None
+        if meas:   # PMC-measured HBM bytes of this class per step, and per C-ABI call like `bytes`
+            row["traffic_per_step"] = round(meas["hbm_bytes_per_step"])
+            row["traffic"] = round(meas["hbm_bytes_per_step"] / c["calls"])
+            if c["bytes"] > 0:
+                row["traffic_over_algorithmic"] = round(meas["hbm_bytes_per_step"] / c["bytes"], 3)
         table[cls] = row
     out["classes"] = table
     if table:
         cls, row = max(table.items(), key=lambda kv: kv[1]["ms"])
         out["roofline"] = {"bound": row.get("bound"), "achieved": row.get("achieved"), "peak": row.get("peak"),
-                           "unit": row.get("unit"), "frac": row.get("frac"), "traffic": None,
+                           "unit": row.get("unit"), "frac": row.get("frac"), "traffic": row.get("traffic"),
                            "kernel": f"{cls} (all layers of the step, {row['calls']} C-ABI calls)",
-                           "share_of_step": row["share_of_step"], "avg_launch_ms": round(row["ms"] / row["calls"], 4)}
+                           "share_of_step": row["share_of_step"], "avg_launch_ms": round(row["ms"] / row["calls"], 4),
+                           "traffic_unit": "HBM bytes per C-ABI call of the class (rocprofv3 FETCH_SIZE / WRITE_SIZE "
+                                           "passes, roofline_traffic.json train_legs)"}
     if groups:
         key, (cnt, ms, fl) = max(groups.items(), key=lambda kv: kv[1][1])
         avg = ms / cnt

@@ -11,6 +11,8 @@
 //   bilinear with zero padding: taps outside [0,W-1]x[0,H-1] contribute 0       (:163-169)
 // Feature maps are read in place through the roi's batch index; the reference's
 // index_select copy of N full maps (:156) is not materialised.
+#include <cstdlib>
+
 #include "common.h"
 #include "hiseg_head_train.h"
 
@@ -47,7 +49,7 @@ __device__ __forceinline__ float src_coord(float lo, float len, float g, int siz
   return fsub(fmul(fadd(nrm, 1.0f), __fdiv_rn((float)size, 2.0f)), 0.5f);
 }
 
-template <typename TO>
+template <typename TO, bool VEC>
 __global__ void __launch_bounds__(256) roi_align_kernel(hiseg_roi_align_desc d) {
   const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long total = (long long)d.N * d.oh * d.ow;
@@ -80,33 +82,45 @@ __global__ void __launch_bounds__(256) roi_align_kernel(hiseg_roi_align_desc d) 
 
   const int Cout = d.aff_w ? d.n_aff : d.C;
   const long long plane = (long long)d.H * d.W;
-  for (int c = 0; c < Cout; ++c) {
-    float v = 0.f;
-    if (bvalid) {
-      const float* src = d.feat + ((long long)b * d.C + (d.aff_w ? 0 : c)) * plane;
-      float aw = 1.f, ab = 0.f;
-      const bool aff = d.aff_w != nullptr;
-      if (aff) { aw = d.aff_w[c]; ab = d.aff_b ? d.aff_b[c] : 0.f; }
-      auto tap = [&](bool ok, int yy, int xx) -> float {
-        if (!ok) return 0.f;
-        const float u = src[(long long)yy * d.W + xx];
-        return aff ? fadd(fmul(aw, u), ab) : u;
-      };
-      const float v_nw = tap(vy0 && vx0, y0, x0);
-      const float v_ne = tap(vy0 && vx1, y0, x0 + 1);
-      const float v_sw = tap(vy1 && vx0, y0 + 1, x0);
-      const float v_se = tap(vy1 && vx1, y0 + 1, x0 + 1);
-      v = fadd(fadd(fadd(fmul(v_nw, w_nw), fmul(v_ne, w_ne)), fmul(v_sw, w_sw)), fmul(v_se, w_se));
-    }
-    if (d.o_nchw) {
-      reinterpret_cast<float*>(d.out)[(((long long)n * Cout + c) * d.oh + i) * d.ow + j] = v;
-    } else {
-      Elem<TO>::store(d.out, gid * d.o_cstride + d.o_coff + c, v);
-    }
+  const bool aff = d.aff_w != nullptr;
+  const float* src0 = d.feat + (bvalid ? b : 0) * d.C * plane;
+  const long long o_nw = (long long)y0 * d.W + x0;   // tap offsets, used only where valid
+  auto value = [&](int c) __attribute__((always_inline)) -> float {
+    if (!bvalid) return 0.f;
+    const float* src = src0 + (aff ? 0 : (long long)c * plane);
+    float aw = 1.f, ab = 0.f;
+    if (aff) { aw = d.aff_w[c]; ab = d.aff_b ? d.aff_b[c] : 0.f; }
+    auto tap = [&](bool ok, long long off) -> float {
+      if (!ok) return 0.f;
+      const float u = src[off];
+      return aff ? fadd(fmul(aw, u), ab) : u;
+    };
+    const float v_nw = tap(vy0 && vx0, o_nw);
+    const float v_ne = tap(vy0 && vx1, o_nw + 1);
+    const float v_sw = tap(vy1 && vx0, o_nw + d.W);
+    const float v_se = tap(vy1 && vx1, o_nw + d.W + 1);
+    return fadd(fadd(fadd(fmul(v_nw, w_nw), fmul(v_ne, w_ne)), fmul(v_sw, w_sw)), fmul(v_se, w_se));
+  };
+  if (d.o_nchw) {
+    for (int c = 0; c < Cout; ++c)
+      reinterpret_cast<float*>(d.out)[(((long long)n * Cout + c) * d.oh + i) * d.ow + j] = value(c);
+    return;
   }
-  if (!d.o_nchw) {
-    for (int c = Cout; c < d.zero_to; ++c) Elem<TO>::store(d.out, gid * d.o_cstride + d.o_coff + c, 0.f);
+  if (VEC) {
+    // the whole padded pixel (channels, then zeros up to zero_to == o_cstride) as 16-B stores: one per 8 bf16 /
+    // 4 f32 channels instead of one 2- / 4-B store per channel, each lane's pixel 16-B aligned (checked on the host)
+    constexpr int K = Chunk<TO>::N;
+    uint4* dst = reinterpret_cast<uint4*>(reinterpret_cast<TO*>(d.out) + gid * d.o_cstride);
+    for (int q = 0; q < d.o_cstride / K; ++q) {
+      float v[K];
+#pragma unroll
+      for (int e = 0; e < K; ++e) v[e] = q * K + e < Cout ? value(q * K + e) : 0.f;
+      dst[q] = Chunk<TO>::pack(v);
+    }
+    return;
   }
+  for (int c = 0; c < Cout; ++c) Elem<TO>::store(d.out, gid * d.o_cstride + d.o_coff + c, value(c));
+  for (int c = Cout; c < d.zero_to; ++c) Elem<TO>::store(d.out, gid * d.o_cstride + d.o_coff + c, 0.f);
 }
 
 // Backward into the output_conv affine (see hiseg_roi_align_bwd_affine): per sample, the same taps
@@ -177,6 +191,11 @@ __global__ void roi_bwd_sum_kernel(const float* part, int nblk, float* dw, float
 
 using namespace hiseg;
 
+static bool getenv_flag(const char* name, int dflt) {   // read per call (A/B timing, the equivalence test)
+  const char* e = getenv(name);
+  return e ? atoi(e) != 0 : dflt != 0;
+}
+
 extern "C" int hiseg_roi_align_ws(int N) { (void)N; return kRoiBwdBlocks * 4; }
 
 extern "C" int hiseg_roi_align_bwd_affine(const hiseg_roi_align_desc* d, const void* g, int g_dtype, int g_cstride,
@@ -210,9 +229,18 @@ extern "C" int hiseg_roi_align_fwd(const hiseg_roi_align_desc* d, hiseg_stream_t
   const long long total = (long long)d->N * d->oh * d->ow;
   dim3 grid((unsigned)((total + 255) / 256));
   hipStream_t s = (hipStream_t)stream;
-  if (d->out_dtype == HISEG_BF16)
-    hipLaunchKernelGGL(roi_align_kernel<bf16_t>, grid, dim3(256), 0, s, *d);
-  else
-    hipLaunchKernelGGL(roi_align_kernel<float>, grid, dim3(256), 0, s, *d);
+  // whole-pixel 16-B stores: NHWC output written from channel 0 through the padding (zero_to == o_cstride), pixel
+  // stride a whole number of 16-B chunks, 16-B aligned base
+  const int esz = d->out_dtype == HISEG_BF16 ? 2 : 4;
+  const bool vec = !d->o_nchw && d->o_coff == 0 && d->zero_to == d->o_cstride && (d->o_cstride * esz) % 16 == 0 &&
+                   (reinterpret_cast<uintptr_t>(d->out) & 15) == 0 && getenv_flag("HISEG_ROI_VEC", 1);
+#define ROI_L(TO)                                                                          \
+  do {                                                                                     \
+    if (vec) hipLaunchKernelGGL((roi_align_kernel<TO, true>), grid, dim3(256), 0, s, *d);  \
+    else hipLaunchKernelGGL((roi_align_kernel<TO, false>), grid, dim3(256), 0, s, *d);     \
+  } while (0)
+  if (d->out_dtype == HISEG_BF16) ROI_L(bf16_t);
+  else ROI_L(float);
+#undef ROI_L
   return hiseg_check_launch("roi_align");
 }

@@ -1157,13 +1157,13 @@ def test_dwconv_lds_tile_bit_identical_to_gather_kernel(shape, monkeypatch):
     assert torch.equal(g_one[0], g1[0])
 
 
-@pytest.mark.parametrize("case", [(4, 20, 20, 3840, 160, 5, 1), (2, 40, 40, 240, 10, 3, 2), (3, 15, 11, 100, 25, 3, 1),
+@pytest.mark.parametrize("case", [(4, 20, 20, 3840, 160, 5, 1), (2, 40, 40, 240, 10, 3, 2), (3, 15, 11, 104, 25, 3, 1),
                                   (2, 9, 7, 1152, 48, 5, 1), (1, 30, 30, 2304, 96, 3, 1)])
 def test_se_two_launch_matches_three_launch_and_f64(case, monkeypatch):
     """The two-launch SqueezeExcite (se_pool_w1_kernel + se_gate_out_kernel: the pooled channels multiplied into
     W1 per 64-channel block, hidden partials parked in the partial columns that block alone read) against the
     three-launch path (HISEG_SE2=0: gap_reduce, se_hidden, se_out) and a float64 restatement, at the B7 / B0 deep
-    shapes, a ragged channel block (C = 100), Cr not a multiple of 4 (scalar W2 rows) and the gather kernel's many
+    shapes, a ragged channel block (C = 104), Cr not a multiple of 4 (scalar W2 rows) and the gather kernel's many
     partials; batch-invariant (image 0 alone gives the same gate bits); the module-level se_gate as well."""
     from hiseg import ops
     N, H, W, C, cr, k, stride = case
@@ -1201,3 +1201,38 @@ def test_se_two_launch_matches_three_launch_and_f64(case, monkeypatch):
     one = ops.Act(A.t[:H * W * A.cstride].clone(), 1, H, W, C, A.cstride, 0)
     _, g_one = ops.dwconv_se_gate(one, wd, sc, sh, k, stride, 3, w1, b1, w2, b2, 3)
     assert torch.equal(g_one[0], g1[0])
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_roi_align_whole_pixel_stores_bit_identical(dt, monkeypatch):
+    """RoIAlign into NHWC with whole-pixel 16-B stores (channels then the zero padding, HISEG_ROI_VEC=1) against the
+    per-channel stores (HISEG_ROI_VEC=0): bit-identical at C2's shapes -- the RGB crop (3 -> cstride 8 / 4) and the
+    1 -> 2 output_conv affine over the UNet logit -- including ROIs outside the image, a bad batch index and a NaN
+    coordinate (zero outputs), and the padding is written (NaN-prefilled outputs)."""
+    from hiseg import ops
+    g = torch.Generator(device=DEV).manual_seed(47)
+    B, H, W, N, oh, ow = 4, 120, 160, 37, 64, 48
+    images = torch.rand(B, 3, H, W, device=DEV, generator=g)
+    u = torch.randn(B, 1, H, W, device=DEV, generator=g)
+    x1 = torch.rand(N, device=DEV, generator=g) * 500 - 40
+    y1 = torch.rand(N, device=DEV, generator=g) * 380 - 40
+    rois = torch.stack([torch.randint(0, B, (N,), device=DEV, generator=g).float(), x1, y1,
+                        x1 + torch.rand(N, device=DEV, generator=g) * 300 + 1,
+                        y1 + torch.rand(N, device=DEV, generator=g) * 200 + 1], 1)
+    rois[3, 0] = B + 2          # batch index out of range
+    rois[5, 1] = float("nan")   # NaN coordinate
+    aw, ab = torch.randn(2, device=DEV, generator=g), torch.randn(2, device=DEV, generator=g)
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("HISEG_ROI_VEC", mode)
+        outs = []
+        for feat, kw, C in ((images, {}, 3), (u, {"aff_w": aw, "aff_b": ab}, 2)):
+            o = ops.Act.new(N, oh, ow, C, dt, torch.device(DEV), zero=False)
+            o.t.fill_(float("nan"))
+            ops.roi_align(feat, rois, oh, ow, 480.0, 640.0, True, out=o, zero_to=o.cstride, **kw)
+            outs.append(o.t.clone())
+        res[mode] = outs
+    torch.cuda.synchronize()
+    for a, b in zip(res["1"], res["0"]):
+        assert torch.isfinite(a.float()).all()
+        assert torch.equal(a, b)
