@@ -256,10 +256,16 @@ __global__ void __launch_bounds__(256) se_pool_w1_kernel(float* partial, int spl
 #pragma unroll
       for (int j = 0; j < 16; ++j) q[j] = reinterpret_cast<const float4*>(wr)[j];
 #pragma unroll
-      for (int j = 0; j < 16; ++j)
-        s += q[j].x * mloc[4 * j] + q[j].y * mloc[4 * j + 1] + q[j].z * mloc[4 * j + 2] + q[j].w * mloc[4 * j + 3];
+      for (int j = 0; j < 16; ++j) {
+        // explicit fused multiply-adds in the scalar path's order: which path runs depends on W1's alignment only,
+        // and left to contraction the vectoriser paired these products into packed multiplies (no fusion)
+        s = __builtin_fmaf(q[j].x, mloc[4 * j], s);
+        s = __builtin_fmaf(q[j].y, mloc[4 * j + 1], s);
+        s = __builtin_fmaf(q[j].z, mloc[4 * j + 2], s);
+        s = __builtin_fmaf(q[j].w, mloc[4 * j + 3], s);
+      }
     } else {
-      for (int j = 0; j < w; ++j) s += wr[j] * mloc[j];
+      for (int j = 0; j < w; ++j) s = __builtin_fmaf(wr[j], mloc[j], s);
     }
     partial[se_hpart_at(n, splits, C, cb, r)] = s;
   }
@@ -269,7 +275,12 @@ template <bool V4>
 __global__ void __launch_bounds__(256) se_gate_out_kernel(const float* partial, int splits, int C, const float* b1,
                                                           int Cr, int act, float beta, const float* w2, const float* b2,
                                                           float* gate) {
-  extern __shared__ __attribute__((aligned(16))) float hid[];
+  // 64 channels per block, four threads per channel, each over a quarter of the channel's W2 row (at most Cr / 4
+  // floats, its loads all in flight), combined in a fixed order: 256 channels per block with one thread per row
+  // (40 float4 loads each at the B7's Cr = 160, a few in flight at a time) ran 8-15 us per call on 60 blocks
+  extern __shared__ __attribute__((aligned(16))) float se_lds[];
+  float* hid = se_lds;                        // [Cr]
+  float* red = se_lds + ((Cr + 3) & ~3);      // [4][64]
   const int n = blockIdx.x, t = threadIdx.x;
   const int ncb = (C + 63) / 64;
   for (int r = t; r < Cr; r += 256) {
@@ -279,45 +290,54 @@ __global__ void __launch_bounds__(256) se_gate_out_kernel(const float* partial, 
     hid[r] = apply_act(s + (b1 ? b1[r] : 0.f), act, beta);
   }
   __syncthreads();
-  const int c = blockIdx.y * 256 + t;
-  if (c >= C) return;
-  const float* wr = w2 + (long long)c * Cr;
+  const int cl = t & 63, part = t >> 6;
+  const int c = blockIdx.y * 64 + cl;
+  const int Q = ((Cr + 15) / 16) * 4;   // per-part row span, a multiple of 4 (float4 aligned in every row)
+  const int rb = part * Q, re = rb + Q < Cr ? rb + Q : Cr;
   float s = 0.f;
-  if (V4) {
-    int r = 0;
-    for (; r + 32 <= Cr; r += 32) {
-      float4 q[8];
+  if (c < C) {
+    const float* wr = w2 + (long long)c * Cr;
+    if (V4) {
+      int r = rb;
+      for (; r + 16 <= re; r += 16) {
+        float4 q[4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) q[j] = reinterpret_cast<const float4*>(wr + r)[j];
+        for (int j = 0; j < 4; ++j) q[j] = *reinterpret_cast<const float4*>(wr + r + 4 * j);
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        s += q[j].x * hid[r + 4 * j] + q[j].y * hid[r + 4 * j + 1] + q[j].z * hid[r + 4 * j + 2] +
-             q[j].w * hid[r + 4 * j + 3];
+        for (int j = 0; j < 4; ++j) {   // explicit fused multiply-adds, the scalar path's order
+          s = __builtin_fmaf(q[j].x, hid[r + 4 * j], s);
+          s = __builtin_fmaf(q[j].y, hid[r + 4 * j + 1], s);
+          s = __builtin_fmaf(q[j].z, hid[r + 4 * j + 2], s);
+          s = __builtin_fmaf(q[j].w, hid[r + 4 * j + 3], s);
+        }
+      }
+      for (; r < re; ++r) s = __builtin_fmaf(wr[r], hid[r], s);
+    } else {
+      for (int r = rb; r < re; ++r) s = __builtin_fmaf(wr[r], hid[r], s);
     }
-    for (; r < Cr; r += 4) {
-      const float4 q = *reinterpret_cast<const float4*>(wr + r);
-      s += q.x * hid[r] + q.y * hid[r + 1] + q.z * hid[r + 2] + q.w * hid[r + 3];
-    }
-  } else {
-    for (int r = 0; r < Cr; ++r) s += wr[r] * hid[r];
   }
-  gate[(long long)n * C + c] = sigmoidf_(s + (b2 ? b2[c] : 0.f));
+  red[part * 64 + cl] = s;
+  __syncthreads();
+  if (part == 0 && c < C) {
+    const float g = ((red[cl] + red[64 + cl]) + red[128 + cl]) + red[192 + cl];
+    gate[(long long)n * C + c] = sigmoidf_(g + (b2 ? b2[c] : 0.f));
+  }
 }
 
 // the hidden partials of every channel block fit in the partial columns it read: Cr <= splits x (its width)
 static bool se2_fits(int splits, int C, int Cr) {
   const int wl = C - ((C + 63) / 64 - 1) * 64;
-  return Cr <= (long long)splits * wl && Cr <= 16384;
+  return Cr <= (long long)splits * wl && Cr <= 4096;
 }
 
 static void se_two_launch(float* partial, int splits, int N, int HW, int C, const float* w1, const float* b1, int Cr,
                           const float* w2, const float* b2, int act, float beta, float* gate, hipStream_t s) {
   const bool v1 = (reinterpret_cast<uintptr_t>(w1) & 15) == 0 && C % 4 == 0;
   const bool v2 = (reinterpret_cast<uintptr_t>(w2) & 15) == 0 && Cr % 4 == 0;
-  const dim3 g1(N, (C + 63) / 64), g2(N, (C + 255) / 256);
+  const dim3 g1(N, (C + 63) / 64), g2(N, (C + 63) / 64);
   if (v1) hipLaunchKernelGGL(se_pool_w1_kernel<true>, g1, dim3(256), 0, s, partial, splits, HW, C, w1, Cr);
   else hipLaunchKernelGGL(se_pool_w1_kernel<false>, g1, dim3(256), 0, s, partial, splits, HW, C, w1, Cr);
-  const size_t lds = (size_t)Cr * sizeof(float);
+  const size_t lds = (size_t)(((Cr + 3) & ~3) + 256) * sizeof(float);
   if (v2) hipLaunchKernelGGL(se_gate_out_kernel<true>, g2, dim3(256), lds, s, partial, splits, C, b1, Cr, act, beta, w2, b2, gate);
   else hipLaunchKernelGGL(se_gate_out_kernel<false>, g2, dim3(256), lds, s, partial, splits, C, b1, Cr, act, beta, w2, b2, gate);
 }
@@ -577,16 +597,30 @@ __global__ void __launch_bounds__(256) dwconv_t_kernel(const void* in, int H, in
   const int iy0 = oy0 * ST - KS / 2, ix0 = ox0 * ST - KS / 2;
   const int nch = C >> 3;   // 8-channel chunks
   // ---- input window -> LDS: 8 chunks (128 B) per pixel, zeros outside the image / past C
+  // batches of 8 loads per thread in flight before their LDS writes (a load -> wait -> write loop left every block
+  // waiting out ~8 global latencies one after another)
   const uint4* src = reinterpret_cast<const uint4*>(in) + (long long)n * H * W * nch;
-  for (int idx = t; idx < IH * IW * 8; idx += 256) {
-    const int pix = idx >> 3, ck = idx & 7;
-    const int hy = pix / IW, hx = pix - hy * IW;
-    const int iy = iy0 + hy, ix = ix0 + hx, ch = (g0 >> 3) + ck;
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W && ch < nch) v = src[((long long)iy * W + ix) * nch + ch];
-    *reinterpret_cast<uint4*>(dws + pix * kDwPS + ck * 16) = v;
+  constexpr int NLD = (IH * IW * 8 + 255) / 256;
+#pragma unroll
+  for (int b0 = 0; b0 < NLD; b0 += 8) {
+    uint4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int idx = t + 256 * (b0 + u);
+      const int pix = idx >> 3, ck = idx & 7;
+      const int hy = pix / IW, hx = pix - hy * IW;
+      const int iy = iy0 + hy, ix = ix0 + hx, ch = (g0 >> 3) + ck;
+      v[u] = make_uint4(0u, 0u, 0u, 0u);
+      if (b0 + u < NLD && idx < IH * IW * 8 && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W && ch < nch)
+        v[u] = src[((long long)iy * W + ix) * nch + ch];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int idx = t + 256 * (b0 + u);
+      if (b0 + u < NLD && idx < IH * IW * 8)
+        *reinterpret_cast<uint4*>(dws + (idx >> 3) * kDwPS + (idx & 7) * 16) = v[u];
+    }
   }
-  __syncthreads();
   // ---- compute: thread = channel quad qd (16 per block) x strips it, it + 16 (two per thread)
   const int qd = t & 15, it = t >> 4;
   const int c = g0 + qd * 4;
@@ -600,6 +634,10 @@ __global__ void __launch_bounds__(256) dwconv_t_kernel(const void* in, int H, in
   }
 #pragma unroll
   for (int e = 0; e < 4; ++e) { sc[e] = scale[cc + e]; sh[e] = shift[cc + e]; }
+  // held in registers for both strips (the compiler otherwise re-loads each tap's weights at its use)
+#pragma unroll
+  for (int k = 0; k < KS * KS; ++k) asm volatile("" : "+v"(wk[k][0]), "+v"(wk[k][1]), "+v"(wk[k][2]), "+v"(wk[k][3]));
+  __syncthreads();
   const int nq = C >> 2;
   uint2* dst = reinterpret_cast<uint2*>(out) + (long long)n * Ho * Wo * nq;
 #pragma unroll
@@ -993,19 +1031,21 @@ extern "C" int hiseg_dw_gap_tiles(int N, int Ho, int Wo) {
   return t < by_len ? t : by_len;
 }
 
-// Which depthwise kernel takes a layer: the LDS-tiled one for bf16 stride-1 layers of >= 192 channels
-// (tools/dw_bench.py: 1.2-6x the register-gather kernel on the B7 / B0 stages of >= 240 channels; the stride-2
-// windows (76-90 KiB, one block per CU) and the narrow wide-image layers are faster gathered).
-static bool dw_use_tiles(int dtype, int C, int stride) {
-  const char* e = getenv("HISEG_DWCONV_T");   // 0: never (A/B timing, the bit-identity test); read per call
-  return dtype == HISEG_BF16 && stride == 1 && C >= 192 && !(e && atoi(e) == 0);
+// Which depthwise kernel takes a layer: the LDS-tiled one for bf16 layers of 192..2047 channels, stride 1 or k5.
+static bool dw_use_tiles(int dtype, int C, int K, int stride) {
+  // HISEG_DWCONV_T: 0 never, 2 every bf16 layer (A/B timing, the bit-identity test); read per call
+  const char* e = getenv("HISEG_DWCONV_T");
+  const int m = e ? atoi(e) : 1;
+  if (dtype != HISEG_BF16 || m == 0) return false;
+  // tools/dw_bench.py (profiles/r4_dw_bench.txt): the tiles win on the 240..1344-channel stride-1 layers and the k5
+  // stride-2 one; the gather kernel on the narrow layers, the k3 stride-2 one and the 20 x 20 x >= 2304-channel ones
+  return m == 2 || (C >= 192 && C < 2048 && (stride == 1 || K == 5));
 }
 
 extern "C" int hiseg_dw_gap_parts(int dtype, int N, int Ho, int Wo, int C, int K, int stride) {
   // SE-pool partials per image of this layer: one per 8 x 16 output tile for the LDS-tiled kernel (independent of
   // the batch), else hiseg_dw_gap_tiles' strip ranges
-  (void)K;
-  if (dw_use_tiles(dtype, C, stride)) return ((Ho + kDwTH - 1) / kDwTH) * ((Wo + kDwTW - 1) / kDwTW);
+  if (dw_use_tiles(dtype, C, K, stride)) return ((Ho + kDwTH - 1) / kDwTH) * ((Wo + kDwTW - 1) / kDwTW);
   return hiseg_dw_gap_tiles(N, Ho, Wo);
 }
 
@@ -1044,7 +1084,7 @@ static int dwconv_launch(int dtype, const void* in, int N, int H, int W, int C, 
   dim3 gridq(tiles, N, (nq + ctq - 1) / ctq);
   // HISEG_DWCONV_Q=0: the round-2 v5 bf16 kernel (8 channels per thread, weights re-read per strip), A/B only
   static const bool dwq = [] { const char* e = getenv("HISEG_DWCONV_Q"); return !(e && atoi(e) == 0); }();
-  const bool dwt = dw_use_tiles(dtype, C, stride);
+  const bool dwt = dw_use_tiles(dtype, C, K, stride);
   const int tiles2 = ((Ho + kDwTH - 1) / kDwTH) * ((Wo + kDwTW - 1) / kDwTW);
   const dim3 gridt(tiles2, N, (C + kDwCG - 1) / kDwCG);
 #define DW_L(KS, ST)                                                                                          \

@@ -223,21 +223,29 @@ __global__ void __launch_bounds__(256) bn_stats_vec_kernel(const void* z, long l
   my[0] = n;
 #pragma unroll
   for (int k = 0; k < V; ++k) { my[1 + k] = mean[k]; my[1 + V + k] = m2[k]; }
-  __syncthreads();
-  if (r == 0 && ch < NCH) {
-    for (int rr = 1; rr < R; ++rr) {
-      const float* o = sh + (rr * CT + cl) * (2 * V + 1);
+  // pairwise (tree) merge of the R pixel rows, fixed order: the one-thread walk over R - 1 rows was a dependent chain
+  // of divisions (R = 128 for the 16-channel decoder layers: 31 us per 26 MB layer)
+  for (int step = 1; step < R; step <<= 1) {
+    __syncthreads();
+    if (r % (2 * step) == 0 && r + step < R && ch < NCH) {
+      const float* o = sh + ((r + step) * CT + cl) * (2 * V + 1);
       const float nb = o[0];
-      if (nb == 0.f) continue;
-      const float na = n, nt = na + nb;
+      if (nb != 0.f) {
+        const float na = n, nt = na + nb;
 #pragma unroll
-      for (int k = 0; k < V; ++k) {
-        const float d = o[1 + k] - mean[k];
-        mean[k] += d * (nb / nt);
-        m2[k] += o[1 + V + k] + d * d * (na * nb / nt);
+        for (int k = 0; k < V; ++k) {
+          const float d = o[1 + k] - mean[k];
+          mean[k] += d * (nb / nt);
+          m2[k] += o[1 + V + k] + d * d * (na * nb / nt);
+        }
+        n = nt;
+        my[0] = n;
+#pragma unroll
+        for (int k = 0; k < V; ++k) { my[1 + k] = mean[k]; my[1 + V + k] = m2[k]; }
       }
-      n = nt;
     }
+  }
+  if (r == 0 && ch < NCH) {
     float* out = partial + (long long)blockIdx.x * 3 * C + ch * V;
 #pragma unroll
     for (int k = 0; k < V; ++k) { out[k] = n; out[C + k] = mean[k]; out[2 * C + k] = m2[k]; }
@@ -410,7 +418,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_vec_kernel(hiseg_bn_bwd_des
 #pragma unroll
     for (int k = 0; k < V; ++k) { mu[k] = d.mean[c + k]; inv[k] = d.invstd[c + k]; }
     if constexpr (MODE == kGReLU || MODE == kGPre) bn_pre_tables<V>(d, c, fs, fh);
-    for (int p = (int)b + r; p < (int)e; p += R) {
+#pragma unroll 4
+    for (int p = (int)b + r; p < (int)e; p += R) {   // (unrolled: four pixels' loads in flight)
       float g[V], z[V];
       ldv<T>(d.z, (long long)p * d.z_cstride + d.z_coff + c, z);
       bn_gv<T, MODE>(d, p, c, g, z, fs, fh);
@@ -424,13 +433,18 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_vec_kernel(hiseg_bn_bwd_des
   float* my = sh + t * 3 * V;
 #pragma unroll
   for (int k = 0; k < V; ++k) { my[k] = s1[k]; my[V + k] = s2[k]; my[2 * V + k] = s3[k]; }
-  __syncthreads();
-  if (r == 0 && ch < NCH) {
-    for (int rr = 1; rr < R; ++rr) {
-      const float* o = sh + (rr * CT + cl) * 3 * V;
+  // pairwise (tree) sum of the R pixel rows, fixed order (was one thread walking R - 1 rows)
+  for (int step = 1; step < R; step <<= 1) {
+    __syncthreads();
+    if (r % (2 * step) == 0 && r + step < R && ch < NCH) {
+      const float* o = sh + ((r + step) * CT + cl) * 3 * V;
 #pragma unroll
       for (int k = 0; k < V; ++k) { s1[k] += o[k]; s2[k] += o[V + k]; s3[k] += o[2 * V + k]; }
+#pragma unroll
+      for (int k = 0; k < V; ++k) { my[k] = s1[k]; my[V + k] = s2[k]; my[2 * V + k] = s3[k]; }
     }
+  }
+  if (r == 0 && ch < NCH) {
     float* out = d.partial + (long long)blockIdx.x * 3 * C + c;
 #pragma unroll
     for (int k = 0; k < V; ++k) { out[k] = s1[k]; out[C + k] = s2[k]; out[2 * C + k] = s3[k]; }

@@ -1126,7 +1126,8 @@ def test_dwconv_lds_tile_bit_identical_to_gather_kernel(shape, monkeypatch):
     once; bf16 stride-1 layers of >= 192 channels) against the register-gather kernel (dwconv_q_kernel,
     HISEG_DWCONV_T=0): bit-identical outputs (same taps, order and epilogue) at ragged tiles and partial channel
     groups, k3 / k5; the fused SE pool and gate within f32 re-association (one partial per tile instead of per strip
-    range), the gate batch-invariant.  Stride-2 layers stay on the gather kernel either way."""
+    range), the gate batch-invariant (the automatic choice's tiled layers).  HISEG_DWCONV_T=2 forces the tiled kernel
+on the stride-2 and narrow layers the automatic choice gives the gather kernel."""
     from hiseg import ops
     N, H, W, C, k, stride = shape
     dt = torch.bfloat16
@@ -1138,17 +1139,17 @@ def test_dwconv_lds_tile_bit_identical_to_gather_kernel(shape, monkeypatch):
     w1, b1 = torch.randn(cr, C, device=DEV, generator=g) * 0.1, torch.randn(cr, device=DEV, generator=g) * 0.1
     w2, b2 = torch.randn(C, cr, device=DEV, generator=g) * 0.1, torch.randn(C, device=DEV, generator=g) * 0.1
     res = {}
-    for mode in ("1", "0"):
+    for mode in ("2", "0"):   # 2: the LDS-tiled kernel for every bf16 layer, stride 2 and narrow ones included
         monkeypatch.setenv("HISEG_DWCONV_T", mode)
         plain = ops.dwconv(A, wd, sc, sh, k, stride, 3).t.clone()
         h, gate = ops.dwconv_se_gate(A, wd, sc, sh, k, stride, 3, w1, b1, w2, b2, 3)
         res[mode] = (plain, h.t.clone(), gate.clone())
     torch.cuda.synchronize()
-    (p1, h1, g1), (p0, h0, g0) = res["1"], res["0"]
+    (p1, h1, g1), (p0, h0, g0) = res["2"], res["0"]
     assert torch.isfinite(p1.float()).all()
     assert torch.equal(p1, p0) and torch.equal(h1, h0) and torch.equal(p1, h1)
     assert (g1 - g0).abs().max().item() < 1e-5
-    if stride != 1 or C < 192:
+    if not (192 <= C < 2048 and (stride == 1 or k == 5)):   # the automatic choice's tiled layers (dw_use_tiles)
         return
     # batch invariance of the pooled gate (tile partials do not depend on the batch): image 0 alone
     monkeypatch.setenv("HISEG_DWCONV_T", "1")
@@ -1195,9 +1196,14 @@ def test_se_two_launch_matches_three_launch_and_f64(case, monkeypatch):
     xm = A.to_nchw().double().mean((2, 3))
     ref_s = torch.sigmoid(F.silu(xm @ w1.double().t() + b1.double()) @ w2.double().t() + b2.double())
     assert (s1.double() - ref_s).abs().max().item() < 1e-5
-    if stride != 1 or C < 192 or N == 1:
-        return
+    # the float4 weight paths are taken by alignment: misaligned copies of W1 / W2 give the same bits
     monkeypatch.setenv("HISEG_SE2", "1")
+    w1u = torch.empty(w1.numel() + 1, device=DEV)[1:].view_as(w1).copy_(w1)
+    w2u = torch.empty(w2.numel() + 1, device=DEV)[1:].view_as(w2).copy_(w2)
+    _, g_u = ops.dwconv_se_gate(A, wd, sc, sh, k, stride, 3, w1u, b1, w2u, b2, 3)
+    assert torch.equal(g_u, g1)
+    if not (192 <= C < 2048 and (stride == 1 or k == 5)) or N == 1:   # tiled layers: batch-independent partials
+        return
     one = ops.Act(A.t[:H * W * A.cstride].clone(), 1, H, W, C, A.cstride, 0)
     _, g_one = ops.dwconv_se_gate(one, wd, sc, sh, k, stride, 3, w1, b1, w2, b2, 3)
     assert torch.equal(g_one[0], g1[0])

@@ -1,5 +1,5 @@
-"""Depthwise conv timing per EfficientNet layer shape (developer tool, GPU): the LDS-tiled kernel (default) vs the
-register-gather kernel (HISEG_DWCONV_T=0), HIP events, algorithmic GB/s (input + output read / written once).
+"""Depthwise conv timing per EfficientNet layer shape (developer tool, GPU): the automatic choice, the LDS-tiled kernel
+forced for every layer (HISEG_DWCONV_T=2) and the register-gather kernel (HISEG_DWCONV_T=0), HIP events, algorithmic GB/s (input + output read / written once).
 
 Usage: python tools/dw_bench.py [--reps 20]"""
 import argparse
@@ -35,7 +35,7 @@ def main():
         Ho, Wo = (H + 2 * (k // 2) - k) // st + 1, (W + 2 * (k // 2) - k) // st + 1
         nbytes = (N * H * W * C + N * Ho * Wo * C) * 2
         row = []
-        for mode in ("1", "0"):
+        for mode in ("1", "2", "0"):
             os.environ["HISEG_DWCONV_T"] = mode
             for _ in range(3):
                 ops.dwconv_se_gate(x, w, sc, sh, k, st, 3, w1, b1, w2, b2, 3)
@@ -46,7 +46,7 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / a.reps
-            row.append(f"{'lds' if mode == '1' else 'gather'} {ms * 1e3:8.1f} us {nbytes / ms / 1e6:7.0f} GB/s")
+            row.append(f"{ {'1': 'auto', '2': 'lds', '0': 'gather'}[mode]} {ms * 1e3:8.1f} us {nbytes / ms / 1e6:7.0f} GB/s")
         print(f"{name:22s} " + "   ".join(row), flush=True)
 
 
