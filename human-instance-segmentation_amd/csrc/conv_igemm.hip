@@ -298,7 +298,10 @@ static int splitk_bco(int cp) { return cp >= 96 && igemm_bco(cp) == 128 ? 128 : 
 
 template <typename T, typename TO>
 static int launch_typed(const ConvArgs& a, hipStream_t s, int splits = 1) {
-  if (splits > 1) {
+  // SE-gated layers as the split-K ones: the narrow 16 / 32 x 256 tiles gather their gated A chunks through
+  // registers (the B7's 480 -> 80 projections over 4 x 80 x 80 at 16 x 256 tiles: 66 us per launch)
+  static const bool gated_wide = [] { const char* e = getenv("HISEG_GATED_WIDE"); return !(e && atoi(e) == 0); }();
+  if (splits > 1 || (gated_wide && a.d.in_scale != nullptr)) {
     if (splitk_bco(a.d.Cout_pad) == 128) return launch_cfg<T, TO, 128, 128, 2, 2>(a, s, splits);
     return launch_cfg<T, TO, 64, 128, 2, 2>(a, s, splits);
   }

@@ -260,14 +260,26 @@ __global__ void __launch_bounds__(256) bn_finalize_par_kernel(const float* parti
   __shared__ double sn[256], sm[256], sq[256];
   const int c = blockIdx.x, t = threadIdx.x;
   double n = 0, mean = 0, m2 = 0;
-  for (int s = t; s < S; s += 256) {
-    const float* p = partial + (long long)s * 3 * C;
-    const double nb = p[c];
-    if (nb == 0) continue;
-    const double d = p[C + c] - mean, nt = n + nb;
-    mean += d * nb / nt;
-    m2 += p[2 * C + c] + d * d * n * nb / nt;
-    n = nt;
+  // a thread's (up to four) partials loaded before its merges: one round of load latency instead of four
+  for (int s0 = t; s0 < S; s0 += 1024) {
+    float pn[4], pm[4], pq[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int s = s0 + 256 * u;
+      const float* p = partial + (long long)(s < S ? s : 0) * 3 * C;
+      pn[u] = s < S ? p[c] : 0.f;
+      pm[u] = p[C + c];
+      pq[u] = p[2 * C + c];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const double nb = pn[u];
+      if (nb == 0) continue;
+      const double d = pm[u] - mean, nt = n + nb;
+      mean += d * nb / nt;
+      m2 += pq[u] + d * d * n * nb / nt;
+      n = nt;
+    }
   }
   sn[t] = n; sm[t] = mean; sq[t] = m2;
   __syncthreads();
@@ -455,9 +467,18 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_par_kernel(hiseg_bn_bwd_d
   __shared__ double a1[256], a2[256], a3[256];
   const int c = blockIdx.x, t = threadIdx.x, C = d.C;
   double s1 = 0, s2 = 0, s3 = 0;
-  for (int s = t; s < S; s += 256) {
-    const float* p = d.partial + (long long)s * 3 * C;
-    s1 += p[c]; s2 += p[C + c]; s3 += p[2 * C + c];
+  for (int s0 = t; s0 < S; s0 += 1024) {   // (up to four partials' loads in flight, then the sums in order)
+    float v1[4], v2[4], v3[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int s = s0 + 256 * u;
+      const float* p = d.partial + (long long)(s < S ? s : 0) * 3 * C;
+      v1[u] = s < S ? p[c] : 0.f;
+      v2[u] = s < S ? p[C + c] : 0.f;
+      v3[u] = s < S ? p[2 * C + c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { s1 += v1[u]; s2 += v2[u]; s3 += v3[u]; }
   }
   a1[t] = s1; a2[t] = s2; a3[t] = s3;
   __syncthreads();
