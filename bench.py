@@ -695,7 +695,13 @@ def call_profile(step, leg=None):
             gbs = c["bytes"] / (c["bytes_ms"] * 1e-3) / 1e9
             row.update(bound="hbm", achieved=round(gbs, 1), peak=PEAK_HBM_GBS, unit="GB/s",
                        frac=round(gbs / PEAK_HBM_GBS, 4), bytes=c["bytes"])
-        meas = load_class_traffic(leg).get(cls) if leg else None
+        legt = load_class_traffic(leg) if leg else {}
+        meas = legt.get(cls)
+        if meas is None and cls in ("conv forward", "conv data gradient"):
+            # one PMC class for both (the same kernels run the forward and the data gradient)
+            both = legt.get("conv forward + data gradient")
+            if both:
+                row["traffic_per_step_fwd_plus_dgrad"] = round(both["hbm_bytes_per_step"])
         if meas:   # PMC-measured HBM bytes of this class per step, and per C-ABI call like `bytes`
             row["traffic_per_step"] = round(meas["hbm_bytes_per_step"])
             row["traffic"] = round(meas["hbm_bytes_per_step"] / c["calls"])
