@@ -708,6 +708,13 @@ def call_profile(step, leg=None):
             if c["bytes"] > 0:
                 row["traffic_over_algorithmic"] = round(meas["hbm_bytes_per_step"] / c["bytes"], 3)
         table[cls] = row
+    both = (load_class_traffic(leg) if leg else {}).get("conv forward + data gradient")
+    if both:   # per call over the forward and data-gradient calls together (the PMC pass cannot tell them apart)
+        convs = [table[k] for k in ("conv forward", "conv data gradient") if k in table]
+        ncalls = sum(r["calls"] for r in convs)
+        for r in convs:
+            r["traffic"] = round(both["hbm_bytes_per_step"] / ncalls) if ncalls else None
+            r["traffic_scope"] = "conv forward + data gradient calls together (one PMC class)"
     out["classes"] = table
     if table:
         cls, row = max(table.items(), key=lambda kv: kv[1]["ms"])
