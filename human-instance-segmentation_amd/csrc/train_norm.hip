@@ -430,8 +430,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_vec_kernel(hiseg_bn_bwd_des
 #pragma unroll
     for (int k = 0; k < V; ++k) { mu[k] = d.mean[c + k]; inv[k] = d.invstd[c + k]; }
     if constexpr (MODE == kGReLU || MODE == kGPre) bn_pre_tables<V>(d, c, fs, fh);
-#pragma unroll 4
-    for (int p = (int)b + r; p < (int)e; p += R) {   // (unrolled: four pixels' loads in flight)
+    // (a four-way unroll here measured slower: 75 -> 91 and 103 -> 146 us on the train step's 256-channel layers)
+    for (int p = (int)b + r; p < (int)e; p += R) {
       float g[V], z[V];
       ldv<T>(d.z, (long long)p * d.z_cstride + d.z_coff + c, z);
       bn_gv<T, MODE>(d, p, c, g, z, fs, fh);

@@ -44,7 +44,7 @@ __device__ __forceinline__ ww_v4s_t ww_tr(unsigned byte_addr) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((ww_lds_v4s_t*)(uintptr_t)byte_addr);
 }
 
-template <int BC, int NW, int PB, int STAGES>
+template <int BC, int NW, int PB, int STAGES, bool BPRE = false>
 __global__ void __launch_bounds__(NW * 64, 1) conv_wgrad_wide_kernel(WgradArgs a) {
   constexpr int BK = 256;
   constexpr int KS = PB / 32;              // 32-pixel k-steps per stage
@@ -232,6 +232,32 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_wgrad_wide_kernel(WgradArgs a
     for (int j = 0; j < TN; ++j) bfr[j] = rdB(0, j);
 #pragma unroll
     for (int i = 0; i < TM; ++i) af[i] = rdA(0, i);
+    if constexpr (BPRE && KS == 2) {
+      // k-step 1's B fragments read into a second set during k-step 0's first rows (two per row), so k-step 1's
+      // first MFMAs do not wait for them; A as before (row i of k-step 1 after row i of k-step 0)
+      static_assert(TN <= 2 * TM, "B prefetch spread");
+      bf16x8_t bnx[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        af[i] = rdA(1, i);
+        if (2 * i < TN) bnx[2 * i] = rdB(1, 2 * i);
+        if (2 * i + 1 < TN) bnx[2 * i + 1] = rdB(1, 2 * i + 1);
+        if (more && i < 2 * NI) issue_part(nxt % STAGES, i);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bnx[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      continue;
+    }
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
 #pragma unroll
@@ -297,10 +323,10 @@ int wgrad_wide_bc(const hiseg_conv2d_desc* d, int Cg, int Kg, int Cin, int M, in
   return Cg % 256 == 0 ? 256 : 0;   // (the 256 x 128 tile measured slower than the 128 x 128 kernel)
 }
 
-template <int BC, int NW, int PB, int STAGES>
+template <int BC, int NW, int PB, int STAGES, bool BPRE = false>
 static int wide_launch(const WgradArgs& a, hipStream_t s) {
   constexpr size_t lds = (size_t)STAGES * (2 + BC / 128) * PB * 256;
-  auto kern = conv_wgrad_wide_kernel<BC, NW, PB, STAGES>;
+  auto kern = conv_wgrad_wide_kernel<BC, NW, PB, STAGES, BPRE>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -320,7 +346,10 @@ int wgrad_wide_try(const WgradArgs& a, hipStream_t s) {
   // same box, tools/wgrad_bench.py.)
   // (32-pixel stages in a 4-deep ring, the same kernel at <256, 4, 32, 4>: 1.229 vs 1.212 ms, same box -- the
   // DMA lookahead is not what holds it at ~0.31 of peak)
-  const int r = wide_launch<256, 4, 64, 2>(a, s);
+  // k-step 1's B fragments prefetched during k-step 0 (1.2075 vs 1.2225 ms on the 256-channel class, same checksum;
+  // HISEG_WGRAD_BPRE=0 restores the late reads for A/B timing)
+  static const int bpre = [] { const char* e = getenv("HISEG_WGRAD_BPRE"); return e ? atoi(e) : 1; }();
+  const int r = bpre ? wide_launch<256, 4, 64, 2, true>(a, s) : wide_launch<256, 4, 64, 2>(a, s);
   return r < 0 ? r : 1;
 }
 
