@@ -1,3 +1,4 @@
+#include <cstdlib>
 // Train-mode BatchNorm, Dropout2d masks and the element-wise backward kernels of the ROI path
 // (gfx950).  All of them are HBM-streaming passes over NHWC activations: f32 arithmetic,
 // storage in the compute dtype, statistics as deterministic per-split partials (no atomics)
@@ -311,7 +312,7 @@ __global__ void __launch_bounds__(256) bn_finalize_par_kernel(const float* parti
 
 // Element-wise passes: block = CT chunk lanes x R pixel rows (as the reductions), blocks stride over pixel
 // rows; 32-bit pixel indices (P < 2^31, checked on the host), no per-element 64-bit division.
-template <typename T>
+template <typename T, int U = 1>
 __global__ void __launch_bounds__(256) bn_apply_vec_kernel(hiseg_bn_apply_desc d) {
   constexpr int V = Chunk<T>::N;
   const int NCH = d.C / V;
@@ -326,25 +327,37 @@ __global__ void __launch_bounds__(256) bn_apply_vec_kernel(hiseg_bn_apply_desc d
   float sc[V], sf[V];
 #pragma unroll
   for (int k = 0; k < V; ++k) { sc[k] = d.per_sample ? 0.f : d.scale[c + k]; sf[k] = d.per_sample ? 0.f : d.shift[c + k]; }
-  for (int p = blockIdx.x * R + r; p < P; p += gridDim.x * R) {
-    float v[V], rr[V];
-    ldv<T>(d.z, (long long)p * d.z_cstride + d.z_coff + c, v);
-    if (d.residual) ldv<T>(d.residual, (long long)p * d.r_cstride + d.r_coff + c, rr);
-    const float* cm = d.chan_mul ? d.chan_mul + (long long)(p / d.HW) * d.C + c : nullptr;
-    if (d.per_sample) {   // LayerNorm2d: the sample's folded tables
-      const long long tb = (long long)(p / d.HW) * d.C + c;
+  // U pixels per iteration, their loads issued together (the pixels and the per-element arithmetic are U = 1's)
+  const int stride = gridDim.x * R;
+  for (int p0 = blockIdx.x * R + r; p0 < P; p0 += U * stride) {
+    float v[U][V], rr[U][V];
 #pragma unroll
-      for (int k = 0; k < V; ++k) { sc[k] = d.scale[tb + k]; sf[k] = d.shift[tb + k]; }
+    for (int u = 0; u < U; ++u) {
+      const int p = p0 + u * stride;
+      if (p >= P) continue;
+      ldv<T>(d.z, (long long)p * d.z_cstride + d.z_coff + c, v[u]);
+      if (d.residual) ldv<T>(d.residual, (long long)p * d.r_cstride + d.r_coff + c, rr[u]);
     }
 #pragma unroll
-    for (int k = 0; k < V; ++k) {
-      float x = v[k] * sc[k] + sf[k];
-      if (d.residual) x += rr[k];
-      x = apply_act(x, d.act, d.act_beta);
-      if (cm) x *= cm[k];
-      v[k] = x;
+    for (int u = 0; u < U; ++u) {
+      const int p = p0 + u * stride;
+      if (p >= P) continue;
+      const float* cm = d.chan_mul ? d.chan_mul + (long long)(p / d.HW) * d.C + c : nullptr;
+      if (d.per_sample) {   // LayerNorm2d: the sample's folded tables
+        const long long tb = (long long)(p / d.HW) * d.C + c;
+#pragma unroll
+        for (int k = 0; k < V; ++k) { sc[k] = d.scale[tb + k]; sf[k] = d.shift[tb + k]; }
+      }
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        float x = v[u][k] * sc[k] + sf[k];
+        if (d.residual) x += rr[u][k];
+        x = apply_act(x, d.act, d.act_beta);
+        if (cm) x *= cm[k];
+        v[u][k] = x;
+      }
+      stv<T>(d.y, (long long)p * d.y_cstride + d.y_coff + c, v[u]);
     }
-    stv<T>(d.y, (long long)p * d.y_cstride + d.y_coff + c, v);
   }
 }
 
@@ -503,7 +516,7 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_par_kernel(hiseg_bn_bwd_d
   }
 }
 
-template <typename T, int MODE>
+template <typename T, int MODE, int U = 1>
 __global__ void __launch_bounds__(256) bn_bwd_apply_vec_kernel(hiseg_bn_bwd_desc d, int S) {
   constexpr int V = Chunk<T>::N;
   const int C = d.C;
@@ -524,22 +537,34 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_vec_kernel(hiseg_bn_bwd_desc
   }
   if constexpr (MODE == kGReLU || MODE == kGPre) bn_pre_tables<V>(d, c, fs, fh);
   const int P = (int)d.P;
-  for (int p = blockIdx.x * R + r; p < P; p += gridDim.x * R) {
-    float g[V], z[V], o[V];
-    ldv<T>(d.z, (long long)p * d.z_cstride + d.z_coff + c, z);
-    bn_gv<T, MODE>(d, p, c, g, z, fs, fh);
+  const int stride = gridDim.x * R;
+  for (int p0 = blockIdx.x * R + r; p0 < P; p0 += U * stride) {
+    float g[U][V], z[U][V];
 #pragma unroll
-    for (int k = 0; k < V; ++k) o[k] = k0[k] * (g[k] - k1[k] - (z[k] - mu[k]) * inv[k] * k2[k]);
-    stv<T>(d.dz, (long long)p * d.dz_cstride + d.dz_coff + c, o);
-    if (d.dres) {
-      const long long off = (long long)p * d.dres_cstride + d.dres_coff + c;
-      if (d.dres_accumulate) {
-        float r[V];
-        ldv<T>(d.dres, off, r);
+    for (int u = 0; u < U; ++u) {   // U pixels' loads together (bn_gv loads dy / y / residual)
+      const int p = p0 + u * stride;
+      if (p >= P) continue;
+      ldv<T>(d.z, (long long)p * d.z_cstride + d.z_coff + c, z[u]);
+      bn_gv<T, MODE>(d, p, c, g[u], z[u], fs, fh);
+    }
 #pragma unroll
-        for (int k = 0; k < V; ++k) g[k] += r[k];
+    for (int u = 0; u < U; ++u) {
+      const int p = p0 + u * stride;
+      if (p >= P) continue;
+      float o[V];
+#pragma unroll
+      for (int k = 0; k < V; ++k) o[k] = k0[k] * (g[u][k] - k1[k] - (z[u][k] - mu[k]) * inv[k] * k2[k]);
+      stv<T>(d.dz, (long long)p * d.dz_cstride + d.dz_coff + c, o);
+      if (d.dres) {
+        const long long off = (long long)p * d.dres_cstride + d.dres_coff + c;
+        if (d.dres_accumulate) {
+          float rv[V];
+          ldv<T>(d.dres, off, rv);
+#pragma unroll
+          for (int k = 0; k < V; ++k) g[u][k] += rv[k];
+        }
+        stv<T>(d.dres, off, g[u]);
       }
-      stv<T>(d.dres, off, g);
     }
   }
 }
@@ -1057,6 +1082,14 @@ using namespace hiseg;
 
 extern "C" int hiseg_bn_partials(void) { return kBnSplits; }
 
+// pixels per iteration of the element-wise BN passes (HISEG_BN_U, read per call: A/B timing; same results).  Two
+// measured no faster (tools/bn_bench.py, profiles/r4_bn_bench.txt: apply 5.1-5.4 TB/s, backward 4.3-4.7 TB/s of
+// algorithmic bytes at U = 1 -- 0.7-0.85 of the ~6.3 TB/s a copy reaches), so U = 1 stays
+static int bn_unroll() {
+  const char* e = getenv("HISEG_BN_U");
+  return e && atoi(e) == 2 ? 2 : 1;
+}
+
 // 16-B chunk path eligibility: channel count, strides and offsets in whole chunks, aligned base.
 static bool vec_ok(int dtype, int C, const void* p, int cs, int coff) {
   const int v = dtype == HISEG_BF16 ? 8 : 4;
@@ -1126,8 +1159,12 @@ extern "C" int hiseg_bn_apply(const hiseg_bn_apply_desc* d, hiseg_stream_t strea
   HISEG_REQUIRE(d->P < (1ll << 31), HISEG_ERR_BAD_SHAPE, "bn_apply: too many pixels");
   if (vec_ok(d->dtype, d->C, d->z, d->z_cstride, d->z_coff) && vec_ok(d->dtype, d->C, d->y, d->y_cstride, d->y_coff) &&
       vec_ok(d->dtype, d->C, d->residual, d->r_cstride, d->r_coff)) {
-    DISPATCH_T(d->dtype, hipLaunchKernelGGL(bn_apply_vec_kernel<T>, vec_grid(d->P, d->C, d->dtype), dim3(256),
-                                            0, (hipStream_t)stream, *d));
+    if (bn_unroll() == 2)
+      DISPATCH_T(d->dtype, hipLaunchKernelGGL((bn_apply_vec_kernel<T, 2>), vec_grid(d->P, d->C, d->dtype), dim3(256),
+                                              0, (hipStream_t)stream, *d));
+    else
+      DISPATCH_T(d->dtype, hipLaunchKernelGGL((bn_apply_vec_kernel<T, 1>), vec_grid(d->P, d->C, d->dtype), dim3(256),
+                                              0, (hipStream_t)stream, *d));
     return hiseg_check_launch("bn_apply");
   }
   DISPATCH_T(d->dtype, hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(ew_blocks(d->P * d->C)), dim3(256), 0,
@@ -1160,7 +1197,10 @@ extern "C" int hiseg_bn_bwd(const hiseg_bn_bwd_desc* d, hiseg_stream_t stream) {
   do {                                                                                                        \
     DISPATCH_T(dt, hipLaunchKernelGGL((bn_bwd_reduce_vec_kernel<T, M>), rgrid, dim3(256), 0, s, *d));         \
     hipLaunchKernelGGL(bn_bwd_finalize_par_kernel, fin_grid(C), dim3(256), 0, s, *d, S);                          \
-    DISPATCH_T(dt, hipLaunchKernelGGL((bn_bwd_apply_vec_kernel<T, M>), agrid, dim3(256), 0, s, *d, S));       \
+    if (bn_unroll() == 2)                                                                                     \
+      DISPATCH_T(dt, hipLaunchKernelGGL((bn_bwd_apply_vec_kernel<T, M, 2>), agrid, dim3(256), 0, s, *d, S));  \
+    else                                                                                                      \
+      DISPATCH_T(dt, hipLaunchKernelGGL((bn_bwd_apply_vec_kernel<T, M, 1>), agrid, dim3(256), 0, s, *d, S));  \
   } while (0)
     switch (mode) {
       case kGNone: BN_BWD_VEC(kGNone); break;

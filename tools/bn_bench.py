@@ -1,122 +1,79 @@
-"""HBM rate of the train-mode BatchNorm passes on the ROI head's shapes (developer tool, GPU).
-
-Times hiseg_bn_stats (+finalize), hiseg_bn_apply and hiseg_bn_bwd (reduce + finalize + apply) with HIP
-events on the launch stream and prints algorithmic GB/s per call (bytes each pass must move once).
-Run under `rocprofv3 --kernel-trace --stats` for the per-kernel split.
-Usage: python tools/bn_bench.py [--reps 20]
-"""
-import argparse
+"""Train-mode BatchNorm element-wise passes at the ROI head's shapes (developer tool, GPU): hiseg_bn_apply (ReLU,
+residual) and hiseg_bn_bwd (ReLU at the pre-activation, residual gradient) with one pixel per thread iteration
+(HISEG_BN_U=1) and two (HISEG_BN_U=2); HIP events, GB/s of algorithmic bytes, bit-identity of the two forms."""
 import ctypes
-import json
 import os
 import sys
 
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "human-instance-segmentation_amd"))
-import torch  # noqa: E402
+import torch
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "human-instance-segmentation_amd"))
 from hiseg import _lib as L  # noqa: E402
 
 DEV = "cuda"
-# name: (P, C, residual)
-SHAPES = {
-    "head256_64x48": (256 * 64 * 48, 256, False),
-    "head256_64x48_res": (256 * 64 * 48, 256, True),
-    "grid128_128x96": (256 * 128 * 96, 128, False),
-    "grid128_128x96_res": (256 * 128 * 96, 128, True),
-    "head64_64x48": (256 * 64 * 48, 64, False),
-}
+SHAPES = [("c256_64x48x256", 256 * 64 * 48, 256), ("c128_128x96x256", 256 * 128 * 96, 128),
+          ("c64_64x48x256", 256 * 64 * 48, 64)]
 
 
-def timed(fn, reps):
-    s = torch.cuda.current_stream()
+def timed(fn, reps=20):
     for _ in range(3):
         fn()
+    torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(s)
+    e0.record()
     for _ in range(reps):
         fn()
-    e1.record(s)
+    e1.record()
     torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / reps
+    return e0.elapsed_time(e1) / reps * 1e3
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--shapes", default=",".join(SHAPES))
-    args = ap.parse_args()
-    lib = L.lib()
-    st = L.stream_ptr()
-    out = {}
-    for name in args.shapes.split(","):
-        P, C, res = SHAPES[name]
-        g = torch.Generator(device=DEV).manual_seed(0)
-        mk = lambda: torch.randn(P * C, device=DEV, generator=g).to(torch.bfloat16)  # noqa: E731
-        z, dy, y = mk(), mk(), mk()
-        r = mk() if res else None
-        dz = torch.empty_like(z)
-        dres = torch.zeros_like(z) if res else None
-        S = lib.hiseg_bn_partials()
-        part = torch.empty((S + 1) * 3 * C, device=DEV)
-        f = lambda: torch.empty(C, device=DEV)  # noqa: E731
-        gamma, beta = torch.ones(C, device=DEV), torch.zeros(C, device=DEV)
-        mean, invstd, scale, shift, dg, db = f(), f(), f(), f(), torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
-        bpe = P * C * 2
-
-        def stats():
-            L.check(lib.hiseg_bn_stats(L.HISEG_BF16, z.data_ptr(), P, C, C, 0, part.data_ptr(), st), "stats")
-            L.check(lib.hiseg_bn_finalize(part.data_ptr(), C, P, gamma.data_ptr(), beta.data_ptr(), 1e-5, 0.1, None,
-                                          None, mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(),
-                                          shift.data_ptr(), st), "finalize")
-        stats()
-
-        ad = L.BnApplyDesc()
-        ad.dtype, ad.P, ad.HW, ad.C = L.HISEG_BF16, P, 64 * 48, C
-        ad.z, ad.z_cstride, ad.z_coff = z.data_ptr(), C, 0
-        ad.scale, ad.shift = scale.data_ptr(), shift.data_ptr()
-        if res:
-            ad.residual, ad.r_cstride, ad.r_coff = r.data_ptr(), C, 0
-        ad.act = L.ACT_RELU
-        ad.y, ad.y_cstride, ad.y_coff = y.data_ptr(), C, 0
-
-        def apply():
-            L.check(lib.hiseg_bn_apply(ctypes.byref(ad), st), "apply")
-
-        bd = L.BnBwdDesc()
-        bd.dtype, bd.P, bd.HW, bd.C = L.HISEG_BF16, P, 64 * 48, C
-        bd.dy, bd.dy_cstride, bd.dy_coff = dy.data_ptr(), C, 0
-        bd.y, bd.y_cstride, bd.y_coff = y.data_ptr(), C, 0
-        bd.z, bd.z_cstride, bd.z_coff = z.data_ptr(), C, 0
-        bd.act = L.ACT_RELU
-        bd.mean, bd.invstd, bd.gamma, bd.beta = mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr()
-        bd.partial = part.data_ptr()
-        bd.dgamma, bd.dbeta, bd.accumulate_params = dg.data_ptr(), db.data_ptr(), 1
-        bd.dz, bd.dz_cstride, bd.dz_coff = dz.data_ptr(), C, 0
-        if res:
-            bd.dres, bd.dres_cstride, bd.dres_coff, bd.dres_accumulate = dres.data_ptr(), C, 0, 0
-        else:
-            bd.fwd_scale, bd.fwd_shift = scale.data_ptr(), shift.data_ptr()
-
-        def bwd():
-            L.check(lib.hiseg_bn_bwd(ctypes.byref(bd), st), "bwd")
-
-        row = {}
-        ms = timed(stats, args.reps)
-        row["stats"] = {"ms": round(ms, 4), "GBps": round(bpe / ms / 1e6, 1)}
-        ms = timed(apply, args.reps)
-        nb = bpe * (3 if res else 2)
-        row["apply"] = {"ms": round(ms, 4), "GBps": round(nb / ms / 1e6, 1)}
-        ms = timed(bwd, args.reps)
-        # reduce: dy, z (+ y when the mask comes from y); apply: dy, z (+y), dz (+dres)
-        nb = bpe * ((3 + 5) if res else (2 + 3))
-        row["bwd"] = {"ms": round(ms, 4), "GBps": round(nb / ms / 1e6, 1)}
-        out[name] = row
-        print(name, json.dumps(row), flush=True)
-        del z, dy, y, r, dz, dres
-        torch.cuda.empty_cache()
-    os.makedirs("gpurun_out", exist_ok=True)
-    with open("gpurun_out/bn_bench.json", "w") as fh:
-        json.dump(out, fh, indent=1)
+    lib, st = L.lib(), L.stream_ptr()
+    for name, P, C in SHAPES:
+        g = torch.Generator(device=DEV).manual_seed(1)
+        mk = lambda: torch.randn(P * C, device=DEV, generator=g).to(torch.bfloat16)   # noqa: E731
+        z, res, dy = mk(), mk(), mk()
+        y, dz, dres = (torch.empty(P * C, device=DEV, dtype=torch.bfloat16) for _ in range(3))
+        scale, shift = torch.rand(C, device=DEV, generator=g) + 0.5, torch.randn(C, device=DEV, generator=g) * 0.1
+        mean, invstd = torch.randn(C, device=DEV, generator=g) * 0.1, torch.rand(C, device=DEV, generator=g) + 0.5
+        gamma, beta = torch.rand(C, device=DEV, generator=g) + 0.5, torch.randn(C, device=DEV, generator=g) * 0.1
+        part = torch.empty((lib.hiseg_bn_partials() + 1) * 3 * C, device=DEV)
+        dgamma, dbeta = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        a = L.BnApplyDesc()
+        a.dtype, a.P, a.HW, a.C = L.HISEG_BF16, P, 64 * 48, C
+        a.z, a.z_cstride, a.z_coff = z, C, 0
+        a.scale, a.shift = scale, shift
+        a.residual, a.r_cstride, a.r_coff = res, C, 0
+        a.act, a.act_beta = 1, 1.0
+        a.y, a.y_cstride, a.y_coff = y, C, 0
+        b = L.BnBwdDesc()
+        b.dtype, b.P, b.HW, b.C = L.HISEG_BF16, P, 64 * 48, C
+        b.dy, b.dy_cstride, b.dy_coff = dy, C, 0
+        b.y, b.y_cstride, b.y_coff = y, C, 0
+        b.z, b.z_cstride, b.z_coff = z, C, 0
+        b.act, b.act_beta = 1, 1.0
+        b.mean, b.invstd, b.gamma, b.beta = mean, invstd, gamma, beta
+        b.partial, b.dgamma, b.dbeta, b.accumulate_params = part, dgamma, dbeta, 0
+        b.dz, b.dz_cstride, b.dz_coff = dz, C, 0
+        b.dres, b.dres_cstride, b.dres_coff, b.dres_accumulate = dres, C, 0, 0
+        b.fwd_scale, b.fwd_shift = scale, shift
+        b.residual, b.r_cstride, b.r_coff = res, C, 0
+        out, outs = [], {}
+        for u in ("1", "2"):
+            os.environ["HISEG_BN_U"] = u
+            fa = lambda: L.check(lib.hiseg_bn_apply(ctypes.byref(a), st), "bn_apply")   # noqa: E731
+            fb = lambda: L.check(lib.hiseg_bn_bwd(ctypes.byref(b), st), "bn_bwd")      # noqa: E731
+            fa()
+            fb()
+            torch.cuda.synchronize()
+            outs[u] = (y.clone(), dz.clone(), dres.clone())
+            ta, tb = timed(fa), timed(fb)
+            ab = P * C * 2 * 3 / ta / 1e3
+            bb = P * C * 2 * 7 / tb / 1e3   # reduce: dy, z, residual; apply: dy, z, residual, write dz, dres
+            out.append(f"U={u}: apply {ta:7.1f} us {ab:6.0f} GB/s  bwd {tb:7.1f} us {bb:6.0f} GB/s")
+        same = all(torch.equal(p, q) for p, q in zip(outs["1"], outs["2"]))
+        print(f"{name:18s} " + " | ".join(out) + f" | identical {same}", flush=True)
 
 
 if __name__ == "__main__":
