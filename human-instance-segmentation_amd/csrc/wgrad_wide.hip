@@ -349,6 +349,11 @@ int wgrad_wide_try(const WgradArgs& a, hipStream_t s) {
   // k-step 1's B fragments prefetched during k-step 0 (1.2075 vs 1.2225 ms on the 256-channel class, same checksum;
   // HISEG_WGRAD_BPRE=0 restores the late reads for A/B timing)
   static const int bpre = [] { const char* e = getenv("HISEG_WGRAD_BPRE"); return e ? atoi(e) : 1; }();
+  // (Counters, profiles/r4_wgrad_counters.txt: the MFMA pipe is busy 33 % of the kernel's cycles; per 64-pixel stage a
+  // wave issues 128 MFMAs and ~270 other VALU, ~140 SALU, 64 LDS and 16 DMA instructions, and waits 26 % of its
+  // cycles at s_waitcnt / the barrier and 29 % issue-stalled -- one wave per SIMD has no partner to fill them.  The
+  // eight-wave form that would give it one still needs 256 VGPRs + 36 spilled for its 128 accumulators plus the
+  // hoisted fragment / DMA addresses, as in round 3.)
   const int r = bpre ? wide_launch<256, 4, 64, 2, true>(a, s) : wide_launch<256, 4, 64, 2>(a, s);
   return r < 0 ? r : 1;
 }
