@@ -283,7 +283,10 @@ def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=6
     if world == 1:   # per-call profile of one eager step, before the graph capture
         step()
         step()
+        # serial teacher for the per-call profile (concurrent branches would overlap the HIP-event intervals)
+        model.concurrent_teacher = False
         prof = call_profile(step, "distill")
+        del model.concurrent_teacher
     graphable = graph and (world == 1 or _backend(dist) == "nccl")
     run = hiseg.GraphedStep(step, lambda: state["opt"]) if graphable else step
     for _ in range(max(warmup, 3 if run is not step else 1)):

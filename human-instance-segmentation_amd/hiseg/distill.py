@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from collections.abc import Mapping
 from typing import Dict, Optional, Tuple
 
@@ -313,7 +314,29 @@ class DistillationUNetWrapper(nn.Module):
             self.teacher.eval()   # the teacher always runs in eval mode (train_distillation_staged.py:270-271)
         return self
 
+    # the frozen teacher's forward and the student's forward are independent until the loss: on a GPU the teacher
+    # runs on a side stream beside the student (both are chains of small kernels that leave most CUs idle; forked
+    # from and joined back into the caller's stream, so a captured HIP graph holds them as parallel branches).
+    # Same kernels, same inputs: the results are the serial order's bit for bit.  HISEG_SERIAL_TEACHER=1: serial.
+    concurrent_teacher = os.environ.get("HISEG_SERIAL_TEACHER", "1") != "1"
+
+    def _side(self, device):
+        st = self.__dict__.get("_teacher_stream")
+        if st is None or st.device != device:
+            st = self.__dict__["_teacher_stream"] = torch.cuda.Stream(device=device)
+        return st
+
     def forward(self, x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        if self.teacher is not None and x.is_cuda and self.concurrent_teacher:
+            main = torch.cuda.current_stream(x.device)
+            side = self._side(x.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                t = self.teacher(x)
+            s = self.student(x)
+            main.wait_stream(side)
+            t.record_stream(main)
+            return s, t
         s = self.student(x)
         if self.teacher is not None:
             t = self.teacher(x)

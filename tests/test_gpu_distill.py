@@ -234,3 +234,42 @@ def test_distill_bf16_progressive_schedule_runs():
         losses.append(loss.item())
     assert all(np.isfinite(losses)), losses
     assert losses[3] < losses[0] and losses[-1] < losses[4], losses
+
+
+@pytest.mark.parametrize("graphed", [False, True])
+def test_concurrent_teacher_stream_equals_serial(graphed, monkeypatch):
+    """The frozen teacher's forward on a side stream beside the student's (DistillationUNetWrapper, forked from and
+    joined into the caller's stream; a captured graph holds both branches) gives the serial order's loss, student
+    gradients and updated parameters bit for bit over three bf16 decoder-only steps, eager and graphed."""
+    import filler
+    import hiseg
+    from hiseg.distill import DistillationUNetWrapper
+    x = torch.from_numpy(filler.normal(41, (2, 3, 128, 128))).to(DEV)
+    _, _, m = __import__("oracle.distill", fromlist=["np_inputs"]).np_inputs(42, 2, 128, 128)
+    m = m.to(DEV)
+    res = {}
+    for conc in (False, True):
+        monkeypatch.setattr(DistillationUNetWrapper, "concurrent_teacher", conc)
+        model, loss_fn = _distill_model(torch.bfloat16)
+        model = model.to(DEV).train()
+        state = {"opt": None}
+
+        def step():
+            s, t = model(x)
+            loss, _ = loss_fn(s, t, m)
+            if state["opt"] is None:
+                state["opt"] = hiseg.FusedAdamW(model.student, lr=1e-3, weight_decay=1e-4, max_grad_norm=1.0,
+                                                params=model.student.get_decoder_parameters())
+            state["opt"].zero_grad()
+            loss.backward()
+            state["opt"].step()
+            return loss
+
+        run = hiseg.GraphedStep(step, lambda: state["opt"]) if graphed else step
+        losses = [run().detach().clone() for _ in range(5 if graphed else 3)]
+        torch.cuda.synchronize()
+        res[conc] = (torch.stack(losses), [p.detach().clone() for p in model.student.parameters()])
+    (l0, p0), (l1, p1) = res[False], res[True]
+    assert torch.isfinite(l0).all()
+    assert torch.equal(l0, l1), (l0, l1)
+    assert all(torch.equal(a, b) for a, b in zip(p0, p1))
