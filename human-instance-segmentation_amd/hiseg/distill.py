@@ -318,7 +318,7 @@ class DistillationUNetWrapper(nn.Module):
     # runs on a side stream beside the student (both are chains of small kernels that leave most CUs idle; forked
     # from and joined back into the caller's stream, so a captured HIP graph holds them as parallel branches).
     # Same kernels, same inputs: the results are the serial order's bit for bit.  HISEG_SERIAL_TEACHER=1: serial.
-    concurrent_teacher = os.environ.get("HISEG_SERIAL_TEACHER", "1") != "1"
+    concurrent_teacher = os.environ.get("HISEG_SERIAL_TEACHER", "0") != "1"
 
     def _side(self, device):
         st = self.__dict__.get("_teacher_stream")
