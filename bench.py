@@ -735,6 +735,9 @@ def call_profile(step, leg=None):
                                  "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "kernel": key,
                                  "launches_timed": cnt, "avg_launch_ms": round(avg, 4), "flop_per_launch": fl,
                                  "share_of_step": round(ms / step_ms, 4) if step_ms > 0 else None}
+        out["top_layers"] = [{"layer": k, "launches": cnt, "ms": round(ms, 3),
+                              "tflops": round(fl * cnt / (ms * 1e-3) / 1e12, 1) if ms > 0 else None}
+                             for k, (cnt, ms, fl) in sorted(groups.items(), key=lambda kv: -kv[1][1])[:10]]
         all_fl = sum(g[2] * g[0] for g in groups.values())
         out["conv_tflops"] = round(all_fl / (conv_ms * 1e-3) / 1e12, 1) if conv_ms > 0 else None
     return out

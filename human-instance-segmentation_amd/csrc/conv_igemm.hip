@@ -286,8 +286,13 @@ static int launch_cfg(const ConvArgs& a, hipStream_t s, int splits) {
 // Tile choice: the widest Cout tile whose overhang past Cout_pad adds <= 1/6 to the MFMA work.
 static int igemm_bco(int cp) {
   auto fits = [&](int bco) { return ((cp + bco - 1) / bco) * bco * 6 <= cp * 7; };
+  auto padded = [&](int bco) { return ((cp + bco - 1) / bco) * bco; };
   if (cp >= 96 && fits(128)) return 128;
   if (cp >= 48 && fits(64)) return 64;
+  // >= 48 columns that fit neither: the 64 / 128 tile with the less overhang (tie: 128), not the narrow 32 / 16 x
+  // 256 tiles -- one or four MFMAs per wave per k-step ran the B1 EnhancedUNet's 72- and 144-channel 3x3 layers
+  // at 53-80 TFLOP/s (tools: bench.py call_profile top_layers, C3)
+  if (cp >= 48) return padded(64) < padded(128) ? 64 : 128;
   if (fits(32)) return 32;
   return 16;
 }
