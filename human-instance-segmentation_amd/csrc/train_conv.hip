@@ -682,12 +682,72 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* ws, int 
   }
 }
 
+// 3x3 single-source layers: one item = (GEMM column j, 4 consecutive input channels) over all 9 taps, so an item's
+// 36 sums are 36 consecutive floats of the reference layout [Cout][Cin][3][3] -- nine 16-B stores -- where the
+// quad-of-K kernel above scatters 4-B stores 9 floats apart (the write traffic of the 768-channel 3x3 layers of the
+// B7 head: 137 us per reduce).  Four split groups per item and the fixed combine order as above.
+__global__ void __launch_bounds__(256) wgrad_reduce_taps_kernel(const float* ws, int splits, hiseg_wgrad_map m,
+                                                                float* gw, float* gb, int acc) {
+  __shared__ float4 red[4][9][64];
+  const int ql = threadIdx.x & 63, sg = threadIdx.x >> 6;
+  const int Cin = m.ca, nc4 = Cin >> 2;
+  const long long idx = (long long)blockIdx.x * 64 + ql;
+  const bool live = idx < (long long)m.Cout * nc4;
+  const int j = live ? (int)(idx / nc4) : 0;
+  const int ci0 = live ? 4 * (int)(idx - (long long)j * nc4) : 0;
+  const long long plane = (long long)m.Cg * m.Kg;
+  const float* src = ws + (long long)j * m.Kg + ci0;
+  float4 t9[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) t9[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (live) {
+    for (int sp = sg; sp < splits; sp += 4) {
+      float4 a[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) a[t] = *reinterpret_cast<const float4*>(src + sp * plane + t * Cin);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) { t9[t].x += a[t].x; t9[t].y += a[t].y; t9[t].z += a[t].z; t9[t].w += a[t].w; }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 9; ++t) red[sg][t][ql] = t9[t];
+  __syncthreads();
+  if (sg != 0 || !live) return;
+  auto add4 = [](float4 x, float4 y) { return make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w); };
+  float o[36];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const float4 v = add4(add4(red[0][t][ql], red[1][t][ql]), add4(red[2][t][ql], red[3][t][ql]));
+    o[t] = v.x; o[9 + t] = v.y; o[18 + t] = v.z; o[27 + t] = v.w;   // [channel][tap]
+  }
+  float4* dst = reinterpret_cast<float4*>(gw + ((long long)j * Cin + ci0) * 9);
+#pragma unroll
+  for (int q = 0; q < 9; ++q) {
+    float4 v = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+    if (acc) v = add4(dst[q], v);
+    dst[q] = v;
+  }
+  if (m.want_bias && gb && ci0 == 0) {   // the GEMM-bias column (k = 9 Cin), splits in order
+    float b = 0.f;
+    for (int sp = 0; sp < splits; ++sp) b += ws[sp * plane + (long long)j * m.Kg + 9 * Cin];
+    gb[j] = acc ? gb[j] + b : b;
+  }
+}
+
 extern "C" int hiseg_conv2d_wgrad_reduce(const float* ws, int splits, const hiseg_wgrad_map* map, float* gw, float* gb,
                                          int accumulate, hiseg_stream_t stream) {
   HISEG_REQUIRE(ws && map && gw && splits > 0, HISEG_ERR_BAD_ARG, "wgrad_reduce: null argument");
   const hiseg_wgrad_map m = *map;
   HISEG_REQUIRE(!m.convT || m.Cout % 4 == 0, HISEG_ERR_BAD_SHAPE, "wgrad_reduce: convT Cout");
   HISEG_REQUIRE(m.Kg % 4 == 0 && al16(ws), HISEG_ERR_BAD_SHAPE, "wgrad_reduce: partial rows must be 16-B aligned");
+  const char* te = getenv("HISEG_WGRAD_REDUCE_TAPS");   // 0: the quad-of-K kernel (A/B, the equivalence test)
+  const bool taps_ok = !(te && atoi(te) == 0);
+  if (taps_ok && !m.convT && m.KH == 3 && m.KW == 3 && m.cb == 0 && m.ca == m.ca_real && m.ca % 4 == 0 && al16(gw)) {
+    const long long items = (long long)m.Cout * (m.ca / 4);
+    hipLaunchKernelGGL(wgrad_reduce_taps_kernel, dim3((unsigned)((items + 63) / 64)), dim3(256), 0,
+                       (hipStream_t)stream, ws, splits, m, gw, gb, accumulate);
+    return hiseg_check_launch("wgrad_reduce");
+  }
   const long long n = (long long)m.Cout * ((m.KH * m.KW * (m.ca + m.cb) + (m.want_bias ? 1 : 0) + 3) / 4);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, (hipStream_t)stream, ws,
                      splits, m, gw, gb, accumulate);
