@@ -763,30 +763,32 @@ __device__ __forceinline__ int real_channel(const hiseg_pack_entry& e, int cp) {
 
 __global__ void __launch_bounds__(256) pack_weights_kernel(const hiseg_pack_entry* table) {
   const hiseg_pack_entry e = table[blockIdx.y];
-  for (long long idx = (long long)blockIdx.x * 256 + threadIdx.x; idx < e.total; idx += (long long)gridDim.x * 256) {
+  // 32-bit element indices (total is an int): the 64-bit divisions of the index decomposition were software
+  // routines that made this launch 0.9 ms of the B7 train step
+  for (int idx = blockIdx.x * 256 + threadIdx.x; idx < e.total; idx += gridDim.x * 256) {
     int row, k;
     const int cinp = e.ca + e.cb;
     const int mode = e.mode & 7;
     if (e.mode & HISEG_PACK_FRAG) {   // fragment order: idx = (((((ct*ncb + cb)*taps + tap)*2 + s)*4 + lg)*16 + r)*8 + el
       const int kc = mode == 0 ? cinp : e.cop;   // K channels per tap
       const int taps = e.KH * e.KW, ncb = kc >> 6;
-      long long t = idx;
-      const int el = (int)(t & 7); t >>= 3;
-      const int r = (int)(t & 15); t >>= 4;
-      const int lg = (int)(t & 3); t >>= 2;
-      const int s = (int)(t & 1); t >>= 1;
-      const int tap = (int)(t % taps); t /= taps;
-      const int cb = (int)(t % ncb);
-      const int ct = (int)(t / ncb);
+      int t = idx;
+      const int el = t & 7; t >>= 3;
+      const int r = t & 15; t >>= 4;
+      const int lg = t & 3; t >>= 2;
+      const int s = t & 1; t >>= 1;
+      const int tap = t % taps; t /= taps;
+      const int cb = t % ncb;
+      const int ct = t / ncb;
       row = ct * 16 + r;
       k = tap * kc + cb * 64 + s * 32 + lg * 8 + el;
     } else {
-      row = (int)(idx / e.K_pad);
-      k = (int)(idx - (long long)row * e.K_pad);
+      row = idx / e.K_pad;
+      k = idx - row * e.K_pad;
     }
     float v = 0.f;
     if (mode == HISEG_PACK_BIAS) {  // bias -> f32 epilogue shift, replicated per ConvTranspose sub-pixel block
-      v = e.src[idx % e.Cout];
+      v = e.src[idx % e.Cout];   // (32-bit)
     } else if (mode == 0) {     // conv forward: [co][tap*cinp + cp]
       if (row < e.Cout && k < e.KH * e.KW * cinp) {
         const int tap = k / cinp, ci = real_channel(e, k - tap * cinp);
