@@ -763,8 +763,8 @@ __device__ __forceinline__ int real_channel(const hiseg_pack_entry& e, int cp) {
 
 __global__ void __launch_bounds__(256) pack_weights_kernel(const hiseg_pack_entry* table) {
   const hiseg_pack_entry e = table[blockIdx.y];
-  // 32-bit element indices (total is an int): the 64-bit divisions of the index decomposition were software
-  // routines that made this launch 0.9 ms of the B7 train step
+  // 32-bit element indices (total is an int; the 64-bit divisions were software routines -- measured no faster:
+  // the launch, 0.9 ms of the B7 train step, is bound by the gathered / transposed f32 reads of the dgrad layouts)
   for (int idx = blockIdx.x * 256 + threadIdx.x; idx < e.total; idx += gridDim.x * 256) {
     int row, k;
     const int cinp = e.ca + e.cb;
