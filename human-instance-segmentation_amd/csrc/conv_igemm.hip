@@ -327,7 +327,16 @@ static int launch_typed(const ConvArgs& a, hipStream_t s, int splits = 1) {
 // Cout_pad f32.
 static int splitk_plan(const ConvArgs& a) {
   const hiseg_conv2d_desc& d = a.d;
-  if (d.dtype != HISEG_BF16 || d.KH != 1 || d.KW != 1 || d.convT || a.nK < 6) return 1;
+  if (d.dtype != HISEG_BF16 || d.convT || a.nK < 6) return 1;
+  // 3x3 layers over images of <= 256 pixels with long K (the B7 EnhancedUNet's 768-channel 3x3 pair over 16 x 12:
+  // the halo kernel gets one 16 x 16 tile per image x 6 Cout tiles = 48 workgroups, 118 TFLOP/s): nK / 4 splits,
+  // 2..8, on the generic kernel (per-image grid and layer only, as below)
+  if (d.KH == 3 && d.KW == 3 && d.stride == 1 && d.a_up == 1 && (long long)d.Ho * d.Wo <= 256 && a.nK >= 24 &&
+      d.in_scale == nullptr) {
+    int sp = a.nK / 4;
+    return sp > 8 ? 8 : sp;
+  }
+  if (d.KH != 1 || d.KW != 1) return 1;
   // ungated layers take the LDS-DMA ring kernel (conv_fast.hip), which keeps more K blocks in flight: only long
   // K loops split there (the 384 -> 2304 expansion over 4 x 20 x 20 pixels: 17 us unsplit, 31 us split in two)
   if (d.in_scale == nullptr && a.nK < 24) return 1;
@@ -380,7 +389,7 @@ static bool release_variant(int v) {
 
 // Workspace bytes the automatic choice uses for this layer (split-K generic kernel), 0 when it needs none.
 extern "C" long long hiseg_conv2d_workspace_bytes(const hiseg_conv2d_desc* d) {
-  if (d == nullptr || d->dtype != HISEG_BF16 || d->KH != 1 || d->KW != 1 || d->convT || d->N <= 0) return 0;
+  if (d == nullptr || d->dtype != HISEG_BF16 || d->convT || d->N <= 0) return 0;
   const long long M = (long long)d->N * d->Ho * d->Wo;
   if (M >= (1ll << 31) || d->K_pad % 64) return 0;
   ConvArgs a;

@@ -321,9 +321,11 @@ def conv2d(p: ConvPlan, xa: Act, xb: Optional[Act] = None, out: Optional[Act] = 
     if p.weight_frag is not None:
         d.weight_frag = p.weight_frag
     ws = None
-    if p.kh * p.kw == 1 and p.k_pad >= 384 and dt == torch.bfloat16 and not p.convT:
-        # small-grid, long-K 1x1 layers (the EfficientNet's deep SE-gated projections) split their K loop over
-        # workgroups into this stream-ordered workspace (hiseg_conv2d_workspace_bytes: 0 when the layer does not)
+    if dt == torch.bfloat16 and not p.convT and ((p.kh * p.kw == 1 and p.k_pad >= 384) or
+                                                 (p.kh * p.kw == 9 and p.k_pad >= 1536 and d.Ho * d.Wo <= 256)):
+        # small-grid, long-K 1x1 layers (the EfficientNet's deep SE-gated projections) and 3x3 layers over images of
+        # <= 256 pixels split their K loop over workgroups into this stream-ordered workspace
+        # (hiseg_conv2d_workspace_bytes: 0 when the layer does not)
         nbytes = L.lib().hiseg_conv2d_workspace_bytes(ctypes.byref(d))
         if nbytes > 0:
             ws = torch.empty(nbytes, dtype=torch.uint8, device=xa.t.device)

@@ -39,8 +39,10 @@ _P = ctypes.c_void_p
 _DGRAD_VARIANT = int(os.environ.get("HISEG_DGRAD_VARIANT", "0"))
 
 
-def _dgrad_launch(dg) -> int:
+def _dgrad_launch(dg, device=None) -> int:
     lib = L.lib()
+    if device is not None:
+        _splitk_workspace(dg, dg.KH, dg.KW, device)
     if _DGRAD_VARIANT:
         return lib.hiseg_conv2d_fwd_variant(ctypes.byref(dg), _DGRAD_VARIANT, _stream())
     return lib.hiseg_conv2d_fwd(ctypes.byref(dg), _stream())
@@ -381,8 +383,18 @@ def conv_fwd(S: TrainState, p: TConv, xa: Act, xb: Optional[Act] = None, *, act=
     if out is None:
         out = Act.new(xa.N, oH, oW, p.cout, out_dtype or xa.dtype, xa.t.device)
     d = _desc(S, p, xa, xb, out, act=act, out2=out2)
+    _splitk_workspace(d, p.kh, p.kw, xa.t.device)
     _chk(L.lib().hiseg_conv2d_fwd(ctypes.byref(d), _stream()), "conv2d(train)")
     return out, d
+
+
+def _splitk_workspace(d: L.Conv2dDesc, kh: int, kw: int, device) -> None:
+    """The split-K workspace of a small-image, long-K 3x3 layer (hiseg_conv2d_workspace_bytes; stream-ordered, held
+    by the descriptor until the launch is enqueued)."""
+    if kh == 3 and kw == 3 and d.Ho * d.Wo <= 256 and d.K_pad >= 1536 and d.dtype == L.HISEG_BF16 and not d.convT:
+        nbytes = L.lib().hiseg_conv2d_workspace_bytes(ctypes.byref(d))
+        if nbytes > 0:
+            d.workspace, d.workspace_bytes = torch.empty(nbytes, dtype=torch.uint8, device=device), nbytes
 
 
 def _needs_wgrad(p: TConv) -> bool:
@@ -448,12 +460,12 @@ def conv_bwd(T: Tape, p: TConv, d: L.Conv2dDesc, xa: Act, xb: Optional[Act], dz:
         if acc:
             dg.residual, dg.r_cstride, dg.r_coff = gx, gx.cstride, gx.coff
         dg.out, dg.o_cstride, dg.o_coff = gx, gx.cstride, gx.coff
-        _chk(_dgrad_launch(dg), "conv2d(dgrad)")
+        _chk(_dgrad_launch(dg, dz.t.device), "conv2d(dgrad)")
         T.mark(xa)
     else:
         tmp = Act.new(xa.N, xa.H, xa.W, p.ca + p.cb, dz.dtype, dz.t.device, cpad=p.ca + p.cb, zero=False)
         dg.out, dg.o_cstride, dg.o_coff = tmp, tmp.cstride, 0
-        _chk(_dgrad_launch(dg), "conv2d(dgrad)")
+        _chk(_dgrad_launch(dg, dz.t.device), "conv2d(dgrad)")
         for src_act, off, c in ((xa, 0, p.ca), (xb, p.ca, p.cb)):
             g, acc = T.grad(src_act)
             part = tmp.slice(off, c)

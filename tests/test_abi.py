@@ -65,7 +65,7 @@ def test_release_library_refuses_diagnostic_conv_variants():
     from hiseg import _lib as L
     d = L.Conv2dDesc()
     d.dtype = d.out_dtype = 1  # bf16
-    d.N, d.H, d.W, d.Ho, d.Wo = 1, 16, 16, 16, 16
+    d.N, d.H, d.W, d.Ho, d.Wo = 1, 32, 32, 32, 32   # (> 256 pixels per image: the 3x3 split-K plan does not apply)
     d.KH, d.KW, d.stride, d.pad = 3, 3, 1, 1
     fake = 1 << 20
     with L.raw_pointers():   # never launched: the library refuses the variant first
@@ -114,7 +114,10 @@ def test_conv_splitk_workspace_plan_is_batch_invariant():
     assert ws(4, 80, 80, 480, 80) == 0           # > 1600 pixels per image: unsplit
     assert ws(4, 20, 20, 384, 2304, gated=False) == 0   # ungated, short K: the LDS-DMA ring kernel
     assert ws(4, 20, 20, 288, 48) == 0           # the 10-k-step pointwise kernel takes it
-    assert ws(4, 20, 20, 2304, 384, k=3) == 0    # 3x3: never split
+    assert ws(4, 20, 20, 2304, 384, k=3) == 0    # 3x3 over 400-pixel images: never split
+    for N in (1, 8):                              # 3x3 over <= 256-pixel images with K >= 1536: nK / 4 splits (<= 8)
+        assert ws(N, 16, 12, 768, 768, gated=False, k=3) == N * 8 * 16 * 12 * 768 * 4
+    assert ws(4, 16, 12, 64, 64, gated=False, k=3) == 0   # short K
 
 
 def test_descriptor_holds_plain_tensors_and_activation_views():
