@@ -240,6 +240,16 @@ def train_bench(device, dtype, rank, world, dist, steps, warmup, preset=None, ba
     return out
 
 
+def _release_leg():
+    """Between legs: collect the finished leg's graphs / closures (reference cycles keep a GraphedStep, its captured
+    graph and that graph's private memory pool alive until the cyclic collector runs), then return the cached
+    blocks.  Without it a leg measured 7-40 % slower after another leg in the same process than alone."""
+    import gc
+    torch.cuda.synchronize()
+    gc.collect()
+    torch.cuda.empty_cache()
+
+
 def _backend(dist):
     return dist.get_backend() if dist else None
 
@@ -291,6 +301,16 @@ def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=6
     run = hiseg.GraphedStep(step, lambda: state["opt"]) if graphable else step
     for _ in range(max(warmup, 3 if run is not step else 1)):
         loss = run()
+    if os.environ.get("HISEG_BENCH_STEP_TIMES") == "1":   # developer knob: per-replay times on stderr
+        ts = []
+        for _ in range(8):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            run()
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(round(e0.elapsed_time(e1), 2))
+        print(f"distill per-replay ms: {ts}", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -858,25 +878,32 @@ def main():
         args.train_only, args.no_train = True, True
         out["distill"] = distill_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2,
                                        graph=not args.eager_train)
+    distill_first = None
     if not args.train_only:
         out = infer_bench(args, device, dtype, rank, world, dist)
+    if not args.no_distill and not args.train_only and not args.distill_only:
+        # the distillation leg right after the inference leg: its step forks the teacher onto a side stream, and its
+        # replays measured 9.5-10 ms alone or after the inference leg but 13.5-17 ms after the train legs in the same
+        # process (tools/stream_probe.py, HISEG_BENCH_STEP_TIMES=1); the inference leg, first, measured 8 % slower
+        # after the distillation leg
+        _release_leg()
+        distill_first = distill_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2,
+                                      graph=not args.eager_train)
     if not args.no_train:
-        torch.cuda.empty_cache()
+        _release_leg()
         out["train"] = train_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), max(2, args.warmup),
                                    local_first=True, graph_train=not args.eager_train)
         if not args.no_presets:
-            torch.cuda.empty_cache()
+            _release_leg()
             out["train_c3"] = train_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2, preset="b1",
                                           batch=32, rois_per_img=1, hw=(640, 640), graph_train=not args.eager_train)
-            torch.cuda.empty_cache()
+            _release_leg()
             out["train_c4"] = train_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2, preset="b7",
                                           batch=8, rois_per_img=1, hw=(640, 640), graph_train=not args.eager_train)
-    if not args.no_distill and not args.train_only:
-        torch.cuda.empty_cache()
-        out["distill"] = distill_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2,
-                                       graph=not args.eager_train)
+    if distill_first is not None:
+        out["distill"] = distill_first
     if not args.train_only and world == 1:
-        torch.cuda.empty_cache()
+        _release_leg()
         out["eval"] = eval_bench(device)
         out["datapath"] = data_bench(device)
     if rank == 0:

@@ -328,9 +328,10 @@ static int launch_typed(const ConvArgs& a, hipStream_t s, int splits = 1) {
 static int splitk_plan(const ConvArgs& a) {
   const hiseg_conv2d_desc& d = a.d;
   if (d.dtype != HISEG_BF16 || d.convT || a.nK < 6) return 1;
-  // 3x3 layers over images of <= 256 pixels with long K (the B7 EnhancedUNet's 768-channel 3x3 pair over 16 x 12:
+  // 3x3 layers over images of <= 256 pixels with long K (the B7 EnhancedUNet's 768-channel 3x3 pair over 8 x 16 x 12:
   // the halo kernel gets one 16 x 16 tile per image x 6 Cout tiles = 48 workgroups, 118 TFLOP/s): nK / 4 splits,
-  // 2..8, on the generic kernel (per-image grid and layer only, as below)
+  // 2..8, on the generic kernel -- when the caller passes the workspace (the train engine does for <= 8192 pixels in
+  // all; a large batch of such images fills the GPU on the halo kernel)
   if (d.KH == 3 && d.KW == 3 && d.stride == 1 && d.a_up == 1 && (long long)d.Ho * d.Wo <= 256 && a.nK >= 24 &&
       d.in_scale == nullptr) {
     int sp = a.nK / 4;

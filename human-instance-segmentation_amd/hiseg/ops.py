@@ -276,11 +276,13 @@ def fold_affine(cout: int, bias: Optional[torch.Tensor], bn, device):
 def conv2d(p: ConvPlan, xa: Act, xb: Optional[Act] = None, out: Optional[Act] = None, *, a_up: int = 1,
            residual: Optional[Act] = None, mul: Optional[Act] = None, out2: Optional[Act] = None,
            in_scale: Optional[torch.Tensor] = None, out_dtype: Optional[torch.dtype] = None,
-           variant: int = 0, out_cpad: Optional[int] = None) -> Act:
+           variant: int = 0, out_cpad: Optional[int] = None, split_k_3x3: bool = False) -> Act:
     """hiseg_conv2d_fwd.  Returns the output Act (allocated when ``out`` is None; ``out_cpad``: its channel
     stride, the pad channels zero).
 
-    ``variant`` != 0 forces a kernel variant (hiseg_conv2d_fwd_variant; -1 = generic kernel).
+    ``variant`` != 0 forces a kernel variant (hiseg_conv2d_fwd_variant; -1 = generic kernel).  ``split_k_3x3``
+    passes the split-K workspace to a 3x3 layer too (images of <= 256 pixels, K >= 1536: the library then splits
+    its K loop; the train engine's small-batch choice, off on the inference path).
     """
     dt = xa.dtype
     H, W = xa.H * a_up, xa.W * a_up
@@ -322,10 +324,11 @@ def conv2d(p: ConvPlan, xa: Act, xb: Optional[Act] = None, out: Optional[Act] = 
         d.weight_frag = p.weight_frag
     ws = None
     if dt == torch.bfloat16 and not p.convT and ((p.kh * p.kw == 1 and p.k_pad >= 384) or
-                                                 (p.kh * p.kw == 9 and p.k_pad >= 1536 and d.Ho * d.Wo <= 256)):
-        # small-grid, long-K 1x1 layers (the EfficientNet's deep SE-gated projections) and 3x3 layers over images of
-        # <= 256 pixels split their K loop over workgroups into this stream-ordered workspace
-        # (hiseg_conv2d_workspace_bytes: 0 when the layer does not)
+                                                 (split_k_3x3 and p.kh * p.kw == 9)):
+        # small-grid, long-K 1x1 layers (the EfficientNet's deep SE-gated projections) split their K loop over
+        # workgroups into this stream-ordered workspace (hiseg_conv2d_workspace_bytes: 0 when the layer does not).
+        # (The 3x3 small-image split is the train engine's alone: it pays only for a small batch, and the inference
+        # path's kernel choice must not depend on the batch.)
         nbytes = L.lib().hiseg_conv2d_workspace_bytes(ctypes.byref(d))
         if nbytes > 0:
             ws = torch.empty(nbytes, dtype=torch.uint8, device=xa.t.device)

@@ -389,9 +389,12 @@ def conv_fwd(S: TrainState, p: TConv, xa: Act, xb: Optional[Act] = None, *, act=
 
 
 def _splitk_workspace(d: L.Conv2dDesc, kh: int, kw: int, device) -> None:
-    """The split-K workspace of a small-image, long-K 3x3 layer (hiseg_conv2d_workspace_bytes; stream-ordered, held
-    by the descriptor until the launch is enqueued)."""
-    if kh == 3 and kw == 3 and d.Ho * d.Wo <= 256 and d.K_pad >= 1536 and d.dtype == L.HISEG_BF16 and not d.convT:
+    """The split-K workspace of a small-image, long-K 3x3 layer over a small batch (<= 8192 pixels in all: the B7
+    EnhancedUNet's 768-channel pair over 8 x 16 x 12; the ROI heads' 16 x 12 levels over 256 ROIs fill the GPU on
+    the halo kernel and would move 400 MB of partials) -- hiseg_conv2d_workspace_bytes; stream-ordered, held by
+    the descriptor until the launch is enqueued.  Without a workspace the library does not split."""
+    if (kh == 3 and kw == 3 and d.Ho * d.Wo <= 256 and d.N * d.Ho * d.Wo <= 8192 and d.K_pad >= 1536 and
+            d.dtype == L.HISEG_BF16 and not d.convT):
         nbytes = L.lib().hiseg_conv2d_workspace_bytes(ctypes.byref(d))
         if nbytes > 0:
             d.workspace, d.workspace_bytes = torch.empty(nbytes, dtype=torch.uint8, device=device), nbytes

@@ -924,8 +924,7 @@ def test_conv_hwr_bit_identical_to_halo_kernel(name):
         assert torch.equal(ys[v], y82), v
     for v in (96, 97):            # kx-major taps with B reuse: variant 86's
         assert torch.equal(ys[v], y86), v
-    if H * W > 256 or Cin * 9 < 1536:   # (smaller images with K >= 1536 take the split-K generic kernel)
-        assert torch.equal(auto, ys[97])   # the automatic choice takes variant 97
+    assert torch.equal(auto, ys[97])   # the automatic choice takes variant 97
 
 
 @pytest.mark.parametrize("shape", [(2, 64, 0, 64, 64, 48, True), (3, 64, 0, 64, 21, 37, False), (2, 128, 0, 64, 16, 33, True),
@@ -955,11 +954,7 @@ def test_conv_hwr_wide_tile_bit_identical(shape):
     torch.cuda.synchronize()
     assert torch.isfinite(y100.float()).all()
     assert torch.equal(y100, ref)
-    if H * W <= 256 and 9 * (Ca + Cb) >= 1536:   # the automatic choice splits K on the generic kernel
-        assert ((auto.float() - ref.float()).abs().max() / ref.float().abs().max()).item() < 8e-3
-        if Cout % 128 == 0:
-            assert torch.equal(y97, ref) and torch.equal(y101, ref)
-    elif Cout % 128 == 0:
+    if Cout % 128 == 0:
         assert torch.equal(y97, ref) and torch.equal(y101, ref)
         assert torch.equal(auto, y97)
     else:
@@ -1088,9 +1083,7 @@ def test_conv_automatic_choice_within_bf16(name):
     # the halo kernel also takes two-source layers whose sources are whole 32-channel slices (round 2 v10)
     halo = (not convT and k == 3 and Cb % 32 == 0 and not mul and not o2 and Cout % 128 == 0 and Ca % 32 == 0
             and Ca >= 64)
-    # 3x3 layers over images of <= 256 pixels with K >= 1536: the generic kernel split over K (other f32 order)
-    splitk = not convT and k == 3 and H * W <= 256 and 9 * (Ca + Cb) >= 1536
-    if halo or splitk:
+    if halo:
         assert ((y - ref).abs().max() / ref.abs().max()).item() < 8e-3
     else:
         assert torch.equal(y, ref)
@@ -1123,8 +1116,7 @@ def test_conv_hwt_bit_identical_to_hwr(shape):
     torch.cuda.synchronize()
     assert torch.isfinite(outs[97].float()).all()
     assert torch.equal(outs[103], outs[97])
-    if H * W > 256:   # (images of <= 256 pixels with K >= 1536 take the split-K generic kernel automatically)
-        assert torch.equal(outs[0], outs[97])
+    assert torch.equal(outs[0], outs[97])
 
 
 @pytest.mark.parametrize("shape", [(2, 37, 45, 240, 5, 1), (3, 20, 20, 2304, 5, 1), (2, 33, 47, 144, 3, 2),
@@ -1255,9 +1247,9 @@ def test_roi_align_whole_pixel_stores_bit_identical(dt, monkeypatch):
 @pytest.mark.parametrize("shape", [(3, 768, 768, 16, 12, True), (2, 256, 256, 12, 10, False), (5, 192, 384, 8, 8, True)])
 def test_conv3x3_small_image_splitk(shape):
     """3x3 layers over images of <= 256 pixels with K >= 1536 (the B7 EnhancedUNet's 768-channel pair at 16 x 12)
-    split their K loop over workgroups on the generic kernel (hiseg_conv2d_workspace_bytes > 0): against the halo
-    kernel (variant 97) within bf16 rounding and against float32 torch, and batch-invariant bit for bit (the plan
-    depends on the per-image grid only)."""
+    split their K loop over workgroups on the generic kernel when the caller passes the workspace (the train engine
+    does for small batches; hiseg_conv2d_workspace_bytes > 0): against the halo kernel (variant 97) within bf16
+    rounding and against float32 torch, and batch-invariant bit for bit (the split depends on the per-image grid)."""
     from hiseg import ops
     N, Ci, Co, H, W, res = shape
     dt = torch.bfloat16
@@ -1268,7 +1260,7 @@ def test_conv3x3_small_image_splitk(shape):
     b = torch.randn(Co, device=DEV, generator=g) * 0.1
     p = ops.pack_conv(w, b, None, 1, dt, DEV, pad=1)
     R = ops.Act.from_nchw(torch.randn(N, Co, H, W, device=DEV, generator=g), dt) if res else None
-    out = ops.conv2d(p, xa, residual=R).to_nchw().float()
+    out = ops.conv2d(p, xa, residual=R, split_k_3x3=True).to_nchw().float()
     ref = F.conv2d(x.to(dt).float(), w.to(dt).float(), b, padding=1)
     if res:
         ref = ref + R.to_nchw().float()
@@ -1279,5 +1271,5 @@ def test_conv3x3_small_image_splitk(shape):
         assert _rel(out.cpu(), h.cpu()) < 1e-2
     one = ops.Act.from_nchw(x[:1].contiguous(), dt)
     R1 = ops.Act.from_nchw(R.to_nchw()[:1].contiguous(), dt) if res else None
-    o1 = ops.conv2d(p, one, residual=R1).to_nchw()
-    assert torch.equal(o1[0], ops.conv2d(p, xa, residual=R).to_nchw()[0])
+    o1 = ops.conv2d(p, one, residual=R1, split_k_3x3=True).to_nchw()
+    assert torch.equal(o1[0], ops.conv2d(p, xa, residual=R, split_k_3x3=True).to_nchw()[0])
