@@ -88,7 +88,9 @@ class GraphedStep:
             # the optimizer or the model's flat layout / packing table was re-allocated since the capture
             self.graph, self.calls = None, 1
         if self.calls <= self.eager:
-            s = torch.cuda.Stream()
+            s = self.__dict__.get("_warm")   # one warm-up side stream per instance (not one per eager call)
+            if s is None:
+                s = self._warm = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
                 out = self.fn()
