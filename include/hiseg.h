@@ -133,8 +133,10 @@ typedef struct hiseg_conv2d_desc {
   const void* weight_frag;
   float act_beta;           /* Swish beta (act == HISEG_ACT_SWISH); ignored otherwise        */
   /* Optional caller workspace (device memory, stream-ordered like the operands): the automatic
-   * choice splits the K loop of a small-grid 1x1 layer over workgroups when it holds at least
-   * hiseg_conv2d_workspace_bytes(d) bytes; null keeps every layer unsplit. */
+   * choice splits the K loop of a small-grid 1x1 layer -- or of a 3x3 layer over images of <= 256
+   * pixels with K >= 1536 -- over workgroups when it holds at least hiseg_conv2d_workspace_bytes(d)
+   * bytes; null keeps every layer unsplit.  The plan depends on the layer and the per-image grid only;
+   * whether to pass a workspace for a 3x3 layer is the caller's choice (it pays for small batches). */
   void* workspace; long long workspace_bytes;
 } hiseg_conv2d_desc;
 int hiseg_conv2d_fwd(const hiseg_conv2d_desc* d, hiseg_stream_t stream);
