@@ -1,3 +1,4 @@
+#include <cstdlib>
 // Training kernels of the refined hierarchical head's non-conv ops (gfx950):
 //   * SpatialAttentionModule (attention_modules.py:67-113) train forward (+ Dropout2d) / backward
 //   * ChannelAttentionModule (attention_modules.py:10-64) train forward (+ Dropout2d) / backward
@@ -580,6 +581,7 @@ __global__ void __launch_bounds__(256) ubf_fwd_kernel(UbfArgs u, const void* tfe
 // partial layout per block: [32 g][32 gx][32 x][64 dW1][2 db1]  (162)
 // LayerNorm (u.ln): sb blocks per sample, block j of sample n covers a slice of that sample only, so the
 // per-block channel sums add up to per-(sample, channel) sums.
+template <bool U2>
 __global__ void __launch_bounds__(256) ubf_bwd1_kernel(UbfArgs u, const float* dlogits, const float* dbgfg_ext,
                                                        const float* dtn_ext, const float* bgfg, const float* tn,
                                                        float* db_out, float* dtn_out, float* partial, int sb) {
@@ -601,6 +603,15 @@ __global__ void __launch_bounds__(256) ubf_bwd1_kernel(UbfArgs u, const float* d
   const float mu = u.ln ? u.mean[ns] : u.mean[c], inv = u.ln ? u.invstd[ns] : u.invstd[c];
   const float scc = u.ln ? u.scale[ns * 32 + c] : u.scale[c], shc = u.ln ? u.shift[ns * 32 + c] : u.shift[c];
   const float w0 = u.u1_w[c], w1 = u.u1_w[32 + c];
+  // the thread's ConvTranspose weights for the 4 sub-pixels and its bias, loaded once (U2; the U1 form re-reads them
+  // per pixel through ubf_z: the stores below may alias them as far as the compiler knows)
+  float zw0[4], zw1[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    zw0[q] = u.ut_w[(c * 2 + (q >> 1)) * 2 + (q & 1)];
+    zw1[q] = u.ut_w[((32 + c) * 2 + (q >> 1)) * 2 + (q & 1)];
+  }
+  const float zb = u.ut_b[c];
   float sg = 0.f, sgx = 0.f, sx = 0.f, dw0 = 0.f, dw1 = 0.f, db0s = 0.f, db1s = 0.f;
   // (n, Y, X) of p advanced incrementally by the row stride 8: the 64-bit div / mod per pixel dominated the loop
   int X, Y;
@@ -611,40 +622,75 @@ __global__ void __launch_bounds__(256) ubf_bwd1_kernel(UbfArgs u, const float* d
     Y = (int)(tt % H);
     n = tt / H;
   }
-  for (long long p = b + r; p < e; p += 8, X += 8) {
-    while (X >= W) {
-      X -= W;
-      if (++Y == H) { Y = 0; ++n; }
-    }
-    const long long pp = (long long)Y * W + X;
-    const float* G = bgfg + n * 2 * plane + pp;
-    const float* Tn = tn + n * 2 * plane + pp;
-    const float* dL = dlogits + n * 3 * plane + pp;
-    const float g0 = G[0], g1 = G[plane], t0 = Tn[0], t1 = Tn[plane];
-    const float dL0 = dL[0], dL1 = dL[plane], dL2 = dL[2 * plane];
-    const float mx = fmaxf(g0, g1);
-    const float ex0 = __expf(g0 - mx), ex1 = __expf(g1 - mx);
+  struct In { float g0, g1, t0, t1, dL0, dL1, dL2, e0, e1, f0, f1, l0, l1; long long pp, n; int X, Y; };
+  auto load = [&](long long nn, int YY, int XX) __attribute__((always_inline)) -> In {
+    In v;
+    const long long pp = (long long)YY * W + XX;
+    const float* G = bgfg + nn * 2 * plane + pp;
+    const float* Tn = tn + nn * 2 * plane + pp;
+    const float* dL = dlogits + nn * 3 * plane + pp;
+    v.g0 = G[0]; v.g1 = G[plane]; v.t0 = Tn[0]; v.t1 = Tn[plane];
+    v.dL0 = dL[0]; v.dL1 = dL[plane]; v.dL2 = dL[2 * plane];
+    v.e0 = dbgfg_ext ? dbgfg_ext[nn * 2 * plane + pp] : 0.f;
+    v.e1 = dbgfg_ext ? dbgfg_ext[nn * 2 * plane + plane + pp] : 0.f;
+    v.f0 = dtn_ext ? dtn_ext[nn * 2 * plane + pp] : 0.f;
+    v.f1 = dtn_ext ? dtn_ext[nn * 2 * plane + plane + pp] : 0.f;
+    const float* lo = u.low + ((nn * u.h + (YY >> 1)) * u.w + (XX >> 1)) * 2;
+    v.l0 = lo[0]; v.l1 = lo[1];
+    v.pp = pp; v.n = nn; v.X = XX; v.Y = YY;
+    return v;
+  };
+  auto body = [&](const In& v, long long p) __attribute__((always_inline)) {
+    const float mx = fmaxf(v.g0, v.g1);
+    const float ex0 = __expf(v.g0 - mx), ex1 = __expf(v.g1 - mx);
     const float pf = ex1 / (ex0 + ex1);
-    const float dpf = dL1 * t0 + dL2 * t1;
+    const float dpf = v.dL1 * v.t0 + v.dL2 * v.t1;
     const float dsg = dpf * pf * (1.f - pf);
-    float db0 = dL0 - dsg, db1 = dL1 + dL2 + dsg;
-    float dt0 = dL1 * pf, dt1 = dL2 * pf;
-    if (dbgfg_ext) { db0 += dbgfg_ext[n * 2 * plane + pp]; db1 += dbgfg_ext[n * 2 * plane + plane + pp]; }
-    if (dtn_ext) { dt0 += dtn_ext[n * 2 * plane + pp]; dt1 += dtn_ext[n * 2 * plane + plane + pp]; }
+    float db0 = v.dL0 - dsg, db1 = v.dL1 + v.dL2 + dsg;
+    float dt0 = v.dL1 * pf, dt1 = v.dL2 * pf;
+    if (dbgfg_ext) { db0 += v.e0; db1 += v.e1; }
+    if (dtn_ext) { dt0 += v.f0; dt1 += v.f1; }
     if (c == 0) {
       db_out[p * 2] = db0; db_out[p * 2 + 1] = db1;
       dtn_out[p * 2] = dt0; dtn_out[p * 2 + 1] = dt1;
       db0s += db0; db1s += db1;
     }
-    const int q = (Y & 1) * 2 + (X & 1);
-    const float* lo = u.low + ((n * u.h + (Y >> 1)) * u.w + (X >> 1)) * 2;
-    const float z = ubf_z(u, lo[0], lo[1], c, q);
+    const int q = (v.Y & 1) * 2 + (v.X & 1);
+    const float z = U2 ? v.l0 * zw0[q] + v.l1 * zw1[q] + zb : ubf_z(u, v.l0, v.l1, c, q);
     const float pre = z * scc + shc;
     const float a = apply_act(pre, u.act, u.beta);
     const float g = (w0 * db0 + w1 * db1) * act_grad_pre(pre, u.act, u.beta);
     const float xh = (z - mu) * inv;
     sg += g; sgx += g * xh; sx += xh;
     dw0 += db0 * a; dw1 += db1 * a;
+  };
+  auto step = [&]() __attribute__((always_inline)) {
+    X += 8;
+    while (X >= W) {
+      X -= W;
+      if (++Y == H) { Y = 0; ++n; }
+    }
+  };
+  long long p = b + r;
+  while (X >= W) {   // (b + r may start past a row end only through the initial decomposition: never; kept for form)
+    X -= W;
+    if (++Y == H) { Y = 0; ++n; }
+  }
+  if (U2) {
+    // two pixels per iteration, both pixels' loads issued before either's arithmetic; the sums in pixel order
+    for (; p + 8 < e; p += 16) {
+      const In va = load(n, Y, X);
+      step();
+      const In vb = load(n, Y, X);
+      step();
+      body(va, p);
+      body(vb, p + 8);
+    }
+  }
+  for (; p < e; p += 8) {
+    const In va = load(n, Y, X);
+    step();
+    body(va, p);
   }
   red[r][c] = sg; red[r][32 + c] = sgx; red[r][64 + c] = sx; red[r][96 + c] = dw0; red[r][128 + c] = dw1;
   if (c == 0) { red[r][160] = db0s; red[r][161] = db1s; }
@@ -1038,8 +1084,14 @@ extern "C" int hiseg_ubf_train_bwd(const hiseg_ubf_desc* d, const float* dlogits
   float* coef = ws + part_len;               // [96] (BN)
   float* coef_ln = coef + 96;                // [N][2] (LN)
   float* dbias = coef_ln + 2LL * d->N;       // [N][32] (LN)
-  hipLaunchKernelGGL(ubf_bwd1_kernel, dim3(nb1), dim3(256), 0, s, u, dlogits, dbgfg_ext, dtn_ext, d->bgfg, d->tn,
-                     db_buf, dtn_out, part, sb);
+  // HISEG_UBF_U2=0: the one-pixel loop with per-pixel weight reads (A/B timing; same results)
+  const char* ue = getenv("HISEG_UBF_U2");
+  if (!(ue && atoi(ue) == 0))
+    hipLaunchKernelGGL(ubf_bwd1_kernel<true>, dim3(nb1), dim3(256), 0, s, u, dlogits, dbgfg_ext, dtn_ext, d->bgfg,
+                       d->tn, db_buf, dtn_out, part, sb);
+  else
+    hipLaunchKernelGGL(ubf_bwd1_kernel<false>, dim3(nb1), dim3(256), 0, s, u, dlogits, dbgfg_ext, dtn_ext, d->bgfg,
+                       d->tn, db_buf, dtn_out, part, sb);
   if (d->layernorm)
     hipLaunchKernelGGL(ubf_ln_fin_kernel, dim3(d->N), dim3(32), 0, s, u, part, sb, coef_ln, dbias);
   hipLaunchKernelGGL(ubf_fin1_kernel, dim3(1), dim3(192), 0, s, u, part, nb1, Pm, coef, g->dgamma, g->dbeta,

@@ -1024,3 +1024,29 @@ def test_train_step_independent_of_allocator_churn_between_forward_and_backward(
         grads.append(S.flat.grad.clone())
     assert torch.isfinite(grads[0]).all()
     assert torch.equal(grads[0], grads[1])
+
+
+def test_ubf_backward_two_pixel_loop_bit_identical(monkeypatch):
+    """The upsample_bg_fg backward's first pass with two pixels per iteration and its ConvTranspose weights held in
+    registers (HISEG_UBF_U2, default) against the one-pixel loop (HISEG_UBF_U2=0): same per-pixel arithmetic, sums in
+    pixel order -- a bf16 B0 train step's loss and every parameter gradient equal bit for bit."""
+    import hiseg
+    from hiseg import train_engine as TE
+    images = torch.from_numpy(filler.uniform(71, (2, 3, 96, 128))).to(DEV)
+    u = torch.from_numpy(filler.normal(72, (2, 1, 96, 128)) * 2.0).to(DEV)
+    rois = torch.tensor([[0, .10, .10, .40, .90], [1, .35, .15, .80, .95], [0, .55, .05, .95, .70]]).to(DEV)
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("HISEG_UBF_U2", mode)
+        m = _model(torch.bfloat16).to(DEV).train()
+        for mm in (m.roi_align_mask, m.roi_align_rgb):
+            mm.spatial_scale_h, mm.spatial_scale_w = 96, 128
+        tgt = torch.from_numpy(filler.ellipse_targets(73, 3, *m.mask_size)).to(DEV)
+        logits, aux = TE.train_forward(m, images, rois, u_override=u)
+        loss, _ = hiseg.RefinedHierarchicalLoss()(logits, tgt, aux)
+        loss.backward()
+        torch.cuda.synchronize()
+        res[mode] = (loss.detach().clone(), [p.grad.detach().clone() for p in m.parameters() if p.grad is not None])
+    (l1, g1), (l0, g0) = res["1"], res["0"]
+    assert torch.isfinite(l1) and torch.equal(l1, l0)
+    assert len(g1) == len(g0) and all(torch.equal(a, b) for a, b in zip(g1, g0))
