@@ -302,15 +302,17 @@ def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=6
     for _ in range(max(warmup, 3 if run is not step else 1)):
         loss = run()
     if os.environ.get("HISEG_BENCH_STEP_TIMES") == "1":   # developer knob: per-replay times on stderr
-        ts = []
+        ts, hs = [], []
         for _ in range(8):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
+            h0 = time.perf_counter()
             run()
+            hs.append(round((time.perf_counter() - h0) * 1e3, 2))
             e1.record()
             torch.cuda.synchronize()
             ts.append(round(e0.elapsed_time(e1), 2))
-        print(f"distill per-replay ms: {ts}", file=sys.stderr, flush=True)
+        print(f"distill per-replay ms: {ts} host enqueue ms: {hs}", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
