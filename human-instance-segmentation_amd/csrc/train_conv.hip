@@ -270,7 +270,10 @@ __device__ __forceinline__ v4s_t tr_read(unsigned byte_addr) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_t*)(uintptr_t)byte_addr);
 }
 
-template <int BC, int WK, int WC, int STAGES>
+// INC: stride 1, no upsampled source, no ConvTranspose and Ho x Wo = H x W -- each DMA row's X and dY byte offsets
+// advance by PB pixels' stride per stage, kept in registers (wgrad_wide.hip's SHT 2), instead of the per-stage
+// (n, y, x) -> offset products
+template <int BC, int WK, int WC, int STAGES, bool INC = false>
 __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
   constexpr int BK = 128, PB = 64;
   constexpr int TM = BK / (WK * 16), TN = BC / (WC * 16);
@@ -351,6 +354,16 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
     py[i] = tt % d.Ho;
     pn[i] = tt / d.Ho;
   }
+  unsigned ob[4], yb[4];   // INC: byte offsets of the row's tap-shifted X pixel (+ channel) and of its dY pixel
+  if constexpr (INC) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int toff = (ky[i] - d.pad) * d.W + kx[i] - d.pad;
+      ob[i] = xd[i] + 2u * (unsigned)xo[i] + 2u * (unsigned)(pp[i] + toff) * (unsigned)xcs[i];
+      yb[i] = 2u * (unsigned)pp[i] * (unsigned)a.dy_cs;
+    }
+  }
+  const unsigned yb_step = 2u * PB * (unsigned)a.dy_cs;
   const int adv_x = PB % d.Wo, adv_y = PB / d.Wo;
   const unsigned lds_base = (unsigned)(uintptr_t)(lds_void_t*)smem;
 
@@ -359,6 +372,22 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const unsigned row_base = 256u * (unsigned)(4 * (w + 4 * i));
+      if constexpr (INC) {
+        const int iy = py[i] - d.pad + ky[i];
+        const int ix = px[i] - d.pad + kx[i];
+        const bool okx = xo[i] >= 0 && pp[i] < a.M && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+        wg_dma16(rX, sb + row_base, okx ? ob[i] : OOB);
+        const bool oky = yo[i] >= 0 && pp[i] < a.M;
+        wg_dma16(rY, sb + IMG + row_base, oky ? yb[i] + 2u * (unsigned)yo[i] : OOB);
+        ob[i] += (unsigned)xcs[i] * (2u * PB);
+        yb[i] += yb_step;
+        pp[i] += PB;
+        px[i] += adv_x;
+        py[i] += adv_y;
+        if (px[i] >= d.Wo) { px[i] -= d.Wo; ++py[i]; }
+        while (py[i] >= d.Ho) py[i] -= d.Ho;
+        continue;
+      }
       const int iy = py[i] * d.stride - d.pad + ky[i];
       const int ix = px[i] * d.stride - d.pad + kx[i];
       const bool okx = xo[i] >= 0 && pp[i] < a.M && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
@@ -458,10 +487,10 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
   }
 }
 
-template <int BC, int WK, int WC, int STAGES>
+template <int BC, int WK, int WC, int STAGES, bool INC = false>
 static int wgrad_tr_launch(const WgradArgs& a, hipStream_t s) {
   const size_t lds = (size_t)STAGES * 2 * 64 * 256;
-  auto kern = conv_wgrad_tr_kernel<BC, WK, WC, STAGES>;
+  auto kern = conv_wgrad_tr_kernel<BC, WK, WC, STAGES, INC>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -509,7 +538,12 @@ static int wgrad_tr_try(const WgradArgs& a, hipStream_t s) {
       b.x_tile_src = 1;
     }
   }
-  const int r = b.Cg >= 128 ? wgrad_tr_launch<128, 2, 2, 2>(b, s)
+  // incremental DMA offsets (INC above; HISEG_WGRAD_INC=0 for A/B timing, read per call)
+  const char* e = getenv("HISEG_WGRAD_INC");
+  const bool inc = !(e && atoi(e) == 0) && !d.convT && d.stride == 1 && d.a_up == 1 && d.Ho == d.H && d.Wo == d.W;
+  const int r = inc && b.Cg >= 128 ? wgrad_tr_launch<128, 2, 2, 2, true>(b, s)
+              : inc && b.Cg >= 64  ? wgrad_tr_launch<64, 4, 1, 2, true>(b, s)
+              : b.Cg >= 128 ? wgrad_tr_launch<128, 2, 2, 2>(b, s)
               : b.Cg >= 64  ? wgrad_tr_launch<64, 4, 1, 2>(b, s)
               : b.Cg >= 32  ? wgrad_tr_launch<32, 4, 1, 2>(b, s)
                             : wgrad_tr_launch<16, 4, 1, 2>(b, s);

@@ -44,7 +44,13 @@ __device__ __forceinline__ ww_v4s_t ww_tr(unsigned byte_addr) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((ww_lds_v4s_t*)(uintptr_t)byte_addr);
 }
 
-template <int BC, int NW, int PB, int STAGES, bool BPRE = false>
+// SHT 1: one source and 256-multiple Cin -- both 128-column X images of a K tile lie in the same tap (their channel
+// offsets 128 apart, both valid or both not), so a row block's tap position, bounds and pixel offset are computed
+// once for the two (the per-stage DMA address math was ~60 % of the wave's VALU instructions,
+// profiles/r4_wgrad_counters.txt).  SHT 2, also stride 1, no upsampled source and Ho x Wo = H x W: the X and dY
+// byte offsets of a row block advance by a uniform PB pixels' stride per stage, kept in registers -- the per-stage
+// math is the two bounds compares.
+template <int BC, int NW, int PB, int STAGES, bool BPRE = false, int SHT = 0>
 __global__ void __launch_bounds__(NW * 64, 1) conv_wgrad_wide_kernel(WgradArgs a) {
   constexpr int BK = 256;
   constexpr int KS = PB / 32;              // 32-pixel k-steps per stage
@@ -125,6 +131,18 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_wgrad_wide_kernel(WgradArgs a
     py[i] = tt % d.Ho;
     pn[i] = tt / d.Ho;
   }
+  // SHT 2: byte offsets of row block i's X source pixel (tap-shifted, image 0's channel) and dY pixel
+  unsigned ob[NI], yb[NI];
+  if constexpr (SHT == 2) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int kk = xk[0][i];
+      const int toff = ((kk & 15) - d.pad) * d.W + ((kk >> 4) & 15) - d.pad;
+      ob[i] = dA + 2u * (unsigned)xo[0][i] + 2u * (unsigned)(pp[i] + toff) * (unsigned)d.a_cstride;
+      yb[i] = 2u * (unsigned)pp[i] * (unsigned)a.dy_cs;
+    }
+  }
+  const unsigned ob_step = 2u * PB * (unsigned)d.a_cstride, yb_step = 2u * PB * (unsigned)a.dy_cs;
   const int adv_x = PB % d.Wo, adv_y = PB / d.Wo;
   const unsigned lds_base = (unsigned)(uintptr_t)(ww_lds_void_t*)smem;
 
@@ -135,7 +153,26 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_wgrad_wide_kernel(WgradArgs a
     const unsigned sb = lds_base + (unsigned)(s * STAGE);
     const int i = p >> 1;
     const unsigned row_base = 256u * (unsigned)(4 * (w + NW * i));
-    if ((p & 1) == 0) {
+    if ((p & 1) == 0 && SHT == 2) {
+      const int kk = xk[0][i];
+      const int iy = py[i] - d.pad + (kk & 15);
+      const int ix = px[i] - d.pad + ((kk >> 4) & 15);
+      const bool ok = xo[0][i] >= 0 && pp[i] < a.M && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+      ww_dma16(rX, sb + row_base, ok ? ob[i] : OOB);
+      ww_dma16(rX, sb + (unsigned)IMG + row_base, ok ? ob[i] + 256u : OOB);
+    } else if ((p & 1) == 0 && SHT == 1) {
+      const int kk = xk[0][i];
+      const int iy = py[i] * d.stride - d.pad + (kk & 15);
+      const int ix = px[i] * d.stride - d.pad + ((kk >> 4) & 15);
+      const bool ok = pp[i] < a.M && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+      const int sh = (kk >> 8) & 1, Hs = d.H >> sh, Ws = d.W >> sh;
+      const unsigned pix = (unsigned)(((pn[i] * Hs + (iy >> sh)) * Ws + (ix >> sh)) * d.a_cstride);
+#pragma unroll
+      for (int h = 0; h < NXH; ++h) {
+        const unsigned offx = ok && xo[h][i] >= 0 ? dA + (pix + (unsigned)xo[h][i]) * 2u : OOB;
+        ww_dma16(rX, sb + (unsigned)(h * IMG) + row_base, offx);
+      }
+    } else if ((p & 1) == 0) {
 #pragma unroll
       for (int h = 0; h < NXH; ++h) {
         const int kk = xk[h][i];
@@ -159,8 +196,13 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_wgrad_wide_kernel(WgradArgs a
           const int qq = (yv >> 28) & 3;
           yp = (pn[i] * (2 * d.Ho) + 2 * py[i] + (qq >> 1)) * (2 * d.Wo) + 2 * px[i] + (qq & 1);
         }
-        const unsigned offy = oky ? (unsigned)((yp * a.dy_cs + (yv & 0x0fffffff)) * 2) : OOB;
+        unsigned offy = oky ? (unsigned)((yp * a.dy_cs + (yv & 0x0fffffff)) * 2) : OOB;
+        if constexpr (SHT == 2) offy = oky ? yb[i] + 2u * (unsigned)yv : OOB;
         ww_dma16(rY, sb + (unsigned)((NXH + hh) * IMG) + row_base, offy);
+      }
+      if constexpr (SHT == 2) {
+        ob[i] += ob_step;
+        yb[i] += yb_step;
       }
       pp[i] += PB;
       px[i] += adv_x;
@@ -323,10 +365,10 @@ int wgrad_wide_bc(const hiseg_conv2d_desc* d, int Cg, int Kg, int Cin, int M, in
   return Cg % 256 == 0 ? 256 : 0;   // (the 256 x 128 tile measured slower than the 128 x 128 kernel)
 }
 
-template <int BC, int NW, int PB, int STAGES, bool BPRE = false>
+template <int BC, int NW, int PB, int STAGES, bool BPRE = false, int SHT = 0>
 static int wide_launch(const WgradArgs& a, hipStream_t s) {
   constexpr size_t lds = (size_t)STAGES * (2 + BC / 128) * PB * 256;
-  auto kern = conv_wgrad_wide_kernel<BC, NW, PB, STAGES, BPRE>;
+  auto kern = conv_wgrad_wide_kernel<BC, NW, PB, STAGES, BPRE, SHT>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -354,7 +396,18 @@ int wgrad_wide_try(const WgradArgs& a, hipStream_t s) {
   // cycles at s_waitcnt / the barrier and 29 % issue-stalled -- one wave per SIMD has no partner to fill them.  The
   // eight-wave form that would give it one still needs 256 VGPRs + 36 spilled for its 128 accumulators plus the
   // hoisted fragment / DMA addresses, as in round 3.)
-  const int r = bpre ? wide_launch<256, 4, 64, 2, true>(a, s) : wide_launch<256, 4, 64, 2>(a, s);
+  // Shared-tap DMA addressing (SHT above; HISEG_WGRAD_SHT=1 / 0 for A/B timing, read per call): 1.19 -> 1.12 (SHT 1)
+  // -> 1.04 ms (SHT 2) on the 256-channel class, same checksum (profiles/r4_wgrad_sht.txt).  (Folding the fragment
+  // reads' stage / k-step offsets into immediates -- image-major ring, stage loop unrolled by two -- spilled 104
+  // VGPRs: the remaining one v_add per LDS read stays.)
+  const char* e = getenv("HISEG_WGRAD_SHT");
+  int sht = e ? atoi(e) : 2;
+  if (a.d.Cb != 0 || a.Cin % 256 != 0) sht = 0;
+  if (sht >= 2 && !(a.d.stride == 1 && a.d.a_up == 1 && a.d.Ho == a.d.H && a.d.Wo == a.d.W)) sht = 1;
+  const int r = !bpre ? wide_launch<256, 4, 64, 2>(a, s)
+              : sht >= 2 ? wide_launch<256, 4, 64, 2, true, 2>(a, s)
+              : sht == 1 ? wide_launch<256, 4, 64, 2, true, 1>(a, s)
+                         : wide_launch<256, 4, 64, 2, true>(a, s);
   return r < 0 ? r : 1;
 }
 

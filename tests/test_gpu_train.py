@@ -123,6 +123,7 @@ def test_conv_backward_matches_autograd(case, dt):
 WIDE_WGRAD_CASES = [  # (cin, cout, k, H, W, N, bias, two-source split): 128-multiple GEMM columns (wgrad_wide.hip)
     (256, 256, 3, 16, 12, 2, False, None),
     (256, 256, 3, 32, 24, 4, False, None),        # many pixel splits
+    (256, 256, 3, 12, 10, 2, True, None),         # bias column in the last K tile of a shared-tap layer
     (128, 128, 3, 9, 7, 2, True, None),           # ragged K tile (1152 + bias column), C tile 128
     (256, 128, 3, 12, 10, 2, False, None),
     (128, 256, 3, 12, 10, 3, True, None),
@@ -163,6 +164,50 @@ def test_wgrad_wide_matches_f64_of_bf16_operands(case, reduce_taps, monkeypatch)
     assert rel(conv.weight.grad, wr.grad) < 1e-4
     if bias:
         assert rel(conv.bias.grad, br.grad) < 1e-4
+
+
+TR_WGRAD_CASES = [  # (cin, cout, k, H, W, N, bias, two-source split): conv_wgrad_tr_kernel's 128 / 64-column tiles
+    (128, 128, 3, 12, 10, 3, True, None),
+    (64, 64, 3, 16, 12, 2, False, None),
+    (128, 64, 3, 9, 7, 2, True, None),           # ragged pixel block, bias column
+    (128, 128, 3, 10, 8, 2, False, (64, 64)),    # decoder concat: two 64-channel sources
+    (96, 128, 1, 8, 6, 2, True, None),
+]
+
+
+@pytest.mark.parametrize("knob,values,case",
+                         [("HISEG_WGRAD_SHT", ("2", "1", "0"), c) for c in WIDE_WGRAD_CASES
+                          if c[0] % 256 == 0 and c[7] is None] +
+                         [("HISEG_WGRAD_INC", ("1", "0"), c) for c in TR_WGRAD_CASES])
+def test_wgrad_dma_addressing_bit_identical(knob, values, case, monkeypatch):
+    """The weight-gradient kernels' cheaper DMA addressing lands the same operands as the per-stage (n, y, x)
+    products: equal gradients.  Wide tile (wgrad_wide.hip, one source, 256-multiple Cin): the shared-tap addressing
+    of its two X images with and without per-stage incremental byte offsets (HISEG_WGRAD_SHT=2 / 1) vs 0;
+    conv_wgrad_tr_kernel: incremental offsets (HISEG_WGRAD_INC=1) vs 0, one and two sources."""
+    from hiseg.ops import Act
+    cin, cout, k, H, W, N, bias, split = case
+    dt = torch.bfloat16
+    x = torch.from_numpy(filler.normal(11, (N, cin, H, W))).to(DEV)
+    g = torch.from_numpy(filler.normal(12, (N, cout, H, W))).to(DEV)
+    grads = []
+    for v in values:
+        monkeypatch.setenv(knob, v)
+        conv = nn.Conv2d(cin, cout, k, padding=k // 2, bias=bias)
+        filler.fill_module(conv, seed=17)
+        TE, S, T = engine(_Holder(c=conv), dt)
+        if split is None:
+            xa, xb = Act.from_nchw(x, dt), None
+        else:
+            xa, xb = Act.from_nchw(x[:, :split[0]], dt), Act.from_nchw(x[:, split[0]:], dt)
+        y = TE.conv_plain(T, conv, TE.ACT_NONE, xa, xb, split=split)
+        inject(T, y, g, dt)
+        S.flat.prepare_backward()
+        T.run_backward()
+        grads.append((conv.weight.grad.clone(), conv.bias.grad.clone() if bias else None))
+    for gw, gb in grads[1:]:
+        assert torch.equal(grads[0][0], gw)
+        if bias:
+            assert torch.equal(grads[0][1], gb)
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
