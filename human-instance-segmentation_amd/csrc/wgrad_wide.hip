@@ -50,7 +50,10 @@ __device__ __forceinline__ ww_v4s_t ww_tr(unsigned byte_addr) {
 // profiles/r4_wgrad_counters.txt).  SHT 2, also stride 1, no upsampled source and Ho x Wo = H x W: the X and dY
 // byte offsets of a row block advance by a uniform PB pixels' stride per stage, kept in registers -- the per-stage
 // math is the two bounds compares.
-template <int BC, int NW, int PB, int STAGES, bool BPRE = false, int SHT = 0>
+// TOG: image-major ring (image m of stage s at (m STAGES + s) IMG, so the stage is address bit 14) and per-lane
+// fragment-read addresses held in registers, flipped once per stage -- each LDS read is a register + an immediate
+// k-step offset instead of a v_add per read
+template <int BC, int NW, int PB, int STAGES, bool BPRE = false, int SHT = 0, bool TOG = false>
 __global__ void __launch_bounds__(NW * 64, 1) conv_wgrad_wide_kernel(WgradArgs a) {
   constexpr int BK = 256;
   constexpr int KS = PB / 32;              // 32-pixel k-steps per stage
@@ -145,12 +148,15 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_wgrad_wide_kernel(WgradArgs a
   const unsigned ob_step = 2u * PB * (unsigned)d.a_cstride, yb_step = 2u * PB * (unsigned)a.dy_cs;
   const int adv_x = PB % d.Wo, adv_y = PB / d.Wo;
   const unsigned lds_base = (unsigned)(uintptr_t)(ww_lds_void_t*)smem;
+  static_assert(!TOG || (STAGES == 2 && IMG == 16384 && BPRE && KS == 2), "toggled fragment addressing");
+  auto img_off = [&](int s, int m) __attribute__((always_inline)) -> unsigned {
+    return TOG ? (unsigned)((m * STAGES + s) * IMG) : (unsigned)(s * STAGE + m * IMG);
+  };
 
   // DMA of a stage in 2 NI parts (part p: row block i = p / 2 of the X images if p is even, of the dY images if odd;
   // the odd part advances the row block's pixels), interleaved with the previous stage's MFMA rows so the DMA
   // issue (about 100 cycles per 1-KiB piece) hides under them
   auto issue_part = [&](int s, int p) __attribute__((always_inline)) {
-    const unsigned sb = lds_base + (unsigned)(s * STAGE);
     const int i = p >> 1;
     const unsigned row_base = 256u * (unsigned)(4 * (w + NW * i));
     if ((p & 1) == 0 && SHT == 2) {
@@ -158,8 +164,8 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_wgrad_wide_kernel(WgradArgs a
       const int iy = py[i] - d.pad + (kk & 15);
       const int ix = px[i] - d.pad + ((kk >> 4) & 15);
       const bool ok = xo[0][i] >= 0 && pp[i] < a.M && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
-      ww_dma16(rX, sb + row_base, ok ? ob[i] : OOB);
-      ww_dma16(rX, sb + (unsigned)IMG + row_base, ok ? ob[i] + 256u : OOB);
+      ww_dma16(rX, lds_base + img_off(s, 0) + row_base, ok ? ob[i] : OOB);
+      ww_dma16(rX, lds_base + img_off(s, 1) + row_base, ok ? ob[i] + 256u : OOB);
     } else if ((p & 1) == 0 && SHT == 1) {
       const int kk = xk[0][i];
       const int iy = py[i] * d.stride - d.pad + (kk & 15);
@@ -170,7 +176,7 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_wgrad_wide_kernel(WgradArgs a
 #pragma unroll
       for (int h = 0; h < NXH; ++h) {
         const unsigned offx = ok && xo[h][i] >= 0 ? dA + (pix + (unsigned)xo[h][i]) * 2u : OOB;
-        ww_dma16(rX, sb + (unsigned)(h * IMG) + row_base, offx);
+        ww_dma16(rX, lds_base + img_off(s, h) + row_base, offx);
       }
     } else if ((p & 1) == 0) {
 #pragma unroll
@@ -184,7 +190,7 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_wgrad_wide_kernel(WgradArgs a
         const unsigned offx = okx ? (fb ? dB : dA) + (unsigned)((((pn[i] * Hs + (iy >> sh)) * Ws + (ix >> sh)) *
                                                                   (fb ? d.b_cstride : d.a_cstride) + xo[h][i]) * 2)
                                   : OOB;
-        ww_dma16(rX, sb + (unsigned)(h * IMG) + row_base, offx);
+        ww_dma16(rX, lds_base + img_off(s, h) + row_base, offx);
       }
     } else {
 #pragma unroll
@@ -198,7 +204,7 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_wgrad_wide_kernel(WgradArgs a
         }
         unsigned offy = oky ? (unsigned)((yp * a.dy_cs + (yv & 0x0fffffff)) * 2) : OOB;
         if constexpr (SHT == 2) offy = oky ? yb[i] + 2u * (unsigned)yv : OOB;
-        ww_dma16(rY, sb + (unsigned)((NXH + hh) * IMG) + row_base, offy);
+        ww_dma16(rY, lds_base + img_off(s, NXH + hh) + row_base, offy);
       }
       if constexpr (SHT == 2) {
         ob[i] += ob_step;
@@ -229,6 +235,22 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_wgrad_wide_kernel(WgradArgs a
   const int yimg = (wc * WCOLS) / 128;
   const int ych0 = ((wc * WCOLS) % 128) / 8;
 
+  // TOG: rows 8g + q (+ 4) of a k-step (k-step 1's rows 32 below: the swizzle repeats every 16 rows), channel pair
+  // 2i (+ 1), this wave's X / dY image, stage 0
+  unsigned oX[TOG ? TM : 1][2], oY[TOG ? TN : 1][2];
+  if constexpr (TOG) {
+#pragma unroll
+    for (int hi = 0; hi < 2; ++hi) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        oX[i][hi] = lds_base + img_off(0, wk) + ww_swz(8 * g + q + 4 * hi, 2 * i + (pq >> 1)) + 8u * (pq & 1);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        oY[j][hi] = lds_base + img_off(0, NXH + yimg) + ww_swz(8 * g + q + 4 * hi, ych0 + 2 * j + (pq >> 1)) +
+                    8u * (pq & 1);
+    }
+  }
+
 #pragma unroll
   for (int s0 = 0; s0 < STAGES - 1; ++s0)
     if (s0 < nit) issue(s0);
@@ -237,14 +259,13 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_wgrad_wide_kernel(WgradArgs a
     if (STAGES > 2 && it + STAGES - 2 < nit) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NLW * (STAGES - 2)) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (bias_lanes) {   // the GEMM-bias column: X = 1 in every row, written over the landed DMA zeros
-      const unsigned sb = lds_base + (unsigned)(cur * STAGE);
 #pragma unroll
       for (int h = 0; h < NXH; ++h)
 #pragma unroll
         for (int i = 0; i < NI; ++i)
           if (bias_lanes & (1u << (NI * h + i)))
             *reinterpret_cast<ww_lds_v4u_t*>(
-                (uintptr_t)(sb + (unsigned)(h * IMG) + 256u * (unsigned)(4 * (w + NW * i)) + 16u * (unsigned)lane)) =
+                (uintptr_t)(lds_base + img_off(cur, h) + 256u * (unsigned)(4 * (w + NW * i)) + 16u * (unsigned)lane)) =
                 ww_v4u_t{0x3f80u, 0u, 0u, 0u};
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -253,18 +274,28 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_wgrad_wide_kernel(WgradArgs a
     const int nxt = it + STAGES - 1;   // the stage whose DMA this iteration issues (into stage it-1's buffer)
     const bool more = nxt < nit;
 
-    const unsigned sX = lds_base + (unsigned)(cur * STAGE) + (unsigned)(wk * IMG);
-    const unsigned sY = lds_base + (unsigned)(cur * STAGE) + (unsigned)((NXH + yimg) * IMG);
+    const unsigned sX = lds_base + img_off(cur, wk);
+    const unsigned sY = lds_base + img_off(cur, NXH + yimg);
     // k-step 0 fragments, then per A row i: its MFMAs, after which af[i] takes row i of k-step 1 (the reads land
     // under the remaining rows' MFMAs); k-step 1's B fragments after the last row
     bf16x8_t af[TM], bfr[TN];
     auto rdA = [&](int ks, int i) __attribute__((always_inline)) -> bf16x8_t {
+      if constexpr (TOG) {
+        const ww_v4s_t lo = ww_tr(oX[i][0] + (unsigned)(ks * 32 * 256));
+        const ww_v4s_t hi = ww_tr(oX[i][1] + (unsigned)(ks * 32 * 256));
+        return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
       const int r0 = ks * 32 + 8 * g + q, ch = 2 * i + (pq >> 1);
       const ww_v4s_t lo = ww_tr(sX + ww_swz(r0, ch) + 8u * (pq & 1));
       const ww_v4s_t hi = ww_tr(sX + ww_swz(r0 + 4, ch) + 8u * (pq & 1));
       return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
     };
     auto rdB = [&](int ks, int j) __attribute__((always_inline)) -> bf16x8_t {
+      if constexpr (TOG) {
+        const ww_v4s_t lo = ww_tr(oY[j][0] + (unsigned)(ks * 32 * 256));
+        const ww_v4s_t hi = ww_tr(oY[j][1] + (unsigned)(ks * 32 * 256));
+        return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
       const int r0 = ks * 32 + 8 * g + q, ch = ych0 + 2 * j + (pq >> 1);
       const ww_v4s_t lo = ww_tr(sY + ww_swz(r0, ch) + 8u * (pq & 1));
       const ww_v4s_t hi = ww_tr(sY + ww_swz(r0 + 4, ch) + 8u * (pq & 1));
@@ -297,6 +328,15 @@ __global__ void __launch_bounds__(NW * 64, 1) conv_wgrad_wide_kernel(WgradArgs a
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bnx[j], acc[i][j], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (TOG) {   // the next stage's buffer
+#pragma unroll
+        for (int hi = 0; hi < 2; ++hi) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) oX[i][hi] ^= (unsigned)IMG;
+#pragma unroll
+          for (int j = 0; j < TN; ++j) oY[j][hi] ^= (unsigned)IMG;
+        }
       }
       continue;
     }
@@ -365,10 +405,10 @@ int wgrad_wide_bc(const hiseg_conv2d_desc* d, int Cg, int Kg, int Cin, int M, in
   return Cg % 256 == 0 ? 256 : 0;   // (the 256 x 128 tile measured slower than the 128 x 128 kernel)
 }
 
-template <int BC, int NW, int PB, int STAGES, bool BPRE = false, int SHT = 0>
+template <int BC, int NW, int PB, int STAGES, bool BPRE = false, int SHT = 0, bool TOG = false>
 static int wide_launch(const WgradArgs& a, hipStream_t s) {
   constexpr size_t lds = (size_t)STAGES * (2 + BC / 128) * PB * 256;
-  auto kern = conv_wgrad_wide_kernel<BC, NW, PB, STAGES, BPRE, SHT>;
+  auto kern = conv_wgrad_wide_kernel<BC, NW, PB, STAGES, BPRE, SHT, TOG>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -404,7 +444,10 @@ int wgrad_wide_try(const WgradArgs& a, hipStream_t s) {
   int sht = e ? atoi(e) : 2;
   if (a.d.Cb != 0 || a.Cin % 256 != 0) sht = 0;
   if (sht >= 2 && !(a.d.stride == 1 && a.d.a_up == 1 && a.d.Ho == a.d.H && a.d.Wo == a.d.W)) sht = 1;
+  const char* et = getenv("HISEG_WGRAD_TOG");
+  const bool tog = !(et && atoi(et) == 0);
   const int r = !bpre ? wide_launch<256, 4, 64, 2>(a, s)
+              : sht >= 2 && tog ? wide_launch<256, 4, 64, 2, true, 2, true>(a, s)
               : sht >= 2 ? wide_launch<256, 4, 64, 2, true, 2>(a, s)
               : sht == 1 ? wide_launch<256, 4, 64, 2, true, 1>(a, s)
                          : wide_launch<256, 4, 64, 2, true>(a, s);
