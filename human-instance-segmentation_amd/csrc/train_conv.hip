@@ -273,7 +273,9 @@ __device__ __forceinline__ v4s_t tr_read(unsigned byte_addr) {
 // INC: stride 1, no upsampled source, no ConvTranspose and Ho x Wo = H x W -- each DMA row's X and dY byte offsets
 // advance by PB pixels' stride per stage, kept in registers (wgrad_wide.hip's SHT 2), instead of the per-stage
 // (n, y, x) -> offset products
-template <int BC, int WK, int WC, int STAGES, bool INC = false>
+// TOG (STAGES == 2): image-major ring (X of stage s at s IMG, dY at (2 + s) IMG, so the stage is address bit 14) and
+// per-lane fragment-read addresses in registers, flipped once per stage (wgrad_wide.hip's TOG)
+template <int BC, int WK, int WC, int STAGES, bool INC = false, bool TOG = false>
 __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
   constexpr int BK = 128, PB = 64;
   constexpr int TM = BK / (WK * 16), TN = BC / (WC * 16);
@@ -367,8 +369,14 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
   const int adv_x = PB % d.Wo, adv_y = PB / d.Wo;
   const unsigned lds_base = (unsigned)(uintptr_t)(lds_void_t*)smem;
 
+  static_assert(!TOG || (STAGES == 2 && IMG == 16384), "toggled fragment addressing");
+  // LDS byte offsets of stage s's X and dY images
+  auto xoff = [&](int s) __attribute__((always_inline)) -> unsigned { return (unsigned)(TOG ? s * IMG : s * STAGE); };
+  auto yoff = [&](int s) __attribute__((always_inline)) -> unsigned {
+    return (unsigned)(TOG ? (STAGES + s) * IMG : s * STAGE + IMG);
+  };
   auto issue = [&](int s) __attribute__((always_inline)) {
-    const unsigned sb = lds_base + (unsigned)(s * STAGE);
+    const unsigned sb = lds_base + xoff(s), sby = lds_base + yoff(s);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const unsigned row_base = 256u * (unsigned)(4 * (w + 4 * i));
@@ -378,7 +386,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
         const bool okx = xo[i] >= 0 && pp[i] < a.M && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
         wg_dma16(rX, sb + row_base, okx ? ob[i] : OOB);
         const bool oky = yo[i] >= 0 && pp[i] < a.M;
-        wg_dma16(rY, sb + IMG + row_base, oky ? yb[i] + 2u * (unsigned)yo[i] : OOB);
+        wg_dma16(rY, sby + row_base, oky ? yb[i] + 2u * (unsigned)yo[i] : OOB);
         ob[i] += (unsigned)xcs[i] * (2u * PB);
         yb[i] += yb_step;
         pp[i] += PB;
@@ -400,7 +408,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
       if (d.convT)   // the dY pixel of sub-pixel q: (n, 2y + q/2, 2x + q%2) of the 2H x 2W output grid
         yp = (pn[i] * (2 * d.Ho) + 2 * py[i] + (yq[i] >> 1)) * (2 * d.Wo) + 2 * px[i] + (yq[i] & 1);
       const unsigned offy = oky ? (unsigned)((yp * a.dy_cs + yo[i]) * 2) : OOB;
-      wg_dma16(rY, sb + IMG + row_base, offy);
+      wg_dma16(rY, sby + row_base, offy);
       // advance this row by PB pixels
       pp[i] += PB;
       px[i] += adv_x;
@@ -420,6 +428,20 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
   // lane 4q+p of the group addresses row q, columns 4p..4p+3 of its 16-column block
   const int g = lane >> 4, q = (lane & 15) >> 2, pq = lane & 3;
 
+  // TOG: rows 8g + q (+ 4) of a k-step (k-step 1's rows 32 below), this wave's channel pairs, stage 0
+  unsigned oX[TOG ? TM : 1][2], oY[TOG ? TN : 1][2];
+  if constexpr (TOG) {
+#pragma unroll
+    for (int hi = 0; hi < 2; ++hi) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        oX[i][hi] = lds_base + xoff(0) + trswz(8 * g + q + 4 * hi, (wk * TM * 16 + i * 16) / 8 + (pq >> 1)) + 8u * (pq & 1);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        oY[j][hi] = lds_base + yoff(0) + trswz(8 * g + q + 4 * hi, (wc * TN * 16 + j * 16) / 8 + (pq >> 1)) + 8u * (pq & 1);
+    }
+  }
+
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nit) issue(s);
@@ -434,7 +456,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
     }
     if (bias_lanes) {   // the GEMM-bias column: X = 1 in every row (rows past M meet zero dY), written over the
                         // DMA's zeros once this stage landed
-      const unsigned sb = lds_base + (unsigned)((it % STAGES) * STAGE);
+      const unsigned sb = lds_base + xoff(it % STAGES);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         if (bias_lanes & (1u << i))
@@ -446,8 +468,8 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
     asm volatile("" ::: "memory");
     if (it + STAGES - 1 < nit) issue((it + STAGES - 1) % STAGES);
 
-    const unsigned sX = lds_base + (unsigned)((it % STAGES) * STAGE);
-    const unsigned sY = sX + IMG;
+    const unsigned sX = lds_base + xoff(it % STAGES);
+    const unsigned sY = lds_base + yoff(it % STAGES);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int r0 = ks * 32 + 8 * g + q;
@@ -455,15 +477,19 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int ch = (wk * TM * 16 + i * 16) / 8 + (pq >> 1);
-        const v4s_t lo = tr_read(sX + trswz(r0, ch) + 8u * (pq & 1));
-        const v4s_t hi = tr_read(sX + trswz(r0 + 4, ch) + 8u * (pq & 1));
+        const unsigned lo_a = TOG ? oX[i][0] + (unsigned)(ks * 32 * 256) : sX + trswz(r0, ch) + 8u * (pq & 1);
+        const unsigned hi_a = TOG ? oX[i][1] + (unsigned)(ks * 32 * 256) : sX + trswz(r0 + 4, ch) + 8u * (pq & 1);
+        const v4s_t lo = tr_read(lo_a);
+        const v4s_t hi = tr_read(hi_a);
         af[i] = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int ch = (wc * TN * 16 + j * 16) / 8 + (pq >> 1);
-        const v4s_t lo = tr_read(sY + trswz(r0, ch) + 8u * (pq & 1));
-        const v4s_t hi = tr_read(sY + trswz(r0 + 4, ch) + 8u * (pq & 1));
+        const unsigned lo_a = TOG ? oY[j][0] + (unsigned)(ks * 32 * 256) : sY + trswz(r0, ch) + 8u * (pq & 1);
+        const unsigned hi_a = TOG ? oY[j][1] + (unsigned)(ks * 32 * 256) : sY + trswz(r0 + 4, ch) + 8u * (pq & 1);
+        const v4s_t lo = tr_read(lo_a);
+        const v4s_t hi = tr_read(hi_a);
         bfr[j] = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       }
 #pragma unroll
@@ -471,6 +497,15 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if constexpr (TOG) {   // the next stage's buffers
+#pragma unroll
+      for (int hi = 0; hi < 2; ++hi) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) oX[i][hi] ^= (unsigned)IMG;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) oY[j][hi] ^= (unsigned)IMG;
+      }
     }
   }
 
@@ -487,10 +522,10 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
   }
 }
 
-template <int BC, int WK, int WC, int STAGES, bool INC = false>
+template <int BC, int WK, int WC, int STAGES, bool INC = false, bool TOG = false>
 static int wgrad_tr_launch(const WgradArgs& a, hipStream_t s) {
   const size_t lds = (size_t)STAGES * 2 * 64 * 256;
-  auto kern = conv_wgrad_tr_kernel<BC, WK, WC, STAGES, INC>;
+  auto kern = conv_wgrad_tr_kernel<BC, WK, WC, STAGES, INC, TOG>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -541,7 +576,11 @@ static int wgrad_tr_try(const WgradArgs& a, hipStream_t s) {
   // incremental DMA offsets (INC above; HISEG_WGRAD_INC=0 for A/B timing, read per call)
   const char* e = getenv("HISEG_WGRAD_INC");
   const bool inc = !(e && atoi(e) == 0) && !d.convT && d.stride == 1 && d.a_up == 1 && d.Ho == d.H && d.Wo == d.W;
-  const int r = inc && b.Cg >= 128 ? wgrad_tr_launch<128, 2, 2, 2, true>(b, s)
+  const char* et = getenv("HISEG_WGRAD_TOG");   // flipped fragment-read registers (TOG above; 0 for A/B timing)
+  const bool tog = !(et && atoi(et) == 0);
+  const int r = inc && tog && b.Cg >= 128 ? wgrad_tr_launch<128, 2, 2, 2, true, true>(b, s)
+              : inc && tog && b.Cg >= 64  ? wgrad_tr_launch<64, 4, 1, 2, true, true>(b, s)
+              : inc && b.Cg >= 128 ? wgrad_tr_launch<128, 2, 2, 2, true>(b, s)
               : inc && b.Cg >= 64  ? wgrad_tr_launch<64, 4, 1, 2, true>(b, s)
               : b.Cg >= 128 ? wgrad_tr_launch<128, 2, 2, 2>(b, s)
               : b.Cg >= 64  ? wgrad_tr_launch<64, 4, 1, 2>(b, s)

@@ -180,13 +180,15 @@ TR_WGRAD_CASES = [  # (cin, cout, k, H, W, N, bias, two-source split): conv_wgra
                           if c[0] % 256 == 0 and c[7] is None] +
                          [("HISEG_WGRAD_TOG", ("1", "0"), c) for c in WIDE_WGRAD_CASES
                           if c[0] % 256 == 0 and c[7] is None] +
+                         [("HISEG_WGRAD_TOG", ("1", "0"), c) for c in TR_WGRAD_CASES] +
                          [("HISEG_WGRAD_INC", ("1", "0"), c) for c in TR_WGRAD_CASES])
 def test_wgrad_dma_addressing_bit_identical(knob, values, case, monkeypatch):
     """The weight-gradient kernels' cheaper DMA addressing lands the same operands as the per-stage (n, y, x)
     products: equal gradients.  Wide tile (wgrad_wide.hip, one source, 256-multiple Cin): the shared-tap addressing
     of its two X images with and without per-stage incremental byte offsets (HISEG_WGRAD_SHT=2 / 1) vs 0, and its
     image-major ring with per-stage flipped fragment-read registers (HISEG_WGRAD_TOG=1) vs the stage-major one;
-    conv_wgrad_tr_kernel: incremental offsets (HISEG_WGRAD_INC=1) vs 0, one and two sources."""
+    conv_wgrad_tr_kernel: incremental offsets (HISEG_WGRAD_INC=1) vs 0 and the flipped read registers (TOG), one and
+    two sources."""
     from hiseg.ops import Act
     cin, cout, k, H, W, N, bias, split = case
     dt = torch.bfloat16
