@@ -28,7 +28,15 @@ namespace hiseg {
 // for 36 K blocks: one global round trip per K block on one workgroup per CU).  Each split stores its raw f32
 // tile to the caller's workspace [split][M][Cout_pad]; conv_splitk_reduce_kernel sums the splits in order and
 // applies the epilogue (deterministic; within f32 re-association of the unsplit kernel).
-template <typename T, typename TO, int BCO, int BPX, int WCO, int WPX, bool SPLIT = false>
+typedef unsigned ig_u4 __attribute__((ext_vector_type(4)));
+
+// LIN (bf16; 1x1, pad 0, one source, no upsampling; the launcher checks every tensor fits one 2^31-byte buffer
+// resource): a chunk's source pixel and channel never change along the K loop except by whole K blocks, so its
+// activation, gate and weight byte offsets are computed once and each K block's loads are buffer loads at those
+// offsets + a wave-uniform (SGPR) K-block offset -- the per-block 64-bit (n, y, x) -> address products and bounds
+// checks were most of the gather's VALU work, the SE-gated layers' more.  Rows outside the GEMM and chunks past
+// Cin load zeros through out-of-range offsets; the same values land in LDS as in the general gather.
+template <typename T, typename TO, int BCO, int BPX, int WCO, int WPX, bool SPLIT = false, bool LIN = false>
 __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
   constexpr int KCH = Chunk<T>::N;
   constexpr int BK = 8 * KCH;
@@ -85,6 +93,28 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
   }
   const int Cin = a.Cin;
   const int KW = d.KW;
+  static_assert(!LIN || sizeof(T) == 2, "LIN: bf16");
+  const unsigned OOB = 0x80000000u;
+  unsigned voff_a[LIN ? A_CH : 1], voff_g[LIN ? A_CH : 1], voff_w[LIN ? W_CH : 1];
+  __amdgpu_buffer_rsrc_t rsA, rsG, rsW;
+  if constexpr (LIN) {
+    rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(d.srcA), (short)0, 0x7fffffff, 0x00020000);
+    rsG = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(d.in_scale ? d.in_scale : reinterpret_cast<const float*>(d.srcA)),
+                                            (short)0, 0x7fffffff, 0x00020000);
+    rsW = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(d.weight), (short)0, 0x7fffffff, 0x00020000);
+    const int ci0 = kb0 * BK + c * KCH;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const bool ok = rn[i] >= 0 && riy[i] >= 0 && riy[i] < d.H && rix[i] >= 0 && rix[i] < d.W;
+      voff_a[i] = ok ? (unsigned)((((rn[i] * a.Hs + riy[i]) * a.Ws + rix[i]) * d.a_cstride + d.a_coff + ci0) * 2) : OOB;
+      voff_g[i] = ok ? (unsigned)((rn[i] * d.Ca + ci0) * 4) : OOB;
+    }
+#pragma unroll
+    for (int i = 0; i < W_CH; ++i) {
+      const int r = (t >> 3) + 32 * i;
+      voff_w[i] = co0 + r < d.Cout_pad ? (unsigned)(((co0 + r) * d.K_pad + ci0) * 2) : OOB;
+    }
+  }
 
   uint4 ra[A_CH], rw[W_CH];
 #pragma unroll
@@ -98,6 +128,29 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
   float4 rg[A_CH][GREG];
   bool rgs[A_CH];
   auto gather = [&](int kb) __attribute__((always_inline)) {
+    if constexpr (LIN) {
+      const unsigned so = __builtin_amdgcn_readfirstlane((unsigned)((kb - kb0) * BK * 2));
+      const bool kc = kb * BK + c * KCH < Cin;   // chunks past Cin (the last K block's padding) are zeros
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        const unsigned va = kc ? voff_a[i] : OOB;
+        ra[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsA, va, so, 0));
+        rgs[i] = false;
+        if (d.in_scale) {
+          rgs[i] = kc && voff_a[i] != OOB;
+          const unsigned vg = rgs[i] ? voff_g[i] : OOB;
+#pragma unroll
+          for (int e = 0; e < GREG; ++e)
+            rg[i][e] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsG, vg + 16u * e, 2u * so, 0));
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < W_CH; ++i) {
+        const int r = (t >> 3) + 32 * i;
+        if (W_FULL || r < BCO) rw[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsW, voff_w[i], so, 0));
+      }
+      return;
+    }
     const bool kvalid = ky < d.KH;
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
@@ -267,10 +320,40 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvArgs a, int
   conv_epilogue<T, TO>(a, px, co, acc);
 }
 
+// The LIN gather applies (bf16 checked by the caller): 1x1, pad 0, one un-upsampled source, gate rows 16-B aligned,
+// every tensor within one buffer resource.  HISEG_IGEMM_LIN=0 keeps the general gather (A/B timing and the
+// equivalence test; read per call).
+static bool lin_ok(const ConvArgs& a) {
+  const hiseg_conv2d_desc& d = a.d;
+  const char* e = getenv("HISEG_IGEMM_LIN");
+  if (e && atoi(e) == 0) return false;
+  if (d.KH != 1 || d.KW != 1 || d.pad != 0 || d.Cb != 0 || d.a_up != 1 || d.convT) return false;
+  if (d.in_scale && !a.ins_vec) return false;
+  const long long lim = 0x7fff0000ll;
+  if ((long long)d.N * a.Hs * a.Ws * d.a_cstride * 2 >= lim) return false;
+  if ((long long)d.Cout_pad * d.K_pad * 2 >= lim) return false;
+  if (d.in_scale && (long long)d.N * d.Ca * 4 >= lim) return false;
+  return true;
+}
+
 template <typename T, typename TO, int BCO, int BPX, int WCO, int WPX>
 static int launch_cfg(const ConvArgs& a, hipStream_t s, int splits) {
   dim3 grid((a.M + BPX - 1) / BPX, (a.d.Cout_pad + BCO - 1) / BCO, splits > 1 ? splits : 1);
   const size_t lds = 2u * (BCO + BPX) * 8u * 16u;
+  if constexpr (sizeof(T) == 2) {
+    if (lin_ok(a)) {
+      if (splits > 1) {
+        hipLaunchKernelGGL((conv_igemm_kernel<T, TO, BCO, BPX, WCO, WPX, true, true>), grid, dim3(256), lds, s, a);
+        const int r = hiseg_check_launch("conv_igemm_splitk");
+        if (r) return r;
+        const long long n = (long long)a.M * (a.d.Cout_pad >> 2);
+        hipLaunchKernelGGL((conv_splitk_reduce_kernel<T, TO>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, splits);
+        return hiseg_check_launch("conv_splitk_reduce");
+      }
+      hipLaunchKernelGGL((conv_igemm_kernel<T, TO, BCO, BPX, WCO, WPX, false, true>), grid, dim3(256), lds, s, a);
+      return hiseg_check_launch("conv_igemm");
+    }
+  }
   if (splits > 1) {
     hipLaunchKernelGGL((conv_igemm_kernel<T, TO, BCO, BPX, WCO, WPX, true>), grid, dim3(256), lds, s, a);
     const int r = hiseg_check_launch("conv_igemm_splitk");

@@ -55,6 +55,12 @@ def main():
         same61 = torch.equal(o.t, ref)
         err61 = ((o.t.float() - ref.float()).abs().max() / ref.float().abs().max()).item()
         tg, ts, t0, t61 = timed(gated), timed(scale), timed(un0), timed(un61)
+        os.environ["HISEG_IGEMM_LIN"] = "0"
+        tg_nolin, tgen_nolin = timed(gated), timed(lambda: ops.conv2d(p, xs, out=o, residual=r, variant=-1))
+        os.environ.pop("HISEG_IGEMM_LIN")
+        tgen = timed(lambda: ops.conv2d(p, xs, out=o, residual=r, variant=-1))
+        print(f"{name:24s} generic-kernel gather: gated {tg_nolin:7.1f} -> {tg:7.1f} us, ungated (variant -1) "
+              f"{tgen_nolin:7.1f} -> {tgen:7.1f} us", flush=True)
         print(f"{name:24s} gated {tg:7.1f} us | scale {ts:6.1f} + ungated auto {t0:7.1f} (bits equal {same0}) "
               f"/ ring61 {t61:7.1f} (bits equal {same61}, rel err {err61:.1e})", flush=True)
 
