@@ -36,7 +36,11 @@ typedef unsigned ig_u4 __attribute__((ext_vector_type(4)));
 // offsets + a wave-uniform (SGPR) K-block offset -- the per-block 64-bit (n, y, x) -> address products and bounds
 // checks were most of the gather's VALU work, the SE-gated layers' more.  Rows outside the GEMM and chunks past
 // Cin load zeros through out-of-range offsets; the same values land in LDS as in the general gather.
-template <typename T, typename TO, int BCO, int BPX, int WCO, int WPX, bool SPLIT = false, bool LIN = false>
+// LIN 2 (bf16; any KH x KW <= 32 taps and stride, ungated, one un-upsampled source): each thread stages one chunk
+// column, so its (tap, channel) is per thread -- per K block one byte delta ((ky Ws + kx) Cstride + ci) 2 is added
+// to each row's tap-(0, 0) offset, and a per-row tap mask (bit ky KW + kx: the tap lies inside the image) replaces
+// the bounds checks.
+template <typename T, typename TO, int BCO, int BPX, int WCO, int WPX, bool SPLIT = false, int LIN = 0>
 __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
   constexpr int KCH = Chunk<T>::N;
   constexpr int BK = 8 * KCH;
@@ -97,7 +101,30 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
   const unsigned OOB = 0x80000000u;
   unsigned voff_a[LIN ? A_CH : 1], voff_g[LIN ? A_CH : 1], voff_w[LIN ? W_CH : 1];
   __amdgpu_buffer_rsrc_t rsA, rsG, rsW;
-  if constexpr (LIN) {
+  if constexpr (LIN == 2) {
+    rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(d.srcA), (short)0, 0x7fffffff, 0x00020000);
+    rsW = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(d.weight), (short)0, 0x7fffffff, 0x00020000);
+    const int ci0 = kb0 * BK + c * KCH;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {   // voff_a: tap-(0, 0) byte offset (wrapping); voff_g: the row's tap mask
+      unsigned msk = 0u;
+      if (rn[i] >= 0) {
+        for (int ky2 = 0; ky2 < d.KH; ++ky2)
+          for (int kx2 = 0; kx2 < d.KW; ++kx2) {
+            const int iy = riy[i] + ky2, ix = rix[i] + kx2;
+            if (iy >= 0 && iy < d.H && ix >= 0 && ix < d.W) msk |= 1u << (ky2 * d.KW + kx2);
+          }
+      }
+      voff_g[i] = msk;
+      voff_a[i] = (unsigned)(((rn[i] * a.Hs + riy[i]) * a.Ws + rix[i]) * d.a_cstride + d.a_coff) * 2u;
+    }
+#pragma unroll
+    for (int i = 0; i < W_CH; ++i) {
+      const int r = (t >> 3) + 32 * i;
+      voff_w[i] = co0 + r < d.Cout_pad ? (unsigned)(((co0 + r) * d.K_pad + ci0) * 2) : OOB;
+    }
+  }
+  if constexpr (LIN == 1) {
     rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(d.srcA), (short)0, 0x7fffffff, 0x00020000);
     rsG = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(d.in_scale ? d.in_scale : reinterpret_cast<const float*>(d.srcA)),
                                             (short)0, 0x7fffffff, 0x00020000);
@@ -128,7 +155,25 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
   float4 rg[A_CH][GREG];
   bool rgs[A_CH];
   auto gather = [&](int kb) __attribute__((always_inline)) {
-    if constexpr (LIN) {
+    if constexpr (LIN == 2) {
+      const unsigned so = __builtin_amdgcn_readfirstlane((unsigned)((kb - kb0) * BK * 2));
+      const bool kvalid = ky < d.KH;
+      const int tap = ky * KW + kx;
+      const unsigned delta = (unsigned)((ky * a.Ws + kx) * d.a_cstride + ci) * 2u;
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        const bool ok = kvalid && ((voff_g[i] >> tap) & 1u);
+        ra[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsA, ok ? voff_a[i] + delta : OOB, 0u, 0));
+        rgs[i] = false;
+      }
+#pragma unroll
+      for (int i = 0; i < W_CH; ++i) {
+        const int r = (t >> 3) + 32 * i;
+        if (W_FULL || r < BCO) rw[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsW, voff_w[i], so, 0));
+      }
+      return;
+    }
+    if constexpr (LIN == 1) {
       const unsigned so = __builtin_amdgcn_readfirstlane((unsigned)((kb - kb0) * BK * 2));
       const bool kc = kb * BK + c * KCH < Cin;   // chunks past Cin (the last K block's padding) are zeros
 #pragma unroll
@@ -323,17 +368,22 @@ __global__ void __launch_bounds__(256) conv_splitk_reduce_kernel(ConvArgs a, int
 // The LIN gather applies (bf16 checked by the caller): 1x1, pad 0, one un-upsampled source, gate rows 16-B aligned,
 // every tensor within one buffer resource.  HISEG_IGEMM_LIN=0 keeps the general gather (A/B timing and the
 // equivalence test; read per call).
-static bool lin_ok(const ConvArgs& a) {
+static int lin_ok(const ConvArgs& a) {
   const hiseg_conv2d_desc& d = a.d;
   const char* e = getenv("HISEG_IGEMM_LIN");
-  if (e && atoi(e) == 0) return false;
-  if (d.KH != 1 || d.KW != 1 || d.pad != 0 || d.Cb != 0 || d.a_up != 1 || d.convT) return false;
-  if (d.in_scale && !a.ins_vec) return false;
+  const int mode = e ? atoi(e) : 2;   // 0: general gather, 1: 1x1 only, 2: 1x1 and the tap form
+  if (mode == 0) return 0;
+  if (d.Cb != 0 || d.a_up != 1 || d.convT) return 0;
   const long long lim = 0x7fff0000ll;
-  if ((long long)d.N * a.Hs * a.Ws * d.a_cstride * 2 >= lim) return false;
-  if ((long long)d.Cout_pad * d.K_pad * 2 >= lim) return false;
-  if (d.in_scale && (long long)d.N * d.Ca * 4 >= lim) return false;
-  return true;
+  if ((long long)d.N * a.Hs * a.Ws * d.a_cstride * 2 >= lim) return 0;
+  if ((long long)d.Cout_pad * d.K_pad * 2 >= lim) return 0;
+  if (d.KH == 1 && d.KW == 1 && d.pad == 0) {
+    if (d.in_scale && !a.ins_vec) return 0;
+    if (d.in_scale && (long long)d.N * d.Ca * 4 >= lim) return 0;
+    return 1;
+  }
+  if (mode < 2 || d.in_scale || d.KH * d.KW > 32 || a.Cin % 8) return 0;
+  return 2;
 }
 
 template <typename T, typename TO, int BCO, int BPX, int WCO, int WPX>
@@ -341,16 +391,19 @@ static int launch_cfg(const ConvArgs& a, hipStream_t s, int splits) {
   dim3 grid((a.M + BPX - 1) / BPX, (a.d.Cout_pad + BCO - 1) / BCO, splits > 1 ? splits : 1);
   const size_t lds = 2u * (BCO + BPX) * 8u * 16u;
   if constexpr (sizeof(T) == 2) {
-    if (lin_ok(a)) {
+    const int lin = lin_ok(a);
+    if (lin) {
       if (splits > 1) {
-        hipLaunchKernelGGL((conv_igemm_kernel<T, TO, BCO, BPX, WCO, WPX, true, true>), grid, dim3(256), lds, s, a);
+        if (lin == 1) hipLaunchKernelGGL((conv_igemm_kernel<T, TO, BCO, BPX, WCO, WPX, true, 1>), grid, dim3(256), lds, s, a);
+        else hipLaunchKernelGGL((conv_igemm_kernel<T, TO, BCO, BPX, WCO, WPX, true, 2>), grid, dim3(256), lds, s, a);
         const int r = hiseg_check_launch("conv_igemm_splitk");
         if (r) return r;
         const long long n = (long long)a.M * (a.d.Cout_pad >> 2);
         hipLaunchKernelGGL((conv_splitk_reduce_kernel<T, TO>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, splits);
         return hiseg_check_launch("conv_splitk_reduce");
       }
-      hipLaunchKernelGGL((conv_igemm_kernel<T, TO, BCO, BPX, WCO, WPX, false, true>), grid, dim3(256), lds, s, a);
+      if (lin == 1) hipLaunchKernelGGL((conv_igemm_kernel<T, TO, BCO, BPX, WCO, WPX, false, 1>), grid, dim3(256), lds, s, a);
+      else hipLaunchKernelGGL((conv_igemm_kernel<T, TO, BCO, BPX, WCO, WPX, false, 2>), grid, dim3(256), lds, s, a);
       return hiseg_check_launch("conv_igemm");
     }
   }

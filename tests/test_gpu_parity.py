@@ -1275,39 +1275,46 @@ def test_conv3x3_small_image_splitk(shape):
     assert torch.equal(o1[0], ops.conv2d(p, xa, residual=R, split_k_3x3=True).to_nchw()[0])
 
 
-LIN_CASES = {  # (N, Ca, Cout, H, W, stride, SE gate, residual): 1x1 layers of the generic kernel
+LIN_CASES = {  # (N, Ca, Cout, H, W, stride, SE gate, residual[, k]): layers of the generic kernel
     "b7_proj_2304to384_gated_split": (4, 2304, 384, 20, 20, 1, True, True),
     "gated_480to80": (2, 480, 80, 24, 20, 1, True, True),
     "ragged_k_200to72": (2, 200, 72, 13, 11, 1, False, False),
     "stride2_96to40": (2, 96, 40, 17, 15, 2, False, True),
     "narrow_64to16": (2, 64, 16, 30, 30, 1, False, False),
     "expand_160to960": (2, 160, 960, 12, 10, 1, False, False),
+    "k3_72to72": (2, 72, 72, 16, 12, 1, False, True, 3),          # the B1 EnhancedUNet's 72-channel 3x3 class
+    "k3_144to144": (2, 144, 144, 11, 9, 1, False, False, 3),
+    "k3_s2_40to96": (2, 40, 96, 15, 13, 2, False, False, 3),      # chunks cross taps inside a K block
+    "k5_24to32": (2, 24, 32, 10, 14, 1, False, False, 5),
+    "k3_768to768_split": (2, 768, 768, 16, 12, 1, False, False, 3),
 }
 
 
 @pytest.mark.parametrize("name", sorted(LIN_CASES))
 def test_igemm_linear_gather_bit_identical(name, monkeypatch):
-    """The generic kernel's 1x1 gather through per-chunk buffer offsets + a K-block SGPR offset (HISEG_IGEMM_LIN,
-    default on) loads the same activations, gates and weights as the (n, y, x) gather (=0): equal outputs, for the
-    forced generic kernel (-1), the split-K form (99, where the layer splits) and the automatic choice (0) --
-    ragged last K block, stride 2, SE gate, residual, every tile width."""
+    """The generic kernel's buffer-offset gathers (HISEG_IGEMM_LIN=2, the default: 1x1 layers through per-chunk
+    offsets + a K-block SGPR offset; k x k layers through a per-thread tap delta + per-row tap masks) load the same
+    activations, gates and weights as the (n, y, x) gather (=0): equal outputs, for the forced generic kernel (-1),
+    the split-K form (99, where the layer splits) and the automatic choice (0) -- ragged last K block, chunks crossing
+    taps, stride 2, SE gate, residual, every tile width."""
     from hiseg import ops
-    N, Ca, Cout, H, W, stride, ins, res = LIN_CASES[name]
+    N, Ca, Cout, H, W, stride, ins, res = LIN_CASES[name][:8]
+    k = LIN_CASES[name][8] if len(LIN_CASES[name]) > 8 else 1
     dt = torch.bfloat16
     g = torch.Generator(device=DEV).manual_seed(23)
     xa = ops.Act.from_nchw(torch.randn(N, Ca, H, W, device=DEV, generator=g), dt)
-    w = torch.randn(Cout, Ca, 1, 1, device=DEV, generator=g) / Ca ** 0.5
+    w = torch.randn(Cout, Ca, k, k, device=DEV, generator=g) / (Ca * k * k) ** 0.5
     p = ops.pack_conv(w, torch.randn(Cout, device=DEV, generator=g) * 0.1, None, 1, dt, DEV,
-                      stride=stride, pad=0)
+                      stride=stride, pad=k // 2)
     gate = torch.rand(N, p.ca, device=DEV, generator=g) if ins else None
-    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    Ho, Wo = (H + 2 * (k // 2) - k) // stride + 1, (W + 2 * (k // 2) - k) // stride + 1
     R = ops.Act.from_nchw(torch.randn(N, Cout, Ho, Wo, device=DEV, generator=g), dt) if res else None
     variants = (-1, 99, 0) if name.endswith("_split") else (-1, 0)
     for v in variants:
         outs = []
-        for lin in ("1", "0"):
+        for lin in ("2", "0"):
             monkeypatch.setenv("HISEG_IGEMM_LIN", lin)
-            y = ops.conv2d(p, xa, residual=R, in_scale=gate, variant=v)
+            y = ops.conv2d(p, xa, residual=R, in_scale=gate, variant=v, split_k_3x3=(k == 3))
             torch.cuda.synchronize()
             outs.append(y.to_nchw().float())
         assert torch.isfinite(outs[0]).all()
