@@ -446,7 +446,8 @@ static int launch_typed(const ConvArgs& a, hipStream_t s, int splits = 1) {
     if (splitk_bco(a.d.Cout_pad) == 128) return launch_cfg<T, TO, 128, 128, 2, 2>(a, s, splits);
     return launch_cfg<T, TO, 64, 128, 2, 2>(a, s, splits);
   }
-  switch (igemm_bco(a.d.Cout_pad)) {
+  const char* eb = getenv("HISEG_IGEMM_BCO");   // A/B timing: force the Cout tile (read per call)
+  switch (eb ? atoi(eb) : igemm_bco(a.d.Cout_pad)) {
     case 128: return launch_cfg<T, TO, 128, 128, 2, 2>(a, s, splits);
     case 64: return launch_cfg<T, TO, 64, 128, 2, 2>(a, s, splits);
     case 32: return launch_cfg<T, TO, 32, 256, 1, 4>(a, s, splits);
