@@ -643,6 +643,22 @@ def load_class_traffic(leg):
         return {}
 
 
+_SLEEP_CYCLES_PER_MS = None
+
+
+def _gpu_lead(ms):
+    """Queue a GPU spin of about `ms` milliseconds on the current stream (torch.cuda._sleep, calibrated once)."""
+    global _SLEEP_CYCLES_PER_MS
+    if _SLEEP_CYCLES_PER_MS is None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        torch.cuda._sleep(10_000_000)
+        e1.record()
+        torch.cuda.synchronize()
+        _SLEEP_CYCLES_PER_MS = 10_000_000 / max(e0.elapsed_time(e1), 1e-3)
+    torch.cuda._sleep(int(ms * _SLEEP_CYCLES_PER_MS))
+
+
 def call_profile(step, leg=None):
     """One extra (untimed) step with HIP events around every libhiseg C-ABI call on its launch stream:
     per-entry-point GPU time; per kernel class (conv forward / data gradient / weight gradient over all layers,
@@ -652,6 +668,7 @@ def call_profile(step, leg=None):
     from hiseg import _lib as L
     lib = L.lib()
     real, rec = {}, []
+    last_path = lib.hiseg_wgrad_last_path
     names = [n for n in (L.EXPORTED or []) if n.startswith("hiseg_")]
     for name in names:
         fn = getattr(lib, name, None)
@@ -671,6 +688,8 @@ def call_profile(step, leg=None):
                     "dgrad" if sys._getframe(1).f_code.co_name == "_dgrad_launch" else "fwd")
                 key = (f"{kind} {d.KH}x{d.KW}{' T' if d.convT else ''} {d.Ca}+{d.Cb}->{d.Cout} "
                        f"{d.N}x{d.Ho}x{d.Wo}")
+                if kind == "wgrad":   # which kernel took it (wide / transposed-read / generic fallback / f32)
+                    key += f" [{L.WGRAD_PATHS[last_path()]}]"
                 cls = {"fwd": "conv forward", "dgrad": "conv data gradient", "wgrad": "conv weight gradient"}[kind]
                 flops = _conv_flops(d)
             elif cls is not None:
@@ -678,16 +697,31 @@ def call_profile(step, leg=None):
             rec.append((_n, key, cls, flops, nbytes, e0, e1))
             return r
         setattr(lib, name, wrap)
+    # one unprofiled eager step first: the timed legs replay graphs from their own memory pools, so the first eager
+    # step after them meets a cold caching allocator (device allocations -- and frees of cached blocks, which
+    # synchronise the device -- inside the step, each one draining the GPU's lead over the host)
+    step()
+    torch.cuda.synchronize()
     try:
+        L.wgrad_path_stats(reset=True)
+        torch.cuda.synchronize()
+        # An eager step's Python enqueue can be as long as its GPU work (C3 / C4: ~30 ms per ~40), and an event
+        # pair brackets GPU time only while the host stays ahead of the GPU: with an idle queue the interval holds
+        # the host's own gap (an allocator call, the next descriptor's build).  A GPU spin queued first gives the
+        # host that lead, so every interval -- and the step -- is kernel time.
+        _gpu_lead(float(os.environ.get("HISEG_PROFILE_LEAD_MS", "250")))
         t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0.record()
         step()
         t1.record()
+        host_done = time.perf_counter()
         torch.cuda.synchronize()
+        lead_left_ms = (time.perf_counter() - host_done) * 1e3
     finally:
         for name, fn in real.items():
             setattr(lib, name, fn)
     step_ms = t0.elapsed_time(t1)
+    paths = L.wgrad_path_stats()
     by_entry, groups, classes = {}, {}, {}
     for n, k, cls, fl, nb, e0, e1 in rec:
         ms = e0.elapsed_time(e1)
@@ -706,6 +740,9 @@ def call_profile(step, leg=None):
                 c["bytes_ms"] += ms
     conv_ms = sum(g[1] for g in groups.values())
     out = {"step_ms_probed": round(step_ms, 3),
+           # > step_ms: the GPU was still working when the host finished enqueueing, so no interval held host time
+           "host_lead_left_ms": round(lead_left_ms, 3),
+           "wgrad_paths": paths,
            "c_abi_calls": len(rec),
            "conv_share": round(conv_ms / step_ms, 4) if step_ms > 0 else None,
            "top_entry_points_ms": {n: round(ms, 3) for n, ms in sorted(by_entry.items(), key=lambda kv: -kv[1])[:6]}}

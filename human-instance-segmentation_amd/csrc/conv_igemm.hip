@@ -538,6 +538,9 @@ extern "C" long long hiseg_conv2d_workspace_bytes(const hiseg_conv2d_desc* d) {
   a.Hs = d->H / (d->a_up > 0 ? d->a_up : 1);
   a.Ws = d->W / (d->a_up > 0 ? d->a_up : 1);
   if (conv_pw_applies(a)) return 0;
+  // an SE-gated 1x1 layer whose gate table exceeds the pointwise kernel's LDS runs in image ranges on that kernel
+  // (conv2d_impl), never on the split-K path
+  if (d->in_scale && d->KH == 1 && d->KW == 1 && conv_pw_gate_images(a) > 0) return 0;
   return splitk_bytes(a, splitk_plan(a));
 }
 

@@ -1032,11 +1032,19 @@ extern "C" int hiseg_dw_gap_tiles(int N, int Ho, int Wo) {
 }
 
 // Which depthwise kernel takes a layer: the LDS-tiled one for bf16 layers of 192..2047 channels, stride 1 or k5.
+// HISEG_DWCONV_Q=0: the round-2 v5 bf16 kernel (8 channels per thread, weights re-read per strip), A/B only.  It
+// also turns the tiles off, so hiseg_dw_gap_parts (the SE-pool partial count callers size buffers by) and
+// dwconv_launch always agree on the kernel.
+static bool dw_q_enabled() {
+  const char* e = getenv("HISEG_DWCONV_Q");
+  return !(e && atoi(e) == 0);
+}
+
 static bool dw_use_tiles(int dtype, int C, int K, int stride) {
   // HISEG_DWCONV_T: 0 never, 2 every bf16 layer (A/B timing, the bit-identity test); read per call
   const char* e = getenv("HISEG_DWCONV_T");
   const int m = e ? atoi(e) : 1;
-  if (dtype != HISEG_BF16 || m == 0) return false;
+  if (dtype != HISEG_BF16 || m == 0 || !dw_q_enabled()) return false;
   // tools/dw_bench.py (profiles/r4_dw_bench.txt): the tiles win on the 240..1344-channel stride-1 layers and the k5
   // stride-2 one; the gather kernel on the narrow layers, the k3 stride-2 one and the 20 x 20 x >= 2304-channel ones
   return m == 2 || (C >= 192 && C < 2048 && (stride == 1 || K == 5));
@@ -1082,14 +1090,13 @@ static int dwconv_launch(int dtype, const void* in, int N, int H, int W, int C, 
   const int tiles = hiseg_dw_gap_tiles(N, Ho, Wo);
   dim3 grid(tiles, N, (nch + 255) / 256);
   dim3 gridq(tiles, N, (nq + ctq - 1) / ctq);
-  // HISEG_DWCONV_Q=0: the round-2 v5 bf16 kernel (8 channels per thread, weights re-read per strip), A/B only
-  static const bool dwq = [] { const char* e = getenv("HISEG_DWCONV_Q"); return !(e && atoi(e) == 0); }();
+  const bool dwq = dw_q_enabled();
   const bool dwt = dw_use_tiles(dtype, C, K, stride);
   const int tiles2 = ((Ho + kDwTH - 1) / kDwTH) * ((Wo + kDwTW - 1) / kDwTW);
   const dim3 gridt(tiles2, N, (C + kDwCG - 1) / kDwCG);
 #define DW_L(KS, ST)                                                                                          \
   do {                                                                                                        \
-    if (dtype == HISEG_BF16 && dwt && dwq) {                                                                  \
+    if (dtype == HISEG_BF16 && dwt) {                                                                         \
       dw_t_attr<KS, ST>();                                                                                    \
       hipLaunchKernelGGL((dwconv_t_kernel<KS, ST>), gridt, dim3(256), dw_lds(KS, ST), s, in, H, W, C, w,      \
                          scale, shift, act, out, Ho, Wo, gap);                                                \

@@ -17,6 +17,7 @@
 // 128-channel multiples; every other bf16 layer (GEMM-bias columns and ConvTranspose included) takes
 // conv_wgrad_tr_kernel below (LDS-DMA + ds_read_b64_tr_b16, 4.5x faster on the ROI head's 256-channel 3x3
 // layers).
+#include <atomic>
 #include <cstdlib>
 
 #include "conv_common.h"
@@ -275,7 +276,12 @@ __device__ __forceinline__ v4s_t tr_read(unsigned byte_addr) {
 // (n, y, x) -> offset products
 // TOG (STAGES == 2): image-major ring (X of stage s at s IMG, dY at (2 + s) IMG, so the stage is address bit 14) and
 // per-lane fragment-read addresses in registers, flipped once per stage (wgrad_wide.hip's TOG)
-template <int BC, int WK, int WC, int STAGES, bool INC = false, bool TOG = false>
+// XR: two X buffer resources, one per source (x_tile_src 2: the sources lie too far apart for one 2^31-byte
+// resource).  A lane's chunk belongs to one source for the whole kernel, so each X DMA runs once under the exec mask
+// of source-A lanes and once under source-B lanes: masked-off lanes write nothing to LDS, the lanes of a row still
+// fill its 256 B, and the tiles may mix the two sources as in the one-resource mode -- same tiles, same per-element
+// accumulation order, so the result does not depend on where the allocator put the two tensors.
+template <int BC, int WK, int WC, int STAGES, bool INC = false, bool TOG = false, bool XR = false>
 __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
   constexpr int BK = 128, PB = 64;
   constexpr int TM = BK / (WK * 16), TN = BC / (WC * 16);
@@ -309,11 +315,13 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
   // upsampling shift
   const char* const pa = reinterpret_cast<const char*>(d.srcA);
   const char* const pb = d.Cb ? reinterpret_cast<const char*>(d.srcB) : pa;
-  const bool tile_a = d.Cb == 0 || k0 % a.Cin < d.Ca;   // (x_tile_src: the K tile's one source)
-  const char* const xbase = a.x_tile_src ? (tile_a ? pa : pb) : (pa < pb ? pa : pb);
+  const bool tile_a = d.Cb == 0 || k0 % a.Cin < d.Ca;   // (x_tile_src 1: the K tile's one source)
+  const char* const xbase = XR ? pa : a.x_tile_src ? (tile_a ? pa : pb) : (pa < pb ? pa : pb);
   const unsigned dA = a.x_tile_src ? 0u : (unsigned)(pa - xbase), dB = a.x_tile_src ? 0u : (unsigned)(pb - xbase);
   const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(xbase), (short)0, 0x7fffffff,
                                                                        0x00020000);
+  const __amdgpu_buffer_rsrc_t rXb = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(pb), (short)0, 0x7fffffff,
+                                                                        0x00020000);
   const __amdgpu_buffer_rsrc_t rY = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.dy), (short)0, 0x7fffffff,
                                                                        0x00020000);
   const unsigned OOB = 0x80000000u;
@@ -325,6 +333,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
   int pn[4], py[4], px[4], pp[4];       // pixel (n, oy, ox) and flat index of the lane's row
   int yq[4];                            // ConvTranspose: the column's sub-pixel q (output pixel 2y + q/2, 2x + q%2)
   unsigned bias_lanes = 0;              // bit i: this lane's chunk of instruction i is the GEMM-bias column's
+  unsigned b_lanes = 0;                 // XR, bit i: this lane's chunk of instruction i reads source B
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int r = 4 * (w + 4 * i) + (lane >> 4);
@@ -337,6 +346,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
     xcs[i] = la ? d.a_cstride : d.b_cstride;
     xsh[i] = (la && d.a_up == 2) ? 1 : 0;
     xd[i] = la ? dA : dB;
+    if (!la) b_lanes |= 1u << i;
     if (a.want_bias && k == a.Ktot) bias_lanes |= 1u << i;
     ky[i] = tap / d.KW;
     kx[i] = tap - ky[i] * d.KW;
@@ -375,6 +385,15 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
   auto yoff = [&](int s) __attribute__((always_inline)) -> unsigned {
     return (unsigned)(TOG ? (STAGES + s) * IMG : s * STAGE + IMG);
   };
+  // the X DMA of instruction i (XR: from the lane's source's resource, under that source's lanes)
+  auto dma_x = [&](int i, unsigned lds_addr, unsigned voff) __attribute__((always_inline)) {
+    if constexpr (XR) {
+      if (b_lanes & (1u << i)) wg_dma16(rXb, lds_addr, voff);
+      else wg_dma16(rX, lds_addr, voff);
+    } else {
+      wg_dma16(rX, lds_addr, voff);
+    }
+  };
   auto issue = [&](int s) __attribute__((always_inline)) {
     const unsigned sb = lds_base + xoff(s), sby = lds_base + yoff(s);
 #pragma unroll
@@ -384,7 +403,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
         const int iy = py[i] - d.pad + ky[i];
         const int ix = px[i] - d.pad + kx[i];
         const bool okx = xo[i] >= 0 && pp[i] < a.M && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
-        wg_dma16(rX, sb + row_base, okx ? ob[i] : OOB);
+        dma_x(i, sb + row_base, okx ? ob[i] : OOB);
         const bool oky = yo[i] >= 0 && pp[i] < a.M;
         wg_dma16(rY, sby + row_base, oky ? yb[i] + 2u * (unsigned)yo[i] : OOB);
         ob[i] += (unsigned)xcs[i] * (2u * PB);
@@ -402,7 +421,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
       const int sh = xsh[i], Hs = d.H >> sh, Ws = d.W >> sh;
       const unsigned offx =
           okx ? xd[i] + (unsigned)((((pn[i] * Hs + (iy >> sh)) * Ws + (ix >> sh)) * xcs[i] + xo[i]) * 2) : OOB;
-      wg_dma16(rX, sb + row_base, offx);
+      dma_x(i, sb + row_base, offx);
       const bool oky = yo[i] >= 0 && pp[i] < a.M;
       int yp = pp[i];
       if (d.convT)   // the dY pixel of sub-pixel q: (n, 2y + q/2, 2x + q%2) of the 2H x 2W output grid
@@ -522,10 +541,10 @@ __global__ void __launch_bounds__(256) conv_wgrad_tr_kernel(WgradArgs a) {
   }
 }
 
-template <int BC, int WK, int WC, int STAGES, bool INC = false, bool TOG = false>
+template <int BC, int WK, int WC, int STAGES, bool INC = false, bool TOG = false, bool XR = false>
 static int wgrad_tr_launch(const WgradArgs& a, hipStream_t s) {
   const size_t lds = (size_t)STAGES * 2 * 64 * 256;
-  auto kern = conv_wgrad_tr_kernel<BC, WK, WC, STAGES, INC, TOG>;
+  auto kern = conv_wgrad_tr_kernel<BC, WK, WC, STAGES, INC, TOG, XR>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -565,12 +584,12 @@ static int wgrad_tr_try(const WgradArgs& a, hipStream_t s) {
     const long long pa = (long long)(uintptr_t)d.srcA, pb = (long long)(uintptr_t)d.srcB;
     const long long lo = pa < pb ? pa : pb;
     if (pa - lo + span_a >= 0x7fffffffll || pb - lo + span_b >= 0x7fffffffll || hiseg_force_far()) {
-      // A ends on a 128-column tile boundary and (with more than one tap) so does each tap
-      hiseg_note_placement(d.Ca % 128 == 0 && (d.KH * d.KW == 1 || d.Cb % 128 == 0)
-                               ? "wgrad_tr: one source per tile (sources far apart)"
-                               : "wgrad_tr declined -> register-transpose kernel (sources far apart)", &d);
-      if (!(d.Ca % 128 == 0 && (d.KH * d.KW == 1 || d.Cb % 128 == 0))) return 0;
-      b.x_tile_src = 1;
+      // A ends on a 128-column tile boundary and (with more than one tap) so does each tap: one source per tile;
+      // else one resource per source, chosen per lane (XR)
+      const bool aligned = d.Ca % 128 == 0 && (d.KH * d.KW == 1 || d.Cb % 128 == 0);
+      hiseg_note_placement(aligned ? "wgrad_tr: one source per tile (sources far apart)"
+                                   : "wgrad_tr: one resource per source (sources far apart)", &d);
+      b.x_tile_src = aligned ? 1 : 2;
     }
   }
   // incremental DMA offsets (INC above; HISEG_WGRAD_INC=0 for A/B timing, read per call)
@@ -578,6 +597,15 @@ static int wgrad_tr_try(const WgradArgs& a, hipStream_t s) {
   const bool inc = !(e && atoi(e) == 0) && !d.convT && d.stride == 1 && d.a_up == 1 && d.Ho == d.H && d.Wo == d.W;
   const char* et = getenv("HISEG_WGRAD_TOG");   // flipped fragment-read registers (TOG above; 0 for A/B timing)
   const bool tog = !(et && atoi(et) == 0);
+  if (b.x_tile_src == 2) {
+    const int r = inc && b.Cg >= 128 ? wgrad_tr_launch<128, 2, 2, 2, true, true, true>(b, s)
+                : inc && b.Cg >= 64  ? wgrad_tr_launch<64, 4, 1, 2, true, true, true>(b, s)
+                : b.Cg >= 128 ? wgrad_tr_launch<128, 2, 2, 2, false, false, true>(b, s)
+                : b.Cg >= 64  ? wgrad_tr_launch<64, 4, 1, 2, false, false, true>(b, s)
+                : b.Cg >= 32  ? wgrad_tr_launch<32, 4, 1, 2, false, false, true>(b, s)
+                              : wgrad_tr_launch<16, 4, 1, 2, false, false, true>(b, s);
+    return r < 0 ? r : 1;
+  }
   const int r = inc && tog && b.Cg >= 128 ? wgrad_tr_launch<128, 2, 2, 2, true, true>(b, s)
               : inc && tog && b.Cg >= 64  ? wgrad_tr_launch<64, 4, 1, 2, true, true>(b, s)
               : inc && b.Cg >= 128 ? wgrad_tr_launch<128, 2, 2, 2, true>(b, s)
@@ -604,6 +632,24 @@ static int wgrad_typed(const WgradArgs& a, hipStream_t s) {
   if (a.Cg >= 64) return wgrad_launch<T, 128, 64, 2, 2>(a, s);
   if (a.Cg >= 32) return wgrad_launch<T, 128, 32, 2, 2>(a, s);
   return wgrad_launch<T, 64, 16, 4, 1>(a, s);
+}
+
+// Which kernel took each weight gradient (hiseg_wgrad_path_stats, hiseg_wgrad_last_path): the wide tile, the
+// transposed-read tile, the generic register-transpose kernel in bf16 (a fallback: HISEG_LOG_WGRAD=1 names the
+// layer), or the f32 kernel (parity mode, by design).
+static std::atomic<long long> g_wgrad_paths[4];
+static thread_local int g_wgrad_last = -1;
+
+static void wgrad_note_path(int path, const hiseg_conv2d_desc* d, int dy_cs, int dy_coff) {
+  g_wgrad_paths[path].fetch_add(1);
+  g_wgrad_last = path;
+  static const bool log = getenv("HISEG_LOG_WGRAD") != nullptr;
+  if (log && path == HISEG_WGRAD_PATH_GENERIC)
+    fprintf(stderr,
+            "[hiseg wgrad] generic kernel: %d+%d -> %d, %dx%d taps s%d p%d, N %d %dx%d -> %dx%d, convT %d up %d, "
+            "A %p cs %d off %d, B %p cs %d off %d, dy cs %d off %d\n",
+            d->Ca, d->Cb, d->Cout, d->KH, d->KW, d->stride, d->pad, d->N, d->H, d->W, d->Ho, d->Wo, d->convT, d->a_up,
+            d->srcA, d->a_cstride, d->a_coff, d->srcB, d->b_cstride, d->b_coff, dy_cs, dy_coff);
 }
 
 static int wgrad_geometry(const hiseg_conv2d_desc* d, int want_bias, int* Cg, int* Kg, int* splits, int* M,
@@ -668,11 +714,28 @@ extern "C" int hiseg_conv2d_wgrad(const hiseg_conv2d_desc* fwd, const void* dy, 
   a.ws = ws;
   hipStream_t s = (hipStream_t)stream;
   const int rw = wgrad_wide_try(a, s);
-  if (rw != 0) return rw < 0 ? rw : HISEG_OK;
+  if (rw != 0) {
+    if (rw > 0) wgrad_note_path(HISEG_WGRAD_PATH_WIDE, fwd, dy_cstride, dy_coff);
+    return rw < 0 ? rw : HISEG_OK;
+  }
   const int rt = wgrad_tr_try(a, s);
-  if (rt != 0) return rt < 0 ? rt : HISEG_OK;
+  if (rt != 0) {
+    if (rt > 0) wgrad_note_path(HISEG_WGRAD_PATH_TR, fwd, dy_cstride, dy_coff);
+    return rt < 0 ? rt : HISEG_OK;
+  }
+  wgrad_note_path(fwd->dtype == HISEG_BF16 ? HISEG_WGRAD_PATH_GENERIC : HISEG_WGRAD_PATH_F32, fwd, dy_cstride, dy_coff);
   return fwd->dtype == HISEG_BF16 ? wgrad_typed<bf16_t>(a, s) : wgrad_typed<float>(a, s);
 }
+
+extern "C" int hiseg_wgrad_path_stats(long long* counts, int reset) {
+  for (int i = 0; i < 4; ++i) {
+    if (counts) counts[i] = g_wgrad_paths[i].load();
+    if (reset) g_wgrad_paths[i] = 0;
+  }
+  return HISEG_OK;
+}
+
+extern "C" int hiseg_wgrad_last_path(void) { return g_wgrad_last; }
 
 // A block = 64 column quads (4 consecutive K columns of one GEMM column j each) x 4 split groups: group g sums splits
 // g, g + 4, ... with eight float4 loads in flight, the groups are combined in LDS in a fixed order, then the quad's

@@ -14,8 +14,9 @@ struct WgradArgs {
   int Cg, Kg;
   int splits, blocks_per_split;  // pixel blocks per split
   float* ws;
-  int x_tile_src;  // transposed-read kernel: 1 = one X source per K tile (two sources too far apart for one
-                   // buffer resource; the layer's tiles never mix them), 0 = per-lane source over one resource
+  int x_tile_src;  // transposed-read kernel: 0 = per-lane source over one resource spanning both; two sources
+                   // too far apart for one 2^31-byte resource: 1 = one X source per K tile (the layer's tiles never
+                   // mix them), 2 = one resource per source, chosen per lane (conv_wgrad_tr_kernel's XR)
 };
 
 }  // namespace hiseg

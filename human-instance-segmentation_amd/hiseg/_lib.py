@@ -283,6 +283,8 @@ def _declare(lib):
         # ---- training (include/hiseg_train.h, hiseg_head_train.h, hiseg_loss.h)
         "hiseg_conv2d_wgrad_dims": ([ctypes.POINTER(Conv2dDesc), c_int, P, P, P], c_int),
         "hiseg_conv2d_wgrad": ([ctypes.POINTER(Conv2dDesc), P, c_int, c_int, c_int, P, c_int, P], c_int),
+        "hiseg_wgrad_path_stats": ([ctypes.POINTER(c_ll), c_int], c_int),
+        "hiseg_wgrad_last_path": ([], c_int),
         "hiseg_conv2d_wgrad_reduce": ([P, c_int, ctypes.POINTER(WgradMap), P, P, c_int, P], c_int),
         "hiseg_pack_weights": ([P, c_int, c_int, P], c_int),
         "hiseg_bn_partials": ([], c_int),
@@ -406,6 +408,17 @@ def placement_stats(reset: bool = False):
     a, b = c_ll(), c_ll()
     check(lib().hiseg_placement_stats(ctypes.byref(a), ctypes.byref(b), int(reset)), "placement_stats")
     return a.value, b.value
+
+
+WGRAD_PATHS = ("wide", "transposed_read", "generic_bf16", "f32")
+
+
+def wgrad_path_stats(reset: bool = False) -> dict:
+    """How many weight gradients each kernel computed since the last reset (include/hiseg_train.h):
+    the wide tile, the transposed-read tile, the generic bf16 fallback, the f32 (parity) kernel."""
+    c = (c_ll * 4)()
+    check(lib().hiseg_wgrad_path_stats(c, int(reset)), "wgrad_path_stats")
+    return dict(zip(WGRAD_PATHS, (int(v) for v in c)))
 
 
 def stream_ptr(device=None) -> int:

@@ -37,6 +37,7 @@ from __future__ import annotations
 
 import json
 import threading
+import weakref
 from typing import Dict, List, Sequence, Tuple
 
 import torch
@@ -112,10 +113,16 @@ def _run_on(spec: dict, state: Sequence[Tensor], skip: str, fn):
     from torch.nn.utils.stateless import _reparametrize_module
     ident = tuple(t.data_ptr() for t in state)
     with lock:
-        if m.__dict__.get("_hiseg_state_ident") != ident:   # another program's weights: no plan carries over
+        # The plans (packed weights) are keyed on the state's addresses.  Weak references tell whether the tensors
+        # that owned them are still alive: if any died, the same address may now hold another program's weights, so
+        # nothing carries over.  A released program's weights are not pinned by the skeleton.
+        refs = m.__dict__.get("_hiseg_state_refs")
+        same = (m.__dict__.get("_hiseg_state_ident") == ident and refs is not None
+                and all(r() is not None for r in refs))
+        if not same:
             m.__dict__.pop("_hiseg_plans", None)
             m.__dict__["_hiseg_state_ident"] = ident
-            m.__dict__["_hiseg_state_held"] = list(state)   # keeps these addresses from being reused meanwhile
+            m.__dict__["_hiseg_state_refs"] = [weakref.ref(t) for t in state]
         with _reparametrize_module(m, dict(zip(names, state))):
             return fn(m)
 

@@ -288,6 +288,9 @@ class Tape:
 
     def __init__(self, S: TrainState):
         self.S = S
+        # a forward that raised before flush_counters left its BatchNorm counters queued: drop them, so the
+        # next forward advances each num_batches_tracked once, as torch does
+        S.nbt = []
         self.ops: List[Callable[[], None]] = []
         self.grads: Dict[int, Act] = {}
         self.written: Dict[int, bool] = {}

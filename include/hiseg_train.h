@@ -32,6 +32,15 @@ extern "C" {
 int hiseg_conv2d_wgrad_dims(const hiseg_conv2d_desc* fwd, int want_bias, int* Cg, int* Kg, int* splits);
 int hiseg_conv2d_wgrad(const hiseg_conv2d_desc* fwd, const void* dy, int dy_cstride, int dy_coff,
                        int want_bias, float* ws, int splits, hiseg_stream_t stream);
+/* Which kernel computed each weight gradient since the last reset: counts[4] indexed by
+ * HISEG_WGRAD_PATH_* (wide 256x256 tile, transposed-read tile, generic bf16 fallback, f32).
+ * hiseg_wgrad_last_path: the path of this thread's last hiseg_conv2d_wgrad (-1 before any). */
+#define HISEG_WGRAD_PATH_WIDE 0
+#define HISEG_WGRAD_PATH_TR 1
+#define HISEG_WGRAD_PATH_GENERIC 2
+#define HISEG_WGRAD_PATH_F32 3
+int hiseg_wgrad_path_stats(long long* counts, int reset);
+int hiseg_wgrad_last_path(void);
 
 /* Sum the split partials and scatter into the reference parameter layouts (f32):
  *   conv : gw[co][ci][ky][kx]  ([Cout][Cin][KH][KW], Cin = ca_real + cb_real), gb[co]
@@ -72,10 +81,14 @@ int hiseg_pack_weights(const hiseg_pack_entry* table_dev, int n, int max_total, 
  * eps 1e-5, momentum 0.1): batch statistics over N*H*W, running-stat update with the
  * unbiased variance, then y = act(z*scale + shift [+ residual]) * chan_mul[n][c].
  * -------------------------------------------------------------------------------------- */
-int hiseg_bn_partials(void);   /* number of pixel splits used by the statistics kernels */
+/* Upper bound on the pixel splits of the statistics / backward-reduce kernels: size `partial`
+ * buffers by it.  The split count actually used depends on P (adaptive, >= 32 pixels per split);
+ * hiseg_bn_stats writes, and hiseg_bn_finalize merges, exactly that count for the same P, so a
+ * caller must not fill `partial` itself and hand it to hiseg_bn_finalize. */
+int hiseg_bn_partials(void);
 int hiseg_bn_stats(int dtype, const void* z, long long P, int C, int cstride, int coff, float* partial,
                    hiseg_stream_t stream);
-/* partial [splits][3][C] -> mean/invstd [C], scale/shift [C] (fold of gamma/beta), running update. */
+/* partial [splits(P)][3][C], as written by hiseg_bn_stats for the same P -> mean/invstd [C], scale/shift [C] (fold of gamma/beta), running update. */
 int hiseg_bn_finalize(const float* partial, int C, long long P, const float* gamma, const float* beta, float eps,
                       float momentum, float* running_mean, float* running_var, float* mean, float* invstd,
                       float* scale, float* shift, hiseg_stream_t stream);

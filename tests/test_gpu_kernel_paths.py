@@ -1,0 +1,88 @@
+"""Which weight-gradient kernel every layer of every train leg takes.
+
+The driver's round-4 C4 record showed one layer class at 2.56 ms per launch, and the builder's trace held generic
+`conv_wgrad_kernel<bf16>` launches no per-layer list explained: a concat layer (the EnhancedUNet decoders' up ++ skip,
+the smp decoder's upsampled conv1) whose two sources the caching allocator happened to place more than 2 GiB apart
+was declined by the transposed-read tile (one buffer resource over both sources) and fell back to the generic
+kernel, 10-80x slower.  The tile now takes such layers with one resource per source.  Here every two-source layer is
+forced onto that far-apart path (HISEG_PLACEMENT_FAR=1, read once per process, hence the subprocess) and one bf16
+train step of the B0 / B1-enhanced / B7-ultra presets and one distillation step with all seven encoder stages
+trainable must run no weight gradient on the generic bf16 kernel (`hiseg_wgrad_path_stats`)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+_SCRIPT = r"""
+import json, sys
+import torch
+import torch.nn as nn
+sys.path[:0] = [sys.argv[1] + "/human-instance-segmentation_amd", sys.argv[1] + "/tests/golden", sys.argv[1] + "/tests",
+                sys.argv[1]]
+import filler
+import hiseg
+from hiseg import _lib as L
+from helpers import configs, hiseg_kwargs
+DEV = "cuda"
+out = {}
+images = torch.from_numpy(filler.uniform(71, (2, 3, 96, 128))).to(DEV)
+rois = torch.tensor([[0, .10, .10, .40, .90], [1, .35, .15, .80, .95], [0, .55, .05, .95, .70]], device=DEV)
+for name in ("b0", "b1", "b7"):
+    kw = hiseg_kwargs(dict(configs()[name]["model_kwargs"]))
+    m = hiseg.create_rgb_hierarchical_model(**kw)
+    filler.fill_module(m)
+    hiseg.set_compute_dtype(m, torch.bfloat16)
+    m = m.to(DEV).train()
+    for mm in (m.roi_align_mask, m.roi_align_rgb):
+        mm.spatial_scale_h, mm.spatial_scale_w = 96, 128
+    ms = kw["mask_size"]
+    mh, mw = ms if isinstance(ms, tuple) else (ms, ms)
+    tgt = torch.from_numpy(filler.ellipse_targets(63, 3, mh, mw)).to(DEV)
+    loss_fn = hiseg.RefinedHierarchicalLoss(use_boundary_aware_loss=True, use_contour_detection=True,
+                                            use_distance_transform=True, boundary_aware_weight=0.1,
+                                            contour_loss_weight=0.1, distance_loss_weight=0.1)
+    L.wgrad_path_stats(reset=True)
+    L.placement_stats(reset=True)
+    logits, aux = m(images, rois)
+    loss, _ = loss_fn(logits, tgt, aux)
+    loss.backward()
+    torch.cuda.synchronize()
+    out[name] = dict(paths=L.wgrad_path_stats(), placement=L.placement_stats(), loss=float(loss))
+model, dloss = hiseg.create_unet_distillation_model("timm-efficientnet-b0", "timm-efficientnet-b7",
+                                                    teacher_checkpoint="absent.pth", device="cpu",
+                                                    progressive_unfreeze=True)
+filler.fill_module(model.student, seed=11)
+filler.fill_module(model.teacher, seed=12)
+hiseg.set_compute_dtype(model, torch.bfloat16)
+model = model.to(DEV).train()
+assert model.unfreeze_encoder_blocks(7, learning_rate_scale=0.3)
+x = torch.from_numpy(filler.normal(33, (2, 3, 96, 128))).to(DEV)
+mask = (torch.from_numpy(filler.uniform(34, (2, 1, 96, 128))) > 0.5).float().to(DEV)
+L.wgrad_path_stats(reset=True)
+s, t = model(x)
+loss, _ = dloss(s, t, mask)
+loss.backward()
+torch.cuda.synchronize()
+out["distill_unfrozen"] = dict(paths=L.wgrad_path_stats(), placement=L.placement_stats(), loss=float(loss))
+print("RESULT " + json.dumps(out))
+"""
+
+
+def test_no_leg_runs_the_generic_weight_gradient_kernel_with_far_sources():
+    env = dict(os.environ, HISEG_PLACEMENT_FAR="1")
+    r = subprocess.run([sys.executable, "-c", _SCRIPT, ROOT], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1]
+    res = json.loads(line[len("RESULT "):])
+    for leg, v in res.items():
+        p = v["paths"]
+        assert p["generic_bf16"] == 0, f"{leg}: generic weight-gradient kernel ran: {p}"
+        assert p["wide"] + p["transposed_read"] > 0, f"{leg}: no weight gradient recorded: {p}"
+        assert v["loss"] == v["loss"], f"{leg}: NaN loss"
+    # the forced far-apart path was exercised (two-source layers exist in every leg)
+    assert all(v["placement"][1] > 0 for v in res.values()), {k: v["placement"] for k, v in res.items()}
