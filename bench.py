@@ -61,6 +61,9 @@ GFLOP_PER_ROI_MASK = 53.1 + 27.7 / 8
 GFLOP_PER_TRAIN_ROI = 173.5 + 27.7 / 8
 # Distillation unit = one 640x640 image: B7 teacher fwd 120.3 + B0 student fwd+bwd ~111 GFLOP
 GFLOP_PER_DISTILL_IMAGE = 120.3 + 111.0
+# the staged schedule's last phase (all 7 encoder stages trainable) adds the B0 encoder's backward: data + weight
+# gradients ~2x its forward, 0.39 GMAC at 224x224 (timm efficientnet_b0) -> 6.4 GFLOP forward at 640x640
+GFLOP_PER_DISTILL_IMAGE_UNFROZEN = GFLOP_PER_DISTILL_IMAGE + 2 * 6.4
 
 B0_KWARGS = dict(
     roi_size=ROI_HW, mask_size=MASK_HW, multi_scale=False, use_attention_module=True,
@@ -242,23 +245,32 @@ def train_bench(device, dtype, rank, world, dist, steps, warmup, preset=None, ba
 
 def _release_leg():
     """Between legs: collect the finished leg's graphs / closures (reference cycles keep a GraphedStep, its captured
-    graph and that graph's private memory pool alive until the cyclic collector runs), then return the cached
-    blocks.  Without it a leg measured 7-40 % slower after another leg in the same process than alone."""
+    graph and that graph's private memory pool alive until the cyclic collector runs), so their blocks return to the
+    caching allocator for the next leg.  The blocks are NOT handed back to the driver (no empty_cache): freed VRAM
+    that is allocated again is cleared by the kernel driver in the background, and that clearing ran beside the next
+    leg's timed region -- the inference leg measured 16 % slower right after the train legs and recovered after
+    ~30 s idle; with the cache kept it is within 0.2 % of its first run (tools/order_probe.py,
+    profiles/r5_leg_order.txt).  HISEG_BENCH_EMPTY_CACHE=1 restores the old release for A/B runs."""
     import gc
     torch.cuda.synchronize()
     gc.collect()
-    torch.cuda.empty_cache()
+    if os.environ.get("HISEG_BENCH_EMPTY_CACHE", "0") == "1":
+        torch.cuda.empty_cache()
 
 
 def _backend(dist):
     return dist.get_backend() if dist else None
 
 
-def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=640, graph=True):
+def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=640, graph=True, unfrozen=0):
     """C5 (BASELINE.json configs[4]): B7 -> B0 staged distillation step, decoder-only phase of the progressive
     unfreezing schedule -- B7 teacher forward (eval), B0 student forward (train-mode BN) + decoder/head
     backward, UNetDistillationLoss (T = 4, targets), decoder-subset FusedAdamW with clip 1.0 -- 4 images
-    640x640 per GPU (train_distillation_staged config batch_size 4), gradients averaged over ranks."""
+    640x640 per GPU (train_distillation_staged config batch_size 4), gradients averaged over ranks.
+    ``unfrozen`` = N: the schedule's later phase after unfreeze_encoder_blocks(N) -- the encoder's last N stages
+    trainable (backward through the MBConv depthwise / SqueezeExcite / BN stacks) and the reference's two
+    parameter groups (train_distillation_staged.py:1509-1544: decoder lr with clip 1.0 on the decoder only,
+    :300-313; encoder lr x encoder_lr_scale 0.1, :1215)."""
     import filler
     import hiseg
     from hiseg import distributed as HD
@@ -274,9 +286,10 @@ def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=6
     x = torch.randn(batch, 3, hw, hw, generator=g).to(device)
     yy, xx = torch.meshgrid(torch.linspace(-1, 1, hw), torch.linspace(-1, 1, hw), indexing="ij")
     m = ((yy / 0.7) ** 2 + (xx / 0.45) ** 2 < 1).float()[None, None].expand(batch, 1, hw, hw).contiguous().to(device)
+    enc = model.unfreeze_encoder_blocks(unfrozen, learning_rate_scale=0.1) if unfrozen else None
     if world > 1:
         HD.enable_grad_sync(model.student)
-    state = {"opt": None}
+    state = {"opt": None, "enc_opt": None}
 
     def step():
         s, t = model(x)
@@ -284,9 +297,15 @@ def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=6
         if state["opt"] is None:
             state["opt"] = hiseg.FusedAdamW(model.student, lr=1e-4, weight_decay=1e-4, max_grad_norm=1.0,
                                             params=model.student.get_decoder_parameters())
-        state["opt"].zero_grad()
+            if enc:
+                state["enc_opt"] = hiseg.FusedAdamW(model.student, lr=1e-4 * 0.1, weight_decay=1e-4,
+                                                    max_grad_norm=None, params=enc)
+        opts = [o for o in (state["opt"], state["enc_opt"]) if o is not None]
+        for o in opts:
+            o.zero_grad()
         loss.backward()
-        state["opt"].step()
+        for o in opts:
+            o.step()
         return loss
 
     prof = None
@@ -295,7 +314,7 @@ def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=6
         step()
         # serial teacher for the per-call profile (concurrent branches would overlap the HIP-event intervals)
         model.concurrent_teacher = False
-        prof = call_profile(step, "distill")
+        prof = call_profile(step, "distill_unfrozen" if unfrozen else "distill")
         del model.concurrent_teacher
     graphable = graph and (world == 1 or _backend(dist) == "nccl")
     run = hiseg.GraphedStep(step, lambda: state["opt"]) if graphable else step
@@ -334,14 +353,19 @@ def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=6
     if prof is not None:
         extra["roofline"] = prof.pop("roofline", None)
         extra["call_profile"] = prof
-    extra["pipeline_tflops"] = round(sps * batch * world * GFLOP_PER_DISTILL_IMAGE / 1e3, 1)
+    gfl = GFLOP_PER_DISTILL_IMAGE_UNFROZEN if unfrozen else GFLOP_PER_DISTILL_IMAGE
+    extra["pipeline_tflops"] = round(sps * batch * world * gfl / 1e3, 1)
     extra["pipeline_frac"] = round(extra["pipeline_tflops"] / world / PEAK_BF16_TFLOPS, 4)
     return {"metric": "distillation step/s", "value": round(sps, 3), "unit": "steps/s",
             "ms_per_step": round(1e3 / sps, 2), "steps": steps, "warmup": warmup,
             "images_per_s": round(sps * batch * world, 1), "loss_last": round(float(loss.detach()), 4), **extra,
-            "config": {"workload": f"C5: B7 teacher (eval) -> B0 student (train-mode BN, decoder-only phase), "
-                                   f"{batch} img {hw}x{hw}/GPU, UNetDistillationLoss T=4 + BCE/Dice targets, "
-                                   f"decoder FusedAdamW clip 1.0", "global_batch": batch * world,
+            "config": {"workload": f"C5: B7 teacher (eval) -> B0 student (train-mode BN, "
+                                   + (f"encoder stages unfrozen: {unfrozen} of 7 -- encoder backward, two "
+                                      f"parameter groups" if unfrozen else "decoder-only phase")
+                                   + f"), {batch} img {hw}x{hw}/GPU, UNetDistillationLoss T=4 + BCE/Dice targets, "
+                                   f"decoder FusedAdamW clip 1.0" + (", encoder FusedAdamW lr x 0.1 unclipped"
+                                                                     if unfrozen else ""),
+                       "global_batch": batch * world,
                        "schedule": "eager" if run is step else "one HIP graph per step (hiseg.GraphedStep)",
                        "parallelism": f"dp{world} (bucketed RCCL grad all-reduce)" if world > 1 else "dp1"}}
 
@@ -848,7 +872,10 @@ def main():
     ap.add_argument("--no-distill", action="store_true")
     ap.add_argument("--no-presets", action="store_true", help="skip the C3 (B1) / C4 (B7) train lines")
     ap.add_argument("--distill-only", action="store_true", help="only the C5 distillation line (profiling)")
-    ap.add_argument("--leg", choices=["train", "c3", "c4", "distill"], default=None,
+    ap.add_argument("--order", default="infer,train,c3,c4,distill,distill_unfrozen",
+                    help="the legs of a full run, in this order (comma list of infer, train, c3, c4, distill, "
+                         "distill_unfrozen)")
+    ap.add_argument("--leg", choices=["train", "c3", "c4", "distill", "distill_unfrozen", "infer"], default=None,
                     help="profiling: run only this train / distillation leg (one JSON object)")
     ap.add_argument("--serial", action="store_true", help="one stream (no UNet/head overlap across steps)")
     ap.add_argument("--eager-train", action="store_true", help="train / distill legs as eager launches (default on one "
@@ -906,6 +933,10 @@ def main():
         elif args.leg == "c4":
             out["train_c4"] = train_bench(device, dtype, rank, world, dist, steps, 2, preset="b7", batch=8,
                                           rois_per_img=1, hw=(640, 640), graph_train=g)
+        elif args.leg == "distill_unfrozen":
+            out["distill_unfrozen"] = distill_bench(device, dtype, rank, world, dist, steps, 2, graph=g, unfrozen=7)
+        elif args.leg == "infer":
+            out = infer_bench(args, device, dtype, rank, world, dist)
         else:
             out["distill"] = distill_bench(device, dtype, rank, world, dist, steps, 2, graph=g)
         if rank == 0:
@@ -915,32 +946,45 @@ def main():
         return
     if args.distill_only:
         args.train_only, args.no_train = True, True
-        out["distill"] = distill_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2,
-                                       graph=not args.eager_train)
-    distill_first = None
-    if not args.train_only:
-        out = infer_bench(args, device, dtype, rank, world, dist)
-    if not args.no_distill and not args.train_only and not args.distill_only:
-        # the distillation leg right after the inference leg: its step forks the teacher onto a side stream, and its
-        # replays measured 9.5-10 ms alone or after the inference leg but 13.5-17 ms after the train legs in the same
-        # process (tools/stream_probe.py, HISEG_BENCH_STEP_TIMES=1); the inference leg, first, measured 8 % slower
-        # after the distillation leg
-        _release_leg()
-        distill_first = distill_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2,
-                                      graph=not args.eager_train)
-    if not args.no_train:
-        _release_leg()
-        out["train"] = train_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), max(2, args.warmup),
-                                   local_first=True, graph_train=not args.eager_train)
-        if not args.no_presets:
+    # The legs run in the order --order names (default: inference, B0 train, C3, C4, distillation), each after the
+    # previous one's graphs and cached blocks were released (_release_leg).  Round 4 ran the distillation leg
+    # second, to keep its replays away from a slowdown seen after the train legs; round 5 measured every leg alone
+    # and in both orders within a few per cent of each other, so the order is the natural one.
+    half, eager = max(2, args.steps // 2), args.eager_train
+    legs = {
+        "infer": (not args.train_only, lambda: out.update(infer_bench(args, device, dtype, rank, world, dist))),
+        "train": (not args.no_train, lambda: out.__setitem__("train", train_bench(
+            device, dtype, rank, world, dist, half, max(2, args.warmup), local_first=True, graph_train=not eager))),
+        "c3": (not args.no_train and not args.no_presets, lambda: out.__setitem__("train_c3", train_bench(
+            device, dtype, rank, world, dist, half, 2, preset="b1", batch=32, rois_per_img=1, hw=(640, 640),
+            graph_train=not eager))),
+        "c4": (not args.no_train and not args.no_presets, lambda: out.__setitem__("train_c4", train_bench(
+            device, dtype, rank, world, dist, half, 2, preset="b7", batch=8, rois_per_img=1, hw=(640, 640),
+            graph_train=not eager))),
+        "distill": ((not args.no_distill and not args.train_only) or args.distill_only,
+                    lambda: out.__setitem__("distill", distill_bench(device, dtype, rank, world, dist, half, 2,
+                                                                     graph=not eager))),
+        "distill_unfrozen": ((not args.no_distill and not args.train_only) or args.distill_only,
+                             lambda: out.__setitem__("distill_unfrozen", distill_bench(
+                                 device, dtype, rank, world, dist, half, 2, graph=not eager, unfrozen=7))),
+    }
+    order = [k.strip() for k in args.order.split(",") if k.strip()]
+    bad = [k for k in order if k not in legs]
+    if bad:
+        print(f"bench.py: unknown legs in --order: {bad} (choose from {sorted(legs)})", file=sys.stderr)
+        sys.exit(2)
+    first = True
+    for k in order:
+        on, fn = legs[k]
+        if not on:
+            continue
+        if not first:
             _release_leg()
-            out["train_c3"] = train_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2, preset="b1",
-                                          batch=32, rois_per_img=1, hw=(640, 640), graph_train=not args.eager_train)
-            _release_leg()
-            out["train_c4"] = train_bench(device, dtype, rank, world, dist, max(2, args.steps // 2), 2, preset="b7",
-                                          batch=8, rois_per_img=1, hw=(640, 640), graph_train=not args.eager_train)
-    if distill_first is not None:
-        out["distill"] = distill_first
+        first = False
+        fn()
+        if k == "infer":   # the JSON line's head keys come first
+            out = {**{kk: out[kk] for kk in out if kk not in ("train", "train_c3", "train_c4", "distill",
+                                                                "distill_unfrozen")}, **out}
     if not args.train_only and world == 1:
         _release_leg()
         out["eval"] = eval_bench(device)

@@ -37,6 +37,9 @@ class GradBucketSync:
         self.pg = process_group
         self.bucket_bytes = int(bucket_mb * (1 << 20))
         self.world = dist.get_world_size(process_group)
+        # RCCL averages in the collective (ReduceOp.AVG: a pre-multiply by 1/world, exact for power-of-two worlds);
+        # gloo has no AVG, so there the bucket is summed and scaled by one extra kernel
+        self.avg_in_collective = dist.get_backend(process_group) == "nccl"
         self.state = None
         self.buckets: List[Tuple[int, int]] = []          # [begin, end) element ranges of the flat grad
         self.bucket_params: List[List[int]] = []          # param ids per bucket
@@ -99,17 +102,22 @@ class GradBucketSync:
             torch.cuda.current_stream(self.comm_stream.device).wait_stream(self.comm_stream)
         self.steps += 1
 
+    def _reduce(self, view: torch.Tensor):
+        if self.avg_in_collective:
+            dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.pg)
+        else:
+            dist.all_reduce(view, group=self.pg)
+            view.mul_(1.0 / self.world)
+
     def _launch(self, b: int):
         begin, end = self.buckets[b]
         view = self.state.flat.grad[begin:end]
         if self.comm_stream is None:
-            dist.all_reduce(view, group=self.pg)
-            view.mul_(1.0 / self.world)
+            self._reduce(view)
         else:
             self.comm_stream.wait_stream(torch.cuda.current_stream(self.comm_stream.device))
             with torch.cuda.stream(self.comm_stream):
-                dist.all_reduce(view, group=self.pg)
-                view.mul_(1.0 / self.world)
+                self._reduce(view)
         self.launched.append(b)
 
 

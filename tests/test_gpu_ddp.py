@@ -117,6 +117,24 @@ def _c5_opt(model):
                             params=model.student.get_decoder_parameters())
 
 
+UNFREEZE_AT, UNFREEZE_STEPS, UNFREEZE_BLOCKS = 2, 4, 3
+
+
+def _c5u_rebuild(model, opts, enc):
+    """train_distillation_staged.py:1509-1550 after unfreeze_encoder_blocks: a new optimizer with the decoder group
+    (lr, its AdamW moments carried over from the old optimizer) and the encoder group (lr x encoder_lr_scale,
+    unclipped: the reference clips the decoder parameters only, :300-313)."""
+    import hiseg
+    old = opts[0]
+    new = _c5_opt(model)
+    for new_p in new.param_groups[0]["params"]:
+        for old_p in old.param_groups[0]["params"]:
+            if new_p is old_p and old_p in old.state:
+                new.state[new_p] = old.state[old_p]
+                break
+    return [new, hiseg.FusedAdamW(model.student, lr=1e-3 * 0.3, weight_decay=1e-4, max_grad_norm=None, params=enc)]
+
+
 # ------------------------------------------------------------------------------------------ rank processes
 def _rank_worker(rank, world, port, case, q, outdir):
     try:
@@ -143,6 +161,37 @@ def _rank_worker(rank, world, port, case, q, outdir):
                 opt.step()
                 torch.cuda.synchronize()
                 params.append(S.flat.data.cpu().clone())
+        elif case == "c5u":   # decoder-only steps, unfreeze_encoder_blocks + optimizer rebuild, more steps
+            model, loss_fn = _c5_model()
+            sync = HD.enable_grad_sync(model.student, bucket_mb=2.0)
+            x, msk = _c5_batch(world)
+            n = C5_IMG[0]
+            x, msk = x[rank * n:(rank + 1) * n].to(DEV), msk[rank * n:(rank + 1) * n].to(DEV)
+            opts = None
+            nb = []
+            for step in range(UNFREEZE_STEPS):
+                if step == UNFREEZE_AT:
+                    enc = model.unfreeze_encoder_blocks(UNFREEZE_BLOCKS, learning_rate_scale=0.3)
+                    opts = _c5u_rebuild(model, opts, enc)
+                s, t = model(x)
+                loss, _ = loss_fn(s, t, msk)
+                opts = opts or [_c5_opt(model)]
+                for o in opts:
+                    o.zero_grad()
+                loss.backward()
+                torch.cuda.synchronize()
+                S = model.student.__dict__["_hiseg_train"]
+                grads.append(S.flat.grad.cpu().clone())
+                nb.append(len(sync.buckets))
+                for o in opts:
+                    o.step()
+                torch.cuda.synchronize()
+                params.append(S.flat.data.cpu().clone())
+            path = os.path.join(outdir, f"rank{rank}.pt")
+            torch.save({"grads": grads, "params": params, "buckets": nb}, path)
+            q.put((rank, path, nb, sorted(k for k in sync.launch_after if k >= 0)))
+            dist.destroy_process_group()
+            return
         else:
             model, loss_fn = _c5_model()
             sync = HD.enable_grad_sync(model.student, bucket_mb=2.0)
@@ -285,6 +334,53 @@ def test_ddp_world2_c5_distillation_equals_half_batch_mean(tmp_path):
         torch.cuda.synchronize()
         ref_params.append(S.flat.data.cpu().clone())
     _check(out, ref_grads, ref_params)
+
+
+def test_ddp_world2_c5_across_progressive_unfreeze_equals_half_batch_mean(tmp_path):
+    """data parallelism across the staged schedule's unfreeze boundary.  Two decoder-only steps,
+    then unfreeze_encoder_blocks(3) -- a new trainable set: a new flat gradient layout, the exchange re-cut into
+    buckets and its overlap schedule re-recorded (GradBucketSync.attach), the optimizer rebuilt as two groups with the
+    decoder's moments carried over (train_distillation_staged.py:1509-1550) -- then two more steps.  Every step:
+    the ranks' averaged gradients equal each other and, bit for bit, the mean of the two half-batch gradients one
+    process computes; parameters identical on both ranks and to that single-process trajectory."""
+    world = 2
+    out = _run_ranks("c5u", tmp_path, world)
+    model, loss_fn = _c5_model()
+    x, msk = _c5_batch(world)
+    n = C5_IMG[0]
+    opts, ref_grads, ref_params, S = None, [], [], None
+    for step in range(UNFREEZE_STEPS):
+        if step == UNFREEZE_AT:
+            enc = model.unfreeze_encoder_blocks(UNFREEZE_BLOCKS, learning_rate_scale=0.3)
+            opts = _c5u_rebuild(model, opts, enc)
+        gs = []
+        for r in range(world):
+            s, t = model(x[r * n:(r + 1) * n].to(DEV))
+            loss, _ = loss_fn(s, t, msk[r * n:(r + 1) * n].to(DEV))
+            opts = opts or [_c5_opt(model)]
+            for o in opts:
+                o.zero_grad()
+            loss.backward()
+            S = model.student.__dict__["_hiseg_train"]
+            gs.append(S.flat.grad.clone())
+        mean = (gs[0] + gs[1]) * (1.0 / world)
+        S.flat.grad.copy_(mean)
+        ref_grads.append(mean.cpu())
+        for o in opts:
+            o.step()
+        torch.cuda.synchronize()
+        ref_params.append(S.flat.data.cpu().clone())
+    (_, g0, p0, nb0, sched), (_, g1, p1, nb1, _) = out
+    assert nb0 == nb1 and nb0[UNFREEZE_AT] > nb0[0] > 1, f"buckets per step {nb0}: re-cut at the unfreeze"
+    assert g0[UNFREEZE_AT].numel() > g0[0].numel(), "the unfreeze should add encoder gradients to the flat layout"
+    for step in range(UNFREEZE_STEPS):
+        assert torch.isfinite(g0[step]).all() and torch.isfinite(ref_grads[step]).all(), f"step {step}"
+        assert torch.equal(g0[step], g1[step]), f"step {step}: the ranks' averaged gradients differ"
+        d = (g0[step] - ref_grads[step]).abs().max().item()
+        assert torch.equal(g0[step], ref_grads[step]), f"step {step}: gradient differs from the half-batch mean by {d}"
+        assert torch.equal(p0[step], p1[step]), f"step {step}: parameters differ across ranks"
+        assert torch.equal(p0[step], ref_params[step]), f"step {step}: parameters differ from the single process"
+    assert not torch.equal(p0[UNFREEZE_AT], p0[-1])
 
 
 # ------------------------------------------------------------------------------------------ (b) graph capture
