@@ -1,0 +1,501 @@
+// Halo-tiled 3x3 convolution, Cout-split waves (gfx950, bf16): the dominant class of the ROI head (256->256 /
+// 128->128 / 128->256 3x3 layers, refinement.py:31-55 ResidualBlock, rgb.py:657-673).
+//
+// conv_hwr.hip gives each wave a 64 Cout x 128-pixel tile (half of the workgroup's 16 x 16 pixels), so every weight
+// fragment is loaded from L2/L1 into registers by the two pixel waves of its Cout group, 4 KiB per wave per K step.
+// Timing ablations of conv_hwr (tools/conv_bench.py, DIAG variants 110+, profiles/r5_hwr_ablation.txt): 0.79 ms on
+// 256->256 @64x48 x 256 ROIs; without its MFMAs 0.55 ms, without the in-loop weight loads 0.63 ms, without the halo
+// DMA 0.65, without both 0.54 (= the MFMA-only time): the vector-memory stream, three quarters of it the weight
+// fragments, is what the MFMAs fail to hide.
+//
+// Here a wave owns 32 output channels of ALL 256 pixels of the tile: 2 x 16 accumulators of v_mfma_f32_16x16x32_bf16
+// (the same 128 registers), 2 weight fragments (2 KiB) per K step instead of 4, and no fragment loaded twice in a
+// workgroup -- half the weight traffic per FLOP.  The B side reads more LDS instead: per (32-channel slice, kx) the
+// wave walks the 18 halo rows of its window once, each row's B fragment (16 pixels x 32 channels, one ds_read_b128)
+// feeding the 3 ky taps x 2 Cout fragments it meets (output rows r - ky), so each fragment is read once per (slice,
+// kx) and a slice costs 54 fragment reads per wave (6 per K step).  The weights of the three ky taps of a kx are
+// loaded one (slice, kx) block ahead.  The halo of the next slice is LDS-DMA'd during the first two kx blocks of a
+// slice into the other buffer; one barrier per slice.
+//
+// Per output element the accumulation order is conv_hwr's (slices in order; within a slice kx-major, ky inner; one
+// 32-channel MFMA per (slice, tap)), so results equal conv_hwr / conv_hw variant 86 bit for bit.
+//
+// NW (waves = 32-Cout groups per workgroup): 4 -> 128 Cout x 256 pixels, two workgroups per CU; 8 -> 256 Cout x 256
+// pixels, one workgroup per CU (the 256-Cout layers read each halo once instead of once per 128-Cout workgroup).
+#include "conv_common.h"
+
+namespace hiseg {
+
+typedef unsigned hc_u4 __attribute__((ext_vector_type(4)));
+typedef unsigned hc_u2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) void hc_lds_void;
+
+__device__ __forceinline__ void hc_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned lds_addr, unsigned voff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :: "s"(__builtin_amdgcn_readfirstlane(lds_addr)), "v"(voff), "s"(rsrc) : "memory");
+}
+
+// ABL (DIAG builds only, timing ablations -- wrong results): bit 0 no weight loads after the prologue, bit 1 no halo
+// DMA after the prologue, bit 2 no B-fragment LDS reads, bit 3 no slice barrier, bit 4 no MFMAs, bit 5 no epilogue
+// (accumulators stored straight, unconverted)
+// RP (NW 4): residual prefetch.  The workgroup takes 80 KiB of LDS instead of 64 (two per CU still fit the 160 KiB):
+// the epilogue tile is bytes [0, 64K) and the two halo buffers sit at [56K, 80K) (X) and [32K, 56K) (Y), the last
+// slice always in X.  The residual rows of tile rows 0..127 ([0, 32K), never a halo) are LDS-DMA'd during slice 0, rows
+// 128..223 ([32K, 56K) = Y, free in the last slice) during the last slice in place of the (absent) next halo, and only
+// rows 224..255 ([56K, 64K), inside X) after the last barrier -- while rows 0..223 are converted.  Without it the
+// whole 64-KiB residual tile was fetched after the last barrier with every wave waiting on it.
+// (Measured and not kept, same box, 256->256 @64x48 x 256 ROIs: weights loaded two kx blocks ahead, 0.698 vs 0.698 ms;
+// a progressive epilogue storing each output row from the accumulators as soon as its last MFMA ran, 8-B stores
+// straight to HBM, 0.728 vs 0.698 ms -- bit-identical both.)
+// HV: the next slice's halo pieces (and, at the end, the residual tile) through registers -- buffer_load_dwordx4 at
+// the start of a kx block, ds_write_b128 at its end -- instead of LDS-DMA; pieces lying wholly past the halo skipped.
+template <int ACT, bool RES, int NW, bool UP = false, int ABL = 0, bool RP = false, bool HV = false>
+__global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(ConvArgs a) {
+  constexpr int BCO = 32 * NW, TM = 2, NR = 16;    // wave tile: 32 Cout x (16 rows x 16 columns)
+  constexpr int TW = 16, HWD = TW + 2;
+  constexpr int NHR = 18 * HWD;                       // halo rows (pixels) of a slice
+  constexpr int PPW = ((NHR + 15) / 16 + NW - 1) / NW;   // halo pieces (16 rows, 1 KiB) per wave per slice
+  constexpr int PH = (PPW + 1) / 2;                   // pieces issued in kx block 0 (the rest in block 1)
+  constexpr int HB = PPW * NW * 1024;                 // bytes of one halo buffer
+  constexpr int NPX = 256;                            // output pixels of the tile
+  static_assert(NW == 4 || NW == 8, "configuration");
+  extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+  const hiseg_conv2d_desc& d = a.d;
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);   // the wave's 32-Cout group
+
+  // ---- XCD-major bijective remap; Cout tiles fastest (the tiles of one pixel block share its halo in L2)
+  const int nco = d.Cout_pad / BCO;
+  const int ntx = (d.W + TW - 1) / TW, nty = (d.H + 15) >> 4;
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xcd = orig & 7, loc = orig >> 3;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int co0 = (wg % nco) * BCO;
+  int tl = wg / nco;
+  const int tx = tl % ntx;
+  tl /= ntx;
+  const int ty = tl % nty;
+  const int n = tl / nty;
+  const int y0 = ty * 16, x0 = tx * TW;
+
+  const unsigned OOB = 0x80000000u;   // >= num_records: loads return zeros
+  const int nsl = a.Cin >> 5;         // 32-channel slices (even: Cin % 64 == 0)
+  const int ncb = a.Cin >> 6;
+  const __amdgpu_buffer_rsrc_t rF = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(d.weight_frag), (short)0, d.Cout_pad * 9 * a.Cin * 2, 0x00020000);
+  constexpr int USH = UP ? 1 : 0;
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(d.srcA), (short)0, d.N * (d.H >> USH) * (d.W >> USH) * d.a_cstride * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(d.Cb ? d.srcB : d.srcA), (short)0, d.Cb ? d.N * d.H * d.W * d.b_cstride * 2 : 0, 0x00020000);
+
+  // ---- A fragments (hiseg.ops.frag_pack): (16-row Cout tile ct, slice sl, tap) at
+  // ((((ct * ncb + sl / 2) * 9 + tap) * 2 + sl % 2) * 64 + lane) * 16 B; the wave's two tiles are ct0, ct0 + 1
+  const unsigned a_ct = (unsigned)((co0 + w * 32) >> 4) * (unsigned)ncb * 18u * 1024u;
+  const unsigned a_ct_step = (unsigned)ncb * 18u * 1024u;
+  // the weights of taps (ky, kx), ky = 0..2, of slice sl: 6 loads (the wave-uniform part in the SGPR offset)
+  auto load_blk = [&](hc_u4 (&af)[3][TM], int sl, int kx) __attribute__((always_inline)) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const unsigned a_lane = a_ct + (unsigned)ln * 16u;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const unsigned so = __builtin_amdgcn_readfirstlane(
+          (((unsigned)(sl >> 1) * 9u + (unsigned)(ky * 3 + kx)) * 2u + (unsigned)(sl & 1)) * 1024u);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[ky][i] = __builtin_amdgcn_raw_buffer_load_b128(rF, a_lane + (unsigned)i * a_ct_step, so, 0);
+    }
+  };
+
+  // ---- halo layout (conv_hwr's): row hr = hy * 18 + hx (64 B = 32 channels), 16-B chunk c at slot c ^ swz(hx),
+  // swz(hx) = 2 ((hx >> 2) & 1); conflict-free B-fragment reads for every column shift kx.  Piece p of wave w = halo
+  // rows 16 (NW p + w) + lane / 4 (one LDS-DMA of 1 KiB).
+  const unsigned lds_base = (unsigned)(uintptr_t)(hc_lds_void*)smem;
+  // halo buffer of slice sl (byte offset in LDS)
+  auto hbuf = [&](int sl) __attribute__((always_inline)) -> int {
+    if constexpr (RP) return ((nsl - 1 - sl) & 1) ? 32 * 1024 : 56 * 1024;
+    else return (sl & 1) * HB;
+  };
+  // the source of halo piece p of slice sl: resource, byte offset
+  auto halo_src = [&](int p, int sl, unsigned& off) __attribute__((always_inline)) -> bool {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int hr = 16 * (NW * p + w) + (ln >> 2);
+    const int hy = hr / HWD, hx = hr - HWD * hy;
+    const int iy = y0 + hy - 1, ix = x0 + hx - 1;
+    const bool ok = hr < NHR && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+    const int chunk = (ln & 3) ^ (((hx >> 2) & 1) << 1);
+    const bool fb = 32 * sl >= d.Ca;
+    const int cs = fb ? d.b_cstride : d.a_cstride, coff = fb ? d.b_coff + 32 * sl - d.Ca : d.a_coff + 32 * sl;
+    if constexpr (UP) {
+      const int ush = fb ? 0 : 1;
+      off = ok ? (unsigned)((((n * (d.H >> ush) + (iy >> ush)) * (d.W >> ush) + (ix >> ush)) * cs + coff + chunk * 8) * 2)
+               : OOB;
+    } else {
+      off = ok ? (unsigned)((((n * d.H + iy) * d.W + ix) * cs + coff + chunk * 8) * 2) : OOB;
+    }
+    return fb;
+  };
+  auto halo_dma = [&](int p, int sl, int boff) __attribute__((always_inline)) {
+    if (16 * (NW * p + w) >= NHR) return;   // a piece wholly past the halo (wave-uniform): nothing to load
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int hr = 16 * (NW * p + w) + (ln >> 2);
+    const int hy = hr / HWD, hx = hr - HWD * hy;
+    const int iy = y0 + hy - 1, ix = x0 + hx - 1;
+    const bool ok = hr < NHR && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+    const int chunk = (ln & 3) ^ (((hx >> 2) & 1) << 1);
+    const bool fb = 32 * sl >= d.Ca;
+    const int cs = fb ? d.b_cstride : d.a_cstride, coff = fb ? d.b_coff + 32 * sl - d.Ca : d.a_coff + 32 * sl;
+    unsigned off;
+    if constexpr (UP) {
+      const int ush = fb ? 0 : 1;
+      off = ok ? (unsigned)((((n * (d.H >> ush) + (iy >> ush)) * (d.W >> ush) + (ix >> ush)) * cs + coff + chunk * 8) * 2)
+               : OOB;
+    } else {
+      off = ok ? (unsigned)((((n * d.H + iy) * d.W + ix) * cs + coff + chunk * 8) * 2) : OOB;
+    }
+    hc_dma16(fb ? rB : rA, lds_base + (unsigned)(boff + 1024 * (NW * p + w)), off);
+  };
+  const char* lds_c = reinterpret_cast<const char*>(smem);
+  // B fragment of halo row r at column shift kx: pixels (r, kx + lane % 16), channels 8 (lane / 16) .. + 7
+  auto rdB = [&](int ln, int boff, int kx, int r) __attribute__((always_inline)) -> hc_u4 {
+    const int hx = (ln & 15) + kx;
+    return *reinterpret_cast<const hc_u4*>(lds_c + boff + (r * HWD + hx) * 64 +
+                                           (((ln >> 4) ^ (((hx >> 2) & 1) << 1)) << 4));
+  };
+
+  floatx4 acc[TM][NR];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- epilogue geometry (conv_hwr's): 256 pixel rows x BCO bf16, 16-B chunk c of row r at slot c ^ (r & SWM);
+  // tile row r = pixel (y0 + r / 16, x0 + r % 16).  Residual piece q (RPI rows, 1 KiB) = rows RPI q .. + RPI - 1,
+  // issued by wave q % NW as its piece k = q / NW.
+  constexpr int EROWB = BCO * 2;
+  constexpr int CPR = BCO / 8;        // 16-B chunks per row
+  constexpr int RPI = 64 / CPR;       // rows per wave instruction
+  constexpr int SWM = CPR - 1;
+  constexpr int NRI = NPX / (RPI * NW);   // residual pieces per wave
+  auto px_of = [&](int r) __attribute__((always_inline)) -> int {
+    const int y = y0 + r / TW, x = x0 + r % TW;
+    return (y < d.Ho && x < d.Wo) ? (n * d.Ho + y) * d.Wo + x : -1;
+  };
+  const __amdgpu_buffer_rsrc_t rR = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(RES ? d.residual : d.out), (short)0, RES ? a.M * d.r_cstride * 2 : 0, 0x00020000);
+  auto res_dma = [&](int k) __attribute__((always_inline)) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int c = ln % CPR;
+    const int r = RPI * (w + NW * k) + ln / CPR;
+    const int px = px_of(r);
+    const unsigned off = px >= 0 ? (unsigned)((px * d.r_cstride + d.r_coff + co0 + ((c ^ (r & SWM)) * 8)) * 2) : OOB;
+    hc_dma16(rR, lds_base + (unsigned)(RPI * (w + NW * k) * EROWB), off);
+  };
+  static_assert(!RP || (NW == 4 && NRI == 16), "residual prefetch layout: 128-Cout tiles");
+
+  // ---- prologue: slice 0's halo, the weights of block (slice 0, kx 0)
+  hc_u4 af[3][TM], an[3][TM];
+#pragma unroll
+  for (int p = 0; p < PPW; ++p) halo_dma(p, 0, hbuf(0));
+  load_blk(af, 0, 0);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");    // the halo pieces (older than the 6 weight loads)
+  __syncthreads();
+
+  // One (slice, kx) block: the next block's weights are loaded first; halo pieces of slice sl + 1 ride in blocks
+  // kx 0 and 1; then the 18 halo rows, each B fragment read two rows ahead and used for the (up to) 3 ky taps x 2
+  // Cout fragments whose output row r - ky lies in the tile.
+  auto block = [&](int sl, auto kxc) __attribute__((always_inline)) {
+    constexpr int KX = decltype(kxc)::value;
+    const int buf = hbuf(sl);
+    const bool more = sl + 1 < nsl;
+    if ((ABL & 1) == 0 && (KX < 2 || more)) load_blk(an, KX < 2 ? sl : sl + 1, KX < 2 ? KX + 1 : 0);
+    hc_u4 hv[HV ? PH : 1];
+    if constexpr (HV && KX < 2) {   // this block's pieces of slice sl + 1's halo, into registers
+      if (more) {
+#pragma unroll
+        for (int q = 0; q < PH; ++q) {
+          const int p = KX * PH + q;
+          if (p < PPW && 16 * (NW * p + w) < NHR) {
+            unsigned off;
+            const bool fb = halo_src(p, sl + 1, off);
+            hv[q] = __builtin_amdgcn_raw_buffer_load_b128(fb ? rB : rA, off, 0, 0);
+          }
+        }
+      }
+    }
+    // This block's LDS-DMA pieces (the next slice's halo; RP: residual rows), issued after row 2's MFMAs.  The
+    // compiler does not see the asm DMA in its vmcnt accounting, so a piece issued before its wait for a weight
+    // fragment of this block would make that wait cover the weight loads issued at the start of this block (measured:
+    // a stall per block); after row 2 every fragment of the block has been waited for, and the pieces get the rest of
+    // this block to land (they are older than the next block's weight loads).
+    auto pieces = [&]() __attribute__((always_inline)) {
+      if constexpr ((ABL & 2) != 0 || HV) {
+      } else if constexpr (KX < 2) {
+        if (more) {
+#pragma unroll
+          for (int p = KX * PH; p < (KX == 0 ? PH : PPW); ++p) halo_dma(p, sl + 1, hbuf(sl + 1));
+        } else if constexpr (RP && RES) {   // last slice: residual rows 128..223 into the free buffer Y
+#pragma unroll
+          for (int k = 8 + 3 * KX; k < 11 + 3 * KX; ++k) res_dma(k);
+        }
+      }
+      if constexpr (RP && RES) {   // slice 0: residual rows 0..127 (pieces 0..7 of each wave: 3, 3, 2 per block)
+        if (sl == 0) {
+#pragma unroll
+          for (int k = 3 * KX; k < (KX == 2 ? 8 : 3 * KX + 3); ++k) res_dma(k);
+        }
+      }
+    };
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    hc_u4 bq[3];
+    if constexpr ((ABL & 4) == 0) {
+      bq[0] = rdB(ln, buf, KX, 0);
+      bq[1] = rdB(ln, buf, KX, 1);
+    } else {
+      bq[0] = bq[1] = bq[2] = af[0][0];
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int r = 0; r < NR + 2; ++r) {
+      if (r == 3) {
+        __builtin_amdgcn_s_setprio(0);
+        pieces();
+        __builtin_amdgcn_s_setprio(1);
+      }
+      if ((ABL & 4) == 0 && r + 2 < NR + 2) bq[(r + 2) % 3] = rdB(ln, buf, KX, r + 2);
+      // keep row r + 2's fragment read ahead of row r's MFMAs (left alone, the scheduler sinks each read next to its
+      // use, and every other row waits out an LDS latency)
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const int j = r - ky;
+        if (j >= 0 && j < NR) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            if constexpr ((ABL & 16) == 0)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[ky][i]),
+                                                                   __builtin_bit_cast(bf16x8_t, bq[r % 3]), acc[i][j], 0,
+                                                                   0, 0);
+            else
+              acc[i][j][0] += __builtin_bit_cast(float, af[ky][i][0]) + __builtin_bit_cast(float, bq[r % 3][1]);
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    if constexpr (HV && KX < 2) {   // ... and into the other halo buffer, lane l at byte 16 l of its piece
+      if (more) {
+        const int nb = hbuf(sl + 1);
+#pragma unroll
+        for (int q = 0; q < PH; ++q) {
+          const int p = KX * PH + q;
+          if (p < PPW && 16 * (NW * p + w) < NHR)
+            *reinterpret_cast<hc_u4*>(reinterpret_cast<char*>(smem) + nb + 1024 * (NW * p + w) + 16 * ln) = hv[q];
+        }
+      }
+    }
+    if constexpr (KX == 2 && (ABL & 8) == 0) {
+      if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // every halo piece (the next weights may fly)
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();   // slice sl+1's halo is in LDS; every wave is done reading slice sl's buffer
+    }
+    if constexpr ((ABL & 1) == 0) {
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[ky][i] = an[ky][i];
+    }
+  };
+  using K0 = std::integral_constant<int, 0>;
+  using K1 = std::integral_constant<int, 1>;
+  using K2 = std::integral_constant<int, 2>;
+  for (int sl = 0; sl < nsl; ++sl) {
+    block(sl, K0{});
+    block(sl, K1{});
+    block(sl, K2{});
+  }
+
+  // ---- epilogue through LDS (conv_hwr's): 256 pixel rows x BCO bf16, 16-B chunk c of row r at slot c ^ (r & SWM);
+  // the residual tile arrives there by LDS-DMA, each lane turns its accumulator quads into bf16 output quads in
+  // place, whole rows leave by 16-B stores.  Tile row r = pixel (y0 + r / 16, x0 + r % 16).
+  if constexpr ((ABL & 32) != 0) {
+    float* o = reinterpret_cast<float*>(d.out) + (long long)wg * 64 * 64 * NW + t;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < NR; ++j) o[(i * NR + j) * 64 * NW] = acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    return;
+  }
+  char* tile = reinterpret_cast<char*>(smem);
+  if constexpr (RES && HV) {   // the residual tile through registers: 16 loads per lane, then 16 LDS stores
+    hc_u4 rv[NRI];
+#pragma unroll
+    for (int k = 0; k < NRI; ++k) {
+      const int c = lane % CPR;
+      const int r = RPI * (w + NW * k) + lane / CPR;
+      const int px = px_of(r);
+      const unsigned off = px >= 0 ? (unsigned)((px * d.r_cstride + d.r_coff + co0 + ((c ^ (r & SWM)) * 8)) * 2) : OOB;
+      rv[k] = __builtin_amdgcn_raw_buffer_load_b128(rR, off, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < NRI; ++k)
+      *reinterpret_cast<hc_u4*>(tile + RPI * (w + NW * k) * EROWB + 16 * lane) = rv[k];
+    __syncthreads();
+  } else if constexpr (RES && !RP) {
+#pragma unroll
+    for (int k = 0; k < NRI; ++k) res_dma(k);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  } else if constexpr (RES) {   // rows 224..255 (pieces 14, 15 of each wave), into buffer X now that it is free
+    res_dma(14);
+    res_dma(15);
+  }
+  floatx4 sc[TM], sh[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int cl = w * 32 + i * 16 + (lane >> 4) * 4;
+    const int cc = co0 + cl < d.Cout ? co0 + cl : 0;
+    sc[i] = *reinterpret_cast<const floatx4*>(d.scale + cc);
+    sh[i] = *reinterpret_cast<const floatx4*>(d.shift + cc);
+  }
+  // accumulator rows j0 .. j1 - 1 (tile rows 16 j + lane % 16) -> bf16 output quads in place
+  auto convert = [&](auto j0c, auto j1c) __attribute__((always_inline)) {
+    constexpr int J0 = decltype(j0c)::value, J1 = decltype(j1c)::value;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = J0; j < J1; ++j) {
+        const int cl = w * 32 + i * 16 + (lane >> 4) * 4;
+        const int r = j * TW + (lane & 15);
+        char* q = tile + r * EROWB + ((((cl >> 3) ^ (r & SWM)) << 4) | ((cl & 4) << 1));
+        const floatx4 ac = acc[i][j];
+        float v[4];
+        uint2 rv = make_uint2(0u, 0u);
+        if constexpr (RES) rv = *reinterpret_cast<const uint2*>(q);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = ac[e] * sc[i][e] + sh[i][e];
+          if constexpr (RES) v[e] += Quad<bf16_t>::get(rv, e);
+          if constexpr (ACT == HISEG_ACT_RELU) v[e] = v[e] > 0.f ? v[e] : 0.f;
+        }
+        uint2 o;
+        o.x = f2bf2(v[0], v[1]);
+        o.y = f2bf2(v[2], v[3]);
+        *reinterpret_cast<uint2*>(q) = o;
+      }
+  };
+  if constexpr (RES && RP) {
+    convert(std::integral_constant<int, 0>{}, std::integral_constant<int, 14>{});
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();   // rows 224..255 of the residual landed (every wave's pieces)
+    convert(std::integral_constant<int, 14>{}, std::integral_constant<int, NR>{});
+  } else {
+    convert(std::integral_constant<int, 0>{}, std::integral_constant<int, NR>{});
+  }
+  __syncthreads();
+  constexpr int NST = NPX * CPR / (NW * 64);   // NPX rows x CPR chunks over the workgroup's threads
+#pragma unroll 4
+  for (int k = 0; k < NST; ++k) {
+    const int idx = t + NW * 64 * k;
+    const int r = idx / CPR, c = idx % CPR;
+    const int px = px_of(r), co = co0 + 8 * c;
+    const uint4 v = *reinterpret_cast<const uint4*>(tile + r * EROWB + ((c ^ (r & SWM)) << 4));
+    if (px >= 0 && co < d.Cout)
+      *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(d.out) + (long long)px * d.o_cstride + d.o_coff + co) = v;
+  }
+}
+
+template <int ACT, bool RES, int NW, bool UP = false, int ABL = 0, bool RP = false, bool HV = false>
+static int launch_hwc(const ConvArgs& a, hipStream_t s) {
+  const hiseg_conv2d_desc& d = a.d;
+  constexpr int BCO = 32 * NW;
+  constexpr int PPW = ((18 * 18 + 15) / 16 + NW - 1) / NW;
+  constexpr size_t halo2 = (size_t)2 * PPW * NW * 1024, epi = (size_t)256 * BCO * 2;
+  const int tiles = d.N * ((d.H + 15) / 16) * ((d.W + 15) / 16);
+  const int nco = d.Cout_pad / BCO;
+  const size_t lds = RP ? (size_t)80 * 1024 : (halo2 > epi ? halo2 : epi);
+  auto kern = conv_hwc_kernel<ACT, RES, NW, UP, ABL, RP, HV>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(tiles * nco), dim3(NW * 64), lds, s, a);
+  return hiseg_check_launch("conv_hwc");
+}
+
+template <int NW, bool RP = false, bool HV = false>
+static int launch_hwc_nw(const ConvArgs& a, hipStream_t s) {
+  const hiseg_conv2d_desc& d = a.d;
+  if (d.a_up == 2) return launch_hwc<HISEG_ACT_RELU, false, NW, true, 0, false, HV>(a, s);   // (checked the form)
+  const bool res = d.residual != nullptr, relu = d.act == HISEG_ACT_RELU;
+  return res ? (relu ? launch_hwc<HISEG_ACT_RELU, true, NW, false, 0, RP, HV>(a, s)
+                     : launch_hwc<HISEG_ACT_NONE, true, NW, false, 0, RP, HV>(a, s))
+             : (relu ? launch_hwc<HISEG_ACT_RELU, false, NW, false, 0, false, HV>(a, s)
+                     : launch_hwc<HISEG_ACT_NONE, false, NW, false, 0, false, HV>(a, s));
+}
+
+// 1 = launched, 0 = the layer does not qualify (caller falls back), <0 on error.  Variant 104: 128-Cout workgroups
+// (four waves, two per CU); 105: 256-Cout workgroups (eight waves, one per CU; Cout a multiple of 256); 106: 104 with
+// the residual prefetch (RP).  The layer
+// rules are conv_hwr_try's (the same operands, weight fragments and halo).
+int conv_hwc_try(const ConvArgs& a, hipStream_t s, int variant) {
+  const hiseg_conv2d_desc& d = a.d;
+#ifdef HISEG_DIAG
+  if (variant >= 150 && variant < 214) {   // timing ablations of variant 104 (res + ReLU only; output buffer as
+                                          // scratch: the ABL 32 store writes one float per thread and MFMA row)
+    if (d.weight_frag == nullptr || !d.residual || d.act != HISEG_ACT_RELU || d.a_up != 1 || d.Cout % 128) return 0;
+    int r;
+    switch (variant - 150) {
+      case 1: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 1>(a, s); break;
+      case 2: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 2>(a, s); break;
+      case 3: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 3>(a, s); break;
+      case 4: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 4>(a, s); break;
+      case 8: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 8>(a, s); break;
+      case 15: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 15>(a, s); break;
+      case 16: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 16>(a, s); break;
+      case 32: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 32>(a, s); break;
+      case 47: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 47>(a, s); break;
+      default: return 0;
+    }
+    return r < 0 ? r : 1;
+  }
+#endif
+  if ((variant < 104 || variant > 107) || d.weight_frag == nullptr) return 0;
+  if (d.dtype != HISEG_BF16 || d.out_dtype != HISEG_BF16) return 0;
+  if ((d.a_up != 1 && d.a_up != 2) || d.in_scale != nullptr || d.convT || d.mul != nullptr || d.out2 != nullptr)
+    return 0;
+  if (d.KH != 3 || d.KW != 3 || d.stride != 1 || d.pad != 1 || d.Ho != d.H || d.Wo != d.W) return 0;
+  if (d.act != HISEG_ACT_NONE && d.act != HISEG_ACT_RELU) return 0;
+  if (d.Ca % 32 != 0 || d.Cb % 32 != 0 || (d.Ca + d.Cb) % 64 != 0 || d.Ca < 64 || d.K_pad != 9 * (d.Ca + d.Cb))
+    return 0;
+  if ((d.a_cstride | d.a_coff) & 7) return 0;
+  if (d.Cb && (d.srcB == nullptr || ((d.b_cstride | d.b_coff) & 7))) return 0;
+  if ((d.Cout & (variant == 105 ? 255 : 127)) || d.Cout_pad != d.Cout || ((d.o_cstride | d.o_coff) & 7) ||
+      (d.residual && ((d.r_cstride | d.r_coff) & 7)))
+    return 0;
+  if ((((uintptr_t)d.scale | (uintptr_t)d.shift | (uintptr_t)d.out | (uintptr_t)d.residual |
+        (uintptr_t)d.weight_frag) & 15))
+    return 0;
+  const long long span_a = (long long)d.N * (d.H / d.a_up) * (d.W / d.a_up) * d.a_cstride * 2;
+  const long long span_b = d.Cb ? (long long)d.N * d.H * d.W * d.b_cstride * 2 : 0;
+  const long long span_w = (long long)d.Cout_pad * d.K_pad * 2;
+  const long long span_r = d.residual ? (long long)a.M * d.r_cstride * 2 : 0;
+  if (span_a >= 0x7fffffffll || span_b >= 0x7fffffffll || span_w >= 0x7fffffffll || span_r >= 0x7fffffffll) return 0;
+  if ((long long)d.N * d.H * d.W >= (1ll << 29)) return 0;
+  if (d.a_up == 2 && (d.residual || d.act != HISEG_ACT_RELU)) return 0;   // the smp decoder conv1 form only
+  const int r = variant == 105 ? launch_hwc_nw<8>(a, s)
+              : variant == 106 ? launch_hwc_nw<4, true>(a, s)
+              : variant == 107 ? launch_hwc_nw<4, false, true>(a, s)
+                               : launch_hwc_nw<4>(a, s);
+  return r < 0 ? r : 1;
+}
+
+}  // namespace hiseg

@@ -41,7 +41,9 @@ typedef __attribute__((address_space(3))) void hr_lds_void;
 // 128-Cout x 16 x 16 workgroup of four waves; (1, 2) a 64-Cout x 16 x 32 workgroup of four waves (the 64-channel
 // layers: every wave keeps the 64 x 128 wave tile); (2, 2) 128 Cout x 16 x 32 with eight waves.  The per-element
 // accumulation order is the same for every configuration: results are bit-identical across them.
-template <int ACT, bool RES, int SCH, bool UP = false, int WCO = 2, int TWB = 1>
+// ABL (DIAG builds only, timing ablations -- wrong results): bit 0 no A loads in the K loop, bit 1 no halo DMA after
+// the prologue, bit 2 no B-fragment LDS reads after the prologue, bit 3 no slice barrier, bit 4 no MFMAs.
+template <int ACT, bool RES, int SCH, bool UP = false, int WCO = 2, int TWB = 1, int ABL = 0>
 __global__ void __launch_bounds__(WCO * TWB * 128, (WCO * TWB > 2) ? 1 : 2) conv_hwr_kernel(ConvArgs a) {
   constexpr int BCO = 64 * WCO, TM = 4, TN = 8;
   constexpr int TW = 16 * TWB, NPW = 2 * TWB, NW = WCO * NPW, HWD = TW + 2;
@@ -183,15 +185,20 @@ __global__ void __launch_bounds__(WCO * TWB * 128, (WCO * TWB > 2) ? 1 : 2) conv
     if constexpr ((SCH & 2) != 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
+      if constexpr ((ABL & 16) == 0) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[i]),
-                                                             __builtin_bit_cast(bf16x8_t, bf[j + KY]), acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[i]),
+                                                               __builtin_bit_cast(bf16x8_t, bf[j + KY]), acc[i][j], 0, 0, 0);
+      } else {
+        acc[i][0][0] += __builtin_bit_cast(float, af[i][0]) + __builtin_bit_cast(float, bf[KY][1]);
+      }
       __builtin_amdgcn_sched_barrier(0);
-      if (load_next) af[i] = __builtin_amdgcn_raw_buffer_load_b128(rF, a_lane + (unsigned)i * a_ct_step, so, 0);
+      if ((ABL & 1) == 0 && load_next)
+        af[i] = __builtin_amdgcn_raw_buffer_load_b128(rF, a_lane + (unsigned)i * a_ct_step, so, 0);
     }
     if constexpr ((SCH & 2) != 0) __builtin_amdgcn_s_setprio(0);
-    if constexpr (read_b) {
+    if constexpr (read_b && (ABL & 4) == 0) {
       if constexpr (REUSE) {   // the next kx's window: rows 0..9 at column shift kx + 1
 #pragma unroll
         for (int k = 0; k < NB; ++k) bf[k] = rdB(ln, buf, st / 3 + 1, k);
@@ -201,16 +208,18 @@ __global__ void __launch_bounds__(WCO * TWB * 128, (WCO * TWB > 2) ? 1 : 2) conv
       }
     }
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (st < 6) {   // pieces st, st + 6 of slice sl + 1's halo
+    if constexpr (st < 6 && (ABL & 2) == 0) {   // pieces st, st + 6 of slice sl + 1's halo
       if (more) {
 #pragma unroll
         for (int p = st; p < PPW; p += 6) halo_dma(p, sl + 1, buf ^ 1);
       }
     }
     if constexpr (st == 8) {
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      __syncthreads();   // slice sl+1's halo is in LDS; every wave is done reading slice sl's buffer
-      if (more) {
+      if constexpr ((ABL & 8) == 0) {
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        __syncthreads();   // slice sl+1's halo is in LDS; every wave is done reading slice sl's buffer
+      }
+      if (more && (ABL & 4) == 0) {
 #pragma unroll
         for (int k = 0; k < NB; ++k) bf[k] = rdB(ln, buf ^ 1, 0, k);
       }
@@ -301,7 +310,7 @@ __global__ void __launch_bounds__(WCO * TWB * 128, (WCO * TWB > 2) ? 1 : 2) conv
   }
 }
 
-template <int ACT, bool RES, int SCH, bool UP = false, int WCO = 2, int TWB = 1>
+template <int ACT, bool RES, int SCH, bool UP = false, int WCO = 2, int TWB = 1, int ABL = 0>
 static int launch_hwr(const ConvArgs& a, hipStream_t s) {
   const hiseg_conv2d_desc& d = a.d;
   constexpr int BCO = 64 * WCO, TW = 16 * TWB, NW = WCO * 2 * TWB;
@@ -310,7 +319,7 @@ static int launch_hwr(const ConvArgs& a, hipStream_t s) {
   const int tiles = d.N * ((d.H + 15) / 16) * ((d.W + TW - 1) / TW);
   const int nco = d.Cout_pad / BCO;
   const size_t lds = halo2 > epi ? halo2 : epi;
-  auto kern = conv_hwr_kernel<ACT, RES, SCH, UP, WCO, TWB>;
+  auto kern = conv_hwr_kernel<ACT, RES, SCH, UP, WCO, TWB, ABL>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -348,6 +357,24 @@ static int launch_hwr_wide(const ConvArgs& a, hipStream_t s) {
 // (64-multiple Cout), 101 = SCH 6 on 128-Cout x 16 x 32-pixel tiles with eight waves.
 int conv_hwr_try(const ConvArgs& a, hipStream_t s, int variant) {
   const hiseg_conv2d_desc& d = a.d;
+#ifdef HISEG_DIAG
+  if (variant >= 110 && variant < 142) {   // timing ablations of the automatic configuration (res + ReLU only)
+    if (d.weight_frag == nullptr || !d.residual || d.act != HISEG_ACT_RELU || d.a_up != 1) return 0;
+    int r;
+    switch (variant - 110) {
+      case 1: r = launch_hwr<HISEG_ACT_RELU, true, 6, false, 2, 1, 1>(a, s); break;
+      case 2: r = launch_hwr<HISEG_ACT_RELU, true, 6, false, 2, 1, 2>(a, s); break;
+      case 4: r = launch_hwr<HISEG_ACT_RELU, true, 6, false, 2, 1, 4>(a, s); break;
+      case 8: r = launch_hwr<HISEG_ACT_RELU, true, 6, false, 2, 1, 8>(a, s); break;
+      case 15: r = launch_hwr<HISEG_ACT_RELU, true, 6, false, 2, 1, 15>(a, s); break;
+      case 16: r = launch_hwr<HISEG_ACT_RELU, true, 6, false, 2, 1, 16>(a, s); break;
+      case 7: r = launch_hwr<HISEG_ACT_RELU, true, 6, false, 2, 1, 7>(a, s); break;
+      case 3: r = launch_hwr<HISEG_ACT_RELU, true, 6, false, 2, 1, 3>(a, s); break;
+      default: return 0;
+    }
+    return r < 0 ? r : 1;
+  }
+#endif
   if (!((variant >= 92 && variant <= 97) || variant == 100 || variant == 101) || d.weight_frag == nullptr) return 0;
   if (d.dtype != HISEG_BF16 || d.out_dtype != HISEG_BF16) return 0;
   if ((d.a_up != 1 && d.a_up != 2) || d.in_scale != nullptr || d.convT || d.mul != nullptr || d.out2 != nullptr)

@@ -500,6 +500,7 @@ int conv_hw_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_pw_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_hwr_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_hwt_try(const ConvArgs& a, hipStream_t s, int variant);
+int conv_hwc_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_small_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_rows_try(const ConvArgs& a, hipStream_t s, int variant);
 bool conv_pw_applies(const ConvArgs& a);
@@ -522,7 +523,7 @@ extern "C" int hiseg_conv2d_fwd(const hiseg_conv2d_desc* d, hiseg_stream_t strea
 static bool release_variant(int v) {
   return v == -1 || v == 0 || (v >= 1 && v <= 8) || v == 50 || v == 51 || v == 52 || v == 54 || v == 58 ||
          (v >= 60 && v <= 69) || v == 70 || v == 71 || v == 72 || v == 74 || v == 80 || v == 82 || v == 84 || v == 86 ||
-         v == 88 || v == 89 || v == 90 || (v >= 92 && v <= 101) || v == 103;
+         v == 88 || v == 89 || v == 90 || (v >= 92 && v <= 101) || v == 103 || (v >= 104 && v <= 107);
 }
 
 // Workspace bytes the automatic choice uses for this layer (split-K generic kernel), 0 when it needs none.
@@ -661,8 +662,11 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
   } else if (variant == 90) {
     const int r = conv_pw_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
-  } else if ((variant >= 92 && variant <= 97) || variant == 100 || variant == 101) {
+  } else if ((variant >= 92 && variant <= 97) || variant == 100 || variant == 101 || (variant >= 110 && variant < 142)) {
     const int r = conv_hwr_try(a, s, variant);
+    if (r != 0) return r < 0 ? r : HISEG_OK;
+  } else if ((variant >= 104 && variant <= 107) || (variant >= 150 && variant < 214)) {
+    const int r = conv_hwc_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
   } else if (variant == 103) {
     const int r = conv_hwt_try(a, s, variant);
@@ -723,6 +727,14 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
     // MFMA-priority configuration (variant 97; tools/conv_bench.py, profiles/r3_conv_bench_hwr*.json: 0.732 vs
     // 0.793 ms (variant 86) on 256->256 @64x48 x256 ROIs, 0.879 vs 0.930 ms on 128->128 @128x96, 0.364 vs 0.408 ms
     // on 128->256; bit-identical to variant 86)
+    // Round 5: the Cout-split form of the same kernel (conv_hwc.hip, variant 104: each wave 32 Cout x all 256 pixels
+    // of the tile -- half the weight-fragment loads, each halo row's B fragment reused across the 3 ky taps;
+    // tools/conv_bench.py, profiles/r5_conv_hwc.txt: 256->256 @64x48 x256 ROIs 0.736 -> 0.678 ms, 128->128 @128x96
+    // 0.875 -> 0.799, 128->256 0.369 -> 0.345; bit-identical to variant 97 / 86)
+    if (v == 0 && !four_waves && halo && d->weight_frag != nullptr && d->Cout % 128 == 0) {
+      const int r = conv_hwc_try(a, s, 104);
+      if (r != 0) return r < 0 ? r : HISEG_OK;
+    }
     if (v == 0 && !four_waves && halo && d->weight_frag != nullptr && d->Cout % 128 == 0) {
       const int r = conv_hwr_try(a, s, 97);
       if (r != 0) return r < 0 ? r : HISEG_OK;

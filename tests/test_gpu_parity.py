@@ -1119,6 +1119,61 @@ def test_conv_hwt_bit_identical_to_hwr(shape):
     assert torch.equal(outs[0], outs[97])
 
 
+@pytest.mark.parametrize("shape", [(2, 256, 0, 256, 64, 48, True, True), (3, 128, 0, 128, 37, 21, True, False),
+                                   (2, 128, 0, 256, 33, 17, False, True), (2, 128, 128, 128, 32, 24, False, True),
+                                   (2, 64, 64, 384, 20, 30, True, True), (1, 256, 0, 128, 16, 16, False, False),
+                                   (2, 192, 64, 256, 9, 23, True, False)])
+def test_conv_hwc_bit_identical_to_hwr(shape):
+    """Variants 104 / 106 (conv_hwc.hip, round 5: each wave 32 Cout x all 256 pixels of the tile, every halo row's B
+    fragment reused across the 3 ky taps; 106 with the residual tile prefetched into LDS) and 105 (256-Cout workgroups):
+    conv_hwr's per-element accumulation order (channel-major slices, kx-major / ky-inner taps, one 32-channel MFMA per
+    (slice, tap)) -- equal to variant 97 bit for bit: ragged pixel tiles, residual / ReLU / none, two sources, Cout
+    128 / 256 / 384; the automatic choice takes 104 for 128-multiple Cout.  Outputs NaN-prefilled."""
+    from hiseg import ops
+    N, Ca, Cb, Cout, H, W, res, relu = shape
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(37)
+    xa = ops.Act.from_nchw(torch.randn(N, Ca, H, W, device=DEV, generator=g), dt)
+    xb = ops.Act.from_nchw(torch.randn(N, Cb, H, W, device=DEV, generator=g), dt) if Cb else None
+    w = torch.randn(Cout, Ca + Cb, 3, 3, device=DEV, generator=g) / ((Ca + Cb) * 9) ** 0.5
+    p = ops.pack_conv(w, torch.randn(Cout, device=DEV, generator=g) * 0.1, None, int(relu), dt, DEV, pad=1,
+                      split=(Ca, Cb) if Cb else None)
+    assert p.weight_frag is not None
+    R = ops.Act.from_nchw(torch.randn(N, Cout, H, W, device=DEV, generator=g), dt) if res else None
+    outs = {}
+    vs = (97, 104, 106, 0) + ((105,) if Cout % 256 == 0 else ())
+    for v in vs:
+        o = ops.Act.new(N, H, W, Cout, dt, torch.device(DEV))
+        o.t.fill_(float("nan"))
+        outs[v] = ops.conv2d(p, xa, xb, out=o, residual=R, variant=v).t.clone()
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[97].float()).all()
+    for v in vs:
+        assert torch.equal(outs[v], outs[97]), f"variant {v}"
+
+
+@pytest.mark.parametrize("shape", [(2, 320, 128, 256, 30, 40), (2, 256, 64, 128, 20, 24), (1, 128, 64, 128, 18, 34)])
+def test_conv_hwc_upsampled_decoder_bit_identical(shape):
+    """The smp decoder's conv1 form (src A nearest-x2 upsampled, src B the encoder skip; ReLU, no residual) on
+    conv_hwc (variant 104) equals conv_hwr (97) bit for bit."""
+    from hiseg import ops
+    N, Ca, Cb, Cout, H, W = shape
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(43)
+    xa = ops.Act.from_nchw(torch.randn(N, Ca, H // 2, W // 2, device=DEV, generator=g), dt)
+    xb = ops.Act.from_nchw(torch.randn(N, Cb, H, W, device=DEV, generator=g), dt)
+    w = torch.randn(Cout, Ca + Cb, 3, 3, device=DEV, generator=g) / ((Ca + Cb) * 9) ** 0.5
+    p = ops.pack_conv(w, torch.randn(Cout, device=DEV, generator=g) * 0.1, None, 1, dt, DEV, pad=1, split=(Ca, Cb))
+    outs = {}
+    for v in (97, 104, 0):
+        o = ops.Act.new(N, H, W, Cout, dt, torch.device(DEV))
+        o.t.fill_(float("nan"))
+        outs[v] = ops.conv2d(p, xa, xb, out=o, a_up=2, variant=v).t.clone()
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[97].float()).all()
+    assert torch.equal(outs[104], outs[97]) and torch.equal(outs[0], outs[97])
+
+
 @pytest.mark.parametrize("shape", [(2, 37, 45, 240, 5, 1), (3, 20, 20, 2304, 5, 1), (2, 33, 47, 144, 3, 2),
                                    (2, 40, 40, 480, 5, 2), (1, 9, 7, 192, 3, 1), (2, 64, 48, 200, 3, 1)])
 def test_dwconv_lds_tile_bit_identical_to_gather_kernel(shape, monkeypatch):

@@ -23,6 +23,7 @@ DEV = "cuda"
 # name: (N, Ca, Cb, Cout, H, W, k, residual)
 SHAPES = {
     "res256_3x3_64x48": (256, 256, 0, 256, 64, 48, 3, True),
+    "c256to256_3x3_64x48": (256, 256, 0, 256, 64, 48, 3, False),
     "res128_3x3_128x96": (256, 128, 0, 128, 128, 96, 3, True),
     "c128to256_3x3_64x48": (256, 128, 0, 256, 64, 48, 3, False),
     "res64_3x3_64x48": (256, 64, 0, 64, 64, 48, 3, True),
