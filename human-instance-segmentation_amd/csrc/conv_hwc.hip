@@ -47,9 +47,9 @@ __device__ __forceinline__ void hc_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned l
 // (Measured and not kept, same box, 256->256 @64x48 x 256 ROIs: weights loaded two kx blocks ahead, 0.698 vs 0.698 ms;
 // a progressive epilogue storing each output row from the accumulators as soon as its last MFMA ran, 8-B stores
 // straight to HBM, 0.728 vs 0.698 ms -- bit-identical both.)
-// HV: the next slice's halo pieces (and, at the end, the residual tile) through registers -- buffer_load_dwordx4 at
-// the start of a kx block, ds_write_b128 at its end -- instead of LDS-DMA; pieces lying wholly past the halo skipped.
-template <int ACT, bool RES, int NW, bool UP = false, int ABL = 0, bool RP = false, bool HV = false>
+// (Also measured and not kept: the halo pieces and the residual tile through registers -- buffer_load_dwordx4, then
+// ds_write_b128 -- instead of LDS-DMA, 0.710 vs 0.695 ms.)
+template <int ACT, bool RES, int NW, bool UP = false, int ABL = 0, bool RP = false>
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(ConvArgs a) {
   constexpr int BCO = 32 * NW, TM = 2, NR = 16;    // wave tile: 32 Cout x (16 rows x 16 columns)
   constexpr int TW = 16, HWD = TW + 2;
@@ -118,26 +118,6 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
   auto hbuf = [&](int sl) __attribute__((always_inline)) -> int {
     if constexpr (RP) return ((nsl - 1 - sl) & 1) ? 32 * 1024 : 56 * 1024;
     else return (sl & 1) * HB;
-  };
-  // the source of halo piece p of slice sl: resource, byte offset
-  auto halo_src = [&](int p, int sl, unsigned& off) __attribute__((always_inline)) -> bool {
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    const int hr = 16 * (NW * p + w) + (ln >> 2);
-    const int hy = hr / HWD, hx = hr - HWD * hy;
-    const int iy = y0 + hy - 1, ix = x0 + hx - 1;
-    const bool ok = hr < NHR && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
-    const int chunk = (ln & 3) ^ (((hx >> 2) & 1) << 1);
-    const bool fb = 32 * sl >= d.Ca;
-    const int cs = fb ? d.b_cstride : d.a_cstride, coff = fb ? d.b_coff + 32 * sl - d.Ca : d.a_coff + 32 * sl;
-    if constexpr (UP) {
-      const int ush = fb ? 0 : 1;
-      off = ok ? (unsigned)((((n * (d.H >> ush) + (iy >> ush)) * (d.W >> ush) + (ix >> ush)) * cs + coff + chunk * 8) * 2)
-               : OOB;
-    } else {
-      off = ok ? (unsigned)((((n * d.H + iy) * d.W + ix) * cs + coff + chunk * 8) * 2) : OOB;
-    }
-    return fb;
   };
   auto halo_dma = [&](int p, int sl, int boff) __attribute__((always_inline)) {
     if (16 * (NW * p + w) >= NHR) return;   // a piece wholly past the halo (wave-uniform): nothing to load
@@ -215,27 +195,13 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
     const int buf = hbuf(sl);
     const bool more = sl + 1 < nsl;
     if ((ABL & 1) == 0 && (KX < 2 || more)) load_blk(an, KX < 2 ? sl : sl + 1, KX < 2 ? KX + 1 : 0);
-    hc_u4 hv[HV ? PH : 1];
-    if constexpr (HV && KX < 2) {   // this block's pieces of slice sl + 1's halo, into registers
-      if (more) {
-#pragma unroll
-        for (int q = 0; q < PH; ++q) {
-          const int p = KX * PH + q;
-          if (p < PPW && 16 * (NW * p + w) < NHR) {
-            unsigned off;
-            const bool fb = halo_src(p, sl + 1, off);
-            hv[q] = __builtin_amdgcn_raw_buffer_load_b128(fb ? rB : rA, off, 0, 0);
-          }
-        }
-      }
-    }
     // This block's LDS-DMA pieces (the next slice's halo; RP: residual rows), issued after row 2's MFMAs.  The
     // compiler does not see the asm DMA in its vmcnt accounting, so a piece issued before its wait for a weight
     // fragment of this block would make that wait cover the weight loads issued at the start of this block (measured:
     // a stall per block); after row 2 every fragment of the block has been waited for, and the pieces get the rest of
     // this block to land (they are older than the next block's weight loads).
     auto pieces = [&]() __attribute__((always_inline)) {
-      if constexpr ((ABL & 2) != 0 || HV) {
+      if constexpr ((ABL & 2) != 0) {
       } else if constexpr (KX < 2) {
         if (more) {
 #pragma unroll
@@ -290,17 +256,6 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
       }
     }
     __builtin_amdgcn_s_setprio(0);
-    if constexpr (HV && KX < 2) {   // ... and into the other halo buffer, lane l at byte 16 l of its piece
-      if (more) {
-        const int nb = hbuf(sl + 1);
-#pragma unroll
-        for (int q = 0; q < PH; ++q) {
-          const int p = KX * PH + q;
-          if (p < PPW && 16 * (NW * p + w) < NHR)
-            *reinterpret_cast<hc_u4*>(reinterpret_cast<char*>(smem) + nb + 1024 * (NW * p + w) + 16 * ln) = hv[q];
-        }
-      }
-    }
     if constexpr (KX == 2 && (ABL & 8) == 0) {
       if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // every halo piece (the next weights may fly)
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -334,21 +289,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
     return;
   }
   char* tile = reinterpret_cast<char*>(smem);
-  if constexpr (RES && HV) {   // the residual tile through registers: 16 loads per lane, then 16 LDS stores
-    hc_u4 rv[NRI];
-#pragma unroll
-    for (int k = 0; k < NRI; ++k) {
-      const int c = lane % CPR;
-      const int r = RPI * (w + NW * k) + lane / CPR;
-      const int px = px_of(r);
-      const unsigned off = px >= 0 ? (unsigned)((px * d.r_cstride + d.r_coff + co0 + ((c ^ (r & SWM)) * 8)) * 2) : OOB;
-      rv[k] = __builtin_amdgcn_raw_buffer_load_b128(rR, off, 0, 0);
-    }
-#pragma unroll
-    for (int k = 0; k < NRI; ++k)
-      *reinterpret_cast<hc_u4*>(tile + RPI * (w + NW * k) * EROWB + 16 * lane) = rv[k];
-    __syncthreads();
-  } else if constexpr (RES && !RP) {
+  if constexpr (RES && !RP) {
 #pragma unroll
     for (int k = 0; k < NRI; ++k) res_dma(k);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -412,7 +353,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
   }
 }
 
-template <int ACT, bool RES, int NW, bool UP = false, int ABL = 0, bool RP = false, bool HV = false>
+template <int ACT, bool RES, int NW, bool UP = false, int ABL = 0, bool RP = false>
 static int launch_hwc(const ConvArgs& a, hipStream_t s) {
   const hiseg_conv2d_desc& d = a.d;
   constexpr int BCO = 32 * NW;
@@ -421,7 +362,7 @@ static int launch_hwc(const ConvArgs& a, hipStream_t s) {
   const int tiles = d.N * ((d.H + 15) / 16) * ((d.W + 15) / 16);
   const int nco = d.Cout_pad / BCO;
   const size_t lds = RP ? (size_t)80 * 1024 : (halo2 > epi ? halo2 : epi);
-  auto kern = conv_hwc_kernel<ACT, RES, NW, UP, ABL, RP, HV>;
+  auto kern = conv_hwc_kernel<ACT, RES, NW, UP, ABL, RP>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -431,15 +372,14 @@ static int launch_hwc(const ConvArgs& a, hipStream_t s) {
   return hiseg_check_launch("conv_hwc");
 }
 
-template <int NW, bool RP = false, bool HV = false>
+template <int NW, bool RP = false>
 static int launch_hwc_nw(const ConvArgs& a, hipStream_t s) {
   const hiseg_conv2d_desc& d = a.d;
-  if (d.a_up == 2) return launch_hwc<HISEG_ACT_RELU, false, NW, true, 0, false, HV>(a, s);   // (checked the form)
+  if (d.a_up == 2) return launch_hwc<HISEG_ACT_RELU, false, NW, true>(a, s);   // (conv_hwc_try checked the form)
   const bool res = d.residual != nullptr, relu = d.act == HISEG_ACT_RELU;
-  return res ? (relu ? launch_hwc<HISEG_ACT_RELU, true, NW, false, 0, RP, HV>(a, s)
-                     : launch_hwc<HISEG_ACT_NONE, true, NW, false, 0, RP, HV>(a, s))
-             : (relu ? launch_hwc<HISEG_ACT_RELU, false, NW, false, 0, false, HV>(a, s)
-                     : launch_hwc<HISEG_ACT_NONE, false, NW, false, 0, false, HV>(a, s));
+  return res ? (relu ? launch_hwc<HISEG_ACT_RELU, true, NW, false, 0, RP>(a, s)
+                     : launch_hwc<HISEG_ACT_NONE, true, NW, false, 0, RP>(a, s))
+             : (relu ? launch_hwc<HISEG_ACT_RELU, false, NW>(a, s) : launch_hwc<HISEG_ACT_NONE, false, NW>(a, s));
 }
 
 // 1 = launched, 0 = the layer does not qualify (caller falls back), <0 on error.  Variant 104: 128-Cout workgroups
@@ -468,7 +408,7 @@ int conv_hwc_try(const ConvArgs& a, hipStream_t s, int variant) {
     return r < 0 ? r : 1;
   }
 #endif
-  if ((variant < 104 || variant > 107) || d.weight_frag == nullptr) return 0;
+  if ((variant < 104 || variant > 106) || d.weight_frag == nullptr) return 0;
   if (d.dtype != HISEG_BF16 || d.out_dtype != HISEG_BF16) return 0;
   if ((d.a_up != 1 && d.a_up != 2) || d.in_scale != nullptr || d.convT || d.mul != nullptr || d.out2 != nullptr)
     return 0;
@@ -493,7 +433,6 @@ int conv_hwc_try(const ConvArgs& a, hipStream_t s, int variant) {
   if (d.a_up == 2 && (d.residual || d.act != HISEG_ACT_RELU)) return 0;   // the smp decoder conv1 form only
   const int r = variant == 105 ? launch_hwc_nw<8>(a, s)
               : variant == 106 ? launch_hwc_nw<4, true>(a, s)
-              : variant == 107 ? launch_hwc_nw<4, false, true>(a, s)
                                : launch_hwc_nw<4>(a, s);
   return r < 0 ? r : 1;
 }
