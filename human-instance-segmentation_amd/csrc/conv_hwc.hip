@@ -49,7 +49,15 @@ __device__ __forceinline__ void hc_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned l
 // straight to HBM, 0.728 vs 0.698 ms -- bit-identical both.)
 // (Also measured and not kept: the halo pieces and the residual tile through registers -- buffer_load_dwordx4, then
 // ds_write_b128 -- instead of LDS-DMA, 0.710 vs 0.695 ms.)
-template <int ACT, bool RES, int NW, bool UP = false, int ABL = 0, bool RP = false>
+// ST: BatchNorm batch statistics of the output fused into the epilogue (train mode, the conv feeding a BatchNorm: no
+// activation, no residual; advanced/normalization_comparison.py:181-182).  The epilogue's store loop already moves
+// every bf16 output chunk through registers: each thread accumulates shifted sums of its 8 channels over the 16
+// pixels it stores, the 4 threads of a chunk in a wave are Chan-merged in a fixed order, and each wave writes count,
+// mean and M2 per channel as split (pixel tile, wave) of d.stats_partial [S][3][Cout] (S = hiseg_conv2d_stats_tiles),
+// the layout hiseg_bn_finalize_n merges -- the separate statistics pass (one read of z) is gone.  (Measured first
+// forms: statistics from the accumulators spilled 65 registers in the K loop, conv forward +15 %; a Welford update per
+// pixel plus a cross-wave LDS merge and barrier, conv forward +6 %.)
+template <int ACT, bool RES, int NW, bool UP = false, int ABL = 0, bool RP = false, bool ST = false>
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(ConvArgs a) {
   constexpr int BCO = 32 * NW, TM = 2, NR = 16;    // wave tile: 32 Cout x (16 rows x 16 columns)
   constexpr int TW = 16, HWD = TW + 2;
@@ -342,6 +350,17 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
   }
   __syncthreads();
   constexpr int NST = NPX * CPR / (NW * 64);   // NPX rows x CPR chunks over the workgroup's threads
+  // ST: thread t stores chunk t % CPR (8 channels) of rows t / CPR + 16 k: 16 pixels of those channels pass through its
+  // registers; it sums them shifted by its first valid value (shifted sums: no division in the loop, no cancellation
+  // over 16 values), then the 4 threads of a chunk in the wave are Chan-merged (fixed order) and the wave writes its
+  // partial as split (pixel tile, wave) -- no cross-wave merge, no extra barrier
+  float sk[8], s1[8], s2[8];
+  int sn = 0;
+  if constexpr (ST) {
+    static_assert(!RES && ACT == HISEG_ACT_NONE && NW == 4, "fused statistics: the conv feeding a BatchNorm");
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sk[e] = s1[e] = s2[e] = 0.f;
+  }
 #pragma unroll 4
   for (int k = 0; k < NST; ++k) {
     const int idx = t + NW * 64 * k;
@@ -350,10 +369,57 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
     const uint4 v = *reinterpret_cast<const uint4*>(tile + r * EROWB + ((c ^ (r & SWM)) << 4));
     if (px >= 0 && co < d.Cout)
       *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(d.out) + (long long)px * d.o_cstride + d.o_coff + co) = v;
+    if constexpr (ST) {
+      if (px >= 0) {
+        const unsigned wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = __builtin_bit_cast(float, (e & 1) ? (wv[e >> 1] & 0xffff0000u) : (wv[e >> 1] << 16));
+          if (sn == 0) sk[e] = x;
+          const float dx = x - sk[e];
+          s1[e] += dx;
+          s2[e] = fmaf(dx, dx, s2[e]);
+        }
+        ++sn;
+      }
+    }
+  }
+  if constexpr (ST) {
+    float nn = (float)sn, mu[8], q2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      mu[e] = sn ? sk[e] + s1[e] / nn : 0.f;
+      q2[e] = sn ? fmaxf(s2[e] - s1[e] * s1[e] / nn, 0.f) : 0.f;
+    }
+#pragma unroll
+    for (int m = 16; m < 64; m <<= 1) {   // lanes ^ 16, ^ 32: the wave's 4 threads of the chunk
+      const float nb = __shfl_xor(nn, m, 64);
+      const float nt = nn + nb;
+      const float fb = nt > 0.f ? nb / nt : 0.f, fab = nt > 0.f ? nn * nb / nt : 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float mb = __shfl_xor(mu[e], m, 64), qb = __shfl_xor(q2[e], m, 64);
+        const float dd = mb - mu[e];
+        mu[e] += dd * fb;
+        q2[e] += qb + dd * dd * fab;
+      }
+      nn = nt;
+    }
+    if (lane < 16) {
+      const long long C = d.Cout;
+      float* part = a.d.stats_partial + ((long long)((n * nty + ty) * ntx + tx) * NW + w) * 3 * C;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int ch = co0 + 8 * lane + e;
+        part[ch] = nn;
+        part[C + ch] = mu[e];
+        part[2 * C + ch] = q2[e];
+      }
+    }
   }
 }
 
-template <int ACT, bool RES, int NW, bool UP = false, int ABL = 0, bool RP = false>
+template <int ACT, bool RES, int NW, bool UP = false, int ABL = 0, bool RP = false, bool ST = false>
 static int launch_hwc(const ConvArgs& a, hipStream_t s) {
   const hiseg_conv2d_desc& d = a.d;
   constexpr int BCO = 32 * NW;
@@ -362,7 +428,7 @@ static int launch_hwc(const ConvArgs& a, hipStream_t s) {
   const int tiles = d.N * ((d.H + 15) / 16) * ((d.W + 15) / 16);
   const int nco = d.Cout_pad / BCO;
   const size_t lds = RP ? (size_t)80 * 1024 : (halo2 > epi ? halo2 : epi);
-  auto kern = conv_hwc_kernel<ACT, RES, NW, UP, ABL, RP>;
+  auto kern = conv_hwc_kernel<ACT, RES, NW, UP, ABL, RP, ST>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -380,6 +446,47 @@ static int launch_hwc_nw(const ConvArgs& a, hipStream_t s) {
   return res ? (relu ? launch_hwc<HISEG_ACT_RELU, true, NW, false, 0, RP>(a, s)
                      : launch_hwc<HISEG_ACT_NONE, true, NW, false, 0, RP>(a, s))
              : (relu ? launch_hwc<HISEG_ACT_RELU, false, NW>(a, s) : launch_hwc<HISEG_ACT_NONE, false, NW>(a, s));
+}
+
+// Whether variant `variant` takes the layer (the layer rules are conv_hwr_try's: the same operands, weight fragments and
+// halo; with d.stats_partial the fused-statistics form: variant 104, no activation, no residual).
+static bool conv_hwc_applies(const ConvArgs& a, int variant) {
+  const hiseg_conv2d_desc& d = a.d;
+  if ((variant < 104 || variant > 106) || d.weight_frag == nullptr) return false;
+  if (d.dtype != HISEG_BF16 || d.out_dtype != HISEG_BF16) return false;
+  if ((d.a_up != 1 && d.a_up != 2) || d.in_scale != nullptr || d.convT || d.mul != nullptr || d.out2 != nullptr)
+    return false;
+  if (d.KH != 3 || d.KW != 3 || d.stride != 1 || d.pad != 1 || d.Ho != d.H || d.Wo != d.W) return false;
+  if (d.act != HISEG_ACT_NONE && d.act != HISEG_ACT_RELU) return false;
+  if (d.Ca % 32 != 0 || d.Cb % 32 != 0 || (d.Ca + d.Cb) % 64 != 0 || d.Ca < 64 || d.K_pad != 9 * (d.Ca + d.Cb))
+    return false;
+  if ((d.a_cstride | d.a_coff) & 7) return false;
+  if (d.Cb && (d.srcB == nullptr || ((d.b_cstride | d.b_coff) & 7))) return false;
+  if ((d.Cout & (variant == 105 ? 255 : 127)) || d.Cout_pad != d.Cout || ((d.o_cstride | d.o_coff) & 7) ||
+      (d.residual && ((d.r_cstride | d.r_coff) & 7)))
+    return false;
+  if ((((uintptr_t)d.scale | (uintptr_t)d.shift | (uintptr_t)d.out | (uintptr_t)d.residual |
+        (uintptr_t)d.weight_frag) & 15))
+    return false;
+  const long long span_a = (long long)d.N * (d.H / d.a_up) * (d.W / d.a_up) * d.a_cstride * 2;
+  const long long span_b = d.Cb ? (long long)d.N * d.H * d.W * d.b_cstride * 2 : 0;
+  const long long span_w = (long long)d.Cout_pad * d.K_pad * 2;
+  const long long span_r = d.residual ? (long long)a.M * d.r_cstride * 2 : 0;
+  if (span_a >= 0x7fffffffll || span_b >= 0x7fffffffll || span_w >= 0x7fffffffll || span_r >= 0x7fffffffll) return false;
+  if ((long long)d.N * d.H * d.W >= (1ll << 29)) return false;
+  // upsampled src A: the smp decoder conv1 form only (ReLU, or no activation when the conv feeds a train-mode BN)
+  if (d.a_up == 2 && (d.residual || d.act != (d.stats_partial ? HISEG_ACT_NONE : HISEG_ACT_RELU))) return false;
+  if (d.stats_partial && (variant != 104 || d.residual || d.act != HISEG_ACT_NONE)) return false;
+  return true;
+}
+
+// BatchNorm statistics partials the automatic choice would fuse into this layer's epilogue (0: none): the pixel tiles
+int conv_hwc_stats_tiles(const ConvArgs& a) {
+  ConvArgs b = a;
+  float dummy;
+  b.d.stats_partial = &dummy;
+  if (!conv_hwc_applies(b, 104)) return 0;
+  return a.d.N * ((a.d.H + 15) / 16) * ((a.d.W + 15) / 16) * 4;   // (pixel tile, wave) splits
 }
 
 // 1 = launched, 0 = the layer does not qualify (caller falls back), <0 on error.  Variant 104: 128-Cout workgroups
@@ -408,29 +515,12 @@ int conv_hwc_try(const ConvArgs& a, hipStream_t s, int variant) {
     return r < 0 ? r : 1;
   }
 #endif
-  if ((variant < 104 || variant > 106) || d.weight_frag == nullptr) return 0;
-  if (d.dtype != HISEG_BF16 || d.out_dtype != HISEG_BF16) return 0;
-  if ((d.a_up != 1 && d.a_up != 2) || d.in_scale != nullptr || d.convT || d.mul != nullptr || d.out2 != nullptr)
-    return 0;
-  if (d.KH != 3 || d.KW != 3 || d.stride != 1 || d.pad != 1 || d.Ho != d.H || d.Wo != d.W) return 0;
-  if (d.act != HISEG_ACT_NONE && d.act != HISEG_ACT_RELU) return 0;
-  if (d.Ca % 32 != 0 || d.Cb % 32 != 0 || (d.Ca + d.Cb) % 64 != 0 || d.Ca < 64 || d.K_pad != 9 * (d.Ca + d.Cb))
-    return 0;
-  if ((d.a_cstride | d.a_coff) & 7) return 0;
-  if (d.Cb && (d.srcB == nullptr || ((d.b_cstride | d.b_coff) & 7))) return 0;
-  if ((d.Cout & (variant == 105 ? 255 : 127)) || d.Cout_pad != d.Cout || ((d.o_cstride | d.o_coff) & 7) ||
-      (d.residual && ((d.r_cstride | d.r_coff) & 7)))
-    return 0;
-  if ((((uintptr_t)d.scale | (uintptr_t)d.shift | (uintptr_t)d.out | (uintptr_t)d.residual |
-        (uintptr_t)d.weight_frag) & 15))
-    return 0;
-  const long long span_a = (long long)d.N * (d.H / d.a_up) * (d.W / d.a_up) * d.a_cstride * 2;
-  const long long span_b = d.Cb ? (long long)d.N * d.H * d.W * d.b_cstride * 2 : 0;
-  const long long span_w = (long long)d.Cout_pad * d.K_pad * 2;
-  const long long span_r = d.residual ? (long long)a.M * d.r_cstride * 2 : 0;
-  if (span_a >= 0x7fffffffll || span_b >= 0x7fffffffll || span_w >= 0x7fffffffll || span_r >= 0x7fffffffll) return 0;
-  if ((long long)d.N * d.H * d.W >= (1ll << 29)) return 0;
-  if (d.a_up == 2 && (d.residual || d.act != HISEG_ACT_RELU)) return 0;   // the smp decoder conv1 form only
+  if (!conv_hwc_applies(a, variant)) return 0;
+  if (d.stats_partial) {   // the fused-statistics epilogue (variant 104 only; conv_hwc_applies checked the form)
+    const int r = d.a_up == 2 ? launch_hwc<HISEG_ACT_NONE, false, 4, true, 0, false, true>(a, s)
+                              : launch_hwc<HISEG_ACT_NONE, false, 4, false, 0, false, true>(a, s);
+    return r < 0 ? r : 1;
+  }
   const int r = variant == 105 ? launch_hwc_nw<8>(a, s)
               : variant == 106 ? launch_hwc_nw<4, true>(a, s)
                                : launch_hwc_nw<4>(a, s);

@@ -501,6 +501,7 @@ int conv_pw_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_hwr_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_hwt_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_hwc_try(const ConvArgs& a, hipStream_t s, int variant);
+int conv_hwc_stats_tiles(const ConvArgs& a);
 int conv_small_try(const ConvArgs& a, hipStream_t s, int variant);
 int conv_rows_try(const ConvArgs& a, hipStream_t s, int variant);
 bool conv_pw_applies(const ConvArgs& a);
@@ -545,6 +546,20 @@ extern "C" long long hiseg_conv2d_workspace_bytes(const hiseg_conv2d_desc* d) {
   return splitk_bytes(a, splitk_plan(a));
 }
 
+extern "C" int hiseg_conv2d_stats_tiles(const hiseg_conv2d_desc* d) {
+  if (d == nullptr || d->dtype != HISEG_BF16 || d->convT || d->N <= 0) return 0;
+  const long long M = (long long)d->N * d->Ho * d->Wo;
+  if (M >= (1ll << 31)) return 0;
+  ConvArgs a;
+  a.d = *d;
+  a.M = (int)M;
+  a.Cin = d->Ca + d->Cb;
+  a.nK = d->K_pad / 64;
+  a.Hs = d->H / (d->a_up > 0 ? d->a_up : 1);
+  a.Ws = d->W / (d->a_up > 0 ? d->a_up : 1);
+  return conv_hwc_stats_tiles(a);
+}
+
 extern "C" int hiseg_conv2d_fwd_variant(const hiseg_conv2d_desc* d, int variant, hiseg_stream_t stream) {
 #ifndef HISEG_DIAG
   HISEG_REQUIRE(release_variant(variant), HISEG_ERR_BAD_ARG,
@@ -577,6 +592,24 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
   HISEG_REQUIRE(!d->convT || (d->KH == 1 && d->KW == 1 && d->stride == 1 && d->pad == 0 && d->Cout % 16 == 0 &&
                               d->Ho == d->H && d->Wo == d->W),
                 HISEG_ERR_BAD_SHAPE, "conv2d: convT requires a 1x1 GEMM with Cout = 4*C, C %% 4 == 0");
+  // BatchNorm statistics fused into the epilogue: only the halo kernel's fused-statistics form computes them, and no
+  // fallback may silently skip them (the caller would finalize garbage)
+  if (d->stats_partial) {
+    HISEG_REQUIRE(variant == 0 || variant == 104, HISEG_ERR_BAD_ARG, "conv2d: stats_partial with variant %d", variant);
+    HISEG_REQUIRE(al16(d->out) && al16(d->scale) && al16(d->shift), HISEG_ERR_BAD_SHAPE, "conv2d: alignment");
+    ConvArgs a;
+    a.d = *d;
+    a.M = (int)((long long)d->N * d->Ho * d->Wo);
+    a.Cin = Cin;
+    a.nK = d->K_pad / bk;
+    a.Hs = d->H / d->a_up;
+    a.Ws = d->W / d->a_up;
+    HISEG_REQUIRE(conv_hwc_stats_tiles(a) > 0, HISEG_ERR_BAD_ARG,
+                  "conv2d: stats_partial set but the layer has no fused-statistics kernel (hiseg_conv2d_stats_tiles)");
+    const int r = conv_hwc_try(a, (hipStream_t)stream, 104);
+    HISEG_REQUIRE(r != 0, HISEG_ERR_BAD_ARG, "conv2d: the fused-statistics kernel declined the layer");
+    return r < 0 ? r : HISEG_OK;
+  }
   // Operands of >= 2 GiB: the LDS-DMA kernels address through 32-bit buffer offsets, so the launch is split
   // into image ranges whose every operand spans < 2 GiB (NHWC images are contiguous blocks; the conv never
   // mixes images), each range a launch of its own on the same stream.

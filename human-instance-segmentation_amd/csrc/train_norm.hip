@@ -1153,6 +1153,16 @@ int bn_finalize_splits(const float* partial, int S, int C, long long P, const fl
   return hiseg_check_launch("bn_finalize");
 }
 
+extern "C" int hiseg_bn_finalize_n(const float* partial, int S, int C, long long P, const float* gamma,
+                                   const float* beta, float eps, float momentum, float* running_mean,
+                                   float* running_var, float* mean, float* invstd, float* scale, float* shift,
+                                   hiseg_stream_t stream) {
+  HISEG_REQUIRE(partial && mean && invstd && scale && shift && C > 0 && S > 0 && P > 0, HISEG_ERR_BAD_ARG,
+                "bn_finalize_n: bad arguments");
+  return bn_finalize_splits(partial, S, C, P, gamma, beta, eps, momentum, running_mean, running_var, mean, invstd,
+                            scale, shift, (hipStream_t)stream);
+}
+
 extern "C" int hiseg_bn_apply(const hiseg_bn_apply_desc* d, hiseg_stream_t stream) {
   HISEG_REQUIRE(d && d->z && d->y && d->scale && d->shift && d->P > 0 && d->C > 0 && d->HW > 0, HISEG_ERR_BAD_ARG,
                 "bn_apply: bad arguments");

@@ -138,6 +138,7 @@ class Conv2dDesc(Desc):
         ("weight_frag", c_void_p),
         ("act_beta", c_float),
         ("workspace", c_void_p), ("workspace_bytes", ctypes.c_longlong),
+        ("stats_partial", c_void_p),
     ]
 
 
@@ -284,6 +285,8 @@ def _declare(lib):
         "hiseg_conv2d_wgrad_dims": ([ctypes.POINTER(Conv2dDesc), c_int, P, P, P], c_int),
         "hiseg_conv2d_wgrad": ([ctypes.POINTER(Conv2dDesc), P, c_int, c_int, c_int, P, c_int, P], c_int),
         "hiseg_wgrad_path_stats": ([ctypes.POINTER(c_ll), c_int], c_int),
+        "hiseg_conv2d_stats_tiles": ([ctypes.POINTER(Conv2dDesc)], c_int),
+        "hiseg_bn_finalize_n": ([P, c_int, c_int, c_ll, P, P, c_float, c_float, P, P, P, P, P, P, P], c_int),
         "hiseg_wgrad_last_path": ([], c_int),
         "hiseg_conv2d_wgrad_reduce": ([P, c_int, ctypes.POINTER(WgradMap), P, P, c_int, P], c_int),
         "hiseg_pack_weights": ([P, c_int, c_int, P], c_int),

@@ -186,8 +186,9 @@ def up_conv_bn_relu(T: TE.Tape, conv: nn.Conv2d, bn: nn.BatchNorm2d, x_low: Act,
     z = Act.new(x_low.N, H, W, p.cout, x_low.dtype, dev)
     d = TE._desc(S, p, x_low, skip, z)
     d.H, d.W, d.Ho, d.Wo, d.a_up = H, W, H, W, 2
-    TE._chk(lib.hiseg_conv2d_fwd(ctypes.byref(d), TE._stream()), "conv2d(decoder)")
-    y, st = TE.bn_forward(T, bn, z, act=ACT_RELU)   # d holds x_low and skip for the weight gradient
+    stats = [] if isinstance(bn, nn.BatchNorm2d) else None
+    TE.conv_fwd(S, p, x_low, skip, d=d, stats=stats)
+    y, st = TE.bn_forward(T, bn, z, act=ACT_RELU, stats=stats)   # d holds x_low and skip for the weight gradient
 
     def back():
         dz = Act.new(z.N, z.H, z.W, z.C, z.dtype, dev, cpad=z.cstride, zero=z.cstride != z.C)

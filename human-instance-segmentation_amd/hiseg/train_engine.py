@@ -377,18 +377,39 @@ def _desc(S: TrainState, p: TConv, xa: Act, xb: Optional[Act], out: Act, *, act=
 
 
 def conv_fwd(S: TrainState, p: TConv, xa: Act, xb: Optional[Act] = None, *, act=ACT_NONE, out_dtype=None,
-             out: Optional[Act] = None, out2: Optional[Act] = None) -> Tuple[Act, L.Conv2dDesc]:
-    if p.convT:
-        oH, oW = 2 * xa.H, 2 * xa.W
+             out: Optional[Act] = None, out2: Optional[Act] = None, stats: Optional[list] = None,
+             d: Optional[L.Conv2dDesc] = None) -> Tuple[Act, L.Conv2dDesc]:
+    """Forward conv of the train path.  ``stats`` (a list): when the library fuses the BatchNorm batch statistics of
+    the output into the conv's epilogue (hiseg_conv2d_stats_tiles > 0: the bf16 3x3 halo-kernel layers), the
+    partials buffer and its split count are appended to it and bn_forward skips its statistics pass.  ``d``: a
+    prepared descriptor (up_conv_bn_relu's upsampled form)."""
+    if d is None:
+        if p.convT:
+            oH, oW = 2 * xa.H, 2 * xa.W
+        else:
+            oH = (xa.H + 2 * p.pad - p.kh) // p.stride + 1
+            oW = (xa.W + 2 * p.pad - p.kw) // p.stride + 1
+        if out is None:
+            out = Act.new(xa.N, oH, oW, p.cout, out_dtype or xa.dtype, xa.t.device)
+        d = _desc(S, p, xa, xb, out, act=act, out2=out2)
+        _splitk_workspace(d, p.kh, p.kw, xa.t.device)
     else:
-        oH = (xa.H + 2 * p.pad - p.kh) // p.stride + 1
-        oW = (xa.W + 2 * p.pad - p.kw) // p.stride + 1
-    if out is None:
-        out = Act.new(xa.N, oH, oW, p.cout, out_dtype or xa.dtype, xa.t.device)
-    d = _desc(S, p, xa, xb, out, act=act, out2=out2)
-    _splitk_workspace(d, p.kh, p.kw, xa.t.device)
+        out = d.out
+    if stats is not None and _fuse_bn_stats():
+        tiles = L.lib().hiseg_conv2d_stats_tiles(ctypes.byref(d))
+        if tiles > 0:
+            part = torch.empty(tiles * 3 * d.Cout, dtype=torch.float32, device=xa.t.device)
+            d.stats_partial = part
+            stats += [part, tiles]
     _chk(L.lib().hiseg_conv2d_fwd(ctypes.byref(d), _stream()), "conv2d(train)")
+    d.stats_partial = None   # the descriptor is reused by the backward (weight gradient)
     return out, d
+
+
+def _fuse_bn_stats() -> bool:
+    """HISEG_FUSED_BN_STATS=0: the separate statistics pass everywhere (A/B timing, the equivalence test); read per
+    call."""
+    return os.environ.get("HISEG_FUSED_BN_STATS", "1") != "0"
 
 
 def _splitk_workspace(d: L.Conv2dDesc, kh: int, kw: int, device) -> None:
@@ -561,24 +582,33 @@ def ln_backward(T: Tape, ln: LayerNorm2d, z: Act, y: Act, st: LNState, dz: Act, 
 
 
 def bn_forward(T: Tape, bn: nn.BatchNorm2d, z: Act, *, act: int, residual: Optional[Act] = None,
-               drop: Optional[torch.Tensor] = None, out: Optional[Act] = None) -> Tuple[Act, BNState]:
-    """Batch statistics of z (+ running update), y = act(bn(z) + residual) * drop."""
+               drop: Optional[torch.Tensor] = None, out: Optional[Act] = None,
+               stats: Optional[list] = None) -> Tuple[Act, BNState]:
+    """Batch statistics of z (+ running update), y = act(bn(z) + residual) * drop.  ``stats`` = [partials, splits]
+    the producing conv's epilogue wrote (conv_fwd), else a statistics pass over z."""
     if isinstance(bn, LayerNorm2d):
         return ln_forward(T, bn, z, act=act, residual=residual, drop=drop, out=out)
     lib = L.lib()
     C = z.C
     P = z.N * z.H * z.W
     st = BNState(C, z.t.device)
-    part = torch.empty(lib.hiseg_bn_partials() * 3 * C, dtype=torch.float32, device=z.t.device)
-    _chk(lib.hiseg_bn_stats(hdtype(z.dtype), z.ptr(), P, C, z.cstride, z.coff, part.data_ptr(), _stream()), "bn_stats")
+    if stats:
+        part, splits = stats
+    else:
+        part, splits = torch.empty(lib.hiseg_bn_partials() * 3 * C, dtype=torch.float32, device=z.t.device), None
+        _chk(lib.hiseg_bn_stats(hdtype(z.dtype), z.ptr(), P, C, z.cstride, z.coff, part.data_ptr(), _stream()),
+             "bn_stats")
     track = bn.track_running_stats and bn.running_mean is not None
     mom = bn.momentum if bn.momentum is not None else 0.1
     if track and bn.num_batches_tracked is not None:
         T.S.nbt.append(bn.num_batches_tracked)
-    _chk(lib.hiseg_bn_finalize(part.data_ptr(), C, P, _ptr(bn.weight), _ptr(bn.bias), float(bn.eps), float(mom),
-                               _ptr(bn.running_mean) if track else None, _ptr(bn.running_var) if track else None,
-                               st.mean.data_ptr(), st.invstd.data_ptr(), st.scale.data_ptr(), st.shift.data_ptr(),
-                               _stream()), "bn_finalize")
+    fin_args = (C, P, _ptr(bn.weight), _ptr(bn.bias), float(bn.eps), float(mom),
+                _ptr(bn.running_mean) if track else None, _ptr(bn.running_var) if track else None,
+                st.mean.data_ptr(), st.invstd.data_ptr(), st.scale.data_ptr(), st.shift.data_ptr(), _stream())
+    if splits is not None:
+        _chk(lib.hiseg_bn_finalize_n(part.data_ptr(), splits, *fin_args), "bn_finalize_n")
+    else:
+        _chk(lib.hiseg_bn_finalize(part.data_ptr(), *fin_args), "bn_finalize")
     if track:   # the kernel updated the running statistics in place: invalidate eval plans folded from them
         torch.autograd.graph.increment_version([bn.running_mean, bn.running_var])
     y = out if out is not None else Act.new(z.N, z.H, z.W, C, z.dtype, z.t.device, cpad=z.cstride)
@@ -639,8 +669,9 @@ def conv_bn_act(T: Tape, conv: nn.Conv2d, bn, act: int, x: Act, xb: Optional[Act
     S = T.S
     bn = _bn_module(bn)
     p = S.conv(conv, split=split, convT=convT)
-    z, d = conv_fwd(S, p, x, xb)
-    y, st = bn_forward(T, bn, z, act=act, residual=residual, drop=drop)
+    stats = [] if isinstance(bn, nn.BatchNorm2d) else None
+    z, d = conv_fwd(S, p, x, xb, stats=stats)
+    y, st = bn_forward(T, bn, z, act=act, residual=residual, drop=drop, stats=stats)
 
     def back():
         dz = Act.new(z.N, z.H, z.W, z.C, z.dtype, z.t.device, cpad=z.cstride, zero=z.cstride != z.C)

@@ -138,10 +138,20 @@ typedef struct hiseg_conv2d_desc {
    * bytes; null keeps every layer unsplit.  The plan depends on the layer and the per-image grid only;
    * whether to pass a workspace for a 3x3 layer is the caller's choice (it pays for small batches). */
   void* workspace; long long workspace_bytes;
+  /* Optional (train mode, the conv feeding a BatchNorm2d): when non-null the automatic choice writes the
+   * BatchNorm batch-statistics partials of its bf16 output here -- [S][3][Cout] f32 (count, mean, M2
+   * per channel over split s: a pixel tile's share of one wave), S = hiseg_conv2d_stats_tiles(d) --
+   * for hiseg_bn_finalize_n
+   * (advanced/normalization_comparison.py:181-182); the call fails when that is 0. */
+  float* stats_partial;
 } hiseg_conv2d_desc;
 int hiseg_conv2d_fwd(const hiseg_conv2d_desc* d, hiseg_stream_t stream);
 /* Workspace bytes hiseg_conv2d_fwd's automatic choice would use for this layer (0: none). */
 long long hiseg_conv2d_workspace_bytes(const hiseg_conv2d_desc* d);
+/* Splits S of the BatchNorm statistics partials the automatic choice fuses into this layer's
+ * epilogue when d->stats_partial is set (bf16 3x3 halo-kernel layers with no activation / residual),
+ * 0 when it does not (the caller then runs hiseg_bn_stats over the output). */
+int hiseg_conv2d_stats_tiles(const hiseg_conv2d_desc* d);
 /* Tuning/test entry: variant -1 forces the generic kernel, 0 = automatic choice (as
  * hiseg_conv2d_fwd), k > 0 selects pipelined-kernel configuration k when the layer qualifies
  * (99: the split-K generic kernel; it needs the workspace and fails when the layer does not split). */

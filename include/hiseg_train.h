@@ -92,6 +92,11 @@ int hiseg_bn_stats(int dtype, const void* z, long long P, int C, int cstride, in
 int hiseg_bn_finalize(const float* partial, int C, long long P, const float* gamma, const float* beta, float eps,
                       float momentum, float* running_mean, float* running_var, float* mean, float* invstd,
                       float* scale, float* shift, hiseg_stream_t stream);
+/* The same merge over an explicit split count: the partials a conv epilogue wrote
+ * (hiseg_conv2d_desc.stats_partial, S = hiseg_conv2d_stats_tiles). */
+int hiseg_bn_finalize_n(const float* partial, int S, int C, long long P, const float* gamma, const float* beta,
+                        float eps, float momentum, float* running_mean, float* running_var, float* mean,
+                        float* invstd, float* scale, float* shift, hiseg_stream_t stream);
 typedef struct hiseg_bn_apply_desc {
   int dtype; long long P; int HW; int C;
   const void* z; int z_cstride, z_coff;

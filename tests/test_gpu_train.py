@@ -1061,6 +1061,56 @@ def test_two_source_results_do_not_depend_on_operand_placement(case):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("case", [(256, 256, 3, 20, 30, 0), (128, 128, 2, 37, 21, 0), (128, 256, 2, 16, 16, 0),
+                                  (320, 256, 2, 16, 20, 64)])
+def test_fused_bn_statistics_match_the_statistics_pass(case, monkeypatch):
+    """Round 5: the conv feeding a train-mode BatchNorm writes the batch-statistics partials of
+    its bf16 output from the epilogue (conv_hwc's ST form: per 16 x 16-pixel tile and channel count / mean / M2,
+    merged by hiseg_bn_finalize_n) instead of a statistics pass over z.  Against HISEG_FUSED_BN_STATS=0 (the pass):
+    the conv output z bit-identical, batch mean / invstd within f32 re-association (1e-5 relative), running stats
+    likewise, the BN output within one bf16 ulp, and the fused path actually taken (hiseg_conv2d_stats_tiles > 0).
+    Ragged tiles; the smp decoder's upsampled conv1 form (Cb > 0: x2-upsampled src A ++ skip)."""
+    from hiseg import _lib as L
+    from hiseg import effunet_train as EU
+    from hiseg.ops import Act
+    ca, cout, N, H, W, cb = case
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(5)
+    up = cb > 0
+    x = torch.randn(N, ca, H // 2 if up else H, W // 2 if up else W, device=DEV, generator=g)
+    sk = torch.randn(N, cb, H, W, device=DEV, generator=g) if up else None
+    res = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("HISEG_FUSED_BN_STATS", fused)
+        conv = nn.Conv2d(ca + cb, cout, 3, padding=1, bias=True)
+        filler.fill_module(conv, seed=66)
+        bn = nn.BatchNorm2d(cout)
+        filler.fill_module(bn, seed=67)
+        TE, S, T = engine(_Holder(c=conv, b=bn), dt)
+        xa = Act.from_nchw(x, dt)
+        seen = []
+        real = TE.bn_forward
+
+        def spy(*a, **k):
+            seen.append(bool(k.get("stats")))
+            return real(*a, **k)
+        monkeypatch.setattr(TE, "bn_forward", spy)
+        if up:
+            y = EU.up_conv_bn_relu(T, conv, bn, xa, Act.from_nchw(sk, dt), need_dx=False)
+        else:
+            y = TE.conv_bn_act(T, conv, bn, TE.ACT_RELU, xa)
+        monkeypatch.setattr(TE, "bn_forward", real)
+        torch.cuda.synchronize()
+        assert seen == [fused == "1"], seen
+        res[fused] = (y.t.float().clone(), bn.running_mean.clone(), bn.running_var.clone())
+    (y1, m1, v1), (y0, m0, v0) = res["1"], res["0"]
+    assert torch.isfinite(y1).all()
+    assert torch.allclose(m1, m0, rtol=1e-5, atol=1e-6) and torch.allclose(v1, v0, rtol=1e-5, atol=1e-6)
+    # one bf16 ulp of the output (the normalised value may round either way when mean / invstd differ in the last bit)
+    assert ((y1 - y0).abs() <= y0.abs() * 2 ** -7 + 1e-6).all()
+    assert (y1 == y0).float().mean() > 0.98
+
+
 @pytest.mark.gpu
 def test_train_step_independent_of_allocator_churn_between_forward_and_backward():
     """Every buffer a backward reads through a raw address stays alive until that backward ran: one bf16 train step
