@@ -92,40 +92,55 @@ __global__ void __launch_bounds__(256) dw_bwd_data_kernel(const void* dy, int N,
   }
 }
 
-// grid (kDwSplits, ceil(nch * K / 256)); thread = (channel chunk, filter row ky), K x V accumulators.
+// grid (kDwSplits, ceil(tasks / TPB)), tasks = (channel chunk, filter row ky) pairs, TPB = min(tasks, 256) of them per
+// block and R = 256 / TPB pixel lanes each: thread (task, r) walks pixels b + r, b + r + R, ... of its split with
+// incrementally advanced (n, oy, ox) (32-bit; no per-pixel division), K x V accumulators (one per kx and channel),
+// then the R lanes of a task are summed in LDS in lane order.  (The first form gave each task ONE thread walking
+// its split's P / 128 pixels with three 64-bit divisions per pixel: the B0 student's 16- and 24-channel layers at
+// 320 x 320 ran 6-12 tasks per block, 128 blocks -- 6.6 ms of the unfrozen distillation step.)
 template <typename T>
 __global__ void __launch_bounds__(256) dw_bwd_weight_kernel(const void* x, const void* dy, int N, int H, int W, int C,
-                                                            int K, int s, int Ho, int Wo, float* ws) {
+                                                            int K, int s, int Ho, int Wo, int TPB, float* ws) {
   constexpr int V = Chunk<T>::N;
+  __shared__ float red[256 * V];
   const int nch = C / V, pad = K / 2, KK = K * K;
-  const int task = blockIdx.y * 256 + threadIdx.x;
-  if (task >= nch * K) return;
-  const int ch = task / K, ky = task - ch * K;
+  const int R = 256 / TPB;
+  const int tl = threadIdx.x % TPB, r = threadIdx.x / TPB;
+  const int task = blockIdx.y * TPB + tl;
+  const bool live = task < nch * K && r < R;
+  const int ch = live ? task / K : 0, ky = live ? task - ch * K : 0;
   const int c = ch * V;
-  const long long P = (long long)N * Ho * Wo;
-  const long long b = P * blockIdx.x / gridDim.x, e = P * (blockIdx.x + 1) / gridDim.x;
+  const int P = N * Ho * Wo;
+  const int b = (int)((long long)P * blockIdx.x / gridDim.x), e = (int)((long long)P * (blockIdx.x + 1) / gridDim.x);
   float acc[5][V];
 #pragma unroll
   for (int kx = 0; kx < 5; ++kx)
 #pragma unroll
     for (int k = 0; k < V; ++k) acc[kx][k] = 0.f;
-  for (long long q = b; q < e; ++q) {
-    const int ox = (int)(q % Wo);
-    const long long r = q / Wo;
-    const int oy = (int)(r % Ho);
-    const int n = (int)(r / Ho);
-    const int iy = oy * s - pad + ky;
-    if ((unsigned)iy >= (unsigned)H) continue;
-    float g[V], v[V];
-    ldc<T>(dy, q * C + c, g);
+  int q = b + r;
+  if (live && q < e) {
+    int ox = q % Wo, t2 = q / Wo, oy = t2 % Ho, n = t2 / Ho;
+    const int dx = R % Wo, dyr = R / Wo;
+    for (; q < e; q += R) {
+      const int iy = oy * s - pad + ky;
+      if ((unsigned)iy < (unsigned)H) {
+        float g[V], v[V];
+        ldc<T>(dy, (long long)q * C + c, g);
+        const long long rowb = ((long long)n * H + iy) * W;
 #pragma unroll
-    for (int kx = 0; kx < 5; ++kx) {
-      if (kx >= K) break;
-      const int ix = ox * s - pad + kx;
-      if ((unsigned)ix >= (unsigned)W) continue;
-      ldc<T>(x, (((long long)n * H + iy) * W + ix) * C + c, v);
+        for (int kx = 0; kx < 5; ++kx) {
+          if (kx >= K) break;
+          const int ix = ox * s - pad + kx;
+          if ((unsigned)ix >= (unsigned)W) continue;
+          ldc<T>(x, (rowb + ix) * C + c, v);
 #pragma unroll
-      for (int k = 0; k < V; ++k) acc[kx][k] += g[k] * v[k];
+          for (int k = 0; k < V; ++k) acc[kx][k] += g[k] * v[k];
+        }
+      }
+      ox += dx;
+      oy += dyr;
+      if (ox >= Wo) { ox -= Wo; ++oy; }
+      while (oy >= Ho) { oy -= Ho; ++n; }
     }
   }
   float* out = ws + (long long)blockIdx.x * C * KK;
@@ -133,7 +148,19 @@ __global__ void __launch_bounds__(256) dw_bwd_weight_kernel(const void* x, const
   for (int kx = 0; kx < 5; ++kx) {
     if (kx >= K) break;
 #pragma unroll
-    for (int k = 0; k < V; ++k) out[(c + k) * KK + ky * K + kx] = acc[kx][k];
+    for (int k = 0; k < V; ++k) red[threadIdx.x * V + k] = acc[kx][k];
+    __syncthreads();
+    if (r == 0 && live) {
+      float sum[V];
+#pragma unroll
+      for (int k = 0; k < V; ++k) sum[k] = red[tl * V + k];
+      for (int rr = 1; rr < R; ++rr)
+#pragma unroll
+        for (int k = 0; k < V; ++k) sum[k] += red[(rr * TPB + tl) * V + k];
+#pragma unroll
+      for (int k = 0; k < V; ++k) out[(c + k) * KK + ky * K + kx] = sum[k];
+    }
+    __syncthreads();
   }
 }
 
@@ -200,9 +227,12 @@ extern "C" int hiseg_dw_bwd_weight(int dtype, const void* x, const void* dy, int
   const int r = dw_check(dtype, N, H, W, C, K, stride, Ho, Wo);
   if (r) return r;
   const int nch = C / (dtype == HISEG_BF16 ? 8 : 4);
+  HISEG_REQUIRE((long long)N * H * W * C < (1ll << 31) && (long long)N * Ho * Wo < (1ll << 31), HISEG_ERR_BAD_SHAPE,
+                "dw_bwd_weight: tensor too large");
   hipStream_t s = (hipStream_t)stream;
-  DW_DISPATCH(dtype, dw_bwd_weight_kernel, dim3(kDwSplits, (nch * K + 255) / 256), dim3(256), 0, s, x, dy, N, H, W, C,
-              K, stride, Ho, Wo, ws);
+  const int tasks = nch * K, TPB = tasks < 256 ? tasks : 256;
+  DW_DISPATCH(dtype, dw_bwd_weight_kernel, dim3(kDwSplits, (tasks + TPB - 1) / TPB), dim3(256), 0, s, x, dy, N, H, W,
+              C, K, stride, Ho, Wo, TPB, ws);
   const int n = C * K * K;
   hipLaunchKernelGGL(dw_weight_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, s, ws, kDwSplits, n, dw);
   return hiseg_check_launch("dw_bwd_weight");

@@ -246,98 +246,130 @@ __global__ void __launch_bounds__(256) sa_bwd3_kernel(const void* dout, long lon
 }
 
 // ======================================================================================= channel attention
-constexpr int kGapSplits = 16;
+// Global-average-pool partials part[n][s][c] over S pixel splits per image, S = ca_splits(N, HW) <= kGapSplits (the
+// workspace size).  (Round 5: S was a fixed 16 -- N x 16 blocks, 64 for the distillation student's 4 images -- and
+// channel counts whose chunk count does not divide 256 (96, 144, 240, 480, 672, 1152: most SqueezeExcite layers) took
+// a one-thread-per-channel kernel with 2-byte loads: the SE forward and backward pools were most of the unfrozen
+// distillation step's SE time.)
+constexpr int kGapSplits = 64;
 
-// part[n][s][c] = sum_{p in split s of image n} x[p][c] (* dout[p][c] * mul[n][c] if dout)
-template <typename T>
-__global__ void __launch_bounds__(256) ca_gap_kernel(const void* x, const void* dout, const float* mul, int HW, int C,
-                                                     float* part) {
-  const int n = blockIdx.x, s = blockIdx.y;
-  const int p0 = (int)((long long)HW * s / kGapSplits), p1 = (int)((long long)HW * (s + 1) / kGapSplits);
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float acc = 0.f;
-    const float m = (dout && mul) ? mul[(long long)n * C + c] : 1.f;
-    for (int p = p0; p < p1; ++p) {
-      const long long i = ((long long)n * HW + p) * C + c;
-      float v = ldT<T>(x, i);
-      if (dout) v *= ldT<T>(dout, i) * m;
-      acc += v;
-    }
-    part[((long long)n * kGapSplits + s) * C + c] = acc;
-  }
+static int ca_splits(int N, int HW) {
+  int s = 1024 / (N > 0 ? N : 1);
+  const int cap = HW / 16 > 0 ? HW / 16 : 1;   // >= 16 pixels per split
+  if (s > cap) s = cap;
+  if (s > kGapSplits) s = kGapSplits;
+  return s < 1 ? 1 : s;
 }
 
-// Same partials, 16-B loads: 256 threads = (256 / nch) pixel lanes x nch channel chunks (nch = C / chunk
-// divides 256), lanes reduced in LDS.
+// part[n][s][c] = sum_{p in split s of image n} x[p][c] (* dout[p][c] * mul[n][c] if dout).  16-B loads: 256 threads =
+// R = 256 / CT pixel lanes x CT channel chunks (CT = min(nch, 256); blockIdx.z: the chunk group), lanes reduced in LDS
+// in lane order.
 template <typename T>
 __global__ void __launch_bounds__(256) ca_gap_vec_kernel(const void* x, const void* dout, const float* mul, int HW,
-                                                         int C, float* part) {
+                                                         int C, int S, float* part) {
   constexpr int K = Chunk<T>::N;
-  extern __shared__ float red[];   // [R][C]
+  __shared__ float red[256 * K];   // [R][CT * K]
   const int n = blockIdx.x, sp = blockIdx.y;
-  const int nch = C / K, R = 256 / nch;
-  const int ch = threadIdx.x % nch, lane = threadIdx.x / nch;
-  const int p0 = (int)((long long)HW * sp / kGapSplits), p1 = (int)((long long)HW * (sp + 1) / kGapSplits);
+  const int nch = C / K;
+  const int CT = nch < 256 ? nch : 256, R = 256 / CT;
+  const int cl = threadIdx.x % CT, lane = threadIdx.x / CT;
+  const int ch = blockIdx.z * 256 + cl;
+  const bool live = lane < R && ch < nch;
+  const int p0 = (int)((long long)HW * sp / S), p1 = (int)((long long)HW * (sp + 1) / S);
   float acc[K], v[K], g[K];
 #pragma unroll
   for (int e = 0; e < K; ++e) acc[e] = 0.f;
-  const uint4* xs = reinterpret_cast<const uint4*>(x) + (long long)n * HW * nch + ch;
-  const uint4* ds = dout ? reinterpret_cast<const uint4*>(dout) + (long long)n * HW * nch + ch : nullptr;
-  for (int p = p0 + lane; p < p1; p += R) {
-    Chunk<T>::unpack(xs[(long long)p * nch], v);
-    if (ds) {
-      Chunk<T>::unpack(ds[(long long)p * nch], g);
+  if (live) {
+    const uint4* xs = reinterpret_cast<const uint4*>(x) + (long long)n * HW * nch + ch;
+    const uint4* ds = dout ? reinterpret_cast<const uint4*>(dout) + (long long)n * HW * nch + ch : nullptr;
+    for (int p = p0 + lane; p < p1; p += R) {
+      Chunk<T>::unpack(xs[(long long)p * nch], v);
+      if (ds) {
+        Chunk<T>::unpack(ds[(long long)p * nch], g);
 #pragma unroll
-      for (int e = 0; e < K; ++e) v[e] *= g[e];
+        for (int e = 0; e < K; ++e) v[e] *= g[e];
+      }
+#pragma unroll
+      for (int e = 0; e < K; ++e) acc[e] += v[e];
     }
+    if (ds && mul) {
 #pragma unroll
-    for (int e = 0; e < K; ++e) acc[e] += v[e];
+      for (int e = 0; e < K; ++e) acc[e] *= mul[(long long)n * C + ch * K + e];
+    }
   }
-  if (ds && mul) {
+  if (lane < R) {
 #pragma unroll
-    for (int e = 0; e < K; ++e) acc[e] *= mul[(long long)n * C + ch * K + e];
+    for (int e = 0; e < K; ++e) red[lane * CT * K + cl * K + e] = acc[e];
   }
-#pragma unroll
-  for (int e = 0; e < K; ++e) red[lane * C + ch * K + e] = acc[e];
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
+  const int cols = CT * K;
+  for (int c = threadIdx.x; c < cols; c += 256) {
+    const int cc = blockIdx.z * 256 * K + c;
+    if (cc >= C) continue;
     float s = 0.f;
-    for (int l = 0; l < R; ++l) s += red[l * C + c];
-    part[((long long)n * kGapSplits + sp) * C + c] = s;
+    for (int l = 0; l < R; ++l) s += red[l * cols + c];
+    part[((long long)n * S + sp) * C + cc] = s;
   }
 }
 
 template <typename T>
-static void ca_gap(const void* x, const void* dout, const float* mul, int N, int HW, int C, float* part, hipStream_t s) {
+static int ca_gap(const void* x, const void* dout, const float* mul, int N, int HW, int C, float* part, hipStream_t s) {
   const int nch = C / Chunk<T>::N;
-  if (nch <= 256 && 256 % nch == 0)
-    hipLaunchKernelGGL(ca_gap_vec_kernel<T>, dim3(N, kGapSplits), dim3(256), (size_t)256 * Chunk<T>::N * sizeof(float),
-                       s, x, dout, mul, HW, C, part);
-  else
-    hipLaunchKernelGGL(ca_gap_kernel<T>, dim3(N, kGapSplits), dim3(256), 0, s, x, dout, mul, HW, C, part);
+  const int S = ca_splits(N, HW);
+  hipLaunchKernelGGL(ca_gap_vec_kernel<T>, dim3(N, S, (nch + 255) / 256), dim3(256), 0, s, x, dout, mul, HW, C, S, part);
+  return S;
+}
+
+// out[r] (r < Cr) = sum_c W[r * ldr + c * ldc] * v[c] with all 256 threads: G = 256 / Cr groups take every G-th c,
+// their partials summed in group order through LDS (scr: >= 256 floats).  Called by every thread of the block.
+__device__ __forceinline__ void block_matvec(const float* W, long long ldr, long long ldc, const float* v, int C, int Cr,
+                                             float* scr, float* out) {
+  if (Cr > 256) {
+    for (int r = threadIdx.x; r < Cr; r += 256) {
+      float s = 0.f;
+      for (int c = 0; c < C; ++c) s += W[r * ldr + c * ldc] * v[c];
+      out[r] = s;
+    }
+    __syncthreads();
+    return;
+  }
+  const int G = 256 / Cr;
+  const int r = threadIdx.x % Cr, gi = threadIdx.x / Cr;
+  float s = 0.f;
+  if (gi < G)
+    for (int c = gi; c < C; c += G) s += W[r * ldr + c * ldc] * v[c];
+  scr[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x < Cr) {
+    float t = 0.f;
+    for (int k = 0; k < G; ++k) t += scr[k * Cr + threadIdx.x];
+    out[threadIdx.x] = t;
+  }
+  __syncthreads();
 }
 
 __device__ __forceinline__ float act_f(float v, int act, float beta) { return apply_act(v, act, beta); }
 __device__ __forceinline__ float act_d(float pre, int act, float beta) { return act_grad_pre(pre, act, beta); }
 
 // per image: gap, hidden pre-activation, gate
-__global__ void __launch_bounds__(256) ca_mlp_kernel(const float* part, int HW, int C, int Cr, const float* w1,
+__global__ void __launch_bounds__(256) ca_mlp_kernel(const float* part, int S, int HW, int C, int Cr, const float* w1,
                                                      const float* w2, int act, float beta, float* gap, float* hpre,
                                                      float* gate, const float* b1 = nullptr, const float* b2 = nullptr) {
   extern __shared__ float sm[];
   float* g = sm;
   float* h = sm + C;
+  float* scr = h + Cr;   // [256]
   const int n = blockIdx.x;
   for (int c = threadIdx.x; c < C; c += 256) {
     float s = 0.f;
-    for (int k = 0; k < kGapSplits; ++k) s += part[((long long)n * kGapSplits + k) * C + c];
+    for (int k = 0; k < S; ++k) s += part[((long long)n * S + k) * C + c];
     g[c] = s / (float)HW;
     gap[(long long)n * C + c] = g[c];
   }
   __syncthreads();
+  block_matvec(w1, C, 1, g, C, Cr, scr, h);   // W1 g (h holds the pre-activation until below)
   for (int r = threadIdx.x; r < Cr; r += 256) {
-    float s = b1 ? b1[r] : 0.f;
-    for (int c = 0; c < C; ++c) s += w1[(long long)r * C + c] * g[c];
+    const float s = h[r] + (b1 ? b1[r] : 0.f);
     hpre[(long long)n * Cr + r] = s;
     h[r] = act_f(s, act, beta);
   }
@@ -396,7 +428,7 @@ __global__ void __launch_bounds__(256) ca_apply_kernel(const void* x, int N, int
 }
 
 // per image: ds = dgate * g (1-g); dh; dgap; per-image weight-gradient rows
-__global__ void __launch_bounds__(256) ca_mlp_bwd_kernel(const float* part, int C, int Cr, const float* w1,
+__global__ void __launch_bounds__(256) ca_mlp_bwd_kernel(const float* part, int S, int C, int Cr, const float* w1,
                                                          const float* w2, int act, float beta, const float* gap,
                                                          const float* hpre,
                                                          const float* gate, float* dgap, float* wpart,
@@ -404,19 +436,19 @@ __global__ void __launch_bounds__(256) ca_mlp_bwd_kernel(const float* part, int 
   extern __shared__ float sm[];
   float* ds = sm;
   float* dh = sm + C;
+  float* scr = dh + Cr;   // [256]
   const int n = blockIdx.x;
   for (int c = threadIdx.x; c < C; c += 256) {
     float s = 0.f;
-    for (int k = 0; k < kGapSplits; ++k) s += part[((long long)n * kGapSplits + k) * C + c];
+    for (int k = 0; k < S; ++k) s += part[((long long)n * S + k) * C + c];
     const float g = gate[(long long)n * C + c];
     ds[c] = s * g * (1.f - g);
     if (bpart) bpart[(long long)n * (Cr + C) + Cr + c] = ds[c];
   }
   __syncthreads();
+  block_matvec(w2, 1, Cr, ds, C, Cr, scr, dh);   // W2^T ds
   for (int r = threadIdx.x; r < Cr; r += 256) {
-    float s = 0.f;
-    for (int c = 0; c < C; ++c) s += w2[(long long)c * Cr + r] * ds[c];
-    dh[r] = s * act_d(hpre[(long long)n * Cr + r], act, beta);
+    dh[r] = dh[r] * act_d(hpre[(long long)n * Cr + r], act, beta);
     if (bpart) bpart[(long long)n * (Cr + C) + r] = dh[r];
   }
   __syncthreads();
@@ -941,8 +973,9 @@ extern "C" int hiseg_attn_channel_train_fwd(int dtype, const void* x, int N, int
                 "attn_channel_train_fwd: bad args");
   HISEG_REQUIRE(C > 0 && C % chunk_of(dtype) == 0, HISEG_ERR_BAD_SHAPE, "attn_channel_train_fwd: C alignment");
   hipStream_t s = (hipStream_t)stream;
-  DISPATCH_T(dtype, ca_gap<T>(x, nullptr, nullptr, N, HW, C, ws, s));
-  hipLaunchKernelGGL(ca_mlp_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, ws, HW, C, Cr, w1, w2, act,
+  int S = 0;
+  DISPATCH_T(dtype, S = ca_gap<T>(x, nullptr, nullptr, N, HW, C, ws, s));
+  hipLaunchKernelGGL(ca_mlp_kernel, dim3(N), dim3(256), (size_t)(C + Cr + 256) * sizeof(float), s, ws, S, HW, C, Cr, w1, w2, act,
                      act_beta, gap, hpre, gate);
   DISPATCH_T(dtype, hipLaunchKernelGGL(ca_apply_kernel<T>, dim3(ca_ranges(N, HW), N),
                                        dim3(256), 0, s, x, N, HW, C, gate, chan_mul, out));
@@ -960,8 +993,9 @@ extern "C" int hiseg_attn_channel_bwd(int dtype, const void* x, int N, int HW, i
   float* part = ws;
   float* dgap = ws + (long long)N * kGapSplits * C;
   float* wpart = dgap + (long long)N * C;
-  DISPATCH_T(dtype, ca_gap<T>(x, dout, chan_mul, N, HW, C, part, s));
-  hipLaunchKernelGGL(ca_mlp_bwd_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, part, C, Cr, w1, w2, act,
+  int S = 0;
+  DISPATCH_T(dtype, S = ca_gap<T>(x, dout, chan_mul, N, HW, C, part, s));
+  hipLaunchKernelGGL(ca_mlp_bwd_kernel, dim3(N), dim3(256), (size_t)(C + Cr + 256) * sizeof(float), s, part, S, C, Cr, w1, w2, act,
                      act_beta, gap, hpre, gate, dgap, wpart);
   sum_rows(wpart, N, 2 * C * Cr, C * Cr, dw1, 1, s);
   sum_rows(wpart + C * Cr, N, 2 * C * Cr, C * Cr, dw2, 1, s);
@@ -984,8 +1018,9 @@ extern "C" int hiseg_se_train_fwd(int dtype, const void* x, int N, int HW, int C
                 HISEG_ERR_BAD_ARG, "se_train_fwd: bad args");
   HISEG_REQUIRE(C > 0 && C % chunk_of(dtype) == 0, HISEG_ERR_BAD_SHAPE, "se_train_fwd: C alignment");
   hipStream_t s = (hipStream_t)stream;
-  DISPATCH_T(dtype, ca_gap<T>(x, nullptr, nullptr, N, HW, C, ws, s));
-  hipLaunchKernelGGL(ca_mlp_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, ws, HW, C, Cr, w1, w2, act,
+  int S = 0;
+  DISPATCH_T(dtype, S = ca_gap<T>(x, nullptr, nullptr, N, HW, C, ws, s));
+  hipLaunchKernelGGL(ca_mlp_kernel, dim3(N), dim3(256), (size_t)(C + Cr + 256) * sizeof(float), s, ws, S, HW, C, Cr, w1, w2, act,
                      1.f, gap, hpre, gate, b1, b2);
   DISPATCH_T(dtype, hipLaunchKernelGGL(ca_apply_kernel<T>, dim3(ca_ranges(N, HW), N),
                                        dim3(256), 0, s, x, N, HW, C, gate, nullptr, out));
@@ -1004,8 +1039,9 @@ extern "C" int hiseg_se_train_bwd(int dtype, const void* x, int N, int HW, int C
   float* dgap = ws + (long long)N * kGapSplits * C;
   float* wpart = dgap + (long long)N * C;
   float* bpart = wpart + (long long)N * 2 * C * Cr;
-  DISPATCH_T(dtype, ca_gap<T>(x, dout, nullptr, N, HW, C, part, s));
-  hipLaunchKernelGGL(ca_mlp_bwd_kernel, dim3(N), dim3(256), (size_t)(C + Cr) * sizeof(float), s, part, C, Cr, w1, w2, act,
+  int S = 0;
+  DISPATCH_T(dtype, S = ca_gap<T>(x, dout, nullptr, N, HW, C, part, s));
+  hipLaunchKernelGGL(ca_mlp_bwd_kernel, dim3(N), dim3(256), (size_t)(C + Cr + 256) * sizeof(float), s, part, S, C, Cr, w1, w2, act,
                      1.f, gap, hpre, gate, dgap, wpart, bpart);
   sum_rows(wpart, N, 2 * C * Cr, C * Cr, dw1, 1, s);
   sum_rows(wpart + C * Cr, N, 2 * C * Cr, C * Cr, dw2, 1, s);

@@ -132,8 +132,9 @@ def test_skeleton_rebuilds_the_module_from_its_spec():
 def test_skeleton_plans_do_not_carry_over_between_state_sets():
     """one skeleton serves every exported program of an architecture; its engine plan cache must not
     survive a change of state set (a plan is keyed by the state tensors' addresses + versions, which a released
-    program's tensors could hand to the next one).  Same state set: plans kept; another set: dropped, and the
-    skeleton holds the set it runs with."""
+    program's tensors could hand to the next one).  Same state set: plans kept; another set: dropped.  ADVICE r4: the
+    skeleton keeps only weak references to the set (a released program's weights are not pinned); a set whose
+    tensors died is treated as another set even at the same addresses."""
     import json
     m = _model(use_contour_detection=False)
     sp = json.loads(X._head_spec(m, "full"))
@@ -143,8 +144,17 @@ def test_skeleton_plans_do_not_carry_over_between_state_sets():
     X._run_on(sp, state_a, X.UNET_PREFIX, lambda k: k.__dict__.__setitem__("_hiseg_plans", {"marker": 1}))
     assert X._run_on(sp, state_a, X.UNET_PREFIX, lambda k: k.__dict__.get("_hiseg_plans")) == {"marker": 1}
     assert X._run_on(sp, state_b, X.UNET_PREFIX, lambda k: k.__dict__.get("_hiseg_plans")) is None
-    held = sk.__dict__["_hiseg_state_held"]
-    assert len(held) == len(state_b) and all(a is b for a, b in zip(held, state_b))
+    refs = sk.__dict__["_hiseg_state_refs"]
+    assert len(refs) == len(state_b) and all(r() is b for r, b in zip(refs, state_b))
+    assert "_hiseg_state_held" not in sk.__dict__
+    X._run_on(sp, state_b, X.UNET_PREFIX, lambda k: k.__dict__.__setitem__("_hiseg_plans", {"marker": 2}))
+    ptrs = [t.data_ptr() for t in state_b]
+    state_c = [t.detach().clone() for t in state_b]
+    del state_b, refs
+    assert all(r() is None for r in sk.__dict__["_hiseg_state_refs"])   # not pinned by the skeleton
+    # a new set (even one that reused the addresses) does not see the released set's plans
+    assert X._run_on(sp, state_c, X.UNET_PREFIX, lambda k: k.__dict__.get("_hiseg_plans")) is None
+    assert ptrs
 
 
 # ------------------------------------------------------------------------------------ ONNX lowerings
