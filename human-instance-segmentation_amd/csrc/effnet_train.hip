@@ -9,8 +9,6 @@
 
 namespace hiseg {
 
-constexpr int kDwSplits = 128;
-
 template <typename T>
 __device__ __forceinline__ void ldc(const void* p, long long i, float* v) {
   Chunk<T>::unpack(*reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(p) + i), v);
@@ -92,7 +90,7 @@ __global__ void __launch_bounds__(256) dw_bwd_data_kernel(const void* dy, int N,
   }
 }
 
-// grid (kDwSplits, ceil(tasks / TPB)), tasks = (channel chunk, filter row ky) pairs, TPB = min(tasks, 256) of them per
+// grid (S = dw_wsplits, ceil(tasks / TPB)), tasks = (channel chunk, filter row ky) pairs, TPB = min(tasks, 256) of them per
 // block and R = 256 / TPB pixel lanes each: thread (task, r) walks pixels b + r, b + r + R, ... of its split with
 // incrementally advanced (n, oy, ox) (32-bit; no per-pixel division), K x V accumulators (one per kx and channel),
 // then the R lanes of a task are summed in LDS in lane order.  (The first form gave each task ONE thread walking
@@ -164,12 +162,35 @@ __global__ void __launch_bounds__(256) dw_bwd_weight_kernel(const void* x, const
   }
 }
 
+// dw[i] += sum_s ws[s][i]: a block = 64 outputs x 4 split groups (group g sums splits g, g + 4, ... in order, four
+// loads in flight), the groups combined in LDS in order.  (One thread per output walking every split in double was
+// 33 us per call on the 288-output layers.)
 __global__ void __launch_bounds__(256) dw_weight_reduce_kernel(const float* ws, int S, int n, float* dw) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  double acc = 0;
-  for (int s = 0; s < S; ++s) acc += ws[(long long)s * n + i];
-  dw[i] += (float)acc;
+  __shared__ float red[4][64];
+  const int ol = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + ol;
+  float acc = 0.f;
+  if (i < n) {
+    int sp = g;
+    for (; sp + 12 < S; sp += 16) {
+      const float a0 = ws[(long long)sp * n + i], a1 = ws[(long long)(sp + 4) * n + i];
+      const float a2 = ws[(long long)(sp + 8) * n + i], a3 = ws[(long long)(sp + 12) * n + i];
+      acc += a0; acc += a1; acc += a2; acc += a3;
+    }
+    for (; sp < S; sp += 4) acc += ws[(long long)sp * n + i];
+  }
+  red[g][ol] = acc;
+  __syncthreads();
+  if (g == 0 && i < n) dw[i] += ((red[0][ol] + red[1][ol]) + red[2][ol]) + red[3][ol];
+}
+
+// pixel splits of the weight gradient: about 32 pixels per thread (R pixel lanes per task), at most kDwMaxSplits
+static int dw_wsplits(long long P, int C, int K, int V) {
+  const int tasks = (C / V) * K, TPB = tasks < 256 ? tasks : 256, R = 256 / TPB;
+  long long sp = P / (32ll * R);
+  if (sp < 1) sp = 1;
+  if (sp > 1024) sp = 1024;
+  return (int)sp;
 }
 
 inline unsigned dw_blocks(long long n) {
@@ -219,7 +240,9 @@ extern "C" int hiseg_dw_bwd_data(int dtype, const void* dy, int N, int H, int W,
   return hiseg_check_launch("dw_bwd_data");
 }
 
-extern "C" long long hiseg_dw_bwd_weight_ws(int C, int K) { return (long long)kDwSplits * C * K * K; }
+extern "C" long long hiseg_dw_bwd_weight_ws(int dtype, int N, int Ho, int Wo, int C, int K) {
+  return (long long)dw_wsplits((long long)N * Ho * Wo, C, K, dtype == HISEG_BF16 ? 8 : 4) * C * K * K;
+}
 
 extern "C" int hiseg_dw_bwd_weight(int dtype, const void* x, const void* dy, int N, int H, int W, int C, int K,
                                    int stride, int Ho, int Wo, float* ws, float* dw, hiseg_stream_t stream) {
@@ -231,9 +254,10 @@ extern "C" int hiseg_dw_bwd_weight(int dtype, const void* x, const void* dy, int
                 "dw_bwd_weight: tensor too large");
   hipStream_t s = (hipStream_t)stream;
   const int tasks = nch * K, TPB = tasks < 256 ? tasks : 256;
-  DW_DISPATCH(dtype, dw_bwd_weight_kernel, dim3(kDwSplits, (tasks + TPB - 1) / TPB), dim3(256), 0, s, x, dy, N, H, W,
+  const int S = dw_wsplits((long long)N * Ho * Wo, C, K, dtype == HISEG_BF16 ? 8 : 4);
+  DW_DISPATCH(dtype, dw_bwd_weight_kernel, dim3(S, (tasks + TPB - 1) / TPB), dim3(256), 0, s, x, dy, N, H, W,
               C, K, stride, Ho, Wo, TPB, ws);
   const int n = C * K * K;
-  hipLaunchKernelGGL(dw_weight_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, s, ws, kDwSplits, n, dw);
+  hipLaunchKernelGGL(dw_weight_reduce_kernel, dim3((n + 63) / 64), dim3(256), 0, s, ws, S, n, dw);
   return hiseg_check_launch("dw_bwd_weight");
 }

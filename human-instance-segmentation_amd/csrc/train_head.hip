@@ -320,66 +320,8 @@ static int ca_gap(const void* x, const void* dout, const float* mul, int N, int 
   return S;
 }
 
-// out[r] (r < Cr) = sum_c W[r * ldr + c * ldc] * v[c] with all 256 threads: G = 256 / Cr groups take every G-th c,
-// their partials summed in group order through LDS (scr: >= 256 floats).  Called by every thread of the block.
-__device__ __forceinline__ void block_matvec(const float* W, long long ldr, long long ldc, const float* v, int C, int Cr,
-                                             float* scr, float* out) {
-  if (Cr > 256) {
-    for (int r = threadIdx.x; r < Cr; r += 256) {
-      float s = 0.f;
-      for (int c = 0; c < C; ++c) s += W[r * ldr + c * ldc] * v[c];
-      out[r] = s;
-    }
-    __syncthreads();
-    return;
-  }
-  const int G = 256 / Cr;
-  const int r = threadIdx.x % Cr, gi = threadIdx.x / Cr;
-  float s = 0.f;
-  if (gi < G)
-    for (int c = gi; c < C; c += G) s += W[r * ldr + c * ldc] * v[c];
-  scr[threadIdx.x] = s;
-  __syncthreads();
-  if (threadIdx.x < Cr) {
-    float t = 0.f;
-    for (int k = 0; k < G; ++k) t += scr[k * Cr + threadIdx.x];
-    out[threadIdx.x] = t;
-  }
-  __syncthreads();
-}
-
 __device__ __forceinline__ float act_f(float v, int act, float beta) { return apply_act(v, act, beta); }
 __device__ __forceinline__ float act_d(float pre, int act, float beta) { return act_grad_pre(pre, act, beta); }
-
-// per image: gap, hidden pre-activation, gate
-__global__ void __launch_bounds__(256) ca_mlp_kernel(const float* part, int S, int HW, int C, int Cr, const float* w1,
-                                                     const float* w2, int act, float beta, float* gap, float* hpre,
-                                                     float* gate, const float* b1 = nullptr, const float* b2 = nullptr) {
-  extern __shared__ float sm[];
-  float* g = sm;
-  float* h = sm + C;
-  float* scr = h + Cr;   // [256]
-  const int n = blockIdx.x;
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float s = 0.f;
-    for (int k = 0; k < S; ++k) s += part[((long long)n * S + k) * C + c];
-    g[c] = s / (float)HW;
-    gap[(long long)n * C + c] = g[c];
-  }
-  __syncthreads();
-  block_matvec(w1, C, 1, g, C, Cr, scr, h);   // W1 g (h holds the pre-activation until below)
-  for (int r = threadIdx.x; r < Cr; r += 256) {
-    const float s = h[r] + (b1 ? b1[r] : 0.f);
-    hpre[(long long)n * Cr + r] = s;
-    h[r] = act_f(s, act, beta);
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float s = b2 ? b2[c] : 0.f;
-    for (int r = 0; r < Cr; ++r) s += w2[(long long)c * Cr + r] * h[r];
-    gate[(long long)n * C + c] = sigmoidf_(s);
-  }
-}
 
 // out = x * gate[n][c] * mul[n][c]   (NHWC, C channels contiguous).  Block = (256 / nch) pixel lanes x nch
 // channel chunks over a pixel range of image blockIdx.y (blockIdx.x = range): the chunk's gate factors stay
@@ -428,42 +370,133 @@ __global__ void __launch_bounds__(256) ca_apply_kernel(const void* x, int N, int
 }
 
 // per image: ds = dgate * g (1-g); dh; dgap; per-image weight-gradient rows
-__global__ void __launch_bounds__(256) ca_mlp_bwd_kernel(const float* part, int S, int C, int Cr, const float* w1,
-                                                         const float* w2, int act, float beta, const float* gap,
-                                                         const float* hpre,
-                                                         const float* gate, float* dgap, float* wpart,
-                                                         float* bpart = nullptr) {
-  extern __shared__ float sm[];
-  float* ds = sm;
-  float* dh = sm + C;
-  float* scr = dh + Cr;   // [256]
-  const int n = blockIdx.x;
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float s = 0.f;
-    for (int k = 0; k < S; ++k) s += part[((long long)n * S + k) * C + c];
+// The channel-attention / SqueezeExcite MLP over the pooled vector, as three wide launches (round 5: one block per
+// image did it all -- 4 blocks for the distillation student's SE layers, 45 us forward / 66 us backward per call):
+//   colsum:  out[n][c] = (sum_k part[n][k][c]) * HW^-1 (forward: the pool)  or  * g (1 - g) (backward: ds)
+//   rowdot:  one 32-lane group per (n, r): s = sum_c W[r ldr + c ldc] v[n][c] (lane-strided, butterfly-reduced)
+//            forward: hpre = s + b1, h = act(hpre);  backward: dh = s * act'(hpre)
+//   coldot:  one thread per (n, c): s = sum_r W[c ldc + r ldr] v[n][r]
+//            forward: gate = sigmoid(s + b2);  backward: dgap = s
+__global__ void __launch_bounds__(256) ca_colsum_kernel(const float* part, int S, int C, float inv_hw, const float* gate,
+                                                        float* out, int out_ld, int out_off, float* out2) {
+  const int n = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const float* p = part + (long long)n * S * C + c;
+  float s = 0.f;
+  int k = 0;
+  for (; k + 3 < S; k += 4) {
+    const float a0 = p[(long long)k * C], a1 = p[(long long)(k + 1) * C], a2 = p[(long long)(k + 2) * C],
+                a3 = p[(long long)(k + 3) * C];
+    s += a0; s += a1; s += a2; s += a3;
+  }
+  for (; k < S; ++k) s += p[(long long)k * C];
+  float v;
+  if (gate) {
     const float g = gate[(long long)n * C + c];
-    ds[c] = s * g * (1.f - g);
-    if (bpart) bpart[(long long)n * (Cr + C) + Cr + c] = ds[c];
+    v = s * g * (1.f - g);
+  } else {
+    v = s * inv_hw;
   }
-  __syncthreads();
-  block_matvec(w2, 1, Cr, ds, C, Cr, scr, dh);   // W2^T ds
-  for (int r = threadIdx.x; r < Cr; r += 256) {
-    dh[r] = dh[r] * act_d(hpre[(long long)n * Cr + r], act, beta);
-    if (bpart) bpart[(long long)n * (Cr + C) + r] = dh[r];
+  out[(long long)n * out_ld + out_off + c] = v;
+  if (out2) out2[(long long)n * C + c] = v;
+}
+
+__global__ void __launch_bounds__(256) ca_rowdot_kernel(const float* W, long long ldr, long long ldc, const float* v,
+                                                        int v_ld, int v_off, int C, int Cr, const float* b1, int act,
+                                                        float beta, float* hpre, float* out, int out_ld, int fwd) {
+  const int n = blockIdx.y, r = blockIdx.x * 8 + (threadIdx.x >> 5), l = threadIdx.x & 31;
+  float s = 0.f;
+  if (r < Cr) {
+    const float* vv = v + (long long)n * v_ld + v_off;
+    for (int c = l; c < C; c += 32) s += W[r * ldr + c * ldc] * vv[c];
   }
-  __syncthreads();
-  float* wp = wpart + (long long)n * 2 * C * Cr;  // [dW1 (Cr x C)][dW2 (C x Cr)]
-  for (int c = threadIdx.x; c < C; c += 256) {
+#pragma unroll
+  for (int m = 16; m > 0; m >>= 1) s += __shfl_xor(s, m, 64);
+  if (l == 0 && r < Cr) {
+    if (fwd) {
+      const float pre = s + (b1 ? b1[r] : 0.f);
+      hpre[(long long)n * Cr + r] = pre;
+      out[(long long)n * out_ld + r] = act_f(pre, act, beta);
+    } else {
+      out[(long long)n * out_ld + r] = s * act_d(hpre[(long long)n * Cr + r], act, beta);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) ca_coldot_kernel(const float* W, long long ldc, long long ldr, const float* v,
+                                                        int v_ld, int C, int Cr, const float* b2, int fwd, float* out) {
+  const int n = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const float* vv = v + (long long)n * v_ld;
+  float s = 0.f;
+  for (int r = 0; r < Cr; ++r) s += W[c * ldc + r * ldr] * vv[r];
+  out[(long long)n * C + c] = fwd ? sigmoidf_(s + (b2 ? b2[c] : 0.f)) : s;
+}
+
+// forward: gap [N][C], hpre [N][Cr], gate [N][C]; h [N][Cr] in scratch
+static void ca_mlp_fwd(const float* part, int S, int N, int HW, int C, int Cr, const float* w1, const float* w2, int act,
+                       float beta, float* gap, float* hpre, float* gate, const float* b1, const float* b2, float* h,
+                       hipStream_t s) {
+  const dim3 cg((C + 255) / 256, N), rg((Cr + 7) / 8, N);
+  hipLaunchKernelGGL(ca_colsum_kernel, cg, dim3(256), 0, s, part, S, C, 1.f / (float)HW, nullptr, gap, C, 0, nullptr);
+  hipLaunchKernelGGL(ca_rowdot_kernel, rg, dim3(256), 0, s, w1, (long long)C, 1ll, gap, C, 0, C, Cr, b1, act, beta, hpre,
+                     h, Cr, 1);
+  hipLaunchKernelGGL(ca_coldot_kernel, cg, dim3(256), 0, s, w2, (long long)Cr, 1ll, h, Cr, C, Cr, b2, 1, gate);
+}
+
+// backward: sd [N][Cr + C] = (dh, ds), dgap [N][C]
+static void ca_mlp_bwd(const float* part, int S, int N, int C, int Cr, const float* w1, const float* w2, int act,
+                       float beta, const float* hpre, const float* gate, float* dgap, float* sd, hipStream_t s) {
+  const dim3 cg((C + 255) / 256, N), rg((Cr + 7) / 8, N);
+  hipLaunchKernelGGL(ca_colsum_kernel, cg, dim3(256), 0, s, part, S, C, 0.f, gate, sd, Cr + C, Cr, nullptr);
+  hipLaunchKernelGGL(ca_rowdot_kernel, rg, dim3(256), 0, s, w2, 1ll, (long long)Cr, sd, Cr + C, Cr, C, Cr, nullptr, act,
+                     beta, const_cast<float*>(hpre), sd, Cr + C, 0);
+  hipLaunchKernelGGL(ca_coldot_kernel, cg, dim3(256), 0, s, w1, 1ll, (long long)C, sd, Cr + C, C, Cr, nullptr, 0, dgap);
+}
+
+// dW1[r][c] += sum_n dh[n][r] gap[n][c]; dW2[c][r] += sum_n ds[n][c] act(hpre[n][r]); db1 += sum_n dh; db2 += sum_n ds
+// (images in order).  One thread per output element over many blocks -- the per-image rows were written by one block
+// per image and summed by four more launches (the distillation student's SE layers: 4 blocks for up to 2 x 55 k
+// outputs).
+__global__ void __launch_bounds__(256) ca_wgrad_kernel(int N, int C, int Cr, const float* sd, const float* gap,
+                                                       const float* hpre, int act, float beta, float* dw1, float* dw2,
+                                                       float* db1, float* db2) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long n1 = (long long)C * Cr;
+  const int ld = Cr + C;
+  if (i < n1) {
+    const int r = (int)(i / C), c = (int)(i - (long long)r * C);
     float s = 0.f;
-    for (int r = 0; r < Cr; ++r) s += w1[(long long)r * C + c] * dh[r];
-    dgap[(long long)n * C + c] = s;
+    for (int n = 0; n < N; ++n) s += sd[(long long)n * ld + r] * gap[(long long)n * C + c];
+    dw1[i] += s;
+  } else if (i < 2 * n1) {
+    const long long j = i - n1;
+    const int c = (int)(j / Cr), r = (int)(j - (long long)c * Cr);
+    float s = 0.f;
+    for (int n = 0; n < N; ++n) s += sd[(long long)n * ld + Cr + c] * act_f(hpre[(long long)n * Cr + r], act, beta);
+    dw2[j] += s;
+  } else if (i < 2 * n1 + Cr) {
+    const int r = (int)(i - 2 * n1);
+    if (db1) {
+      float s = 0.f;
+      for (int n = 0; n < N; ++n) s += sd[(long long)n * ld + r];
+      db1[r] += s;
+    }
+  } else if (i < 2 * n1 + Cr + C) {
+    const int c = (int)(i - 2 * n1 - Cr);
+    if (db2) {
+      float s = 0.f;
+      for (int n = 0; n < N; ++n) s += sd[(long long)n * ld + Cr + c];
+      db2[c] += s;
+    }
   }
-  for (int i = threadIdx.x; i < C * Cr; i += 256) {
-    const int r = i / C, c = i - r * C;
-    wp[i] = dh[r] * gap[(long long)n * C + c];
-    const int c2 = i / Cr, r2 = i - c2 * Cr;
-    wp[C * Cr + i] = ds[c2] * act_f(hpre[(long long)n * Cr + r2], act, beta);
-  }
+}
+
+static void ca_wgrad(int N, int C, int Cr, const float* sd, const float* gap, const float* hpre, int act, float beta,
+                     float* dw1, float* dw2, float* db1, float* db2, hipStream_t s) {
+  const long long n = 2ll * C * Cr + Cr + C;
+  hipLaunchKernelGGL(ca_wgrad_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, N, C, Cr, sd, gap, hpre, act,
+                     beta, dw1, dw2, db1, db2);
 }
 
 // dx = dout*mul*gate + dgap/HW, same block layout as ca_apply_kernel
@@ -975,8 +1008,8 @@ extern "C" int hiseg_attn_channel_train_fwd(int dtype, const void* x, int N, int
   hipStream_t s = (hipStream_t)stream;
   int S = 0;
   DISPATCH_T(dtype, S = ca_gap<T>(x, nullptr, nullptr, N, HW, C, ws, s));
-  hipLaunchKernelGGL(ca_mlp_kernel, dim3(N), dim3(256), (size_t)(C + Cr + 256) * sizeof(float), s, ws, S, HW, C, Cr, w1, w2, act,
-                     act_beta, gap, hpre, gate);
+  ca_mlp_fwd(ws, S, N, HW, C, Cr, w1, w2, act, act_beta, gap, hpre, gate, nullptr, nullptr,
+             ws + (long long)N * kGapSplits * C, s);   // h in the dgap region
   DISPATCH_T(dtype, hipLaunchKernelGGL(ca_apply_kernel<T>, dim3(ca_ranges(N, HW), N),
                                        dim3(256), 0, s, x, N, HW, C, gate, chan_mul, out));
   return hiseg_check_launch("attn_channel_train_fwd");
@@ -995,10 +1028,8 @@ extern "C" int hiseg_attn_channel_bwd(int dtype, const void* x, int N, int HW, i
   float* wpart = dgap + (long long)N * C;
   int S = 0;
   DISPATCH_T(dtype, S = ca_gap<T>(x, dout, chan_mul, N, HW, C, part, s));
-  hipLaunchKernelGGL(ca_mlp_bwd_kernel, dim3(N), dim3(256), (size_t)(C + Cr + 256) * sizeof(float), s, part, S, C, Cr, w1, w2, act,
-                     act_beta, gap, hpre, gate, dgap, wpart);
-  sum_rows(wpart, N, 2 * C * Cr, C * Cr, dw1, 1, s);
-  sum_rows(wpart + C * Cr, N, 2 * C * Cr, C * Cr, dw2, 1, s);
+  ca_mlp_bwd(part, S, N, C, Cr, w1, w2, act, act_beta, hpre, gate, dgap, wpart, s);   // wpart holds sd [N][Cr + C]
+  ca_wgrad(N, C, Cr, wpart, gap, hpre, act, act_beta, dw1, dw2, nullptr, nullptr, s);
   DISPATCH_T(dtype, hipLaunchKernelGGL(ca_dx_kernel<T>, dim3(ca_ranges(N, HW), N),
                                        dim3(256), 0, s, dout, N, HW, C, gate, chan_mul, dgap, dx));
   return hiseg_check_launch("attn_channel_bwd");
@@ -1020,8 +1051,7 @@ extern "C" int hiseg_se_train_fwd(int dtype, const void* x, int N, int HW, int C
   hipStream_t s = (hipStream_t)stream;
   int S = 0;
   DISPATCH_T(dtype, S = ca_gap<T>(x, nullptr, nullptr, N, HW, C, ws, s));
-  hipLaunchKernelGGL(ca_mlp_kernel, dim3(N), dim3(256), (size_t)(C + Cr + 256) * sizeof(float), s, ws, S, HW, C, Cr, w1, w2, act,
-                     1.f, gap, hpre, gate, b1, b2);
+  ca_mlp_fwd(ws, S, N, HW, C, Cr, w1, w2, act, 1.f, gap, hpre, gate, b1, b2, ws + (long long)N * kGapSplits * C, s);
   DISPATCH_T(dtype, hipLaunchKernelGGL(ca_apply_kernel<T>, dim3(ca_ranges(N, HW), N),
                                        dim3(256), 0, s, x, N, HW, C, gate, nullptr, out));
   return hiseg_check_launch("se_train_fwd");
@@ -1041,12 +1071,8 @@ extern "C" int hiseg_se_train_bwd(int dtype, const void* x, int N, int HW, int C
   float* bpart = wpart + (long long)N * 2 * C * Cr;
   int S = 0;
   DISPATCH_T(dtype, S = ca_gap<T>(x, dout, nullptr, N, HW, C, part, s));
-  hipLaunchKernelGGL(ca_mlp_bwd_kernel, dim3(N), dim3(256), (size_t)(C + Cr + 256) * sizeof(float), s, part, S, C, Cr, w1, w2, act,
-                     1.f, gap, hpre, gate, dgap, wpart, bpart);
-  sum_rows(wpart, N, 2 * C * Cr, C * Cr, dw1, 1, s);
-  sum_rows(wpart + C * Cr, N, 2 * C * Cr, C * Cr, dw2, 1, s);
-  sum_rows(bpart, N, Cr + C, Cr, db1, 1, s);
-  sum_rows(bpart + Cr, N, Cr + C, C, db2, 1, s);
+  ca_mlp_bwd(part, S, N, C, Cr, w1, w2, act, 1.f, hpre, gate, dgap, bpart, s);
+  ca_wgrad(N, C, Cr, bpart, gap, hpre, act, 1.f, dw1, dw2, db1, db2, s);
   DISPATCH_T(dtype, hipLaunchKernelGGL(ca_dx_kernel<T>, dim3(ca_ranges(N, HW), N),
                                        dim3(256), 0, s, dout, N, HW, C, gate, nullptr, dgap, dx));
   return hiseg_check_launch("se_train_bwd");

@@ -315,7 +315,7 @@ def _declare(lib):
         "hiseg_dw_train_fwd": ([c_int, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P, c_int, c_int, P], c_int),
         "hiseg_dw_bwd_data": ([c_int, P, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P, c_int, P],
                               c_int),
-        "hiseg_dw_bwd_weight_ws": ([c_int, c_int], c_ll),
+        "hiseg_dw_bwd_weight_ws": ([c_int, c_int, c_int, c_int, c_int, c_int], c_ll),
         "hiseg_dw_bwd_weight": ([c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P],
                                 c_int),
         "hiseg_se_train_ws": ([c_int, c_int, c_int], c_ll),

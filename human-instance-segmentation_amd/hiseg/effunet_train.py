@@ -68,25 +68,61 @@ def dw_bn_silu(T: TE.Tape, conv: nn.Conv2d, bn: nn.BatchNorm2d, x: Act, need_dx:
     Ho, Wo = (x.H + 2 * (k // 2) - k) // st + 1, (x.W + 2 * (k // 2) - k) // st + 1
     dev = x.t.device
     z = Act.new(x.N, Ho, Wo, c, x.dtype, dev, zero=False)
-    TE._chk(lib.hiseg_dw_train_fwd(hdtype(x.dtype), x.ptr(), x.N, x.H, x.W, c, k, st, conv.weight.data_ptr(), z.ptr(),
-                                   Ho, Wo, TE._stream()), "dw_train_fwd")
+    fast = x.dtype == torch.bfloat16 and _fast_dw()
+    if fast:
+        # the inference depthwise kernels (LDS-tiled / register-quad, hiseg_dwconv_fwd) with a unit affine and no
+        # activation: the raw conv the train-mode BN normalises.  Their weight layout is [K*K][C]: the parameter is
+        # transposed once per step (it changes every step).
+        one, zero = _unit_affine(S, c, dev)
+        wt = conv.weight.detach().reshape(c, k * k).t().contiguous()
+        TE._chk(lib.hiseg_dwconv_fwd(hdtype(x.dtype), x.ptr(), x.N, x.H, x.W, c, k, st, wt.data_ptr(), one.data_ptr(),
+                                     zero.data_ptr(), ACT_NONE, z.ptr(), Ho, Wo, TE._stream()), "dwconv(train)")
+    else:
+        TE._chk(lib.hiseg_dw_train_fwd(hdtype(x.dtype), x.ptr(), x.N, x.H, x.W, c, k, st, conv.weight.data_ptr(),
+                                       z.ptr(), Ho, Wo, TE._stream()), "dw_train_fwd")
     y, bst = TE.bn_forward(T, bn, z, act=ACT_SILU)
 
     def back():
         dz = Act.new(z.N, z.H, z.W, c, z.dtype, dev, zero=False)
         TE.bn_backward(T, bn, z, y, bst, dz, act=ACT_SILU)
         if conv.weight.requires_grad:
-            ws = torch.empty(int(lib.hiseg_dw_bwd_weight_ws(c, k)), dtype=torch.float32, device=dev)
+            ws = torch.empty(int(lib.hiseg_dw_bwd_weight_ws(hdtype(x.dtype), x.N, Ho, Wo, c, k)), dtype=torch.float32,
+                             device=dev)
             TE._chk(lib.hiseg_dw_bwd_weight(hdtype(x.dtype), x.ptr(), dz.ptr(), x.N, x.H, x.W, c, k, st, Ho, Wo,
                                             ws.data_ptr(), S.grad(conv.weight).data_ptr(), TE._stream()),
                     "dw_bwd_weight")
         if need_dx:
             gx, acc = T.grad(x)
-            TE._chk(lib.hiseg_dw_bwd_data(hdtype(x.dtype), dz.ptr(), x.N, x.H, x.W, c, k, st, conv.weight.data_ptr(),
-                                          Ho, Wo, gx.ptr(), int(acc), TE._stream()), "dw_bwd_data")
+            if fast and st == 1 and not acc:
+                # stride 1: the data gradient is the same depthwise conv of dz with the kernel rotated by 180 degrees
+                one, zero = _unit_affine(S, c, dev)
+                wf = conv.weight.detach().reshape(c, k, k).flip(1, 2).reshape(c, k * k).t().contiguous()
+                TE._chk(lib.hiseg_dwconv_fwd(hdtype(x.dtype), dz.ptr(), x.N, x.H, x.W, c, k, 1, wf.data_ptr(),
+                                             one.data_ptr(), zero.data_ptr(), ACT_NONE, gx.ptr(), x.H, x.W,
+                                             TE._stream()), "dwconv(train dgrad)")
+            else:
+                TE._chk(lib.hiseg_dw_bwd_data(hdtype(x.dtype), dz.ptr(), x.N, x.H, x.W, c, k, st,
+                                              conv.weight.data_ptr(), Ho, Wo, gx.ptr(), int(acc), TE._stream()),
+                        "dw_bwd_data")
             T.mark(x)
     T.push(back)
     return y
+
+
+def _fast_dw() -> bool:
+    """HISEG_TRAIN_DW_FAST=0: the training depthwise forward / stride-1 data gradient on the plain train kernels
+    (hiseg_dw_train_fwd / hiseg_dw_bwd_data) instead of the inference kernels (A/B timing; read per call)."""
+    import os
+    return os.environ.get("HISEG_TRAIN_DW_FAST", "1") != "0"
+
+
+def _unit_affine(S, c: int, dev) -> tuple:
+    key = ("unit_affine", c, dev)
+    v = S.cached.get(key)
+    if v is None:
+        v = S.cached[key] = (torch.ones(c, dtype=torch.float32, device=dev), torch.zeros(c, dtype=torch.float32,
+                                                                                            device=dev))
+    return v
 
 
 def se_train(T: TE.Tape, se: nn.Module, h: Act) -> Act:

@@ -228,7 +228,7 @@ int hiseg_dw_train_fwd(int dtype, const void* x, int N, int H, int W, int C, int
                        void* out, int Ho, int Wo, hiseg_stream_t stream);
 int hiseg_dw_bwd_data(int dtype, const void* dy, int N, int H, int W, int C, int K, int stride, const float* w,
                       int Ho, int Wo, void* dx, int accumulate, hiseg_stream_t stream);
-long long hiseg_dw_bwd_weight_ws(int C, int K);
+long long hiseg_dw_bwd_weight_ws(int dtype, int N, int Ho, int Wo, int C, int K);   /* floats (pixel splits x C x K*K) */
 int hiseg_dw_bwd_weight(int dtype, const void* x, const void* dy, int N, int H, int W, int C, int K, int stride,
                         int Ho, int Wo, float* ws, float* dw, hiseg_stream_t stream);
 

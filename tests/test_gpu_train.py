@@ -1111,6 +1111,43 @@ def test_fused_bn_statistics_match_the_statistics_pass(case, monkeypatch):
     assert (y1 == y0).float().mean() > 0.98
 
 
+@pytest.mark.parametrize("case", [(32, 3, 1, 2, 40, 48), (144, 5, 1, 2, 20, 24), (96, 3, 2, 2, 33, 27),
+                                  (240, 5, 2, 1, 16, 20), (1152, 3, 1, 2, 10, 10)])
+def test_train_depthwise_on_inference_kernels_matches_train_kernels(case, monkeypatch):
+    """Round 5: the unfrozen EfficientNet stages' depthwise conv (dw_bn_silu) in bf16 runs its forward -- and, at stride
+    1, its data gradient as the conv with the 180-degree rotated kernel -- on the inference depthwise kernels
+    (hiseg_dwconv_fwd, unit affine, no activation) instead of hiseg_dw_train_fwd / hiseg_dw_bwd_data
+    (HISEG_TRAIN_DW_FAST=0).  Both are bf16 executions of the same math: outputs and gradients within bf16 rounding of
+    each other (2e-2 relative to the tensor's scale; the depthwise weight gradient within 2e-2), stride 1 / 2, k 3 / 5,
+    ragged images."""
+    from hiseg import effunet_train as EU
+    from hiseg.ops import Act
+    C, k, st, N, H, W = case
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(9)
+    x = torch.randn(N, C, H, W, device=DEV, generator=g)
+    Ho, Wo = (H + 2 * (k // 2) - k) // st + 1, (W + 2 * (k // 2) - k) // st + 1
+    gy = torch.randn(N, C, Ho, Wo, device=DEV, generator=g)
+    res = {}
+    for fast in ("1", "0"):
+        monkeypatch.setenv("HISEG_TRAIN_DW_FAST", fast)
+        conv = nn.Conv2d(C, C, k, stride=st, padding=k // 2, groups=C, bias=False)
+        filler.fill_module(conv, seed=71)
+        bn = nn.BatchNorm2d(C)
+        filler.fill_module(bn, seed=72)
+        TE, S, T = engine(_Holder(c=conv, b=bn), dt)
+        xa = Act.from_nchw(x, dt)
+        y = EU.dw_bn_silu(T, conv, bn, xa, need_dx=True)
+        inject(T, y, gy, dt)
+        S.flat.prepare_backward()
+        T.run_backward()
+        torch.cuda.synchronize()
+        res[fast] = (y.to_nchw().float(), grad_nchw(T, xa).float(), conv.weight.grad.clone())
+    for a, b in zip(res["1"], res["0"]):
+        assert torch.isfinite(a).all()
+        assert ((a - b).abs().max() / b.abs().max()).item() < 2e-2
+
+
 @pytest.mark.gpu
 def test_train_step_independent_of_allocator_churn_between_forward_and_backward():
     """Every buffer a backward reads through a raw address stays alive until that backward ran: one bf16 train step
