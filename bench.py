@@ -243,14 +243,27 @@ def train_bench(device, dtype, rank, world, dist, steps, warmup, preset=None, ba
     return out
 
 
+def _copy_probe_ms(nbytes=1 << 29):
+    """Median time of three device-to-device copies of `nbytes` (an HBM bandwidth probe, tools/leg_probe.py)."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    b = torch.empty_like(a)
+    ts = []
+    for _ in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    del a, b
+    return sorted(ts)[1]
+
+
 def _release_leg():
-    """Between legs: collect the finished leg's graphs / closures (reference cycles keep a GraphedStep, its captured
-    graph and that graph's private memory pool alive until the cyclic collector runs), so their blocks return to the
-    caching allocator for the next leg.  The blocks are NOT handed back to the driver (no empty_cache): freed VRAM
-    that is allocated again is cleared by the kernel driver in the background, and that clearing ran beside the next
-    leg's timed region -- the inference leg measured 16 % slower right after the train legs and recovered after
-    ~30 s idle; with the cache kept it is within 0.2 % of its first run (tools/order_probe.py,
-    profiles/r5_leg_order.txt).  HISEG_BENCH_EMPTY_CACHE=1 restores the old release for A/B runs."""
+    """Between legs of an --in-process run: collect the finished leg's graphs / closures (reference cycles keep a
+    GraphedStep, its captured graph and that graph's private memory pool alive until the cyclic collector runs).  The
+    cached blocks are kept for the next leg (HISEG_BENCH_EMPTY_CACHE=1 returns them to the driver, after which the
+    inference leg measured up to 16 % slower right after the train legs, profiles/r5_leg_order.txt)."""
     import gc
     torch.cuda.synchronize()
     gc.collect()
@@ -881,6 +894,8 @@ def main():
     ap.add_argument("--eager-train", action="store_true", help="train / distill legs as eager launches (default on one "
                                                                 "GPU: one replayed HIP graph per step)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--in-process", action="store_true",
+                    help="one GPU: run every leg in this process (default: each leg in a child process of its own)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher + rendezvous check only (no GPU work): CPU tests of the multi-rank path")
     args = ap.parse_args()
@@ -946,10 +961,14 @@ def main():
         return
     if args.distill_only:
         args.train_only, args.no_train = True, True
-    # The legs run in the order --order names (default: inference, B0 train, C3, C4, distillation), each after the
-    # previous one's graphs and cached blocks were released (_release_leg).  Round 4 ran the distillation leg
-    # second, to keep its replays away from a slowdown seen after the train legs; round 5 measured every leg alone
-    # and in both orders within a few per cent of each other, so the order is the natural one.
+    # The legs run in the order --order names (default: inference, B0 train, C3, C4, distillation, unfrozen
+    # distillation).  On one GPU each leg runs in a child process of its own (`bench.py --leg L`, whose JSON object
+    # this process merges), so no leg inherits another's device state: round 5 measured the distillation step at
+    # 16.4-16.8 ms per replay after the inference leg in one process against 8.9 alone, and the inference leg 7 %
+    # slower after the train / distillation legs -- state a process keeps: which of the GPU_MAX_HW_QUEUES hardware
+    # queues each stream (and each graph executor's branch stream) was bound to when it first ran, and which streams
+    # share one (hiseg.streams keeps each process at four normal-priority streams).  --in-process
+    # restores one process for all legs (the multi-rank run always uses one process per rank).
     half, eager = max(2, args.steps // 2), args.eager_train
     legs = {
         "infer": (not args.train_only, lambda: out.update(infer_bench(args, device, dtype, rank, world, dist))),
@@ -978,10 +997,13 @@ def main():
         on, fn = legs[k]
         if not on:
             continue
-        if not first:
-            _release_leg()
+        if world == 1 and not args.in_process:
+            out.update(_leg_in_child(k, args))
+        else:
+            if not first:
+                _release_leg()
+            fn()
         first = False
-        fn()
         if k == "infer":   # the JSON line's head keys come first
             out = {**{kk: out[kk] for kk in out if kk not in ("train", "train_c3", "train_c4", "distill",
                                                                 "distill_unfrozen")}, **out}
@@ -999,6 +1021,25 @@ def main():
         print(json.dumps(out))
     if dist:
         dist.destroy_process_group()
+
+
+def _leg_in_child(leg, args):
+    """Run one leg as `bench.py --leg <leg>` in a child process (one GPU) and return its JSON object; the child's
+    stderr passes through."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--leg", leg, "--steps", str(args.steps), "--warmup",
+           str(args.warmup), "--dtype", args.dtype, "--no-cpu-baseline"]
+    if args.serial:
+        cmd.append("--serial")
+    if args.eager_train:
+        cmd.append("--eager-train")
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=None, text=True, env=env)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        print(f"bench.py: leg {leg} failed (exit {r.returncode})", file=sys.stderr)
+        sys.exit(r.returncode or 1)
+    return json.loads(lines[-1])
 
 
 def infer_bench(args, device, dtype, rank, world, dist):

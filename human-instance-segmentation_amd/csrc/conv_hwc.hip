@@ -187,6 +187,14 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
   };
   static_assert(!RP || (NW == 4 && NRI == 16), "residual prefetch layout: 128-Cout tiles");
 
+  // ABL 64 / 128 (DIAG): the second workgroup of each CU in the first dispatch round starts half / a quarter of a
+  // slice late, so the two workgroups sharing each SIMD reach their barriers and DMA waits out of phase
+  if constexpr ((ABL & 192) != 0) {
+    if (orig >= 256 && orig < 512) {
+      if constexpr ((ABL & 64) != 0) __builtin_amdgcn_s_sleep(36);
+      else __builtin_amdgcn_s_sleep(18);
+    }
+  }
   // ---- prologue: slice 0's halo, the weights of block (slice 0, kx 0)
   hc_u4 af[3][TM], an[3][TM];
 #pragma unroll
@@ -496,7 +504,7 @@ int conv_hwc_stats_tiles(const ConvArgs& a) {
 int conv_hwc_try(const ConvArgs& a, hipStream_t s, int variant) {
   const hiseg_conv2d_desc& d = a.d;
 #ifdef HISEG_DIAG
-  if (variant >= 150 && variant < 214) {   // timing ablations of variant 104 (res + ReLU only; output buffer as
+  if (variant >= 150 && variant < 279) {   // timing ablations of variant 104 (res + ReLU only; output buffer as
                                           // scratch: the ABL 32 store writes one float per thread and MFMA row)
     if (d.weight_frag == nullptr || !d.residual || d.act != HISEG_ACT_RELU || d.a_up != 1 || d.Cout % 128) return 0;
     int r;
@@ -510,6 +518,8 @@ int conv_hwc_try(const ConvArgs& a, hipStream_t s, int variant) {
       case 16: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 16>(a, s); break;
       case 32: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 32>(a, s); break;
       case 47: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 47>(a, s); break;
+      case 64: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 64>(a, s); break;
+      case 128: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 128>(a, s); break;
       default: return 0;
     }
     return r < 0 ? r : 1;

@@ -951,7 +951,7 @@ static int chunk_of(int dtype) { return dtype == HISEG_BF16 ? 8 : 4; }
 // train_norm.hip: the BatchNorm statistics merge over an explicit split count
 int bn_finalize_splits(const float* partial, int S, int C, long long P, const float* gamma, const float* beta,
                        float eps, float momentum, float* running_mean, float* running_var, float* mean, float* invstd,
-                       float* scale, float* shift, hipStream_t stream);
+                       float* scale, float* shift, hipStream_t stream, long long rs = 0);
 
 extern "C" int hiseg_attn_spatial_train_fwd(int dtype, const void* x, int N, int H, int W, int C, const float* w7, int k,
                                             const float* chan_mul, float* stats, int* argmax, float* att, void* out,

@@ -320,13 +320,9 @@ class DistillationUNetWrapper(nn.Module):
     # Same kernels, same inputs: the results are the serial order's bit for bit.  HISEG_SERIAL_TEACHER=1: serial.
     concurrent_teacher = os.environ.get("HISEG_SERIAL_TEACHER", "0") != "1"
 
-    _teacher_priority = 0
-
     def _side(self, device):
-        st = self.__dict__.get("_teacher_stream")
-        if st is None or st.device != device:
-            st = self.__dict__["_teacher_stream"] = torch.cuda.Stream(device=device, priority=self._teacher_priority)
-        return st
+        from .streams import role_stream
+        return role_stream("teacher", device)
 
     def forward(self, x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         if self.teacher is not None and x.is_cuda and self.concurrent_teacher:

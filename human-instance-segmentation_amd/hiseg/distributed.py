@@ -27,6 +27,8 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from .streams import role_stream
+
 _SYNC_KEY = "_hiseg_grad_sync"
 
 
@@ -70,7 +72,7 @@ class GradBucketSync:
         self.bucket_params.append(ids)
         self.last_op, self.launch_after = None, {}
         dev = flat.grad.device
-        self.comm_stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
+        self.comm_stream = role_stream("comm", dev) if dev.type == "cuda" else None
 
     # -- tape callbacks (train_engine.Tape.run_backward)
     def begin(self, n_ops: int):

@@ -31,6 +31,8 @@ from typing import Callable, Optional
 
 import torch
 
+from .streams import role_stream
+
 
 class GraphedStep:
     """``gs = GraphedStep(step_fn, optimizer_fn)``; every ``gs()`` runs exactly one training step and returns
@@ -88,9 +90,7 @@ class GraphedStep:
             # the optimizer or the model's flat layout / packing table was re-allocated since the capture
             self.graph, self.calls = None, 1
         if self.calls <= self.eager:
-            s = self.__dict__.get("_warm")   # one warm-up side stream per instance (not one per eager call)
-            if s is None:
-                s = self._warm = torch.cuda.Stream()
+            s = role_stream("warm")   # the warm-up side stream (hiseg.streams: one per process, not per call)
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
                 out = self.fn()
@@ -103,7 +103,7 @@ class GraphedStep:
             g = torch.cuda.CUDAGraph()
             # thread-local capture: RCCL's watchdog thread polls the events of earlier collectives while the step
             # is being captured, which the default (global) mode turns into a capture error in that thread
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            with torch.cuda.graph(g, stream=role_stream("capture"), capture_error_mode="thread_local"):
                 self.out = self.fn()
             self.fp = self._fingerprint()
             if self.fp != before:

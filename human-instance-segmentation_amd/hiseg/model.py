@@ -18,6 +18,7 @@ import torch.nn as nn
 from . import _lib as L
 from . import engine
 from . import export
+from . import streams
 from .effunet import EfficientNetUnet
 from .layers import RefinedHierarchicalSegmentationHead, ResidualBlock, make_act_unet, make_norm
 
@@ -248,7 +249,7 @@ class StreamPipelinedExport:
         self.wrapper = wrapper
         self._raw_unet = None
         if unet_cu_mask is None:
-            self.s_unet = torch.cuda.Stream()
+            self.s_unet = streams.role_stream("unet")
         else:
             import ctypes
             words = (ctypes.c_uint * len(unet_cu_mask))(*[int(w) & 0xFFFFFFFF for w in unet_cu_mask])
@@ -257,7 +258,7 @@ class StreamPipelinedExport:
                     "stream_create_cu_mask")
             self._raw_unet = h.value
             self.s_unet = torch.cuda.ExternalStream(h.value)
-        self.s_head = torch.cuda.Stream(priority=-1) if head_priority else torch.cuda.Stream()
+        self.s_head = streams.role_stream("head" if head_priority else "head_normal")
 
     def __del__(self):
         if getattr(self, "_raw_unet", None):

@@ -93,8 +93,9 @@ int hiseg_bn_finalize(const float* partial, int C, long long P, const float* gam
                       float momentum, float* running_mean, float* running_var, float* mean, float* invstd,
                       float* scale, float* shift, hiseg_stream_t stream);
 /* The same merge over an explicit split count: the partials a conv epilogue wrote
- * (hiseg_conv2d_desc.stats_partial, S = hiseg_conv2d_stats_tiles). */
-int hiseg_bn_finalize_n(const float* partial, int S, int C, long long P, const float* gamma, const float* beta,
+ * (hiseg_conv2d_desc.stats_partial, S = hiseg_conv2d_stats_tiles).  `partial` is scratch the merge consumes: with
+ * more than 256 splits, groups of 64 are pre-merged in place (row 64 g holds group g's merge afterwards). */
+int hiseg_bn_finalize_n(float* partial, int S, int C, long long P, const float* gamma, const float* beta,
                         float eps, float momentum, float* running_mean, float* running_var, float* mean,
                         float* invstd, float* scale, float* shift, hiseg_stream_t stream);
 typedef struct hiseg_bn_apply_desc {

@@ -1062,7 +1062,7 @@ def test_two_source_results_do_not_depend_on_operand_placement(case):
 
 
 @pytest.mark.parametrize("case", [(256, 256, 3, 20, 30, 0), (128, 128, 2, 37, 21, 0), (128, 256, 2, 16, 16, 0),
-                                  (320, 256, 2, 16, 20, 64)])
+                                  (320, 256, 2, 16, 20, 64), (128, 128, 24, 40, 40, 0)])
 def test_fused_bn_statistics_match_the_statistics_pass(case, monkeypatch):
     """Round 5: the conv feeding a train-mode BatchNorm writes the batch-statistics partials of
     its bf16 output from the epilogue (conv_hwc's ST form: per 16 x 16-pixel tile and channel count / mean / M2,
@@ -1109,6 +1109,47 @@ def test_fused_bn_statistics_match_the_statistics_pass(case, monkeypatch):
     # one bf16 ulp of the output (the normalised value may round either way when mean / invstd differ in the last bit)
     assert ((y1 - y0).abs() <= y0.abs() * 2 ** -7 + 1e-6).all()
     assert (y1 == y0).float().mean() > 0.98
+
+
+@pytest.mark.parametrize("S,C", [(40, 64), (3001, 80), (12288, 256)])
+def test_bn_finalize_n_matches_f64_merge(S, C):
+    """hiseg_bn_finalize_n over S split partials [S][3][C] (count, mean, M2; some splits empty): more than 256 splits
+    are pre-merged in groups of 64 in place (bn_premerge_kernel) before the per-channel merge.  Mean / invstd /
+    scale / shift / running statistics against a float64 Chan merge of the same partials (1e-6 relative)."""
+    from hiseg import _lib as L
+    rng = np.random.default_rng(S + C)
+    n = rng.integers(0, 65, size=(S, C)).astype(np.float32)
+    n[rng.random((S, C)) < 0.05] = 0
+    n[0] = 7   # every channel has data
+    mu = (rng.standard_normal((S, C)) * 0.3 + 2.0).astype(np.float32)
+    m2 = (rng.random((S, C)) * n).astype(np.float32)
+    mu[n == 0] = 0
+    m2[n == 0] = 0
+    part = np.stack([n, mu, m2], axis=1)   # [S][3][C]
+    P = int(n.sum(axis=0).max())
+    tot = n.astype(np.float64).sum(axis=0)
+    mean = (n * mu.astype(np.float64)).sum(axis=0) / tot
+    var = (m2.astype(np.float64).sum(axis=0) + (n * (mu.astype(np.float64) - mean) ** 2).sum(axis=0)) / tot
+    gamma = torch.from_numpy(rng.standard_normal(C).astype(np.float32)).to(DEV)
+    beta = torch.from_numpy(rng.standard_normal(C).astype(np.float32)).to(DEV)
+    rm = torch.zeros(C, device=DEV)
+    rv = torch.ones(C, device=DEV)
+    out = [torch.empty(C, device=DEV) for _ in range(4)]
+    pt = torch.from_numpy(part).to(DEV).contiguous()
+    eps, mom = 1e-5, 0.1
+    L.check(L.lib().hiseg_bn_finalize_n(pt.data_ptr(), S, C, P, gamma.data_ptr(), beta.data_ptr(), eps, mom,
+                                        rm.data_ptr(), rv.data_ptr(), *[o.data_ptr() for o in out], L.stream_ptr()),
+            "bn_finalize_n")
+    torch.cuda.synchronize()
+    m_o, inv_o, sc_o, sh_o = [o.double().cpu().numpy() for o in out]
+    inv = 1.0 / np.sqrt(var + eps)
+    g, b = gamma.double().cpu().numpy(), beta.double().cpu().numpy()
+    np.testing.assert_allclose(m_o, mean, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(inv_o, inv, rtol=1e-6)
+    np.testing.assert_allclose(sc_o, g * inv, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(sh_o, b - mean * g * inv, rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(rm.double().cpu().numpy(), mom * mean, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(rv.double().cpu().numpy(), (1 - mom) + mom * var * P / (P - 1), rtol=1e-6)
 
 
 @pytest.mark.parametrize("case", [(32, 3, 1, 2, 40, 48), (144, 5, 1, 2, 20, 24), (96, 3, 2, 2, 33, 27),

@@ -22,10 +22,12 @@ import sys
 R1 = "--r1" in sys.argv
 WIDE = "--wide" in sys.argv    # round 2 v1: conv_wide_kernel<256, 4>
 GRID = 12288 * 512 if R1 else (3072 * 256 if WIDE else 6144 * 256)
-HW = "--hw" in sys.argv        # round 2 v2-v12: conv_hw_kernel<128, ...>; default (round 3): conv_hwr_kernel
+HW = "--hw" in sys.argv        # round 2 v2-v12: conv_hw_kernel<128, ...>
+HWR = "--hwr" in sys.argv      # rounds 3-4: conv_hwr_kernel; default (round 5): conv_hwc_kernel (same grid)
 PREFIX = ("void hiseg::conv_fast_kernel<128, 128" if R1 else
           "void hiseg::conv_wide_kernel<256, 4" if WIDE else
-          "void hiseg::conv_hw_kernel<128" if HW else "void hiseg::conv_hwr_kernel<")
+          "void hiseg::conv_hw_kernel<128" if HW else "void hiseg::conv_hwr_kernel<" if HWR else
+          "void hiseg::conv_hwc_kernel<")
 allrows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 cut_t = next((int(r["Start_Timestamp"]) for r in allrows if "bn_stats" in r["Kernel_Name"]), None)
 rows = [r for r in allrows
@@ -41,7 +43,8 @@ if "--last" in sys.argv:
 d = sorted(d)
 name = ("conv_fast_kernel<128,128,4,2,2,lds-epilogue> grid 12288 x 512" if R1 else
         "conv_wide_kernel<256,4> grid 3072 x 256" if WIDE else
-        "conv_hw_kernel<128> grid 6144 x 256" if HW else "conv_hwr_kernel<ACT, RES, 6> grid 6144 x 256")
+        "conv_hw_kernel<128> grid 6144 x 256" if HW else "conv_hwr_kernel<ACT, RES, 6> grid 6144 x 256" if HWR else
+        "conv_hwc_kernel<ACT, RES, 4> grid 6144 x 256")
 print(json.dumps({"kernel": name + " (256->256 3x3 @64x48 x256 ROIs)",
                   "launches": len(d), "same_grid_launches": len(d_all), "cluster_cut_ms": round(cut, 4), "avg_ms": round(sum(d) / len(d), 4), "median_ms": round(d[len(d) // 2], 4),
                   "min_ms": round(d[0], 4), "max_ms": round(d[-1], 4),

@@ -23,6 +23,7 @@ SHAPES = {
     "w128_3x3_128x96": (256, 128, 128, 128, 96, 3),
     "w64_3x3_64x48": (256, 64, 64, 64, 48, 3),
     "w128_3x3_64x48": (256, 128, 128, 64, 48, 3),
+    "w128to256_3x3_64x48": (256, 128, 256, 64, 48, 3),
 }
 
 
