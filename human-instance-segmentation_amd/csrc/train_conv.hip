@@ -26,6 +26,9 @@
 
 namespace hiseg {
 int wgrad_wide_try(const WgradArgs& a, hipStream_t s);
+int wgrad_hwc_try(const WgradArgs& a, hipStream_t s);
+bool wgrad_hwc_shape_ok(const hiseg_conv2d_desc* d);
+int wgrad_hwc_splits(const hiseg_conv2d_desc* d);
 }
 
 namespace hiseg {
@@ -637,7 +640,7 @@ static int wgrad_typed(const WgradArgs& a, hipStream_t s) {
 // Which kernel took each weight gradient (hiseg_wgrad_path_stats, hiseg_wgrad_last_path): the wide tile, the
 // transposed-read tile, the generic register-transpose kernel in bf16 (a fallback: HISEG_LOG_WGRAD=1 names the
 // layer), or the f32 kernel (parity mode, by design).
-static std::atomic<long long> g_wgrad_paths[4];
+static std::atomic<long long> g_wgrad_paths[5];
 static thread_local int g_wgrad_last = -1;
 
 static void wgrad_note_path(int path, const hiseg_conv2d_desc* d, int dy_cs, int dy_coff) {
@@ -680,6 +683,7 @@ static int wgrad_geometry(const hiseg_conv2d_desc* d, int want_bias, int* Cg, in
   // rounds on 256 CUs, and rounding up (36 tiles x 29 splits = 1044) added a third, nearly empty round that cost
   // a third of the layer's time (the wide kernel, one workgroup per CU, gets a quarter of them per round)
   int sp = (int)(1024 / tiles);
+  if (wgrad_hwc_shape_ok(d)) sp = wgrad_hwc_splits(d);   // the halo tile's own pixel partition (wgrad_hwc.hip)
   if (sp > nblocks) sp = nblocks;
   if (sp < 1) sp = 1;
   *bps = (nblocks + sp - 1) / sp;
@@ -713,6 +717,11 @@ extern "C" int hiseg_conv2d_wgrad(const hiseg_conv2d_desc* fwd, const void* dy, 
   a.splits = splits;
   a.ws = ws;
   hipStream_t s = (hipStream_t)stream;
+  const int rh = wgrad_hwc_try(a, s);
+  if (rh != 0) {
+    if (rh > 0) wgrad_note_path(HISEG_WGRAD_PATH_HWC, fwd, dy_cstride, dy_coff);
+    return rh < 0 ? rh : HISEG_OK;
+  }
   const int rw = wgrad_wide_try(a, s);
   if (rw != 0) {
     if (rw > 0) wgrad_note_path(HISEG_WGRAD_PATH_WIDE, fwd, dy_cstride, dy_coff);
@@ -728,7 +737,7 @@ extern "C" int hiseg_conv2d_wgrad(const hiseg_conv2d_desc* fwd, const void* dy, 
 }
 
 extern "C" int hiseg_wgrad_path_stats(long long* counts, int reset) {
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < 5; ++i) {
     if (counts) counts[i] = g_wgrad_paths[i].load();
     if (reset) g_wgrad_paths[i] = 0;
   }

@@ -402,7 +402,10 @@ int wgrad_wide_bc(const hiseg_conv2d_desc* d, int Cg, int Kg, int Cin, int M, in
       return 0;
     }
   }
-  return Cg % 256 == 0 ? 256 : 0;   // (the 256 x 128 tile measured slower than the 128 x 128 kernel)
+  // (the 256 x 128 tile measured slower than the 128 x 128 kernel; so was this tile on Cin = 128: 128 -> 256 @64x48 x
+  // 256 ROIs 1.078 vs 0.656 ms, its K tiles straddling two taps, profiles/r5_wgrad_hwc.txt)
+  if (Cin % 256) return 0;
+  return Cg % 256 == 0 ? 256 : 0;
 }
 
 template <int BC, int NW, int PB, int STAGES, bool BPRE = false, int SHT = 0, bool TOG = false>

@@ -413,13 +413,13 @@ def placement_stats(reset: bool = False):
     return a.value, b.value
 
 
-WGRAD_PATHS = ("wide", "transposed_read", "generic_bf16", "f32")
+WGRAD_PATHS = ("wide", "transposed_read", "generic_bf16", "f32", "halo")
 
 
 def wgrad_path_stats(reset: bool = False) -> dict:
     """How many weight gradients each kernel computed since the last reset (include/hiseg_train.h):
-    the wide tile, the transposed-read tile, the generic bf16 fallback, the f32 (parity) kernel."""
-    c = (c_ll * 4)()
+    the wide tile, the transposed-read tile, the generic bf16 fallback, the f32 (parity) kernel, the halo tile."""
+    c = (c_ll * 5)()
     check(lib().hiseg_wgrad_path_stats(c, int(reset)), "wgrad_path_stats")
     return dict(zip(WGRAD_PATHS, (int(v) for v in c)))
 

@@ -34,6 +34,19 @@ import torch
 from .streams import role_stream
 
 
+def _drain_rccl_watchdog():
+    """Before a capture in a process with an RCCL process group: give its watchdog thread one poll (every 100 ms) to
+    retire the finished eager collectives.  It queries each tracked collective's end event, and the process group
+    reuses finished collectives' events for the ones recorded during the capture: a poll that reaches a retired
+    collective after its event was re-recorded in the capturing stream fails with hipErrorCapturedEvent and aborts
+    the process (seen once in a full GPU suite run, test_graphed_ddp_step_rccl_world1_equals_eager after 150 other
+    tests; profiles/r5_gpu_suite.txt)."""
+    import time
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
+        time.sleep(0.3)
+
+
 class GraphedStep:
     """``gs = GraphedStep(step_fn, optimizer_fn)``; every ``gs()`` runs exactly one training step and returns
     step_fn's outputs (for replays: the tensors captured, refreshed in place).
@@ -99,6 +112,7 @@ class GraphedStep:
         if self.graph is None or self._lr() != self.lr:
             self.graph = None
             torch.cuda.synchronize()
+            _drain_rccl_watchdog()
             before = self._fingerprint()
             g = torch.cuda.CUDAGraph()
             # thread-local capture: RCCL's watchdog thread polls the events of earlier collectives while the step

@@ -32,13 +32,14 @@ extern "C" {
 int hiseg_conv2d_wgrad_dims(const hiseg_conv2d_desc* fwd, int want_bias, int* Cg, int* Kg, int* splits);
 int hiseg_conv2d_wgrad(const hiseg_conv2d_desc* fwd, const void* dy, int dy_cstride, int dy_coff,
                        int want_bias, float* ws, int splits, hiseg_stream_t stream);
-/* Which kernel computed each weight gradient since the last reset: counts[4] indexed by
- * HISEG_WGRAD_PATH_* (wide 256x256 tile, transposed-read tile, generic bf16 fallback, f32).
+/* Which kernel computed each weight gradient since the last reset: counts[5] indexed by
+ * HISEG_WGRAD_PATH_* (wide 256x256 tile, transposed-read tile, generic bf16 fallback, f32, halo tile).
  * hiseg_wgrad_last_path: the path of this thread's last hiseg_conv2d_wgrad (-1 before any). */
 #define HISEG_WGRAD_PATH_WIDE 0
 #define HISEG_WGRAD_PATH_TR 1
 #define HISEG_WGRAD_PATH_GENERIC 2
 #define HISEG_WGRAD_PATH_F32 3
+#define HISEG_WGRAD_PATH_HWC 4
 int hiseg_wgrad_path_stats(long long* counts, int reset);
 int hiseg_wgrad_last_path(void);
 

@@ -82,7 +82,7 @@ def test_no_leg_runs_the_generic_weight_gradient_kernel_with_far_sources():
     for leg, v in res.items():
         p = v["paths"]
         assert p["generic_bf16"] == 0, f"{leg}: generic weight-gradient kernel ran: {p}"
-        assert p["wide"] + p["transposed_read"] > 0, f"{leg}: no weight gradient recorded: {p}"
+        assert p["wide"] + p["transposed_read"] + p["halo"] > 0, f"{leg}: no weight gradient recorded: {p}"
         assert v["loss"] == v["loss"], f"{leg}: NaN loss"
     # the forced far-apart path was exercised (two-source layers exist in every leg)
     assert all(v["placement"][1] > 0 for v in res.values()), {k: v["placement"] for k, v in res.items()}

@@ -141,6 +141,7 @@ def test_wgrad_wide_matches_f64_of_bf16_operands(case, reduce_taps, monkeypatch)
     stores) and by the quad-of-K kernel (HISEG_WGRAD_REDUCE_TAPS=0)."""
     from hiseg.ops import Act
     monkeypatch.setenv("HISEG_WGRAD_REDUCE_TAPS", reduce_taps)
+    monkeypatch.setenv("HISEG_WGRAD_HWC", "0")   # the transposed-read / wide tiles (the halo tile: below)
     cin, cout, k, H, W, N, bias, split = case
     dt = torch.bfloat16
     conv = nn.Conv2d(cin, cout, k, padding=k // 2, bias=bias)
@@ -160,6 +161,47 @@ def test_wgrad_wide_matches_f64_of_bf16_operands(case, reduce_taps, monkeypatch)
     wr = conv.weight.detach().to(dt).double().requires_grad_(True)
     br = torch.zeros(cout, dtype=torch.float64, device=DEV, requires_grad=True) if bias else None
     yr = F.conv2d(xr, wr, br, padding=k // 2)
+    (yr * g.to(dt).double()).sum().backward()
+    assert rel(conv.weight.grad, wr.grad) < 1e-4
+    if bias:
+        assert rel(conv.bias.grad, br.grad) < 1e-4
+
+
+HWC_WGRAD_CASES = [  # (cin, cout, H, W, N, bias): wgrad_hwc.hip's 64 x 64 x 9-tap tiles over 8 x 16-pixel tiles
+    (256, 256, 20, 30, 3, True),     # ragged pixel tiles both ways, bias column
+    (64, 64, 16, 12, 2, False),
+    (128, 256, 9, 7, 2, True),       # images smaller than one pixel tile
+    (128, 128, 33, 40, 2, False),
+    (192, 64, 64, 48, 4, True),      # the ROI head's grid, many splits
+]
+
+
+@pytest.mark.parametrize("case", HWC_WGRAD_CASES)
+def test_wgrad_hwc_matches_f64_of_bf16_operands(case):
+    """Round 5: the halo weight-gradient tile (3x3 single-source layers, Cin / Cout multiples of 64: 9 tap
+    accumulators of 32 x 32 per wave over double-buffered dY / X-halo pixel tiles, 32x32x16 MFMAs fed by
+    ds_read_b64_tr_b16) against float64 autograd of the same bf16-rounded operands (1e-4 of the max, its only error
+    the f32 accumulation), the bias column included; and the halo path actually taken."""
+    from hiseg import _lib as L
+    from hiseg.ops import Act
+    cin, cout, H, W, N, bias = case
+    dt = torch.bfloat16
+    conv = nn.Conv2d(cin, cout, 3, padding=1, bias=bias)
+    filler.fill_module(conv, seed=19)
+    TE, S, T = engine(_Holder(c=conv), dt)
+    x = torch.from_numpy(filler.normal(13, (N, cin, H, W))).to(DEV)
+    y = TE.conv_plain(T, conv, TE.ACT_NONE, Act.from_nchw(x, dt), None)
+    g = torch.from_numpy(filler.normal(14, (N, cout, H, W))).to(DEV)
+    inject(T, y, g, dt)
+    S.flat.prepare_backward()
+    L.wgrad_path_stats(reset=True)
+    T.run_backward()
+    torch.cuda.synchronize()
+    assert L.wgrad_path_stats()["halo"] == 1
+    xr = x.to(dt).double().requires_grad_(True)
+    wr = conv.weight.detach().to(dt).double().requires_grad_(True)
+    br = torch.zeros(cout, dtype=torch.float64, device=DEV, requires_grad=True) if bias else None
+    yr = F.conv2d(xr, wr, br, padding=1)
     (yr * g.to(dt).double()).sum().backward()
     assert rel(conv.weight.grad, wr.grad) < 1e-4
     if bias:
@@ -190,6 +232,7 @@ def test_wgrad_dma_addressing_bit_identical(knob, values, case, monkeypatch):
     conv_wgrad_tr_kernel: incremental offsets (HISEG_WGRAD_INC=1) vs 0 and the flipped read registers (TOG), one and
     two sources."""
     from hiseg.ops import Act
+    monkeypatch.setenv("HISEG_WGRAD_HWC", "0")   # these knobs belong to the transposed-read / wide tiles
     cin, cout, k, H, W, N, bias, split = case
     dt = torch.bfloat16
     x = torch.from_numpy(filler.normal(11, (N, cin, H, W))).to(DEV)
