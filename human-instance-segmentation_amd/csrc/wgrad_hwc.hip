@@ -54,7 +54,10 @@ constexpr int WH_XI = (WH_NHP + 7) / 8;                                         
 constexpr int WH_STAGE = WH_DY_B + WH_XI * 1024;                                    // 39 936 B
 constexpr int WH_LDS = 2 * WH_STAGE;                                                // two per CU fit 160 KiB
 
-template <bool BIAS>
+// VAR (timing variants, HISEG_WGRAD_HWC_VAR): bit 0 MFMA rows at raised wave priority (s_setprio 1); bit 1 the second
+// workgroup of each CU (dispatch order) starts half a pixel tile late, so the two workgroups sharing each SIMD reach
+// their barriers out of phase
+template <bool BIAS, int VAR = 0>
 __global__ void __launch_bounds__(256, 2) conv_wgrad_hwc_kernel(WgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   const hiseg_conv2d_desc& d = a.d;
@@ -171,6 +174,7 @@ __global__ void __launch_bounds__(256, 2) conv_wgrad_hwc_kernel(WgradArgs a) {
         if (hr + 1 < WH_TR) ar[(hr + 1) & 3] = rdA(hr + 1);
       }
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr ((VAR & 1) != 0) __builtin_amdgcn_s_setprio(1);
       if (hr < WH_TR && do_bias)
         accb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar[hr & 3], ones, accb, 0, 0, 0);
 #pragma unroll
@@ -182,10 +186,14 @@ __global__ void __launch_bounds__(256, 2) conv_wgrad_hwc_kernel(WgradArgs a) {
             acc[ky][kx] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar[r & 3], br[cur][kx], acc[ky][kx], 0, 0, 0);
         }
       }
+      if constexpr ((VAR & 1) != 0) __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
 
+  if constexpr ((VAR & 2) != 0) {
+    if (orig >= 256 && orig < 512) __builtin_amdgcn_s_sleep(72);
+  }
   if (t0 < t1) {
     dma(t0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -258,8 +266,15 @@ int wgrad_hwc_try(const WgradArgs& a, hipStream_t s) {
     }
     hipLaunchKernelGGL(kern, dim3(nwg), dim3(256), WH_LDS, s, a);
   };
-  if (a.want_bias) launch(conv_wgrad_hwc_kernel<true>);
-  else launch(conv_wgrad_hwc_kernel<false>);
+  // default: the stagger (tools/wgrad_bench.py, same box, two alternating runs: 256 -> 256 0.819 vs 0.826 ms,
+  // 128 -> 128 @128x96 0.850 vs 0.861; the raised MFMA priority alone or with it: no gain; profiles/r5_wgrad_hwc.txt)
+  static const int var = [] { const char* e = getenv("HISEG_WGRAD_HWC_VAR"); return e ? atoi(e) : 2; }();
+  switch (var) {
+    case 1: a.want_bias ? launch(conv_wgrad_hwc_kernel<true, 1>) : launch(conv_wgrad_hwc_kernel<false, 1>); break;
+    case 2: a.want_bias ? launch(conv_wgrad_hwc_kernel<true, 2>) : launch(conv_wgrad_hwc_kernel<false, 2>); break;
+    case 3: a.want_bias ? launch(conv_wgrad_hwc_kernel<true, 3>) : launch(conv_wgrad_hwc_kernel<false, 3>); break;
+    default: a.want_bias ? launch(conv_wgrad_hwc_kernel<true>) : launch(conv_wgrad_hwc_kernel<false>);
+  }
   const int r = hiseg_check_launch("conv_wgrad_hwc");
   return r < 0 ? r : 1;
 }
