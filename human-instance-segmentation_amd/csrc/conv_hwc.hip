@@ -63,7 +63,9 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
   constexpr int TW = 16, HWD = TW + 2;
   constexpr int NHR = 18 * HWD;                       // halo rows (pixels) of a slice
   constexpr int PPW = ((NHR + 15) / 16 + NW - 1) / NW;   // halo pieces (16 rows, 1 KiB) per wave per slice
-  constexpr int PH = (PPW + 1) / 2;                   // pieces issued in kx block 0 (the rest in block 1)
+  // pieces issued in kx block 0 (the rest in block 1); DIAG ABL 512: all in block 0, ABL 1024: issued at row 0
+  constexpr int PH = (ABL & 512) ? PPW : (PPW + 1) / 2;
+  constexpr int PROW = (ABL & 1024) ? 0 : 3;
   constexpr int HB = PPW * NW * 1024;                 // bytes of one halo buffer
   constexpr int NPX = 256;                            // output pixels of the tile
   static_assert(NW == 4 || NW == 8, "configuration");
@@ -246,7 +248,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int r = 0; r < NR + 2; ++r) {
-      if (r == 3) {
+      if (r == PROW) {
         __builtin_amdgcn_s_setprio(0);
         pieces();
         __builtin_amdgcn_s_setprio(1);
@@ -504,7 +506,7 @@ int conv_hwc_stats_tiles(const ConvArgs& a) {
 int conv_hwc_try(const ConvArgs& a, hipStream_t s, int variant) {
   const hiseg_conv2d_desc& d = a.d;
 #ifdef HISEG_DIAG
-  if (variant >= 150 && variant < 279) {   // timing ablations of variant 104 (res + ReLU only; output buffer as
+  if (variant >= 150 && variant < 1700) {   // timing ablations of variant 104 (res + ReLU only; output buffer as
                                           // scratch: the ABL 32 store writes one float per thread and MFMA row)
     if (d.weight_frag == nullptr || !d.residual || d.act != HISEG_ACT_RELU || d.a_up != 1 || d.Cout % 128) return 0;
     int r;
@@ -520,6 +522,9 @@ int conv_hwc_try(const ConvArgs& a, hipStream_t s, int variant) {
       case 47: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 47>(a, s); break;
       case 64: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 64>(a, s); break;
       case 128: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 128>(a, s); break;
+      case 512: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 512>(a, s); break;
+      case 1024: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 1024>(a, s); break;
+      case 1536: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 1536>(a, s); break;
       default: return 0;
     }
     return r < 0 ? r : 1;

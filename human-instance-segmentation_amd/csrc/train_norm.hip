@@ -254,40 +254,38 @@ __global__ void __launch_bounds__(256) bn_stats_vec_kernel(const void* z, long l
 }
 
 // Split groups of a large split count (the conv epilogue's fused statistics: one split per (pixel tile, wave), 12 288
-// for a 256-ROI 64x48 layer): one block per (64 channels, KPRE consecutive splits), 4 rows x 64 channel lanes, each
-// row merging every 4th split of the group (Chan, double; coalesced loads across the channel lanes), the 4 rows
-// tree-merged in a fixed order; the group's result overwrites its own first split row (read by this block only), so
-// bn_finalize_par_kernel merges S / KPRE rows at a stride of KPRE rows.  One block per channel reading S strided rows
-// was 85 us per 256-channel layer on 12 288 splits.
+// for a 256-ROI 64x48 layer): one block per (64 channels, KPRE consecutive splits), 4 rows x 64 channel lanes
+// (coalesced loads across the lanes).  Row r sums every 4th split of the group as (n, sum n mean, sum M2 + n mean^2)
+// in double -- no division in the loop -- and the 4 rows' sums are added in a fixed order; the group's (n, mean, M2)
+// overwrites its own first split row (read by this block only), so bn_finalize_par_kernel merges S / KPRE rows at a
+// stride of KPRE rows.  (One block per channel reading S strided rows: 85 us per 256-channel layer on 12 288 splits;
+// this kernel with a Chan merge per split: 17 us.)
 constexpr int KPRE = 64;
 __global__ void __launch_bounds__(256) bn_premerge_kernel(float* partial, int S, int C) {
-  __shared__ double sn[4][64], sm[4][64], sq[4][64];
+  __shared__ double sn[4][64], s1[4][64], s2[4][64];
   const int t = threadIdx.x, l = t & 63, r = t >> 6;
   const int c = blockIdx.x * 64 + l;
   const int s0 = blockIdx.y * KPRE;
-  double n = 0, mean = 0, m2 = 0;
+  double n = 0, a = 0, b = 0;
   if (c < C) {
-    for (int i = r; i < KPRE && s0 + i < S; i += 4) {
+#pragma unroll 4
+    for (int i = r; i < KPRE; i += 4) {
+      if (s0 + i >= S) break;
       const float* p = partial + (long long)(s0 + i) * 3 * C;
-      const double nb = p[c];
-      if (nb == 0) continue;
-      const double d = (double)p[C + c] - mean, nt = n + nb;
-      mean += d * nb / nt;
-      m2 += (double)p[2 * C + c] + d * d * n * nb / nt;
-      n = nt;
+      const double ni = p[c], mi = p[C + c], qi = p[2 * C + c];
+      n += ni;
+      a = fma(ni, mi, a);
+      b += qi + ni * mi * mi;
     }
   }
-  sn[r][l] = n; sm[r][l] = mean; sq[r][l] = m2;
+  sn[r][l] = n; s1[r][l] = a; s2[r][l] = b;
   __syncthreads();
   if (r == 0 && c < C) {
-    for (int k = 1; k < 4; ++k) {
-      const double nb = sn[k][l];
-      if (nb == 0) continue;
-      const double nt = n + nb, d = sm[k][l] - mean;
-      mean += d * nb / nt;
-      m2 += sq[k][l] + d * d * n * nb / nt;
-      n = nt;
-    }
+    n = (sn[0][l] + sn[1][l]) + (sn[2][l] + sn[3][l]);
+    a = (s1[0][l] + s1[1][l]) + (s1[2][l] + s1[3][l]);
+    b = (s2[0][l] + s2[1][l]) + (s2[2][l] + s2[3][l]);
+    const double mean = n > 0 ? a / n : 0.0;
+    const double m2 = n > 0 ? fmax(b - a * mean, 0.0) : 0.0;
     float* o = partial + (long long)s0 * 3 * C;
     o[c] = (float)n;
     o[C + c] = (float)mean;

@@ -37,6 +37,12 @@ SHAPES = {
     "dec16_3x3_480x640": (32, 16, 0, 16, 480, 640, 3, False),
     "dec32_3x3_240x320": (32, 32, 0, 32, 240, 320, 3, False),
     "c16to96_1x1_240x320": (32, 16, 0, 96, 240, 320, 1, False),
+    # the distillation teacher's (B7, 4 x 640 x 640) MBConv expansions
+    "b7exp_48to288_1x1_160x160": (4, 48, 0, 288, 160, 160, 1, False),
+    "b7exp_80to480_1x1_80x80": (4, 80, 0, 480, 80, 80, 1, False),
+    "b7exp_160to960_1x1_40x40": (4, 160, 0, 960, 40, 40, 1, False),
+    "b7exp_224to1344_1x1_40x40": (4, 224, 0, 1344, 40, 40, 1, False),
+    "b7exp_384to2304_1x1_20x20": (4, 384, 0, 2304, 20, 20, 1, False),
     # smp decoder blocks 3/4 (nearest-x2 upsampled src A + skip), B0 at 480x640
     "dec3_up64+32to32_3x3_240x320": (32, 64, 32, 32, 240, 320, 3, False, 2),
     "dec4_up32to16_3x3_480x640": (32, 32, 0, 16, 480, 640, 3, False, 2),
