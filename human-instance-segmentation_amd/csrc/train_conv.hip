@@ -830,39 +830,50 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* ws, int 
 // 3x3 single-source layers: one item = (GEMM column j, 4 consecutive input channels) over all 9 taps, so an item's
 // 36 sums are 36 consecutive floats of the reference layout [Cout][Cin][3][3] -- nine 16-B stores -- where the
 // quad-of-K kernel above scatters 4-B stores 9 floats apart (the write traffic of the 768-channel 3x3 layers of the
-// B7 head: 137 us per reduce).  Four split groups per item and the fixed combine order as above.
+// B7 head: 137 us per reduce).  Sixteen split groups per item, combined in a fixed order.
+// NI items x NG split groups per block: 64 x 4, or 16 x 16 for more than 64 splits (round 5: 64 x 4 left the halo
+// weight-gradient tile's many-split planes latency-bound -- 64 -> 64 at 256 splits: 42 -> 17 us; with 32 splits the
+// 16 x 16 form was 3x slower, its combine left to 16 lanes per block); group g sums splits g, g + NG, ...
+template <int NI, int NG>
 __global__ void __launch_bounds__(256) wgrad_reduce_taps_kernel(const float* ws, int splits, hiseg_wgrad_map m,
                                                                 float* gw, float* gb, int acc) {
-  __shared__ float4 red[4][9][64];
-  const int ql = threadIdx.x & 63, sg = threadIdx.x >> 6;
+  __shared__ float4 red[NG][9][NI];
+  __shared__ float redb[NG][NI];
+  const int il = threadIdx.x % NI, sg = threadIdx.x / NI;
   const int Cin = m.ca, nc4 = Cin >> 2;
-  const long long idx = (long long)blockIdx.x * 64 + ql;
+  const long long idx = (long long)blockIdx.x * NI + il;
   const bool live = idx < (long long)m.Cout * nc4;
   const int j = live ? (int)(idx / nc4) : 0;
   const int ci0 = live ? 4 * (int)(idx - (long long)j * nc4) : 0;
   const long long plane = (long long)m.Cg * m.Kg;
   const float* src = ws + (long long)j * m.Kg + ci0;
+  const bool bias = m.want_bias && gb && ci0 == 0;
   float4 t9[9];
 #pragma unroll
   for (int t = 0; t < 9; ++t) t9[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+  float tb = 0.f;
   if (live) {
-    for (int sp = sg; sp < splits; sp += 4) {
+    for (int sp = sg; sp < splits; sp += NG) {
       float4 a[9];
 #pragma unroll
       for (int t = 0; t < 9; ++t) a[t] = *reinterpret_cast<const float4*>(src + sp * plane + t * Cin);
+      if (bias) tb += src[sp * plane + 9 * Cin];
 #pragma unroll
       for (int t = 0; t < 9; ++t) { t9[t].x += a[t].x; t9[t].y += a[t].y; t9[t].z += a[t].z; t9[t].w += a[t].w; }
     }
   }
 #pragma unroll
-  for (int t = 0; t < 9; ++t) red[sg][t][ql] = t9[t];
+  for (int t = 0; t < 9; ++t) red[sg][t][il] = t9[t];
+  redb[sg][il] = tb;
   __syncthreads();
   if (sg != 0 || !live) return;
   auto add4 = [](float4 x, float4 y) { return make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w); };
   float o[36];
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
-    const float4 v = add4(add4(red[0][t][ql], red[1][t][ql]), add4(red[2][t][ql], red[3][t][ql]));
+    float4 v = red[0][t][il];
+#pragma unroll
+    for (int g = 1; g < NG; ++g) v = add4(v, red[g][t][il]);
     o[t] = v.x; o[9 + t] = v.y; o[18 + t] = v.z; o[27 + t] = v.w;   // [channel][tap]
   }
   float4* dst = reinterpret_cast<float4*>(gw + ((long long)j * Cin + ci0) * 9);
@@ -872,9 +883,10 @@ __global__ void __launch_bounds__(256) wgrad_reduce_taps_kernel(const float* ws,
     if (acc) v = add4(dst[q], v);
     dst[q] = v;
   }
-  if (m.want_bias && gb && ci0 == 0) {   // the GEMM-bias column (k = 9 Cin), splits in order
-    float b = 0.f;
-    for (int sp = 0; sp < splits; ++sp) b += ws[sp * plane + (long long)j * m.Kg + 9 * Cin];
+  if (bias) {   // the GEMM-bias column (k = 9 Cin), the groups in order
+    float b = redb[0][il];
+#pragma unroll
+    for (int g = 1; g < NG; ++g) b += redb[g][il];
     gb[j] = acc ? gb[j] + b : b;
   }
 }
@@ -889,8 +901,12 @@ extern "C" int hiseg_conv2d_wgrad_reduce(const float* ws, int splits, const hise
   const bool taps_ok = !(te && atoi(te) == 0);
   if (taps_ok && !m.convT && m.KH == 3 && m.KW == 3 && m.cb == 0 && m.ca == m.ca_real && m.ca % 4 == 0 && al16(gw)) {
     const long long items = (long long)m.Cout * (m.ca / 4);
-    hipLaunchKernelGGL(wgrad_reduce_taps_kernel, dim3((unsigned)((items + 63) / 64)), dim3(256), 0,
-                       (hipStream_t)stream, ws, splits, m, gw, gb, accumulate);
+    if (splits > 64)
+      hipLaunchKernelGGL((wgrad_reduce_taps_kernel<16, 16>), dim3((unsigned)((items + 15) / 16)), dim3(256), 0,
+                         (hipStream_t)stream, ws, splits, m, gw, gb, accumulate);
+    else
+      hipLaunchKernelGGL((wgrad_reduce_taps_kernel<64, 4>), dim3((unsigned)((items + 63) / 64)), dim3(256), 0,
+                         (hipStream_t)stream, ws, splits, m, gw, gb, accumulate);
     return hiseg_check_launch("wgrad_reduce");
   }
   const long long n = (long long)m.Cout * ((m.KH * m.KW * (m.ca + m.cb) + (m.want_bias ? 1 : 0) + 3) / 4);
