@@ -77,8 +77,12 @@ __global__ void __launch_bounds__(256, 2) conv_wgrad_hwc_kernel(WgradArgs a) {
   const int t0 = split * tps, t1 = t0 + tps < NT ? t0 + tps : NT;
 
   const unsigned OOB = 0x80000000u;
+  // the workgroup's 64 input channels lie in one source (Ca and Cb multiples of 64): source A, or the concat's B
+  const bool srcb = ci0 >= d.Ca;
   const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<void*>(d.srcA), (short)0, d.N * d.H * d.W * d.a_cstride * 2, 0x00020000);
+      const_cast<void*>(srcb ? d.srcB : d.srcA), (short)0, d.N * d.H * d.W * (srcb ? d.b_cstride : d.a_cstride) * 2,
+      0x00020000);
+  const int x_cs = srcb ? d.b_cstride : d.a_cstride, x_c0 = srcb ? d.b_coff + ci0 - d.Ca : d.a_coff + ci0;
   const __amdgpu_buffer_rsrc_t rY = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(a.dy), (short)0, (a.M * a.dy_cs + a.dy_coff + d.Cout) * 2, 0x00020000);
   const unsigned lds_base = (unsigned)(uintptr_t)(wh_lds_void_t*)smem;
@@ -112,7 +116,7 @@ __global__ void __launch_bounds__(256, 2) conv_wgrad_hwc_kernel(WgradArgs a) {
         const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
         const bool ok = hp < WH_NHP && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
         const unsigned off =
-            ok ? (unsigned)((((n * d.H + iy) * d.W + ix) * d.a_cstride + d.a_coff + ci0 + 8 * c) * 2) : OOB;
+            ok ? (unsigned)((((n * d.H + iy) * d.W + ix) * x_cs + x_c0 + 8 * c) * 2) : OOB;
         wh_dma16(rX, sbase + (unsigned)(WH_DY_B + i * 1024), off);
       }
     }
@@ -224,15 +228,19 @@ __global__ void __launch_bounds__(256, 2) conv_wgrad_hwc_kernel(WgradArgs a) {
 }
 
 // The layer rules (shapes only, so the choice never depends on where the allocator put the operands): bf16, 3x3,
-// stride 1, pad 1, one source at full resolution, Cin and Cout multiples of 64, 8-channel-aligned views, every buffer
-// resource under 2^31 bytes.
+// stride 1, pad 1, sources at full resolution (one, or a concat A ++ B: each Cin tile reads one source through a
+// resource of its own), Ca, Cb and Cout multiples of 64, 8-channel-aligned views, every buffer resource under 2^31
+// bytes.
 bool wgrad_hwc_shape_ok(const hiseg_conv2d_desc* d) {
   const char* e = getenv("HISEG_WGRAD_HWC");
   if (e && atoi(e) == 0) return false;
-  if (d->dtype != HISEG_BF16 || d->convT || d->Cb != 0 || d->a_up != 1) return false;
+  if (d->dtype != HISEG_BF16 || d->convT || d->a_up != 1) return false;
   if (d->KH != 3 || d->KW != 3 || d->stride != 1 || d->pad != 1 || d->Ho != d->H || d->Wo != d->W) return false;
-  if (d->Ca % 64 || d->Cout % 64 || d->a_cstride % 8 || d->a_coff % 8) return false;
+  if (d->Ca % 64 || d->Cb % 64 || d->Cout % 64 || d->a_cstride % 8 || d->a_coff % 8) return false;
   if ((long long)d->N * d->H * d->W * d->a_cstride * 2 >= 0x7fffffffll) return false;
+  if (d->Cb && (d->srcB == nullptr || d->b_cstride % 8 || d->b_coff % 8 ||
+                (long long)d->N * d->H * d->W * d->b_cstride * 2 >= 0x7fffffffll))
+    return false;
   return true;
 }
 
@@ -254,7 +262,7 @@ int wgrad_hwc_splits(const hiseg_conv2d_desc* d) {
 int wgrad_hwc_try(const WgradArgs& a, hipStream_t s) {
   const hiseg_conv2d_desc& d = a.d;
   if (!wgrad_hwc_shape_ok(&d)) return 0;
-  if (a.dy_cs % 8 || a.dy_coff % 8 || a.Cin != d.Ca) return 0;
+  if (a.dy_cs % 8 || a.dy_coff % 8 || a.Cin != d.Ca + d.Cb) return 0;
   if (((long long)a.M * a.dy_cs + a.dy_coff + d.Cout) * 2 >= 0x7fffffffll) return 0;
   if (a.Kg < a.Ktot + (a.want_bias ? 1 : 0)) return 0;
   const int nwg = (d.Cout / 64) * (a.Cin / 64) * a.splits;

@@ -84,5 +84,6 @@ def test_no_leg_runs_the_generic_weight_gradient_kernel_with_far_sources():
         assert p["generic_bf16"] == 0, f"{leg}: generic weight-gradient kernel ran: {p}"
         assert p["wide"] + p["transposed_read"] + p["halo"] > 0, f"{leg}: no weight gradient recorded: {p}"
         assert v["loss"] == v["loss"], f"{leg}: NaN loss"
-    # the forced far-apart path was exercised (two-source layers exist in every leg)
-    assert all(v["placement"][1] > 0 for v in res.values()), {k: v["placement"] for k, v in res.items()}
+    # the forced far-apart path was exercised (round 5: the halo tile takes the 64-multiple concat layers with one
+    # resource per source and records no placement; the rest -- upsampled or narrow concats -- still meet it)
+    assert sum(v["placement"][1] for v in res.values()) > 0, {k: v["placement"] for k, v in res.items()}

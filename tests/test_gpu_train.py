@@ -167,12 +167,14 @@ def test_wgrad_wide_matches_f64_of_bf16_operands(case, reduce_taps, monkeypatch)
         assert rel(conv.bias.grad, br.grad) < 1e-4
 
 
-HWC_WGRAD_CASES = [  # (cin, cout, H, W, N, bias): wgrad_hwc.hip's 64 x 64 x 9-tap tiles over 8 x 16-pixel tiles
+HWC_WGRAD_CASES = [  # (cin, cout, H, W, N, bias[, split]): wgrad_hwc.hip's 64 x 64 x 9-tap tiles over 8 x 16 pixels
     (256, 256, 20, 30, 3, True),     # ragged pixel tiles both ways, bias column
     (64, 64, 16, 12, 2, False),
     (128, 256, 9, 7, 2, True),       # images smaller than one pixel tile
     (128, 128, 33, 40, 2, False),
     (192, 64, 64, 48, 4, True),      # the ROI head's grid, many splits
+    (128, 64, 24, 20, 2, True, (64, 64)),     # decoder concat: up ++ skip, one resource per source
+    (192, 128, 16, 18, 2, False, (128, 64)),
 ]
 
 
@@ -184,13 +186,18 @@ def test_wgrad_hwc_matches_f64_of_bf16_operands(case):
     the f32 accumulation), the bias column included; and the halo path actually taken."""
     from hiseg import _lib as L
     from hiseg.ops import Act
-    cin, cout, H, W, N, bias = case
+    cin, cout, H, W, N, bias = case[:6]
+    split = case[6] if len(case) > 6 else None
     dt = torch.bfloat16
     conv = nn.Conv2d(cin, cout, 3, padding=1, bias=bias)
     filler.fill_module(conv, seed=19)
     TE, S, T = engine(_Holder(c=conv), dt)
     x = torch.from_numpy(filler.normal(13, (N, cin, H, W))).to(DEV)
-    y = TE.conv_plain(T, conv, TE.ACT_NONE, Act.from_nchw(x, dt), None)
+    if split is None:
+        y = TE.conv_plain(T, conv, TE.ACT_NONE, Act.from_nchw(x, dt), None)
+    else:
+        y = TE.conv_plain(T, conv, TE.ACT_NONE, Act.from_nchw(x[:, :split[0]], dt), Act.from_nchw(x[:, split[0]:], dt),
+                          split=split)
     g = torch.from_numpy(filler.normal(14, (N, cout, H, W))).to(DEV)
     inject(T, y, g, dt)
     S.flat.prepare_backward()
@@ -1099,7 +1106,7 @@ def test_two_source_results_do_not_depend_on_operand_placement(case):
             res.append((yy.t.clone(), y.t.clone(), conv.weight.grad.clone()))
         paths = L.wgrad_path_stats()
         assert paths["generic_bf16"] == 0, f"generic weight-gradient kernel ran (far={far}): {paths}"
-        assert paths["wide"] + paths["transposed_read"] == 1, paths
+        assert paths["wide"] + paths["transposed_read"] + paths["halo"] == 1, paths
     for a, b in zip(*res):
         assert torch.equal(a, b)
 
