@@ -776,7 +776,11 @@ def call_profile(step, leg=None):
                 c["bytes"] += nb
                 c["bytes_ms"] += ms
     conv_ms = sum(g[1] for g in groups.values())
+    calls_ms = sum(e0.elapsed_time(e1) for _, _, _, _, _, e0, e1 in rec)
     out = {"step_ms_probed": round(step_ms, 3),
+           # GPU time inside the C-ABI calls: the eager step minus its launch gaps between calls (a replayed graph
+           # has almost none), the figure to hold against the graphed ms_per_step
+           "calls_ms_sum": round(calls_ms, 3),
            # > step_ms: the GPU was still working when the host finished enqueueing, so no interval held host time
            "host_lead_left_ms": round(lead_left_ms, 3),
            "wgrad_paths": paths,

@@ -18,7 +18,7 @@ CLASSES = [   # (class name as in bench.call_profile, kernel-name pattern); firs
     ("conv weight gradient", r"wgrad"),
     ("BatchNorm (train)", r"\bbn_|bn_stats|bn_apply|bn_bwd|bn_finalize"),
     ("depthwise conv (+ SE pool)", r"dwconv"),
-    ("conv forward + data gradient", r"conv_(hwr|hwt|hw|fast|wide|igemm|pw|small|rows|splitk_reduce)"),
+    ("conv forward + data gradient", r"conv_(hwc|hwr|hwt|hw|fast|wide|igemm|pw|small|rows|splitk_reduce)"),
 ]
 
 
