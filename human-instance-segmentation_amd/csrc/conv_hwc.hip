@@ -57,23 +57,28 @@ __device__ __forceinline__ void hc_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned l
 // the layout hiseg_bn_finalize_n merges -- the separate statistics pass (one read of z) is gone.  (Measured first
 // forms: statistics from the accumulators spilled 65 registers in the K loop, conv forward +15 %; a Welford update per
 // pixel plus a cross-wave LDS merge and barrier, conv forward +6 %.)
-template <int ACT, bool RES, int NW, bool UP = false, int ABL = 0, bool RP = false, bool ST = false>
+// TWB (pixel blocks per workgroup): 1 -- the workgroup's NW waves are NW 32-Cout groups over one 16 x 16 pixel block
+// (BCO = 32 NW); 2 -- NW / 2 Cout groups over two 16 x 16 blocks side by side (a 16 x 32 tile, one 18 x 34 halo per
+// slice; BCO = 16 NW: the 64-Cout layers).  A wave's tile and loop are the same either way.
+template <int ACT, bool RES, int NW, bool UP = false, int ABL = 0, bool RP = false, bool ST = false, int TWB = 1>
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(ConvArgs a) {
-  constexpr int BCO = 32 * NW, TM = 2, NR = 16;    // wave tile: 32 Cout x (16 rows x 16 columns)
-  constexpr int TW = 16, HWD = TW + 2;
+  constexpr int NCG = NW / TWB;                      // Cout groups of 32
+  constexpr int BCO = 32 * NCG, TM = 2, NR = 16;    // wave tile: 32 Cout x (16 rows x 16 columns)
+  constexpr int TW = 16 * TWB, HWD = TW + 2;
   constexpr int NHR = 18 * HWD;                       // halo rows (pixels) of a slice
   constexpr int PPW = ((NHR + 15) / 16 + NW - 1) / NW;   // halo pieces (16 rows, 1 KiB) per wave per slice
   // pieces issued in kx block 0 (the rest in block 1); DIAG ABL 512: all in block 0, ABL 1024: issued at row 0
   constexpr int PH = (ABL & 512) ? PPW : (PPW + 1) / 2;
   constexpr int PROW = (ABL & 1024) ? 0 : 3;
   constexpr int HB = PPW * NW * 1024;                 // bytes of one halo buffer
-  constexpr int NPX = 256;                            // output pixels of the tile
-  static_assert(NW == 4 || NW == 8, "configuration");
+  constexpr int NPX = 256 * TWB;                      // output pixels of the tile
+  static_assert((NW == 4 || NW == 8) && (TWB == 1 || (TWB == 2 && NW == 4 && !RP)), "configuration");
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   const hiseg_conv2d_desc& d = a.d;
   const int t = threadIdx.x;
   const int lane = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);   // the wave's 32-Cout group
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wc = w % NCG, pb = w / NCG;   // the wave's 32-Cout group and 16-column pixel block
 
   // ---- XCD-major bijective remap; Cout tiles fastest (the tiles of one pixel block share its halo in L2)
   const int nco = d.Cout_pad / BCO;
@@ -103,7 +108,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
 
   // ---- A fragments (hiseg.ops.frag_pack): (16-row Cout tile ct, slice sl, tap) at
   // ((((ct * ncb + sl / 2) * 9 + tap) * 2 + sl % 2) * 64 + lane) * 16 B; the wave's two tiles are ct0, ct0 + 1
-  const unsigned a_ct = (unsigned)((co0 + w * 32) >> 4) * (unsigned)ncb * 18u * 1024u;
+  const unsigned a_ct = (unsigned)((co0 + wc * 32) >> 4) * (unsigned)ncb * 18u * 1024u;
   const unsigned a_ct_step = (unsigned)ncb * 18u * 1024u;
   // the weights of taps (ky, kx), ky = 0..2, of slice sl: 6 loads (the wave-uniform part in the SGPR offset)
   auto load_blk = [&](hc_u4 (&af)[3][TM], int sl, int kx) __attribute__((always_inline)) {
@@ -153,7 +158,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
   const char* lds_c = reinterpret_cast<const char*>(smem);
   // B fragment of halo row r at column shift kx: pixels (r, kx + lane % 16), channels 8 (lane / 16) .. + 7
   auto rdB = [&](int ln, int boff, int kx, int r) __attribute__((always_inline)) -> hc_u4 {
-    const int hx = (ln & 15) + kx;
+    const int hx = (ln & 15) + kx + 16 * pb;
     return *reinterpret_cast<const hc_u4*>(lds_c + boff + (r * HWD + hx) * 64 +
                                            (((ln >> 4) ^ (((hx >> 2) & 1) << 1)) << 4));
   };
@@ -319,7 +324,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
   floatx4 sc[TM], sh[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int cl = w * 32 + i * 16 + (lane >> 4) * 4;
+    const int cl = wc * 32 + i * 16 + (lane >> 4) * 4;
     const int cc = co0 + cl < d.Cout ? co0 + cl : 0;
     sc[i] = *reinterpret_cast<const floatx4*>(d.scale + cc);
     sh[i] = *reinterpret_cast<const floatx4*>(d.shift + cc);
@@ -331,8 +336,8 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = J0; j < J1; ++j) {
-        const int cl = w * 32 + i * 16 + (lane >> 4) * 4;
-        const int r = j * TW + (lane & 15);
+        const int cl = wc * 32 + i * 16 + (lane >> 4) * 4;
+        const int r = j * TW + 16 * pb + (lane & 15);
         char* q = tile + r * EROWB + ((((cl >> 3) ^ (r & SWM)) << 4) | ((cl & 4) << 1));
         const floatx4 ac = acc[i][j];
         float v[4];
@@ -368,6 +373,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
   int sn = 0;
   if constexpr (ST) {
     static_assert(!RES && ACT == HISEG_ACT_NONE && NW == 4, "fused statistics: the conv feeding a BatchNorm");
+    static_assert(CPR == 16 || CPR == 8, "fused statistics: a wave's threads of one chunk are lanes CPR apart");
 #pragma unroll
     for (int e = 0; e < 8; ++e) sk[e] = s1[e] = s2[e] = 0.f;
   }
@@ -402,7 +408,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
       q2[e] = sn ? fmaxf(s2[e] - s1[e] * s1[e] / nn, 0.f) : 0.f;
     }
 #pragma unroll
-    for (int m = 16; m < 64; m <<= 1) {   // lanes ^ 16, ^ 32: the wave's 4 threads of the chunk
+    for (int m = CPR; m < 64; m <<= 1) {   // lanes ^ CPR .. ^ 32: the wave's threads of the chunk
       const float nb = __shfl_xor(nn, m, 64);
       const float nt = nn + nb;
       const float fb = nt > 0.f ? nb / nt : 0.f, fab = nt > 0.f ? nn * nb / nt : 0.f;
@@ -415,7 +421,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
       }
       nn = nt;
     }
-    if (lane < 16) {
+    if (lane < CPR) {
       const long long C = d.Cout;
       float* part = a.d.stats_partial + ((long long)((n * nty + ty) * ntx + tx) * NW + w) * 3 * C;
 #pragma unroll
@@ -429,16 +435,16 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
   }
 }
 
-template <int ACT, bool RES, int NW, bool UP = false, int ABL = 0, bool RP = false, bool ST = false>
+template <int ACT, bool RES, int NW, bool UP = false, int ABL = 0, bool RP = false, bool ST = false, int TWB = 1>
 static int launch_hwc(const ConvArgs& a, hipStream_t s) {
   const hiseg_conv2d_desc& d = a.d;
-  constexpr int BCO = 32 * NW;
-  constexpr int PPW = ((18 * 18 + 15) / 16 + NW - 1) / NW;
-  constexpr size_t halo2 = (size_t)2 * PPW * NW * 1024, epi = (size_t)256 * BCO * 2;
-  const int tiles = d.N * ((d.H + 15) / 16) * ((d.W + 15) / 16);
+  constexpr int BCO = 32 * NW / TWB, TW = 16 * TWB;
+  constexpr int PPW = ((18 * (TW + 2) + 15) / 16 + NW - 1) / NW;
+  constexpr size_t halo2 = (size_t)2 * PPW * NW * 1024, epi = (size_t)256 * TWB * BCO * 2;
+  const int tiles = d.N * ((d.H + 15) / 16) * ((d.W + TW - 1) / TW);
   const int nco = d.Cout_pad / BCO;
   const size_t lds = RP ? (size_t)80 * 1024 : (halo2 > epi ? halo2 : epi);
-  auto kern = conv_hwc_kernel<ACT, RES, NW, UP, ABL, RP, ST>;
+  auto kern = conv_hwc_kernel<ACT, RES, NW, UP, ABL, RP, ST, TWB>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -448,21 +454,23 @@ static int launch_hwc(const ConvArgs& a, hipStream_t s) {
   return hiseg_check_launch("conv_hwc");
 }
 
-template <int NW, bool RP = false>
+template <int NW, bool RP = false, int TWB = 1>
 static int launch_hwc_nw(const ConvArgs& a, hipStream_t s) {
   const hiseg_conv2d_desc& d = a.d;
-  if (d.a_up == 2) return launch_hwc<HISEG_ACT_RELU, false, NW, true>(a, s);   // (conv_hwc_try checked the form)
+  if (d.a_up == 2)   // (conv_hwc_try checked the form)
+    return launch_hwc<HISEG_ACT_RELU, false, NW, true, 0, false, false, TWB>(a, s);
   const bool res = d.residual != nullptr, relu = d.act == HISEG_ACT_RELU;
-  return res ? (relu ? launch_hwc<HISEG_ACT_RELU, true, NW, false, 0, RP>(a, s)
-                     : launch_hwc<HISEG_ACT_NONE, true, NW, false, 0, RP>(a, s))
-             : (relu ? launch_hwc<HISEG_ACT_RELU, false, NW>(a, s) : launch_hwc<HISEG_ACT_NONE, false, NW>(a, s));
+  return res ? (relu ? launch_hwc<HISEG_ACT_RELU, true, NW, false, 0, RP, false, TWB>(a, s)
+                     : launch_hwc<HISEG_ACT_NONE, true, NW, false, 0, RP, false, TWB>(a, s))
+             : (relu ? launch_hwc<HISEG_ACT_RELU, false, NW, false, 0, false, false, TWB>(a, s)
+                     : launch_hwc<HISEG_ACT_NONE, false, NW, false, 0, false, false, TWB>(a, s));
 }
 
 // Whether variant `variant` takes the layer (the layer rules are conv_hwr_try's: the same operands, weight fragments and
-// halo; with d.stats_partial the fused-statistics form: variant 104, no activation, no residual).
+// halo; with d.stats_partial the fused-statistics form: variant 104 / 107, no activation, no residual).
 static bool conv_hwc_applies(const ConvArgs& a, int variant) {
   const hiseg_conv2d_desc& d = a.d;
-  if ((variant < 104 || variant > 106) || d.weight_frag == nullptr) return false;
+  if ((variant < 104 || variant > 107) || d.weight_frag == nullptr) return false;
   if (d.dtype != HISEG_BF16 || d.out_dtype != HISEG_BF16) return false;
   if ((d.a_up != 1 && d.a_up != 2) || d.in_scale != nullptr || d.convT || d.mul != nullptr || d.out2 != nullptr)
     return false;
@@ -472,7 +480,8 @@ static bool conv_hwc_applies(const ConvArgs& a, int variant) {
     return false;
   if ((d.a_cstride | d.a_coff) & 7) return false;
   if (d.Cb && (d.srcB == nullptr || ((d.b_cstride | d.b_coff) & 7))) return false;
-  if ((d.Cout & (variant == 105 ? 255 : 127)) || d.Cout_pad != d.Cout || ((d.o_cstride | d.o_coff) & 7) ||
+  if ((d.Cout & (variant == 105 ? 255 : variant == 107 ? 63 : 127)) || d.Cout_pad != d.Cout ||
+      ((d.o_cstride | d.o_coff) & 7) ||
       (d.residual && ((d.r_cstride | d.r_coff) & 7)))
     return false;
   if ((((uintptr_t)d.scale | (uintptr_t)d.shift | (uintptr_t)d.out | (uintptr_t)d.residual |
@@ -486,7 +495,7 @@ static bool conv_hwc_applies(const ConvArgs& a, int variant) {
   if ((long long)d.N * d.H * d.W >= (1ll << 29)) return false;
   // upsampled src A: the smp decoder conv1 form only (ReLU, or no activation when the conv feeds a train-mode BN)
   if (d.a_up == 2 && (d.residual || d.act != (d.stats_partial ? HISEG_ACT_NONE : HISEG_ACT_RELU))) return false;
-  if (d.stats_partial && (variant != 104 || d.residual || d.act != HISEG_ACT_NONE)) return false;
+  if (d.stats_partial && ((variant != 104 && variant != 107) || d.residual || d.act != HISEG_ACT_NONE)) return false;
   return true;
 }
 
@@ -495,13 +504,14 @@ int conv_hwc_stats_tiles(const ConvArgs& a) {
   ConvArgs b = a;
   float dummy;
   b.d.stats_partial = &dummy;
-  if (!conv_hwc_applies(b, 104)) return 0;
-  return a.d.N * ((a.d.H + 15) / 16) * ((a.d.W + 15) / 16) * 4;   // (pixel tile, wave) splits
+  const int tw = conv_hwc_applies(b, 104) ? 16 : conv_hwc_applies(b, 107) ? 32 : 0;
+  if (tw == 0) return 0;
+  return a.d.N * ((a.d.H + 15) / 16) * ((a.d.W + tw - 1) / tw) * 4;   // (pixel tile, wave) splits
 }
 
 // 1 = launched, 0 = the layer does not qualify (caller falls back), <0 on error.  Variant 104: 128-Cout workgroups
 // (four waves, two per CU); 105: 256-Cout workgroups (eight waves, one per CU; Cout a multiple of 256); 106: 104 with
-// the residual prefetch (RP).  The layer
+// the residual prefetch (RP); 107: 64-Cout workgroups over 16 x 32-pixel tiles (TWB 2; Cout a multiple of 64).  The layer
 // rules are conv_hwr_try's (the same operands, weight fragments and halo).
 int conv_hwc_try(const ConvArgs& a, hipStream_t s, int variant) {
   const hiseg_conv2d_desc& d = a.d;
@@ -531,12 +541,18 @@ int conv_hwc_try(const ConvArgs& a, hipStream_t s, int variant) {
   }
 #endif
   if (!conv_hwc_applies(a, variant)) return 0;
-  if (d.stats_partial) {   // the fused-statistics epilogue (variant 104 only; conv_hwc_applies checked the form)
-    const int r = d.a_up == 2 ? launch_hwc<HISEG_ACT_NONE, false, 4, true, 0, false, true>(a, s)
-                              : launch_hwc<HISEG_ACT_NONE, false, 4, false, 0, false, true>(a, s);
+  if (d.stats_partial) {   // the fused-statistics epilogue (variants 104 / 107; conv_hwc_applies checked the form)
+    int r;
+    if (variant == 107)
+      r = d.a_up == 2 ? launch_hwc<HISEG_ACT_NONE, false, 4, true, 0, false, true, 2>(a, s)
+                      : launch_hwc<HISEG_ACT_NONE, false, 4, false, 0, false, true, 2>(a, s);
+    else
+      r = d.a_up == 2 ? launch_hwc<HISEG_ACT_NONE, false, 4, true, 0, false, true>(a, s)
+                      : launch_hwc<HISEG_ACT_NONE, false, 4, false, 0, false, true>(a, s);
     return r < 0 ? r : 1;
   }
-  const int r = variant == 105 ? launch_hwc_nw<8>(a, s)
+  const int r = variant == 107 ? launch_hwc_nw<4, false, 2>(a, s)
+              : variant == 105 ? launch_hwc_nw<8>(a, s)
               : variant == 106 ? launch_hwc_nw<4, true>(a, s)
                                : launch_hwc_nw<4>(a, s);
   return r < 0 ? r : 1;

@@ -521,10 +521,16 @@ extern "C" int hiseg_conv2d_fwd(const hiseg_conv2d_desc* d, hiseg_stream_t strea
 // The variants a release library accepts: the automatic choice, the generic kernel and every configuration
 // tests/test_gpu_parity.py checks bit for bit.  Timing-only, stamp and experimental kernels exist only in a
 // -DHISEG_DIAG build (Makefile DIAG=1).
+// HISEG_CONV_HWC64=0 (read per call; A/B timing): the 64-Cout layers on conv_hwr (variant 100) instead of conv_hwc 107
+static bool hwc64_mode() {
+  const char* e = getenv("HISEG_CONV_HWC64");
+  return !(e && atoi(e) == 0);
+}
+
 static bool release_variant(int v) {
   return v == -1 || v == 0 || (v >= 1 && v <= 8) || v == 50 || v == 51 || v == 52 || v == 54 || v == 58 ||
          (v >= 60 && v <= 69) || v == 70 || v == 71 || v == 72 || v == 74 || v == 80 || v == 82 || v == 84 || v == 86 ||
-         v == 88 || v == 89 || v == 90 || (v >= 92 && v <= 101) || v == 103 || (v >= 104 && v <= 106);
+         v == 88 || v == 89 || v == 90 || (v >= 92 && v <= 101) || v == 103 || (v >= 104 && v <= 107);
 }
 
 // Workspace bytes the automatic choice uses for this layer (split-K generic kernel), 0 when it needs none.
@@ -595,7 +601,8 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
   // BatchNorm statistics fused into the epilogue: only the halo kernel's fused-statistics form computes them, and no
   // fallback may silently skip them (the caller would finalize garbage)
   if (d->stats_partial) {
-    HISEG_REQUIRE(variant == 0 || variant == 104, HISEG_ERR_BAD_ARG, "conv2d: stats_partial with variant %d", variant);
+    HISEG_REQUIRE(variant == 0 || variant == 104 || variant == 107, HISEG_ERR_BAD_ARG,
+                  "conv2d: stats_partial with variant %d", variant);
     HISEG_REQUIRE(al16(d->out) && al16(d->scale) && al16(d->shift), HISEG_ERR_BAD_SHAPE, "conv2d: alignment");
     ConvArgs a;
     a.d = *d;
@@ -606,7 +613,7 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
     a.Ws = d->W / d->a_up;
     HISEG_REQUIRE(conv_hwc_stats_tiles(a) > 0, HISEG_ERR_BAD_ARG,
                   "conv2d: stats_partial set but the layer has no fused-statistics kernel (hiseg_conv2d_stats_tiles)");
-    const int r = conv_hwc_try(a, (hipStream_t)stream, 104);
+    const int r = conv_hwc_try(a, (hipStream_t)stream, d->Cout % 128 == 0 ? 104 : 107);
     HISEG_REQUIRE(r != 0, HISEG_ERR_BAD_ARG, "conv2d: the fused-statistics kernel declined the layer");
     return r < 0 ? r : HISEG_OK;
   }
@@ -698,7 +705,7 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
   } else if ((variant >= 92 && variant <= 97) || variant == 100 || variant == 101 || (variant >= 110 && variant < 142)) {
     const int r = conv_hwr_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
-  } else if ((variant >= 104 && variant <= 106) || (variant >= 150 && variant < 1700)) {
+  } else if ((variant >= 104 && variant <= 107) || (variant >= 150 && variant < 1700)) {
     const int r = conv_hwc_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
   } else if (variant == 103) {
@@ -772,8 +779,12 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
       const int r = conv_hwr_try(a, s, 97);
       if (r != 0) return r < 0 ? r : HISEG_OK;
     }
-    // 64-multiple Cout (the EnhancedUNet's 64-channel layers, the smp decoder's 64-channel block): the same kernel on
-    // 64-Cout x 16 x 32-pixel tiles (variant 100)
+    // 64-multiple Cout (the EnhancedUNet's 64-channel layers, the smp decoder's 64-channel block): conv_hwc on 64-Cout
+    // x 16 x 32-pixel tiles (variant 107, round 5), else conv_hwr's (variant 100)
+    if (v == 0 && !four_waves && halo && d->weight_frag != nullptr && d->Cout % 64 == 0 && hwc64_mode()) {
+      const int r = conv_hwc_try(a, s, 107);
+      if (r != 0) return r < 0 ? r : HISEG_OK;
+    }
     if (v == 0 && !four_waves && halo && d->weight_frag != nullptr && d->Cout % 64 == 0) {
       const int r = conv_hwr_try(a, s, 100);
       if (r != 0) return r < 0 ? r : HISEG_OK;

@@ -1152,6 +1152,56 @@ def test_conv_hwc_bit_identical_to_hwr(shape):
         assert torch.equal(outs[v], outs[97]), f"variant {v}"
 
 
+@pytest.mark.parametrize("shape", [(2, 64, 0, 64, 64, 48, True, True), (3, 64, 0, 64, 37, 21, False, False),
+                                   (2, 256, 0, 64, 33, 50, False, True), (2, 64, 64, 64, 32, 24, False, True),
+                                   (2, 128, 0, 192, 20, 30, True, True), (1, 64, 0, 64, 9, 7, True, True)])
+def test_conv_hwc64_bit_identical_to_hwr(shape):
+    """Variant 107 (round 5: conv_hwc on 64-Cout workgroups over 16 x 32-pixel tiles, two 16 x 16 pixel blocks side
+    by side sharing one 18 x 34 halo) equals conv_hwr's 64-Cout form (variant 100) bit for bit -- ragged tiles (also
+    images narrower than one block), residual / ReLU / none, two sources, Cout 64 / 192 -- and is the automatic choice
+    for 64-multiple Cout that is no 128-multiple.  Outputs NaN-prefilled."""
+    from hiseg import ops
+    N, Ca, Cb, Cout, H, W, res, relu = shape
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(39)
+    xa = ops.Act.from_nchw(torch.randn(N, Ca, H, W, device=DEV, generator=g), dt)
+    xb = ops.Act.from_nchw(torch.randn(N, Cb, H, W, device=DEV, generator=g), dt) if Cb else None
+    w = torch.randn(Cout, Ca + Cb, 3, 3, device=DEV, generator=g) / ((Ca + Cb) * 9) ** 0.5
+    p = ops.pack_conv(w, torch.randn(Cout, device=DEV, generator=g) * 0.1, None, int(relu), dt, DEV, pad=1,
+                      split=(Ca, Cb) if Cb else None)
+    assert p.weight_frag is not None
+    R = ops.Act.from_nchw(torch.randn(N, Cout, H, W, device=DEV, generator=g), dt) if res else None
+    outs = {}
+    for v in (100, 107, 0):
+        o = ops.Act.new(N, H, W, Cout, dt, torch.device(DEV))
+        o.t.fill_(float("nan"))
+        outs[v] = ops.conv2d(p, xa, xb, out=o, residual=R, variant=v).t.clone()
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[100].float()).all()
+    assert torch.equal(outs[107], outs[100]) and torch.equal(outs[0], outs[100])
+
+
+@pytest.mark.parametrize("shape", [(2, 128, 64, 64, 36, 40), (1, 64, 64, 64, 18, 34)])
+def test_conv_hwc64_upsampled_decoder_bit_identical(shape):
+    """The smp decoder's conv1 form at 64 output channels on variant 107 equals conv_hwr's 64-Cout form (100)."""
+    from hiseg import ops
+    N, Ca, Cb, Cout, H, W = shape
+    dt = torch.bfloat16
+    g = torch.Generator(device=DEV).manual_seed(47)
+    xa = ops.Act.from_nchw(torch.randn(N, Ca, H // 2, W // 2, device=DEV, generator=g), dt)
+    xb = ops.Act.from_nchw(torch.randn(N, Cb, H, W, device=DEV, generator=g), dt)
+    w = torch.randn(Cout, Ca + Cb, 3, 3, device=DEV, generator=g) / ((Ca + Cb) * 9) ** 0.5
+    p = ops.pack_conv(w, torch.randn(Cout, device=DEV, generator=g) * 0.1, None, 1, dt, DEV, pad=1, split=(Ca, Cb))
+    outs = {}
+    for v in (100, 107, 0):
+        o = ops.Act.new(N, H, W, Cout, dt, torch.device(DEV))
+        o.t.fill_(float("nan"))
+        outs[v] = ops.conv2d(p, xa, xb, out=o, a_up=2, variant=v).t.clone()
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[100].float()).all()
+    assert torch.equal(outs[107], outs[100]) and torch.equal(outs[0], outs[100])
+
+
 @pytest.mark.parametrize("shape", [(2, 320, 128, 256, 30, 40), (2, 256, 64, 128, 20, 24), (1, 128, 64, 128, 18, 34)])
 def test_conv_hwc_upsampled_decoder_bit_identical(shape):
     """The smp decoder's conv1 form (src A nearest-x2 upsampled, src B the encoder skip; ReLU, no residual) on

@@ -1112,7 +1112,8 @@ def test_two_source_results_do_not_depend_on_operand_placement(case):
 
 
 @pytest.mark.parametrize("case", [(256, 256, 3, 20, 30, 0), (128, 128, 2, 37, 21, 0), (128, 256, 2, 16, 16, 0),
-                                  (320, 256, 2, 16, 20, 64), (128, 128, 24, 40, 40, 0)])
+                                  (320, 256, 2, 16, 20, 64), (128, 128, 24, 40, 40, 0), (64, 64, 2, 37, 45, 0),
+                                  (128, 64, 2, 18, 34, 64)])
 def test_fused_bn_statistics_match_the_statistics_pass(case, monkeypatch):
     """Round 5: the conv feeding a train-mode BatchNorm writes the batch-statistics partials of
     its bf16 output from the epilogue (conv_hwc's ST form: per 16 x 16-pixel tile and channel count / mean / M2,
