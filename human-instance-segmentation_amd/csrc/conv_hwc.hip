@@ -60,7 +60,13 @@ __device__ __forceinline__ void hc_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned l
 // TWB (pixel blocks per workgroup): 1 -- the workgroup's NW waves are NW 32-Cout groups over one 16 x 16 pixel block
 // (BCO = 32 NW); 2 -- NW / 2 Cout groups over two 16 x 16 blocks side by side (a 16 x 32 tile, one 18 x 34 halo per
 // slice; BCO = 16 NW: the 64-Cout layers).  A wave's tile and loop are the same either way.
-template <int ACT, bool RES, int NW, bool UP = false, int ABL = 0, bool RP = false, bool ST = false, int TWB = 1>
+// BR (round 5): the BatchNorm backward reduction of the layer whose output gradient this data-gradient conv writes
+// (d.bnb_partial, include/hiseg.h), from the same store loop as ST: each thread's 16 stored bf16 values g of its 8
+// channels, g masked by the ReLU of that BatchNorm's forward (bnb_z * bnb_scale + bnb_shift > 0, bnb_z loaded beside
+// the store), summed as g, g * xhat and xhat (xhat = (bnb_z - mean) * invstd); the wave's threads of one chunk are
+// added in a fixed butterfly order and each wave writes one split [3][Cout] -- the reduction pass over (dy, z) is gone.
+template <int ACT, bool RES, int NW, bool UP = false, int ABL = 0, bool RP = false, bool ST = false, int TWB = 1,
+          bool BR = false>
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(ConvArgs a) {
   constexpr int NCG = NW / TWB;                      // Cout groups of 32
   constexpr int BCO = 32 * NCG, TM = 2, NR = 16;    // wave tile: 32 Cout x (16 rows x 16 columns)
@@ -321,6 +327,22 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
     res_dma(14);
     res_dma(15);
   }
+  // BR: this thread's 16 chunks of the BatchNorm input z (the rows and channels it will store), loaded now so their
+  // latency overlaps the conversion and the barrier (in the store loop they cost more than the reduction pass saved)
+  constexpr int NSTZ = NPX * CPR / (NW * 64);
+  uint4 zpre[BR ? NSTZ : 1];
+  if constexpr (BR) {
+#pragma unroll
+    for (int k = 0; k < NSTZ; ++k) {
+      const int idx = t + NW * 64 * k;
+      const int r = idx / CPR, c = idx % CPR;
+      const int px = px_of(r), co = co0 + 8 * c;
+      zpre[k] = (px >= 0 && co < d.Cout)
+                    ? *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(d.bnb_z) +
+                                                      (long long)px * d.bnb_z_cstride + d.bnb_z_coff + co)
+                    : make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
   floatx4 sc[TM], sh[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -371,13 +393,27 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
   // partial as split (pixel tile, wave) -- no cross-wave merge, no extra barrier
   float sk[8], s1[8], s2[8];
   int sn = 0;
+  float bfs[8], bfh[8], bmu[8], binv[8];
+  if constexpr (BR) {
+    static_assert(!RES && !ST && ACT == HISEG_ACT_NONE && NW == 4 && (CPR == 16 || CPR == 8), "fused BN backward");
+    const int cb = co0 + 8 * (t % CPR);   // this thread's 8 channels (the same in every store-loop iteration)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int ch = cb + e < d.Cout ? cb + e : 0;
+      bfs[e] = d.bnb_scale[ch];
+      bfh[e] = d.bnb_shift[ch];
+      bmu[e] = d.bnb_mean[ch];
+      binv[e] = d.bnb_invstd[ch];
+      sk[e] = s1[e] = s2[e] = 0.f;
+    }
+  }
   if constexpr (ST) {
     static_assert(!RES && ACT == HISEG_ACT_NONE && NW == 4, "fused statistics: the conv feeding a BatchNorm");
     static_assert(CPR == 16 || CPR == 8, "fused statistics: a wave's threads of one chunk are lanes CPR apart");
 #pragma unroll
     for (int e = 0; e < 8; ++e) sk[e] = s1[e] = s2[e] = 0.f;
   }
-#pragma unroll 4
+#pragma unroll BR ? NST : 4
   for (int k = 0; k < NST; ++k) {
     const int idx = t + NW * 64 * k;
     const int r = idx / CPR, c = idx % CPR;
@@ -385,6 +421,22 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
     const uint4 v = *reinterpret_cast<const uint4*>(tile + r * EROWB + ((c ^ (r & SWM)) << 4));
     if (px >= 0 && co < d.Cout)
       *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(d.out) + (long long)px * d.o_cstride + d.o_coff + co) = v;
+    if constexpr (BR) {
+      if (px >= 0 && co < d.Cout) {
+        const uint4 zq = zpre[BR ? k : 0];
+        const unsigned wv[4] = {v.x, v.y, v.z, v.w}, zw[4] = {zq.x, zq.y, zq.z, zq.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float g0 = __builtin_bit_cast(float, (e & 1) ? (wv[e >> 1] & 0xffff0000u) : (wv[e >> 1] << 16));
+          const float zf = __builtin_bit_cast(float, (e & 1) ? (zw[e >> 1] & 0xffff0000u) : (zw[e >> 1] << 16));
+          const float g = (d.bnb_act == HISEG_ACT_RELU && !(zf * bfs[e] + bfh[e] > 0.f)) ? 0.f : g0;
+          const float xh = (zf - bmu[e]) * binv[e];
+          sk[e] += g;
+          s1[e] = fmaf(g, xh, s1[e]);
+          s2[e] += xh;
+        }
+      }
+    }
     if constexpr (ST) {
       if (px >= 0) {
         const unsigned wv[4] = {v.x, v.y, v.z, v.w};
@@ -433,9 +485,34 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
       }
     }
   }
+  if constexpr (BR) {
+#pragma unroll
+    for (int m = CPR; m < 64; m <<= 1) {   // lanes ^ CPR .. ^ 32: the wave's threads of the chunk, fixed order
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sk[e] += __shfl_xor(sk[e], m, 64);
+        s1[e] += __shfl_xor(s1[e], m, 64);
+        s2[e] += __shfl_xor(s2[e], m, 64);
+      }
+    }
+    if (lane < CPR) {
+      const long long C = d.Cout;
+      float* part = a.d.bnb_partial + ((long long)((n * nty + ty) * ntx + tx) * NW + w) * 3 * C;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int ch = co0 + 8 * lane + e;
+        if (ch < C) {
+          part[ch] = sk[e];
+          part[C + ch] = s1[e];
+          part[2 * C + ch] = s2[e];
+        }
+      }
+    }
+  }
 }
 
-template <int ACT, bool RES, int NW, bool UP = false, int ABL = 0, bool RP = false, bool ST = false, int TWB = 1>
+template <int ACT, bool RES, int NW, bool UP = false, int ABL = 0, bool RP = false, bool ST = false, int TWB = 1,
+          bool BR = false>
 static int launch_hwc(const ConvArgs& a, hipStream_t s) {
   const hiseg_conv2d_desc& d = a.d;
   constexpr int BCO = 32 * NW / TWB, TW = 16 * TWB;
@@ -444,7 +521,7 @@ static int launch_hwc(const ConvArgs& a, hipStream_t s) {
   const int tiles = d.N * ((d.H + 15) / 16) * ((d.W + TW - 1) / TW);
   const int nco = d.Cout_pad / BCO;
   const size_t lds = RP ? (size_t)80 * 1024 : (halo2 > epi ? halo2 : epi);
-  auto kern = conv_hwc_kernel<ACT, RES, NW, UP, ABL, RP, ST, TWB>;
+  auto kern = conv_hwc_kernel<ACT, RES, NW, UP, ABL, RP, ST, TWB, BR>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -496,6 +573,12 @@ static bool conv_hwc_applies(const ConvArgs& a, int variant) {
   // upsampled src A: the smp decoder conv1 form only (ReLU, or no activation when the conv feeds a train-mode BN)
   if (d.a_up == 2 && (d.residual || d.act != (d.stats_partial ? HISEG_ACT_NONE : HISEG_ACT_RELU))) return false;
   if (d.stats_partial && ((variant != 104 && variant != 107) || d.residual || d.act != HISEG_ACT_NONE)) return false;
+  if (d.bnb_partial &&
+      ((variant != 104 && variant != 107) || d.residual || d.act != HISEG_ACT_NONE || d.stats_partial || d.a_up != 1 ||
+       d.bnb_z == nullptr || ((d.bnb_z_cstride | d.bnb_z_coff) & 7) || ((uintptr_t)d.bnb_z & 15) ||
+       !d.bnb_scale || !d.bnb_shift || !d.bnb_mean || !d.bnb_invstd ||
+       (d.bnb_act != HISEG_ACT_RELU && d.bnb_act != HISEG_ACT_NONE)))
+    return false;
   return true;
 }
 
@@ -503,7 +586,7 @@ static bool conv_hwc_applies(const ConvArgs& a, int variant) {
 int conv_hwc_stats_tiles(const ConvArgs& a) {
   ConvArgs b = a;
   float dummy;
-  b.d.stats_partial = &dummy;
+  if (b.d.bnb_partial == nullptr) b.d.stats_partial = &dummy;   // (a data gradient with bnb_partial: that form)
   const int tw = conv_hwc_applies(b, 104) ? 16 : conv_hwc_applies(b, 107) ? 32 : 0;
   if (tw == 0) return 0;
   return a.d.N * ((a.d.H + 15) / 16) * ((a.d.W + tw - 1) / tw) * 4;   // (pixel tile, wave) splits
@@ -541,6 +624,11 @@ int conv_hwc_try(const ConvArgs& a, hipStream_t s, int variant) {
   }
 #endif
   if (!conv_hwc_applies(a, variant)) return 0;
+  if (d.bnb_partial) {   // the fused BatchNorm-backward reduction (variants 104 / 107; conv_hwc_applies checked it)
+    const int r = variant == 107 ? launch_hwc<HISEG_ACT_NONE, false, 4, false, 0, false, false, 2, true>(a, s)
+                                 : launch_hwc<HISEG_ACT_NONE, false, 4, false, 0, false, false, 1, true>(a, s);
+    return r < 0 ? r : 1;
+  }
   if (d.stats_partial) {   // the fused-statistics epilogue (variants 104 / 107; conv_hwc_applies checked the form)
     int r;
     if (variant == 107)

@@ -600,9 +600,9 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
                 HISEG_ERR_BAD_SHAPE, "conv2d: convT requires a 1x1 GEMM with Cout = 4*C, C %% 4 == 0");
   // BatchNorm statistics fused into the epilogue: only the halo kernel's fused-statistics form computes them, and no
   // fallback may silently skip them (the caller would finalize garbage)
-  if (d->stats_partial) {
+  if (d->stats_partial || d->bnb_partial) {   // (also the fused BatchNorm-backward reduction of a data gradient)
     HISEG_REQUIRE(variant == 0 || variant == 104 || variant == 107, HISEG_ERR_BAD_ARG,
-                  "conv2d: stats_partial with variant %d", variant);
+                  "conv2d: stats_partial / bnb_partial with variant %d", variant);
     HISEG_REQUIRE(al16(d->out) && al16(d->scale) && al16(d->shift), HISEG_ERR_BAD_SHAPE, "conv2d: alignment");
     ConvArgs a;
     a.d = *d;
@@ -612,7 +612,7 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
     a.Hs = d->H / d->a_up;
     a.Ws = d->W / d->a_up;
     HISEG_REQUIRE(conv_hwc_stats_tiles(a) > 0, HISEG_ERR_BAD_ARG,
-                  "conv2d: stats_partial set but the layer has no fused-statistics kernel (hiseg_conv2d_stats_tiles)");
+                  "conv2d: stats_partial / bnb_partial set but the layer has no fused kernel (hiseg_conv2d_stats_tiles)");
     const int r = conv_hwc_try(a, (hipStream_t)stream, d->Cout % 128 == 0 ? 104 : 107);
     HISEG_REQUIRE(r != 0, HISEG_ERR_BAD_ARG, "conv2d: the fused-statistics kernel declined the layer");
     return r < 0 ? r : HISEG_OK;

@@ -1234,7 +1234,39 @@ extern "C" int hiseg_bn_apply(const hiseg_bn_apply_desc* d, hiseg_stream_t strea
   return hiseg_check_launch("bn_apply");
 }
 
-extern "C" int hiseg_bn_bwd(const hiseg_bn_bwd_desc* d, hiseg_stream_t stream) {
+// Group sums of the data-gradient epilogue's backward-reduction partials (hiseg_bn_bwd_desc.partial_splits): block
+// (64 channels, KPRE splits), 4 rows x 64 channel lanes, row r summing every 4th split, the rows added in a fixed
+// order; group g's sums go to row g of `out` (a region after the partials).
+__global__ void __launch_bounds__(256) bn_bwd_premerge_kernel(const float* partial, int S, int C, float* out) {
+  __shared__ float a1[4][64], a2[4][64], a3[4][64];
+  const int t = threadIdx.x, l = t & 63, r = t >> 6;
+  const int c = blockIdx.x * 64 + l;
+  const int s0 = blockIdx.y * KPRE;
+  float x1 = 0.f, x2 = 0.f, x3 = 0.f;
+  if (c < C) {
+#pragma unroll 4
+    for (int i = r; i < KPRE; i += 4) {
+      if (s0 + i >= S) break;
+      const float* p = partial + (long long)(s0 + i) * 3 * C;
+      x1 += p[c];
+      x2 += p[C + c];
+      x3 += p[2 * C + c];
+    }
+  }
+  a1[r][l] = x1; a2[r][l] = x2; a3[r][l] = x3;
+  __syncthreads();
+  if (r == 0 && c < C) {
+    float* o = out + (long long)blockIdx.y * 3 * C;
+    o[c] = (a1[0][l] + a1[1][l]) + (a1[2][l] + a1[3][l]);
+    o[C + c] = (a2[0][l] + a2[1][l]) + (a2[2][l] + a2[3][l]);
+    o[2 * C + c] = (a3[0][l] + a3[1][l]) + (a3[2][l] + a3[3][l]);
+  }
+}
+
+extern "C" int hiseg_bn_bwd(const hiseg_bn_bwd_desc* d_in, hiseg_stream_t stream) {
+  HISEG_REQUIRE(d_in, HISEG_ERR_BAD_ARG, "bn_bwd: null descriptor");
+  hiseg_bn_bwd_desc dd = *d_in;
+  const hiseg_bn_bwd_desc* d = &dd;
   HISEG_REQUIRE(d && d->dy && d->z && d->dz && d->mean && d->invstd && d->partial && d->P > 0 && d->C > 0 && d->HW > 0,
                 HISEG_ERR_BAD_ARG, "bn_bwd: bad arguments");
   const bool pre = d->fwd_scale && d->fwd_shift &&
@@ -1247,8 +1279,23 @@ extern "C" int hiseg_bn_bwd(const hiseg_bn_bwd_desc* d, hiseg_stream_t stream) {
                 "bn_bwd: a smooth activation after a residual add needs the residual (pre-activation)");
   HISEG_REQUIRE(d->P < (1ll << 31), HISEG_ERR_BAD_SHAPE, "bn_bwd: too many pixels");
   hipStream_t s = (hipStream_t)stream;
-  const int S = stat_splits(d->P);
+  int S = stat_splits(d->P);
   const int dt = d->dtype, C = d->C;
+  // the reduction already done by the data-gradient conv's epilogue (hiseg_conv2d_desc.bnb_partial): more than
+  // 4 KPRE splits are summed in groups first, into the region after them
+  const bool pre_red = d->partial_splits > 0;
+  if (pre_red) {
+    S = d->partial_splits;
+    if (S > 4 * KPRE) {
+      const int G = (S + KPRE - 1) / KPRE;
+      float* grp = dd.partial + (long long)S * 3 * C;
+      hipLaunchKernelGGL(bn_bwd_premerge_kernel, dim3((C + 63) / 64, G), dim3(256), 0, s, d->partial, S, C, grp);
+      const int e = hiseg_check_launch("bn_bwd_premerge");
+      if (e) return e;
+      dd.partial = grp;
+      S = G;
+    }
+  }
   if (vec_ok(dt, C, d->dy, d->dy_cstride, d->dy_coff) && vec_ok(dt, C, d->y, d->y_cstride, d->y_coff) &&
       vec_ok(dt, C, d->z, d->z_cstride, d->z_coff) && vec_ok(dt, C, d->dz, d->dz_cstride, d->dz_coff) &&
       vec_ok(dt, C, d->dres, d->dres_cstride, d->dres_coff) && vec_ok(dt, C, d->residual, d->r_cstride, d->r_coff)) {
@@ -1257,7 +1304,8 @@ extern "C" int hiseg_bn_bwd(const hiseg_bn_bwd_desc* d, hiseg_stream_t stream) {
     const int mode = bn_bwd_mode(*d);
 #define BN_BWD_VEC(M)                                                                                         \
   do {                                                                                                        \
-    DISPATCH_T(dt, hipLaunchKernelGGL((bn_bwd_reduce_vec_kernel<T, M>), rgrid, dim3(256), 0, s, *d));         \
+    if (!pre_red)                                                                                             \
+      DISPATCH_T(dt, hipLaunchKernelGGL((bn_bwd_reduce_vec_kernel<T, M>), rgrid, dim3(256), 0, s, *d));       \
     hipLaunchKernelGGL(bn_bwd_finalize_par_kernel, fin_grid(C), dim3(256), 0, s, *d, S);                          \
     if (bn_unroll() == 2)                                                                                     \
       DISPATCH_T(dt, hipLaunchKernelGGL((bn_bwd_apply_vec_kernel<T, M, 2>), agrid, dim3(256), 0, s, *d, S));  \
@@ -1273,7 +1321,8 @@ extern "C" int hiseg_bn_bwd(const hiseg_bn_bwd_desc* d, hiseg_stream_t stream) {
 #undef BN_BWD_VEC
     return hiseg_check_launch("bn_bwd");
   }
-  DISPATCH_T(d->dtype, hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(S, (d->C + 255) / 256), dim3(256), 0, s, *d));
+  if (!pre_red)
+    DISPATCH_T(d->dtype, hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(S, (d->C + 255) / 256), dim3(256), 0, s, *d));
   hipLaunchKernelGGL(bn_bwd_finalize_par_kernel, fin_grid(C), dim3(256), 0, s, *d, S);
   DISPATCH_T(d->dtype, hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(ew_blocks(d->P * d->C)), dim3(256), 0, s, *d, S));
   return hiseg_check_launch("bn_bwd");

@@ -139,6 +139,9 @@ class Conv2dDesc(Desc):
         ("act_beta", c_float),
         ("workspace", c_void_p), ("workspace_bytes", ctypes.c_longlong),
         ("stats_partial", c_void_p),
+        ("bnb_partial", c_void_p), ("bnb_z", c_void_p), ("bnb_z_cstride", c_int), ("bnb_z_coff", c_int),
+        ("bnb_scale", c_void_p), ("bnb_shift", c_void_p), ("bnb_mean", c_void_p), ("bnb_invstd", c_void_p),
+        ("bnb_act", c_int),
     ]
 
 
@@ -180,7 +183,8 @@ class BnBwdDesc(Desc):
                 ("dz", c_void_p), ("dz_cstride", c_int), ("dz_coff", c_int),
                 ("dres", c_void_p), ("dres_cstride", c_int), ("dres_coff", c_int), ("dres_accumulate", c_int),
                 ("beta", c_void_p), ("fwd_scale", c_void_p), ("fwd_shift", c_void_p),
-                ("act_beta", c_float), ("residual", c_void_p), ("r_cstride", c_int), ("r_coff", c_int)]
+                ("act_beta", c_float), ("residual", c_void_p), ("r_cstride", c_int), ("r_coff", c_int),
+                ("partial_splits", c_int)]
 
 
 class LnBwdDesc(Desc):

@@ -296,6 +296,9 @@ class Tape:
         self.written: Dict[int, bool] = {}
         self.keep: List = []
         self.ctx: Dict = {}   # per-forward values the backward needs (output gradients, resize keys)
+        # BatchNorm layers whose backward reduction the one data-gradient conv that writes their output gradient
+        # computes in its epilogue (id(y) -> {"z", "st", "act", "part", "S"}; residual_block, _fused_bn_bwd)
+        self.bnb: Dict[int, dict] = {}
 
     def push(self, fn: Callable[[], None]):
         self.ops.append(fn)
@@ -487,6 +490,20 @@ def conv_bwd(T: Tape, p: TConv, d: L.Conv2dDesc, xa: Act, xb: Optional[Act], dz:
         if acc:
             dg.residual, dg.r_cstride, dg.r_coff = gx, gx.cstride, gx.coff
         dg.out, dg.o_cstride, dg.o_coff = gx, gx.cstride, gx.coff
+        fb = T.bnb.get(id(xa)) if not acc and not _DGRAD_VARIANT else None
+        if fb is not None:   # the producing BatchNorm's backward reduction from this data gradient's epilogue
+            z, st = fb["z"], fb["st"]
+            dg.bnb_partial, dg.bnb_z, dg.bnb_z_cstride, dg.bnb_z_coff = gx, z, z.cstride, z.coff   # (query)
+            dg.bnb_scale, dg.bnb_shift, dg.bnb_mean, dg.bnb_invstd = st.scale, st.shift, st.mean, st.invstd
+            dg.bnb_act = int(fb["act"])
+            S_ = int(lib.hiseg_conv2d_stats_tiles(ctypes.byref(dg)))
+            if S_ > 0:
+                part = torch.empty((S_ + (S_ + 63) // 64 + 1) * 3 * z.C, dtype=torch.float32, device=dz.t.device)
+                dg.bnb_partial = part
+                fb["part"], fb["S"] = part, S_
+            else:
+                for f in ("bnb_partial", "bnb_z", "bnb_scale", "bnb_shift", "bnb_mean", "bnb_invstd"):
+                    setattr(dg, f, None)
         _chk(_dgrad_launch(dg, dz.t.device), "conv2d(dgrad)")
         T.mark(xa)
     else:
@@ -633,8 +650,15 @@ def bn_backward(T: Tape, bn: nn.BatchNorm2d, z: Act, y: Act, st: BNState, dz: Ac
     gy = T.grad_in(y)
     C = z.C
     P = z.N * z.H * z.W
-    part = torch.empty((lib.hiseg_bn_partials() + 1) * 3 * C, dtype=torch.float32, device=z.t.device)
+    fb = T.bnb.pop(id(y), None)
+    if fb is not None and fb["part"] is not None:   # the data gradient's epilogue did the reduction
+        part, pre_splits = fb["part"], fb["S"]
+        FUSED_BN_BWD_TAKEN[0] += 1
+    else:
+        part, pre_splits = torch.empty((lib.hiseg_bn_partials() + 1) * 3 * C, dtype=torch.float32,
+                                       device=z.t.device), 0
     d = L.BnBwdDesc()
+    d.partial_splits = pre_splits
     d.dtype, d.P, d.HW, d.C = hdtype(z.dtype), P, z.H * z.W, C
     d.dy, d.dy_cstride, d.dy_coff = gy, gy.cstride, gy.coff
     d.y, d.y_cstride, d.y_coff = y, y.cstride, y.coff
@@ -662,16 +686,32 @@ def bn_backward(T: Tape, bn: nn.BatchNorm2d, z: Act, y: Act, st: BNState, dz: Ac
         T.mark(residual)
 
 
+FUSED_BN_BWD_TAKEN = [0]   # BatchNorm backward passes that used a data gradient's epilogue reduction (tests)
+
+
+def _fused_bn_bwd() -> bool:
+    """HISEG_FUSED_BN_BWD=1 (read per forward; default off): the ResidualBlocks' first BatchNorm takes its backward
+    reduction from conv2's data-gradient epilogue.  Measured (profiles/r5_fused_bn_bwd.txt): BatchNorm class 18.2 ->
+    16.8 ms per B0 train step, data-gradient class 13.1 -> 14.4 ms, the step unchanged (71.5 vs 71.1-72.1 ms) -- the
+    extra read of z lands in the epilogues every workgroup of the grid runs at the same time, as the residual's does."""
+    return os.environ.get("HISEG_FUSED_BN_BWD", "0") == "1"
+
+
 def conv_bn_act(T: Tape, conv: nn.Conv2d, bn, act: int, x: Act, xb: Optional[Act] = None, *,
                 residual: Optional[Act] = None, drop=None, split=None, convT: bool = False,
-                need_dx: bool = True) -> Act:
-    """Conv (+bias) -> BatchNorm(train) -> (+residual) -> act -> (*Dropout2d mask)."""
+                need_dx: bool = True, sole_consumer: bool = False) -> Act:
+    """Conv (+bias) -> BatchNorm(train) -> (+residual) -> act -> (*Dropout2d mask).  ``sole_consumer``: the caller
+    guarantees one conv alone consumes y (ResidualBlock's conv1 -> conv2), so that conv's data gradient -- the only
+    write of y's gradient -- may compute this BatchNorm's backward reduction in its epilogue."""
     S = T.S
     bn = _bn_module(bn)
     p = S.conv(conv, split=split, convT=convT)
     stats = [] if isinstance(bn, nn.BatchNorm2d) else None
     z, d = conv_fwd(S, p, x, xb, stats=stats)
     y, st = bn_forward(T, bn, z, act=act, residual=residual, drop=drop, stats=stats)
+    if (sole_consumer and isinstance(bn, nn.BatchNorm2d) and residual is None and drop is None and
+            int(act) in (ACT_RELU, ACT_NONE) and z.dtype == torch.bfloat16 and _fused_bn_bwd()):
+        T.bnb[id(y)] = {"z": z, "st": st, "act": int(act), "part": None, "S": 0}
 
     def back():
         dz = Act.new(z.N, z.H, z.W, z.C, z.dtype, z.t.device, cpad=z.cstride, zero=z.cstride != z.C)
@@ -748,7 +788,7 @@ def residual_block(T: Tape, blk: nn.Module, x: Act, drop=None) -> Act:
     the block output (the shared_features Sequential, refinement.py:484-486)."""
     a1 = act_of(blk.activation1 if hasattr(blk, "activation1") else blk.activation)
     a2 = act_of(blk.activation2 if hasattr(blk, "activation2") else blk.activation)
-    h = conv_bn_act(T, blk.conv1, blk.norm1, a1, x)
+    h = conv_bn_act(T, blk.conv1, blk.norm1, a1, x, sole_consumer=True)
     return conv_bn_act(T, blk.conv2, blk.norm2, a2, h, residual=x, drop=drop)
 
 

@@ -144,6 +144,17 @@ typedef struct hiseg_conv2d_desc {
    * for hiseg_bn_finalize_n
    * (advanced/normalization_comparison.py:181-182); the call fails when that is 0. */
   float* stats_partial;
+  /* Optional (round 5, train mode, a data-gradient conv that alone writes the output gradient of a
+   * conv -> BatchNorm2d -> ReLU / identity layer): when bnb_partial is non-null the automatic choice also
+   * writes that BatchNorm's backward reduction from its epilogue -- per split s (S as
+   * hiseg_conv2d_stats_tiles) and output channel c, over the split's pixels: sum g, sum g * xhat, sum xhat
+   * with g = out * act'(bnb_z * bnb_scale + bnb_shift) (bnb_act HISEG_ACT_RELU; HISEG_ACT_NONE: g = out)
+   * and xhat = (bnb_z - bnb_mean) * bnb_invstd -- into bnb_partial [S][3][Cout] for hiseg_bn_bwd
+   * (hiseg_bn_bwd_desc.partial_splits = S); bnb_z is the BatchNorm's input (bf16, Cout channels), the
+   * four tables its forward's folded affine and batch statistics.  Needs no activation / residual of its
+   * own; the call fails when the layer has no such kernel. */
+  float* bnb_partial; const void* bnb_z; int bnb_z_cstride, bnb_z_coff;
+  const float* bnb_scale; const float* bnb_shift; const float* bnb_mean; const float* bnb_invstd; int bnb_act;
 } hiseg_conv2d_desc;
 int hiseg_conv2d_fwd(const hiseg_conv2d_desc* d, hiseg_stream_t stream);
 /* Workspace bytes hiseg_conv2d_fwd's automatic choice would use for this layer (0: none). */

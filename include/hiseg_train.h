@@ -140,6 +140,10 @@ typedef struct hiseg_bn_bwd_desc {
    * the forward's pre-activation z*fwd_scale + fwd_shift + residual -- required for GELU / Swish / SiLU / ReLU
    * after a residual add; GELU and Swish always need fwd_scale / fwd_shift */
   const void* residual; int r_cstride, r_coff;
+  /* round 5, optional: > 0 -- `partial` already holds [partial_splits][3][C] sums of g, g*xhat, xhat written by
+   * the data-gradient conv's epilogue (hiseg_conv2d_desc.bnb_partial); the reduction pass is skipped.  `partial`
+   * then needs (partial_splits + ceil(partial_splits / 64) + 1) * 3 * C floats. */
+  int partial_splits;
 } hiseg_bn_bwd_desc;
 int hiseg_bn_bwd(const hiseg_bn_bwd_desc* d, hiseg_stream_t stream);
 

@@ -1203,6 +1203,42 @@ def test_bn_finalize_n_matches_f64_merge(S, C):
     np.testing.assert_allclose(rv.double().cpu().numpy(), (1 - mom) + mom * var * P / (P - 1), rtol=1e-6)
 
 
+@pytest.mark.parametrize("case", [(256, 3, 20, 30), (128, 2, 37, 21), (64, 2, 33, 50)])
+def test_fused_bn_backward_reduction_matches_the_reduction_pass(case, monkeypatch):
+    """Round 5 (second half): in a ResidualBlock the first BatchNorm's output feeds conv2 alone,
+    so conv2's data gradient -- the one write of that gradient -- computes the BatchNorm backward reduction (sums of
+    g, g * xhat, xhat per channel, g masked by the forward's ReLU) in its epilogue (conv_hwc BR form) and hiseg_bn_bwd
+    skips its reduction pass (partial_splits).  Against HISEG_FUSED_BN_BWD=0: every parameter gradient and the input
+    gradient within f32 re-association of the sums (one bf16 ulp of the tensor's largest value: a coefficient moved
+    by an f32 ulp can round a bf16 dz, and the bf16 input gradient, either way), the fused path taken."""
+    from hiseg import train_engine as TEm
+    from hiseg.layers import ResidualBlock
+    from hiseg.ops import Act
+    C, N, H, W = case
+    dt = torch.bfloat16
+    x = torch.from_numpy(filler.normal(81, (N, C, H, W))).to(DEV)
+    g = torch.from_numpy(filler.normal(82, (N, C, H, W))).to(DEV)
+    res = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("HISEG_FUSED_BN_BWD", fused)
+        blk = ResidualBlock(C, "batchnorm", 8, "relu", 1.0)
+        filler.fill_module(blk, seed=83)
+        TE, S, T = engine(_Holder(b=blk), dt)
+        xa = Act.from_nchw(x, dt)
+        before = TEm.FUSED_BN_BWD_TAKEN[0]
+        y = TE.residual_block(T, blk, xa)
+        inject(T, y, g, dt)
+        S.flat.prepare_backward()
+        T.run_backward()
+        torch.cuda.synchronize()
+        taken = TEm.FUSED_BN_BWD_TAKEN[0] - before
+        assert taken == (1 if fused == "1" else 0), taken
+        res[fused] = [p.grad.detach().float().clone() for p in blk.parameters()] + [grad_nchw(T, xa).clone()]
+    for a, b in zip(res["1"], res["0"]):
+        assert torch.isfinite(a).all()
+        assert (a - b).abs().max() <= 2 ** -7 * b.abs().max() + 1e-6, ((a - b).abs().max(), b.abs().max())
+
+
 @pytest.mark.parametrize("case", [(32, 3, 1, 2, 40, 48), (144, 5, 1, 2, 20, 24), (96, 3, 2, 2, 33, 27),
                                   (240, 5, 2, 1, 16, 20), (1152, 3, 1, 2, 10, 10)])
 def test_train_depthwise_on_inference_kernels_matches_train_kernels(case, monkeypatch):
