@@ -208,6 +208,14 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
       else __builtin_amdgcn_s_sleep(18);
     }
   }
+  // ABL 2048 / 4096 (DIAG): the first round's workgroups start in 4 phases (by dispatch index), 0 .. 3 x ~3 / ~1.5 us
+  // apart, so that the grid's epilogues (every workgroup's at once: an HBM burst) spread over time
+  if constexpr ((ABL & 6144) != 0) {
+    if (orig < 512) {
+      const int ph = (orig >> 3) & 3;
+      for (int i = 0; i < ((ABL & 2048) ? 2 : 1) * ph; ++i) __builtin_amdgcn_s_sleep(94);
+    }
+  }
   // ---- prologue: slice 0's halo, the weights of block (slice 0, kx 0)
   hc_u4 af[3][TM], an[3][TM];
 #pragma unroll
@@ -599,7 +607,7 @@ int conv_hwc_stats_tiles(const ConvArgs& a) {
 int conv_hwc_try(const ConvArgs& a, hipStream_t s, int variant) {
   const hiseg_conv2d_desc& d = a.d;
 #ifdef HISEG_DIAG
-  if (variant >= 150 && variant < 1700) {   // timing ablations of variant 104 (res + ReLU only; output buffer as
+  if (variant >= 150 && variant < 4300) {   // timing ablations of variant 104 (res + ReLU only; output buffer as
                                           // scratch: the ABL 32 store writes one float per thread and MFMA row)
     if (d.weight_frag == nullptr || !d.residual || d.act != HISEG_ACT_RELU || d.a_up != 1 || d.Cout % 128) return 0;
     int r;
@@ -618,6 +626,8 @@ int conv_hwc_try(const ConvArgs& a, hipStream_t s, int variant) {
       case 512: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 512>(a, s); break;
       case 1024: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 1024>(a, s); break;
       case 1536: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 1536>(a, s); break;
+      case 2048: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 2048>(a, s); break;
+      case 4096: r = launch_hwc<HISEG_ACT_RELU, true, 4, false, 4096>(a, s); break;
       default: return 0;
     }
     return r < 0 ? r : 1;

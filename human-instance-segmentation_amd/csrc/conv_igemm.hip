@@ -705,7 +705,7 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
   } else if ((variant >= 92 && variant <= 97) || variant == 100 || variant == 101 || (variant >= 110 && variant < 142)) {
     const int r = conv_hwr_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
-  } else if ((variant >= 104 && variant <= 107) || (variant >= 150 && variant < 1700)) {
+  } else if ((variant >= 104 && variant <= 107) || (variant >= 150 && variant < 4300)) {
     const int r = conv_hwc_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
   } else if (variant == 103) {
