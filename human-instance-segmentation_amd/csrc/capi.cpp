@@ -6,6 +6,11 @@
 #include <string.h>
 #include <atomic>
 #include "hiseg.h"
+#include "hiseg_data.h"
+#include "hiseg_distill.h"
+#include "hiseg_head_train.h"
+#include "hiseg_loss.h"
+#include "hiseg_train.h"
 
 static thread_local char g_err[512] = "";
 
@@ -51,6 +56,19 @@ extern "C" int hiseg_placement_stats(long long* declined, long long* far, int re
     g_place_far = 0;
   }
   return HISEG_OK;
+}
+
+extern "C" int hiseg_struct_sizes(long long* out, int n) {
+  const long long sz[] = {(long long)sizeof(hiseg_roi_align_desc), (long long)sizeof(hiseg_conv2d_desc),
+                          (long long)sizeof(hiseg_wgrad_map),      (long long)sizeof(hiseg_pack_entry),
+                          (long long)sizeof(hiseg_bn_apply_desc),  (long long)sizeof(hiseg_bn_bwd_desc),
+                          (long long)sizeof(hiseg_ln_bwd_desc),    (long long)sizeof(hiseg_ew_view),
+                          (long long)sizeof(hiseg_ubf_desc),       (long long)sizeof(hiseg_ubf_grads),
+                          (long long)sizeof(hiseg_loss_cfg),       (long long)sizeof(hiseg_distill_cfg),
+                          (long long)sizeof(hiseg_roi_target_desc)};
+  const int m = (int)(sizeof(sz) / sizeof(sz[0]));
+  for (int i = 0; i < n && i < m; ++i) out[i] = sz[i];
+  return m;
 }
 
 extern "C" int hiseg_version(void) { return 100; }

@@ -289,6 +289,7 @@ def _declare(lib):
         "hiseg_conv2d_wgrad_dims": ([ctypes.POINTER(Conv2dDesc), c_int, P, P, P], c_int),
         "hiseg_conv2d_wgrad": ([ctypes.POINTER(Conv2dDesc), P, c_int, c_int, c_int, P, c_int, P], c_int),
         "hiseg_wgrad_path_stats": ([ctypes.POINTER(c_ll), c_int], c_int),
+        "hiseg_struct_sizes": ([ctypes.POINTER(c_ll), c_int], c_int),
         "hiseg_conv2d_stats_tiles": ([ctypes.POINTER(Conv2dDesc)], c_int),
         "hiseg_bn_finalize_n": ([P, c_int, c_int, c_ll, P, P, c_float, c_float, P, P, P, P, P, P, P], c_int),
         "hiseg_wgrad_last_path": ([], c_int),

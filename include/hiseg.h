@@ -157,6 +157,10 @@ typedef struct hiseg_conv2d_desc {
   const float* bnb_scale; const float* bnb_shift; const float* bnb_mean; const float* bnb_invstd; int bnb_act;
 } hiseg_conv2d_desc;
 int hiseg_conv2d_fwd(const hiseg_conv2d_desc* d, hiseg_stream_t stream);
+/* sizeof of every descriptor struct of the C ABI, in the order roi_align_desc, conv2d_desc, wgrad_map, pack_entry,
+ * bn_apply_desc, bn_bwd_desc, ln_bwd_desc, ew_view, ubf_desc, ubf_grads, loss_cfg, distill_cfg, roi_target_desc
+ * (the first n of them into out); returns their count.  Bindings check their struct layouts against it. */
+int hiseg_struct_sizes(long long* out, int n);
 /* Workspace bytes hiseg_conv2d_fwd's automatic choice would use for this layer (0: none). */
 long long hiseg_conv2d_workspace_bytes(const hiseg_conv2d_desc* d);
 /* Splits S of the BatchNorm statistics partials the automatic choice fuses into this layer's

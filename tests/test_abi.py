@@ -39,6 +39,21 @@ def test_library_exports_every_declared_symbol():
     assert set(header_functions()) <= set(L.EXPORTED)
 
 
+def test_binding_struct_layouts_match_the_headers():
+    """Every descriptor struct of the C ABI has the size the library was compiled with (hiseg_struct_sizes), so a
+    field added to a header without its ctypes twin -- or in another place -- fails here, not as a silent misread
+    on the GPU (round 5 appended fields to hiseg_conv2d_desc and hiseg_bn_bwd_desc)."""
+    import ctypes
+    from hiseg import _lib as L
+    classes = [L.RoiAlignDesc, L.Conv2dDesc, L.WgradMap, L.PackEntry, L.BnApplyDesc, L.BnBwdDesc, L.LnBwdDesc,
+               L.EwView, L.UbfDesc, L.UbfGrads, L.LossCfg, L.DistillCfg, L.RoiTargetDesc]
+    out = (ctypes.c_longlong * len(classes))()
+    n = L.lib().hiseg_struct_sizes(out, len(classes))
+    assert n == len(classes)
+    for cls, size in zip(classes, out):
+        assert ctypes.sizeof(cls) == size, (cls.__name__, ctypes.sizeof(cls), size)
+
+
 def test_invalid_descriptor_reports_an_error_without_touching_the_gpu():
     import ctypes
     from hiseg import _lib as L
