@@ -304,8 +304,9 @@ def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=6
         HD.enable_grad_sync(model.student)
     state = {"opt": None, "enc_opt": None}
 
-    def step():
-        s, t = model(x)
+    def step(s=None, t=None):
+        if s is None:
+            s, t = model(x)
         loss, _ = loss_fn(s, t, m)
         if state["opt"] is None:
             state["opt"] = hiseg.FusedAdamW(model.student, lr=1e-4, weight_decay=1e-4, max_grad_norm=1.0,
@@ -331,6 +332,34 @@ def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=6
         del model.concurrent_teacher
     graphable = graph and (world == 1 or _backend(dist) == "nccl")
     run = hiseg.GraphedStep(step, lambda: state["opt"]) if graphable else step
+    branch_graphs = graphable and world == 1 and os.environ.get("HISEG_DISTILL_BRANCH_GRAPHS", "1") != "0"
+    pipelined = branch_graphs and os.environ.get("HISEG_DISTILL_PIPELINE", "1") != "0"
+    if branch_graphs:
+        # teacher / student forwards as graphs of their own, launched side by side (GraphedBranchStep)
+        fwd = {}
+
+        def teacher():
+            fwd["t"] = model.teacher(x)
+
+        def student():
+            fwd["s"] = model.student(x)
+
+        def tail():
+            return step(fwd["s"], fwd["t"])
+
+        handoff = None
+        if pipelined:
+            # the frozen eval-mode teacher runs one batch ahead (overlapping this batch's backward): the timed K
+            # steps still run K teacher forwards; the batch is the same synthetic x every step
+            def teacher():
+                fwd["t_next"] = model.teacher(x)
+
+            def handoff():
+                if "t" not in fwd:
+                    fwd["t"] = torch.empty_like(fwd["t_next"])
+                fwd["t"].copy_(fwd["t_next"])
+
+        run = hiseg.GraphedBranchStep(teacher, student, tail, lambda: state["opt"], handoff_fn=handoff)
     for _ in range(max(warmup, 3 if run is not step else 1)):
         loss = run()
     if os.environ.get("HISEG_BENCH_STEP_TIMES") == "1":   # developer knob: per-replay times on stderr
@@ -379,7 +408,10 @@ def distill_bench(device, dtype, rank, world, dist, steps, warmup, batch=4, hw=6
                                    f"decoder FusedAdamW clip 1.0" + (", encoder FusedAdamW lr x 0.1 unclipped"
                                                                      if unfrozen else ""),
                        "global_batch": batch * world,
-                       "schedule": "eager" if run is step else "one HIP graph per step (hiseg.GraphedStep)",
+                       "schedule": "eager" if run is step else (
+                           ("teacher / student-forward / loss-backward-optimizer graphs (hiseg.GraphedBranchStep)"
+                            + (", teacher one batch ahead" if pipelined else "")) if branch_graphs
+                           else "one HIP graph per step (hiseg.GraphedStep)"),
                        "parallelism": f"dp{world} (bucketed RCCL grad all-reduce)" if world > 1 else "dp1"}}
 
 

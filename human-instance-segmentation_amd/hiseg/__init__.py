@@ -17,7 +17,7 @@ from .model import (  # noqa: F401
 
 from .losses import RefinedHierarchicalLoss  # noqa: F401,E402
 from .optim import FusedAdamW, cosine_lr  # noqa: F401,E402
-from .graphs import GraphedStep  # noqa: F401,E402
+from .graphs import GraphedStep, GraphedBranchStep  # noqa: F401,E402
 from .checkpoint import resume_from_checkpoint, save_checkpoint  # noqa: F401,E402
 from .data import GpuRoiBatchBuilder, resize_bilinear_pil  # noqa: F401,E402
 from .metrics import (  # noqa: F401,E402

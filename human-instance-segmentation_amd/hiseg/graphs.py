@@ -131,3 +131,102 @@ class GraphedStep:
         if bump:
             torch.autograd.graph.increment_version(bump)
         return self.out
+
+
+class GraphedBranchStep(GraphedStep):
+    """GraphedStep for a step that opens with two independent branches: ``branch_fn`` on the side stream (the frozen
+    distillation teacher's forward), ``head_fn`` on the caller's stream beside it (the student's forward), then
+    ``tail_fn`` once both are done (loss, backward, optimizer; it returns the step's outputs).  The functions pass
+    values through the caller's closures.
+
+    Why three graphs instead of one (round 5, profiles/r5_distill_branches.txt): a replayed graph's executor enqueues
+    the whole node list of its launch queue -- the first-captured branch and everything after the join -- before the
+    other branch's nodes (2.5 ms of host enqueue per distillation step against 0.5 ms here).  Here the branch graph
+    is launched on the side stream first, the head graph on the caller's stream right after it, and the tail graph
+    behind an event of the side stream.  Eager steps run the same functions on the same streams, so results equal a
+    single-graph GraphedStep of the composed step bit for bit.
+
+    ``handoff_fn`` given: the branch runs one step ahead (software pipelining; valid for a branch that reads no
+    state the step updates -- the frozen, eval-mode teacher).  Call k launches the branch for step k+1, which then
+    overlaps step k's head AND tail; the first call also runs the branch for step 0 first.  ``handoff_fn`` runs on
+    the caller's stream at the start of every call, after the branch launched by the previous call has finished and
+    before the next one starts: it moves the branch's result into the buffer the tail reads (e.g. ``t.copy_(t_next)``)
+    and stages the branch's next input.  Same kernels on the same inputs: the results equal the unpipelined step's."""
+
+    def __init__(self, branch_fn: Callable, head_fn: Callable, tail_fn: Callable,
+                 optimizer_fn: Optional[Callable] = None, eager: int = 2, handoff_fn: Optional[Callable] = None):
+        super().__init__(tail_fn, optimizer_fn, eager)
+        self.branch_fn, self.head_fn, self.handoff_fn = branch_fn, head_fn, handoff_fn
+        self.graphs = None
+        self._ev = None
+        self._primed = False
+
+    def __call__(self):
+        self.calls += 1
+        if self.graphs is not None and self._fingerprint() != self.fp:
+            self.graphs, self.calls = None, 1
+        main = torch.cuda.current_stream()
+        side = role_stream("teacher")
+        if self._ev is None:
+            self._ev = torch.cuda.Event()
+        piped = self.handoff_fn is not None
+        if piped:
+            if not self._primed:   # the branch for the first step
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    self.branch_fn()
+                self._ev.record(side)
+                self._primed = True
+            main.wait_event(self._ev)
+            self.handoff_fn()
+        if self.calls <= self.eager:
+            s = role_stream("warm")
+            s.wait_stream(main)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                self.branch_fn()
+            self._ev.record(side)
+            with torch.cuda.stream(s):
+                self.head_fn()
+                if not piped:
+                    s.wait_stream(side)
+                out = self.fn()
+            main.wait_stream(s)
+            return out
+        if self.graphs is None or self._lr() != self.lr:
+            self.graphs = None
+            torch.cuda.synchronize()
+            _drain_rccl_watchdog()
+            before = self._fingerprint()
+            gb, gh, gt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gb, stream=side, capture_error_mode="thread_local"):
+                self.branch_fn()
+            with torch.cuda.graph(gh, stream=role_stream("capture"), capture_error_mode="thread_local"):
+                self.head_fn()
+            with torch.cuda.graph(gt, stream=role_stream("capture"), capture_error_mode="thread_local"):
+                self.out = self.fn()
+            self.fp = self._fingerprint()
+            if self.fp != before:
+                raise RuntimeError("GraphedBranchStep: the step re-allocated optimizer / model state while it was "
+                                   "being captured; run more eager steps first")
+            self.graphs, self.lr = (gb, gh, gt), self._lr()
+            self.captures += 1
+        gb, gh, gt = self.graphs
+        side.wait_stream(main)   # the previous step's tail (or this step's handoff) is done with the branch buffers
+        with torch.cuda.stream(side):
+            gb.replay()
+        self._ev.record(side)
+        gh.replay()
+        if not piped:
+            main.wait_event(self._ev)
+        gt.replay()
+        o = self._opt()
+        bump = getattr(o, "_bump", None)
+        if bump:
+            torch.autograd.graph.increment_version(bump)
+        return self.out
+
+    def drain(self):
+        """Wait (on the caller's stream) for the branch a pipelined step launched ahead."""
+        if self._ev is not None:
+            torch.cuda.current_stream().wait_event(self._ev)

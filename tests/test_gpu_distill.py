@@ -273,3 +273,131 @@ def test_concurrent_teacher_stream_equals_serial(graphed, monkeypatch):
     assert torch.isfinite(l0).all()
     assert torch.equal(l0, l1), (l0, l1)
     assert all(torch.equal(a, b) for a, b in zip(p0, p1))
+
+
+@pytest.mark.parametrize("unfrozen", [0, 2])
+def test_branch_graphs_equal_single_graph(unfrozen, monkeypatch):
+    """hiseg.GraphedBranchStep (teacher forward, student forward and loss/backward/optimizer as three graphs, the two
+    forwards launched side by side) against the serial step in one GraphedStep graph: loss, student parameters bit
+    for bit over six steps (two eager, capture, three replays), decoder-only and with the encoder's last two stages
+    unfrozen (second FusedAdamW group, backward through the MBConv stack)."""
+    import filler
+    import hiseg
+    from hiseg.distill import DistillationUNetWrapper
+    x = torch.from_numpy(filler.normal(43, (2, 3, 128, 128))).to(DEV)
+    _, _, m = __import__("oracle.distill", fromlist=["np_inputs"]).np_inputs(44, 2, 128, 128)
+    m = m.to(DEV)
+    res = {}
+    for split in (False, True):
+        monkeypatch.setattr(DistillationUNetWrapper, "concurrent_teacher", False)
+        model, loss_fn = _distill_model(torch.bfloat16)
+        model = model.to(DEV).train()
+        enc = model.unfreeze_encoder_blocks(unfrozen, learning_rate_scale=0.1) if unfrozen else None
+        state = {"opt": None, "enc": None}
+        fwd = {}
+
+        def step(s=None, t=None):
+            if s is None:
+                s, t = model(x)
+            loss, _ = loss_fn(s, t, m)
+            if state["opt"] is None:
+                state["opt"] = hiseg.FusedAdamW(model.student, lr=1e-3, weight_decay=1e-4, max_grad_norm=1.0,
+                                                params=model.student.get_decoder_parameters())
+                if enc:
+                    state["enc"] = hiseg.FusedAdamW(model.student, lr=1e-4, weight_decay=1e-4, max_grad_norm=None,
+                                                    params=enc)
+            opts = [o for o in (state["opt"], state["enc"]) if o is not None]
+            for o in opts:
+                o.zero_grad()
+            loss.backward()
+            for o in opts:
+                o.step()
+            return loss
+
+        def teacher():
+            fwd["t"] = model.teacher(x)
+
+        def student():
+            fwd["s"] = model.student(x)
+
+        if split:
+            run = hiseg.GraphedBranchStep(teacher, student, lambda: step(fwd["s"], fwd["t"]), lambda: state["opt"])
+        else:
+            run = hiseg.GraphedStep(step, lambda: state["opt"])
+        losses = [run().detach().clone() for _ in range(6)]
+        torch.cuda.synchronize()
+        if split:
+            assert run.captures == 1
+        res[split] = (torch.stack(losses), [p.detach().clone() for p in model.student.parameters()])
+    (l0, p0), (l1, p1) = res[False], res[True]
+    assert torch.isfinite(l0).all()
+    assert torch.equal(l0, l1), (l0, l1)
+    assert all(torch.equal(a, b) for a, b in zip(p0, p1))
+
+
+def test_pipelined_teacher_equals_serial_step():
+    """GraphedBranchStep with handoff_fn (the frozen teacher's forward for batch k+1 launched during step k, beside
+    step k's student forward and backward) against the serial step, over six steps on six DIFFERENT batches: same
+    losses and student parameters bit for bit -- the handoff stages each batch and its teacher output in order."""
+    import filler
+    import hiseg
+    from hiseg.distill import DistillationUNetWrapper
+    nstep = 6
+    xs = [torch.from_numpy(filler.normal(60 + k, (2, 3, 128, 128))).to(DEV) for k in range(nstep + 1)]
+    _, _, m = __import__("oracle.distill", fromlist=["np_inputs"]).np_inputs(45, 2, 128, 128)
+    m = m.to(DEV)
+    res = {}
+    for piped in (False, True):
+        model, loss_fn = _distill_model(torch.bfloat16)
+        model = model.to(DEV).train()
+        model.concurrent_teacher = False
+        state = {"opt": None}
+        x_cur, x_next = xs[0].clone(), xs[0].clone()
+        fwd, k = {}, [0]
+
+        def step(s=None, t=None):
+            if s is None:
+                s, t = model(x_cur)
+            loss, _ = loss_fn(s, t, m)
+            if state["opt"] is None:
+                state["opt"] = hiseg.FusedAdamW(model.student, lr=1e-3, weight_decay=1e-4, max_grad_norm=1.0,
+                                                params=model.student.get_decoder_parameters())
+            state["opt"].zero_grad()
+            loss.backward()
+            state["opt"].step()
+            return loss
+
+        def teacher():
+            fwd["t_next"] = model.teacher(x_next)
+
+        def student():
+            fwd["s"] = model.student(x_cur)
+
+        def handoff():   # step k: its teacher output and batch in place, batch k+1 staged for the next branch
+            if "t" not in fwd:
+                fwd["t"] = torch.empty_like(fwd["t_next"])
+            fwd["t"].copy_(fwd["t_next"])
+            x_cur.copy_(xs[k[0]])
+            x_next.copy_(xs[k[0] + 1])
+
+        losses = []
+        for i in range(nstep):
+            k[0] = i
+            if piped:
+                if i == 0:
+                    run = hiseg.GraphedBranchStep(teacher, student, lambda: step(fwd["s"], fwd["t"]),
+                                                  lambda: state["opt"], handoff_fn=handoff)
+                losses.append(run().detach().clone())
+            else:
+                x_cur.copy_(xs[i])
+                losses.append(step().detach().clone())
+        if piped:
+            run.drain()
+            assert run.captures == 1
+        torch.cuda.synchronize()
+        res[piped] = (torch.stack(losses), [p.detach().clone() for p in model.student.parameters()])
+    (l0, p0), (l1, p1) = res[False], res[True]
+    assert torch.isfinite(l0).all()
+    assert len(set(l0.tolist())) == nstep   # different batches, different losses
+    assert torch.equal(l0, l1), (l0, l1)
+    assert all(torch.equal(a, b) for a, b in zip(p0, p1))
