@@ -584,15 +584,39 @@ constexpr int kDwTH = 8, kDwTW = 16, kDwCG = 64, kDwPS = kDwCG * 2 + 8;
 template <int KS, int ST>
 __global__ void __launch_bounds__(256) dwconv_t_kernel(const void* in, int H, int W, int C, const float* w,
                                                        const float* scale, const float* shift, int act, void* out,
-                                                       int Ho, int Wo, float* gap) {
+                                                       int Ho, int Wo, float* gap, int xcd) {
   constexpr int IH = (kDwTH - 1) * ST + KS, IW = (kDwTW - 1) * ST + KS;
   constexpr int NIN = (kDwXS - 1) * ST + KS;
   constexpr int NSTRIP = kDwTH * (kDwTW / kDwXS);   // 32 strips of 4 outputs per channel quad
   extern __shared__ __attribute__((aligned(16))) char dws[];
   const int t = threadIdx.x;
-  const int n = blockIdx.y, g0 = blockIdx.z * kDwCG;
+  // block -> (tile, image, channel group): grid (tiles, N, groups) as launched, or (xcd != 0) the XCD-major
+  // bijective remap of the linear block id -- the dispatcher deals consecutive blocks round-robin to the 8 XCDs, so
+  // launched order puts a tile's neighbours (which re-read its halo rows / columns) and the other channel groups of
+  // its pixels (a 64-channel group is 128 B at a pixel stride of 2C bytes: it straddles cache lines it shares with
+  // the next group) behind other L2s; remapped, each XCD works through a contiguous run of (group, tile) blocks.
+  // Same per-tile arithmetic: outputs bit-identical in every order.
+  int bt = blockIdx.x, n = blockIdx.y, gz = blockIdx.z;
+  if (xcd) {
+    const int nwg = gridDim.x * gridDim.y * gridDim.z;
+    const int orig = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int q8 = nwg >> 3, r8 = nwg & 7, xc = orig & 7, loc = orig >> 3;
+    int wg = (xc < r8 ? xc * (q8 + 1) : r8 * (q8 + 1) + (xc - r8) * q8) + loc;
+    if (xcd == 2) {   // channel groups fastest: the groups of one tile share the cache lines a group straddles
+      gz = wg % gridDim.z;
+      wg /= gridDim.z;
+      bt = wg % gridDim.x;
+      n = wg / gridDim.x;
+    } else {
+      bt = wg % gridDim.x;
+      wg /= gridDim.x;
+      n = wg % gridDim.y;
+      gz = wg / gridDim.y;
+    }
+  }
+  const int g0 = gz * kDwCG;
   const int ntx = (Wo + kDwTW - 1) / kDwTW;
-  const int ty = blockIdx.x / ntx, tx = blockIdx.x - ty * ntx;
+  const int ty = bt / ntx, tx = bt - ty * ntx;
   const int oy0 = ty * kDwTH, ox0 = tx * kDwTW;
   const int iy0 = oy0 * ST - KS / 2, ix0 = ox0 * ST - KS / 2;
   const int nch = C >> 3;   // 8-channel chunks
@@ -694,7 +718,7 @@ __global__ void __launch_bounds__(256) dwconv_t_kernel(const void* in, int H, in
     for (int r = 1; r < 16; ++r)
 #pragma unroll
       for (int e = 0; e < 4; ++e) gs[e] += red[(r * 16 + qd) * 4 + e];
-    float* gp = gap + ((long long)n * gridDim.x + blockIdx.x) * C + c;
+    float* gp = gap + ((long long)n * gridDim.x + bt) * C + c;
 #pragma unroll
     for (int e = 0; e < 4; ++e) gp[e] = gs[e];
   }
@@ -1062,6 +1086,14 @@ static size_t dw_lds(int KS, int ST) {
   return win > 256 * 4 * sizeof(float) ? win : 256 * 4 * sizeof(float);
 }
 
+// block order of the LDS-tiled kernel (HISEG_DWCONV_XCD, read per call): 2 (default) XCD-major, channel groups
+// fastest; 1 XCD-major, tiles fastest; 0 launched order.  Round 5 (profiles/r5_dwconv_xcd.txt): HBM bytes per launch
+// 309 -> 208 -> 149 MB on the C2 k5 layer (147 MB algorithmic), time equal or better on every layer shape.
+static int dw_xcd_remap() {
+  const char* e = getenv("HISEG_DWCONV_XCD");
+  return e ? atoi(e) : 2;
+}
+
 // the stride-2 windows exceed the default 64 KiB of dynamic LDS (k5: 19 x 35 pixels = 90 KiB)
 template <int KS, int ST>
 static void dw_t_attr() {
@@ -1099,7 +1131,7 @@ static int dwconv_launch(int dtype, const void* in, int N, int H, int W, int C, 
     if (dtype == HISEG_BF16 && dwt) {                                                                         \
       dw_t_attr<KS, ST>();                                                                                    \
       hipLaunchKernelGGL((dwconv_t_kernel<KS, ST>), gridt, dim3(256), dw_lds(KS, ST), s, in, H, W, C, w,      \
-                         scale, shift, act, out, Ho, Wo, gap);                                                \
+                         scale, shift, act, out, Ho, Wo, gap, dw_xcd_remap());                               \
     }                                                                                                         \
     else if (dtype == HISEG_BF16 && dwq)                                                                      \
       hipLaunchKernelGGL((dwconv_q_kernel<KS, ST>), gridq, dim3(256), 0, s, in, H, W, C, w, scale, shift,     \

@@ -1,7 +1,7 @@
 """Depthwise conv timing per EfficientNet layer shape (developer tool, GPU): the automatic choice, the LDS-tiled kernel
 forced for every layer (HISEG_DWCONV_T=2) and the register-gather kernel (HISEG_DWCONV_T=0), HIP events, algorithmic GB/s (input + output read / written once).
 
-Usage: python tools/dw_bench.py [--reps 20]"""
+Usage: python tools/dw_bench.py [--reps 20] [--shapes a,b] [--modes 1,2,0]"""
 import argparse
 import os
 import sys
@@ -23,9 +23,13 @@ SHAPES = [("b7_s2_k3s2_c192", 4, 320, 320, 192, 3, 2), ("b7_s2_k3s1_c288", 4, 16
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--shapes", default="", help="comma-separated shape names (default: all)")
+    ap.add_argument("--modes", default="1,2,0", help="HISEG_DWCONV_T values: 1 auto, 2 LDS tile, 0 gather")
     a = ap.parse_args()
     dt = torch.bfloat16
     for name, N, H, W, C, k, st in SHAPES:
+        if a.shapes and name not in a.shapes.split(","):
+            continue
         x = ops.Act.from_nchw(torch.randn(N, C, H, W, device="cuda"), dt)
         w = (torch.randn(k * k, C, device="cuda") * 0.3).contiguous()
         sc, sh = torch.ones(C, device="cuda"), torch.zeros(C, device="cuda")
@@ -35,7 +39,7 @@ def main():
         Ho, Wo = (H + 2 * (k // 2) - k) // st + 1, (W + 2 * (k // 2) - k) // st + 1
         nbytes = (N * H * W * C + N * Ho * Wo * C) * 2
         row = []
-        for mode in ("1", "2", "0"):
+        for mode in a.modes.split(","):
             os.environ["HISEG_DWCONV_T"] = mode
             for _ in range(3):
                 ops.dwconv_se_gate(x, w, sc, sh, k, st, 3, w1, b1, w2, b2, 3)
