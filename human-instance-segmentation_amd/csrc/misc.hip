@@ -1069,9 +1069,10 @@ static bool dw_use_tiles(int dtype, int C, int K, int stride) {
   const char* e = getenv("HISEG_DWCONV_T");
   const int m = e ? atoi(e) : 1;
   if (dtype != HISEG_BF16 || m == 0 || !dw_q_enabled()) return false;
-  // tools/dw_bench.py (profiles/r4_dw_bench.txt): the tiles win on the 240..1344-channel stride-1 layers and the k5
-  // stride-2 one; the gather kernel on the narrow layers, the k3 stride-2 one and the 20 x 20 x >= 2304-channel ones
-  return m == 2 || (C >= 192 && C < 2048 && (stride == 1 || K == 5));
+  // tools/dw_bench.py (profiles/r4_dw_bench.txt; round 5 with the XCD-major order, profiles/r5_dwconv_xcd.txt): the
+  // tiles win on the 64..1344-channel stride-1 layers and the >= 192-channel k5 stride-2 ones; the gather kernel on
+  // the 32-channel layers, the k3 stride-2 ones, the 144-channel k5 stride-2 one and the 20 x 20 x >= 2304-channel ones
+  return m == 2 || (C < 2048 && ((stride == 1 && C >= 64) || (K == 5 && C >= 192)));
 }
 
 extern "C" int hiseg_dw_gap_parts(int dtype, int N, int Ho, int Wo, int C, int K, int stride) {

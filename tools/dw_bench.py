@@ -17,7 +17,10 @@ SHAPES = [("b7_s2_k3s2_c192", 4, 320, 320, 192, 3, 2), ("b7_s2_k3s1_c288", 4, 16
           ("b7_s4_k3s1_c960", 4, 40, 40, 960, 3, 1), ("b7_s5_k5s1_c1344", 4, 40, 40, 1344, 5, 1),
           ("b7_s6_k5s1_c2304", 4, 20, 20, 2304, 5, 1), ("b7_s7_k3s1_c3840", 4, 20, 20, 3840, 3, 1),
           ("b0_s1_k3s1_c32", 4, 320, 320, 32, 3, 1), ("b0_s3_k5s1_c240", 4, 80, 80, 240, 5, 1),
-          ("c2_b0_s2_k3s1_c144", 32, 120, 160, 144, 3, 1), ("c2_b0_s3_k5s1_c240", 32, 60, 80, 240, 5, 1)]
+          ("c2_b0_s2_k3s1_c144", 32, 120, 160, 144, 3, 1), ("c2_b0_s3_k5s1_c240", 32, 60, 80, 240, 5, 1),
+          ("c2_b0_s1_k3s1_c32", 32, 240, 320, 32, 3, 1), ("c2_b0_s2_k3s2_c96", 32, 240, 320, 96, 3, 2),
+          ("c2_b0_s3_k5s2_c144", 32, 120, 160, 144, 5, 2), ("c2_b0_s4_k3s2_c240", 32, 60, 80, 240, 3, 2),
+          ("c2_b0_s6_k5s1_c1152", 32, 15, 20, 1152, 5, 1), ("b7_s1_k3s1_c64", 4, 320, 320, 64, 3, 1)]
 
 
 def main():
