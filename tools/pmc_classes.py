@@ -5,7 +5,8 @@ Pass 1: rocprofv3 --pmc FETCH_SIZE --kernel-trace -d <dir_f> -o pmc --output-for
 Pass 2: the same with --pmc WRITE_SIZE into <dir_w>.
 HBM bytes per dispatch = (2 * FETCH_SIZE + WRITE_SIZE) KiB (the gfx950 correction of MI355X_MICROARCH.md, as in
 tools/pmc_hbm.py).  Dispatches map to classes by kernel name; steps are counted by the optimizer's commit kernel.
-The two passes must run the same command (same dispatch sequence); dispatches are matched by their index.
+The two passes must run the same command (same dispatch sequence); dispatches are matched by their index in
+Dispatch_Id order (round 5: start-time order differed between passes where two streams interleave).
 
 Usage: python tools/pmc_classes.py <dir_f> <dir_w> [--step-kernel adamw_seg_commit] [--json out.json --leg NAME]
 """
@@ -24,7 +25,7 @@ CLASSES = [   # (class name as in bench.call_profile, kernel-name pattern); firs
 
 def load(d, counter):
     rows = [r for r in csv.DictReader(open(f"{d}/pmc_counter_collection.csv")) if r["Counter_Name"] == counter]
-    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))   # host enqueue order: the same in both passes with two streams
     return [(r["Kernel_Name"], float(r["Counter_Value"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
             for r in rows]
 
