@@ -483,17 +483,36 @@ __global__ void __launch_bounds__(256) dwconv_kernel(const void* in, int H, int 
 template <int KS, int ST>
 __global__ void __launch_bounds__(256) dwconv_q_kernel(const void* in, int H, int W, int C, const float* w,
                                                        const float* scale, const float* shift, int act, void* out,
-                                                       int Ho, int Wo, float* gap, int CT) {
+                                                       int Ho, int Wo, float* gap, int CT, int xcd) {
   constexpr int NIN = (kDwXS - 1) * ST + KS;
   __shared__ float red[256 * 4];
   const int nq = C >> 2;
-  const int g0 = blockIdx.z * CT;
+  // block order as dwconv_t_kernel's (xcd 2: XCD-major, channel groups fastest; 0: launched order)
+  int tile = blockIdx.x, n = blockIdx.y, gz = blockIdx.z;
+  if (xcd) {
+    const int nwg = gridDim.x * gridDim.y * gridDim.z;
+    const int orig = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int q8 = nwg >> 3, r8 = nwg & 7, xc = orig & 7, loc = orig >> 3;
+    int wg = (xc < r8 ? xc * (q8 + 1) : r8 * (q8 + 1) + (xc - r8) * q8) + loc;
+    if (xcd == 2) {
+      gz = wg % gridDim.z;
+      wg /= gridDim.z;
+      tile = wg % gridDim.x;
+      n = wg / gridDim.x;
+    } else {
+      tile = wg % gridDim.x;
+      wg /= gridDim.x;
+      n = wg % gridDim.y;
+      gz = wg / gridDim.y;
+    }
+  }
+  const int g0 = gz * CT;
   const int R = 256 / CT;
   const int t = threadIdx.x;
   const int cl = t % CT, r = t / CT;
   const int q = g0 + cl < nq ? g0 + cl : nq - 1;   // (a ragged last group's spare lanes redo the last quad)
   const bool live = r < R && g0 + cl < nq;
-  const int n = blockIdx.y, tiles = gridDim.x, tile = blockIdx.x;
+  const int tiles = gridDim.x;
   const int sx = (Wo + kDwXS - 1) / kDwXS;
   const int strips = Ho * sx;
   const int s0 = (int)((long long)strips * tile / tiles), s1 = (int)((long long)strips * (tile + 1) / tiles);
@@ -1095,6 +1114,13 @@ static int dw_xcd_remap() {
   return e ? atoi(e) : 2;
 }
 
+// the same for the gather kernel (HISEG_DWCONV_QXCD, read per call; profiles/r5_dwconv_xcd.txt: order 2 cuts its HBM
+// bytes up to 3.2x -- k5 s1 C2 layer 267 -> 83 MB -- and is 1-13 % faster on all but one layer shape, +1 % there)
+static int dw_xcd_remap_q() {
+  const char* e = getenv("HISEG_DWCONV_QXCD");
+  return e ? atoi(e) : 2;
+}
+
 // the stride-2 windows exceed the default 64 KiB of dynamic LDS (k5: 19 x 35 pixels = 90 KiB)
 template <int KS, int ST>
 static void dw_t_attr() {
@@ -1136,7 +1162,7 @@ static int dwconv_launch(int dtype, const void* in, int N, int H, int W, int C, 
     }                                                                                                         \
     else if (dtype == HISEG_BF16 && dwq)                                                                      \
       hipLaunchKernelGGL((dwconv_q_kernel<KS, ST>), gridq, dim3(256), 0, s, in, H, W, C, w, scale, shift,     \
-                         act, out, Ho, Wo, gap, ctq);                                                         \
+                         act, out, Ho, Wo, gap, ctq, dw_xcd_remap_q());                                       \
     else if (dtype != HISEG_BF16)                                                                             \
       hipLaunchKernelGGL((dwconv_kernel<float, KS, ST>), grid, dim3(256), 0, s, in, H, W, C, w, scale, shift,  \
                          act, out, Ho, Wo, gap);                                                              \
