@@ -600,7 +600,7 @@ __global__ void __launch_bounds__(256) dwconv_q_kernel(const void* in, int H, in
 // fused multiply-adds and epilogue -- so the outputs are bit-identical to it.  SE pool: one partial per (image, tile)
 // (hiseg_dw_gap_tiles = ceil(Ho / 8) x ceil(Wo / 16), independent of the batch).
 constexpr int kDwTH = 8, kDwTW = 16, kDwCG = 64, kDwPS = kDwCG * 2 + 8;
-template <int KS, int ST>
+template <int KS, int ST, bool ZP = false>
 __global__ void __launch_bounds__(256) dwconv_t_kernel(const void* in, int H, int W, int C, const float* w,
                                                        const float* scale, const float* shift, int act, void* out,
                                                        int Ho, int Wo, float* gap, int xcd) {
@@ -669,17 +669,27 @@ __global__ void __launch_bounds__(256) dwconv_t_kernel(const void* in, int H, in
   const int c = g0 + qd * 4;
   const bool live = c < C;
   const int cc = live ? c : 0;
-  float wk[KS * KS][4], sc[4], sh[4], gs[4] = {0.f, 0.f, 0.f, 0.f};
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  float wk[ZP ? 1 : KS * KS][4], sc[4], sh[4], gs[4] = {0.f, 0.f, 0.f, 0.f};
+  f2v wp[ZP ? KS * KS : 1][2];   // ZP: the weights as channel pairs (packed-FMA operands)
 #pragma unroll
   for (int k = 0; k < KS * KS; ++k) {
     const float4 f = *reinterpret_cast<const float4*>(w + k * C + cc);
-    wk[k][0] = f.x; wk[k][1] = f.y; wk[k][2] = f.z; wk[k][3] = f.w;
+    if constexpr (ZP) {
+      wp[k][0] = f2v{f.x, f.y};
+      wp[k][1] = f2v{f.z, f.w};
+    } else {
+      wk[k][0] = f.x; wk[k][1] = f.y; wk[k][2] = f.z; wk[k][3] = f.w;
+    }
   }
 #pragma unroll
   for (int e = 0; e < 4; ++e) { sc[e] = scale[cc + e]; sh[e] = shift[cc + e]; }
   // held in registers for both strips (the compiler otherwise re-loads each tap's weights at its use)
 #pragma unroll
-  for (int k = 0; k < KS * KS; ++k) asm volatile("" : "+v"(wk[k][0]), "+v"(wk[k][1]), "+v"(wk[k][2]), "+v"(wk[k][3]));
+  for (int k = 0; k < KS * KS; ++k) {
+    if constexpr (ZP) asm volatile("" : "+v"(wp[k][0]), "+v"(wp[k][1]));
+    else asm volatile("" : "+v"(wk[k][0]), "+v"(wk[k][1]), "+v"(wk[k][2]), "+v"(wk[k][3]));
+  }
   __syncthreads();
   const int nq = C >> 2;
   uint2* dst = reinterpret_cast<uint2*>(out) + (long long)n * Ho * Wo * nq;
@@ -694,8 +704,37 @@ __global__ void __launch_bounds__(256) dwconv_t_kernel(const void* in, int H, in
     for (int xo = 0; xo < kDwXS; ++xo)
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc[xo][e] = 0.f;
+    if constexpr (ZP) {
+      // no per-tap bounds test -- the window holds zeros outside the image, and fma(w, 0, acc) == acc in value (the
+      // sign of an all-zero sum may differ from skipping the tap): straight-line packed FMAs, no exec-mask branches.
+      // Per element the same fma(w, v, acc) chain in the same tap order as below.
+      f2v a2[kDwXS][2];
 #pragma unroll
-    for (int ky = 0; ky < KS; ++ky) {
+      for (int xo = 0; xo < kDwXS; ++xo) a2[xo][0] = a2[xo][1] = f2v{0.f, 0.f};
+#pragma unroll
+      for (int ky = 0; ky < KS; ++ky) {
+        const char* row = dws + ((ry * ST + ky) * IW + rx * ST) * kDwPS + qd * 8;
+#pragma unroll
+        for (int j = 0; j < NIN; ++j) {
+          const uint2 raw = *reinterpret_cast<const uint2*>(row + j * kDwPS);
+          const f2v v01{__uint_as_float(raw.x << 16), __uint_as_float(raw.x & 0xffff0000u)};
+          const f2v v23{__uint_as_float(raw.y << 16), __uint_as_float(raw.y & 0xffff0000u)};
+#pragma unroll
+          for (int xo = 0; xo < kDwXS; ++xo) {
+            const int kx = j - xo * ST;
+            if (kx < 0 || kx >= KS) continue;
+            a2[xo][0] = __builtin_elementwise_fma(wp[ky * KS + kx][0], v01, a2[xo][0]);
+            a2[xo][1] = __builtin_elementwise_fma(wp[ky * KS + kx][1], v23, a2[xo][1]);
+          }
+        }
+      }
+#pragma unroll
+      for (int xo = 0; xo < kDwXS; ++xo) {
+        acc[xo][0] = a2[xo][0].x; acc[xo][1] = a2[xo][0].y; acc[xo][2] = a2[xo][1].x; acc[xo][3] = a2[xo][1].y;
+      }
+    }
+#pragma unroll
+    for (int ky = 0; ky < (ZP ? 0 : KS); ++ky) {
       const int iy = oy * ST - KS / 2 + ky;
       if ((unsigned)iy >= (unsigned)H) continue;
       const char* row = dws + ((ry * ST + ky) * IW + rx * ST) * kDwPS + qd * 8;
@@ -711,7 +750,7 @@ __global__ void __launch_bounds__(256) dwconv_t_kernel(const void* in, int H, in
           const int kx = j - xo * ST;
           if (kx < 0 || kx >= KS) continue;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) acc[xo][e] += wk[ky * KS + kx][e] * v[e];
+          for (int e = 0; e < 4; ++e) acc[xo][e] += wk[ZP ? 0 : ky * KS + kx][e] * v[e];
         }
       }
     }
@@ -1126,10 +1165,19 @@ template <int KS, int ST>
 static void dw_t_attr() {
   static bool done = false;
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)dwconv_t_kernel<KS, ST>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)dwconv_t_kernel<KS, ST, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)dw_lds(KS, ST));
+    (void)hipFuncSetAttribute((const void*)dwconv_t_kernel<KS, ST, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)dw_lds(KS, ST));
     done = true;
   }
+}
+
+// the LDS-tiled kernel without per-tap bounds tests (k3 only: the k5 form's 25 x 2 packed weight pairs plus a row's
+// hoisted reads need 251-256 VGPRs -- 1-2 waves per SIMD, or spills at 3; HISEG_DWCONV_ZP=0: with them; per call, A/B)
+static bool dw_zero_pad(int K) {
+  const char* e = getenv("HISEG_DWCONV_ZP");
+  return K == 3 && !(e && e[0] == '0');
 }
 
 static int dwconv_launch(int dtype, const void* in, int N, int H, int W, int C, int K, int stride, const float* w,
@@ -1157,8 +1205,12 @@ static int dwconv_launch(int dtype, const void* in, int N, int H, int W, int C, 
   do {                                                                                                        \
     if (dtype == HISEG_BF16 && dwt) {                                                                         \
       dw_t_attr<KS, ST>();                                                                                    \
-      hipLaunchKernelGGL((dwconv_t_kernel<KS, ST>), gridt, dim3(256), dw_lds(KS, ST), s, in, H, W, C, w,      \
-                         scale, shift, act, out, Ho, Wo, gap, dw_xcd_remap());                               \
+      if (dw_zero_pad(KS))                                                                                    \
+        hipLaunchKernelGGL((dwconv_t_kernel<KS, ST, true>), gridt, dim3(256), dw_lds(KS, ST), s, in, H, W, C, \
+                           w, scale, shift, act, out, Ho, Wo, gap, dw_xcd_remap());                           \
+      else                                                                                                    \
+        hipLaunchKernelGGL((dwconv_t_kernel<KS, ST, false>), gridt, dim3(256), dw_lds(KS, ST), s, in, H, W,   \
+                           C, w, scale, shift, act, out, Ho, Wo, gap, dw_xcd_remap());                        \
     }                                                                                                         \
     else if (dtype == HISEG_BF16 && dwq)                                                                      \
       hipLaunchKernelGGL((dwconv_q_kernel<KS, ST>), gridq, dim3(256), 0, s, in, H, W, C, w, scale, shift,     \
