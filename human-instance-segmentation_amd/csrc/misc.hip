@@ -727,6 +727,8 @@ __global__ void __launch_bounds__(256) dwconv_t_kernel(const void* in, int H, in
             a2[xo][1] = __builtin_elementwise_fma(wp[ky * KS + kx][1], v23, a2[xo][1]);
           }
         }
+        // k5: one window row's reads live at a time (hoisting all 5 rows' reads took 251-256 VGPRs)
+        if constexpr (KS == 5) __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
       for (int xo = 0; xo < kDwXS; ++xo) {
@@ -1173,11 +1175,13 @@ static void dw_t_attr() {
   }
 }
 
-// the LDS-tiled kernel without per-tap bounds tests (k3 only: the k5 form's 25 x 2 packed weight pairs plus a row's
-// hoisted reads need 251-256 VGPRs -- 1-2 waves per SIMD, or spills at 3; HISEG_DWCONV_ZP=0: with them; per call, A/B)
+// the LDS-tiled kernel without per-tap bounds tests (HISEG_DWCONV_ZP, read per call: 2 (default) every layer, 1 the
+// k3 layers only, 0 none).  Round 5 (profiles/r5_dwconv_xcd.txt): k3 1-18 % faster, k5 20-31 % (its form holds 248-256
+// VGPRs, 1-2 waves per SIMD, and is still faster than the 3-wave form with the branches)
 static bool dw_zero_pad(int K) {
   const char* e = getenv("HISEG_DWCONV_ZP");
-  return K == 3 && !(e && e[0] == '0');
+  const int m = e ? atoi(e) : 2;
+  return m == 2 || (K == 3 && m == 1);
 }
 
 static int dwconv_launch(int dtype, const void* in, int N, int H, int W, int C, int K, int stride, const float* w,
