@@ -480,7 +480,7 @@ __global__ void __launch_bounds__(256) dwconv_kernel(const void* in, int H, int 
 // holds their K*K x 4 weights in registers for all of its strips; a block is CT channel quads x R strip rows
 // (CT chosen on the host to fill the 256 threads), and the strip ranges are longer (hiseg_dw_gap_tiles).  Per
 // output the arithmetic is the kernel above's: same tap order, same fused multiply-adds, same epilogue.
-template <int KS, int ST>
+template <int KS, int ST, bool ZP = false>
 __global__ void __launch_bounds__(256) dwconv_q_kernel(const void* in, int H, int W, int C, const float* w,
                                                        const float* scale, const float* shift, int act, void* out,
                                                        int Ho, int Wo, float* gap, int CT, int xcd) {
@@ -552,7 +552,9 @@ __global__ void __launch_bounds__(256) dwconv_q_kernel(const void* in, int H, in
 #pragma unroll
         for (int j = 0; j < NIN; ++j) {
           const int ix = ix0 + j;
-          if ((unsigned)ix >= (unsigned)W) continue;
+          // ZP: the out-of-image columns were loaded as zeros above and fma(w, 0, acc) == acc in value -- no
+          // exec-mask branch per tap (as dwconv_t_kernel's ZP form)
+          if (!ZP && (unsigned)ix >= (unsigned)W) continue;
           const float v[4] = {__uint_as_float(raw[j].x << 16), __uint_as_float(raw[j].x & 0xffff0000u),
                               __uint_as_float(raw[j].y << 16), __uint_as_float(raw[j].y & 0xffff0000u)};
 #pragma unroll
@@ -1155,6 +1157,14 @@ static int dw_xcd_remap() {
   return e ? atoi(e) : 2;
 }
 
+// the gather kernel without its per-tap column test (HISEG_DWCONV_QZP=0: with it everywhere; read per call, A/B).
+// Round 5 (profiles/r5_dwconv_xcd.txt): 2-10 % faster on the k3 and k5 stride-2 layers; the k5 stride-1 form drops to
+// 2 waves per SIMD (176 VGPRs) and runs 10-33 % slower, so it keeps the test
+static bool dw_zero_pad_q(int K, int stride) {
+  const char* e = getenv("HISEG_DWCONV_QZP");
+  return !(e && e[0] == '0') && (K == 3 || stride == 2);
+}
+
 // the same for the gather kernel (HISEG_DWCONV_QXCD, read per call; profiles/r5_dwconv_xcd.txt: order 2 cuts its HBM
 // bytes up to 3.2x -- k5 s1 C2 layer 267 -> 83 MB -- and is 1-13 % faster on all but one layer shape, +1 % there)
 static int dw_xcd_remap_q() {
@@ -1217,8 +1227,14 @@ static int dwconv_launch(int dtype, const void* in, int N, int H, int W, int C, 
                            C, w, scale, shift, act, out, Ho, Wo, gap, dw_xcd_remap());                        \
     }                                                                                                         \
     else if (dtype == HISEG_BF16 && dwq)                                                                      \
-      hipLaunchKernelGGL((dwconv_q_kernel<KS, ST>), gridq, dim3(256), 0, s, in, H, W, C, w, scale, shift,     \
-                         act, out, Ho, Wo, gap, ctq, dw_xcd_remap_q());                                       \
+    {                                                                                                         \
+      if (dw_zero_pad_q(KS, ST))                                                                              \
+        hipLaunchKernelGGL((dwconv_q_kernel<KS, ST, true>), gridq, dim3(256), 0, s, in, H, W, C, w, scale,    \
+                           shift, act, out, Ho, Wo, gap, ctq, dw_xcd_remap_q());                              \
+      else                                                                                                    \
+        hipLaunchKernelGGL((dwconv_q_kernel<KS, ST, false>), gridq, dim3(256), 0, s, in, H, W, C, w, scale,   \
+                           shift, act, out, Ho, Wo, gap, ctq, dw_xcd_remap_q());                              \
+    }                                                                                                         \
     else if (dtype != HISEG_BF16)                                                                             \
       hipLaunchKernelGGL((dwconv_kernel<float, KS, ST>), grid, dim3(256), 0, s, in, H, W, C, w, scale, shift,  \
                          act, out, Ho, Wo, gap);                                                              \
