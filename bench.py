@@ -1054,9 +1054,82 @@ def main():
                 out["cpu_baseline_train"] = cpu_train_baseline()
                 if not args.no_presets:
                     out["cpu_baseline_train_c3"] = cpu_train_c3_baseline()
-        print(json.dumps(out))
+        emit(out)
     if dist:
         dist.destroy_process_group()
+
+
+LINE_MAX_BYTES = 4096
+_CONTRACT_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                  "scaling", "vs_baseline", "dtype", "data", "config", "pipeline_tflops", "roofline")
+_ROOFLINE_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel_id", "avg_launch_ms",
+                  "launches_timed", "flop_per_launch", "share_of_step")
+_LEGS = ("train", "train_c3", "train_c4", "distill", "distill_unfrozen", "eval", "datapath")
+_LEG_KEYS = ("value", "unit", "ms_per_step", "ms_per_batch", "avg_launch_ms", "pipeline_frac", "roofline")
+_CPU_KEYS = ("value", "unit", "cores", "kind", "sample")
+
+
+def _compact_roofline(r):
+    if not isinstance(r, dict):
+        return r
+    return {k: r[k] for k in _ROOFLINE_KEYS if k in r}
+
+
+def detail_path():
+    """Where the full result object goes (call profiles, per-class tables, top layers, kernel descriptions):
+    $HISEG_BENCH_DETAIL, else gpurun_out/bench_detail.json under the repo root."""
+    return os.environ.get("HISEG_BENCH_DETAIL") or os.path.join(ROOT, "gpurun_out", "bench_detail.json")
+
+
+def compact_line(out, detail=None):
+    """The one stdout JSON line of a full run: the contract keys of the headline (C2) measurement, its roofline
+    and CPU baseline, and per leg only value / unit / time / pipeline_frac / roofline.  Everything else stays in
+    the detail file.  Bounded by LINE_MAX_BYTES (round 5's 22.5 KB line was cut off by the driver's stdout tail);
+    if a pathological result would exceed it, leg rooflines and then legs are dropped, never the headline."""
+    line = {k: out[k] for k in _CONTRACT_KEYS if k in out}
+    if "roofline" in line:
+        line["roofline"] = _compact_roofline(line["roofline"])
+    for k in ("cpu_baseline", "cpu_baseline_train", "cpu_baseline_train_c3"):
+        if isinstance(out.get(k), dict):
+            line[k] = {kk: out[k][kk] for kk in _CPU_KEYS if kk in out[k]}
+    legs = {}
+    for leg in _LEGS:
+        v = out.get(leg)
+        if not isinstance(v, dict):
+            continue
+        c = {k: v[k] for k in _LEG_KEYS if k in v}
+        if "roofline" in c:
+            c["roofline"] = _compact_roofline(c["roofline"])
+        legs[leg] = c
+    if legs:
+        line["legs"] = legs
+    if detail:
+        line["detail"] = os.path.relpath(detail, ROOT) if os.path.isabs(detail) else detail
+    s = json.dumps(line, separators=(",", ":"))
+    for leg in reversed(list(legs)):
+        if len(s.encode()) <= LINE_MAX_BYTES:
+            break
+        legs[leg].pop("roofline", None)
+        s = json.dumps(line, separators=(",", ":"))
+    for key in ("cpu_baseline_train_c3", "cpu_baseline_train", "data", "legs"):
+        if len(s.encode()) <= LINE_MAX_BYTES:
+            break
+        line.pop(key, None)
+        s = json.dumps(line, separators=(",", ":"))
+    return s
+
+
+def emit(out):
+    """Write the full object to the detail file, then print the compact line (rank 0)."""
+    path = detail_path()
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+    except OSError as e:
+        print(f"bench.py: could not write {path}: {e}", file=sys.stderr)
+        path = None
+    print(compact_line(out, path), flush=True)
 
 
 def _leg_in_child(leg, args):
