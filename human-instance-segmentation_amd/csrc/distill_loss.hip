@@ -22,8 +22,19 @@ __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); 
 // torch.clamp semantics: NaN stays NaN (fminf / fmaxf alone would return a bound)
 __device__ __forceinline__ float clampf(float x, float lo, float hi) { return x != x ? x : fminf(fmaxf(x, lo), hi); }
 
+// A captured step's schedule values live on the device (hiseg_distill_cfg.dev_scalars).
+__device__ __forceinline__ void load_dev_scalars(hiseg_distill_cfg& c) {
+  if (c.dev_scalars) {
+    c.temperature = c.dev_scalars[0];
+    c.kl_weight = c.dev_scalars[1];
+    c.task_weight = c.dev_scalars[2];
+    c.pos_weight = c.dev_scalars[3];
+  }
+}
+
 __global__ void __launch_bounds__(256) distill_partial_kernel(hiseg_distill_cfg c, long long HW, const float* s,
                                                               const float* te, const float* y, float* ws) {
+  load_dev_scalars(c);
   __shared__ float red[kDistQ][256];
   const int b = blockIdx.y, sp = blockIdx.x, S = gridDim.x, t = threadIdx.x;
   const long long beg = HW * sp / S, end = HW * (sp + 1) / S;
@@ -67,6 +78,7 @@ __global__ void __launch_bounds__(256) distill_partial_kernel(hiseg_distill_cfg 
 // Coefficient block (after the B*S*Q partials): [0] c_kl, [1] c_mse, [2] c_bce, [3] c_dice,
 // then per sample u_b = 2 / D_b and v_b = N_b / D_b^2 (d coeff_b / d p = y u_b - v_b).
 __global__ void distill_finalize_kernel(hiseg_distill_cfg c, int B, int S, long long HW, float* ws, float* out) {
+  load_dev_scalars(c);
   __shared__ double per[256][3];
   const int t = threadIdx.x;
   double acc[3] = {0, 0, 0};
@@ -134,6 +146,7 @@ __global__ void distill_finalize_kernel(hiseg_distill_cfg c, int B, int S, long 
 __global__ void __launch_bounds__(256) distill_grad_kernel(hiseg_distill_cfg c, int B, int S, long long HW,
                                                            const float* s, const float* te, const float* y,
                                                            const float* ws, const float* gout, float* ds) {
+  load_dev_scalars(c);
   const float* cf = ws + (long long)B * S * kDistQ;
   const float ckl = cf[0], cmse = cf[1], cbce = cf[2], cdice = cf[3];
   const float go = gout[0];

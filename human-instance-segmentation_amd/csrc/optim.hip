@@ -117,7 +117,12 @@ __global__ void __launch_bounds__(256) adamw_seg_kernel(float* p, float* g, floa
                                                         float b1, float b2, float omb1, float omb2, float decay,
                                                         float eps, const float* partial,
                                                         float max_norm, float* norm_out, const long long* seg_start,
-                                                        int nseg, int* steps, int parity, int* skipped) {
+                                                        int nseg, int* steps, int parity, int* skipped,
+                                                        const float* lr_decay) {
+  if (lr_decay) {   // device-resident schedule values (hiseg_adamw_step_segmented_dev): a replayed graph reads them
+    lr = lr_decay[0];
+    decay = lr_decay[1];
+  }
   __shared__ float s_step[kMaxSeg], s_sbc2[kMaxSeg];
   __shared__ long long s_seg[kMaxSeg + 1];
   __shared__ float s_coef;
@@ -193,9 +198,25 @@ extern "C" int hiseg_adamw_step_segmented(float* p, float* g, float* m, float* v
   HISEG_REQUIRE(nseg >= 1 && nseg <= kMaxSeg, HISEG_ERR_BAD_SHAPE, "adamw_step_segmented: 1..256 segments");
   hipLaunchKernelGGL(adamw_seg_kernel, dim3(kOptBlocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, lr, beta1,
                      beta2, one_minus_beta1, one_minus_beta2, decay, eps, partial, max_norm, norm_out, seg_start, nseg,
-                     steps, parity, skipped);
+                     steps, parity, skipped, (const float*)nullptr);
   hipLaunchKernelGGL(adamw_seg_commit_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, steps, nseg, parity);
   return hiseg_check_launch("adamw_step_segmented");
+}
+
+extern "C" int hiseg_adamw_step_segmented_dev(float* p, float* g, float* m, float* v, long long n,
+                                              const float* lr_decay, float beta1, float beta2, float one_minus_beta1,
+                                              float one_minus_beta2, float eps, const float* partial, float max_norm,
+                                              float* norm_out, const long long* seg_start, int nseg, int* steps,
+                                              int parity, int* skipped, hiseg_stream_t stream) {
+  HISEG_REQUIRE(p && g && m && v && n > 0 && lr_decay && partial && seg_start && steps && skipped &&
+                    (parity == 0 || parity == 1),
+                HISEG_ERR_BAD_ARG, "adamw_step_segmented_dev: bad arguments");
+  HISEG_REQUIRE(nseg >= 1 && nseg <= kMaxSeg, HISEG_ERR_BAD_SHAPE, "adamw_step_segmented_dev: 1..256 segments");
+  hipLaunchKernelGGL(adamw_seg_kernel, dim3(kOptBlocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, 0.f, beta1,
+                     beta2, one_minus_beta1, one_minus_beta2, 0.f, eps, partial, max_norm, norm_out, seg_start, nseg,
+                     steps, parity, skipped, lr_decay);
+  hipLaunchKernelGGL(adamw_seg_commit_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, steps, nseg, parity);
+  return hiseg_check_launch("adamw_step_segmented_dev");
 }
 
 extern "C" int hiseg_adamw_step_guarded(float* p, float* g, float* m, float* v, long long n, float lr, float beta1,

@@ -229,7 +229,8 @@ class LossCfg(ctypes.Structure):
 class DistillCfg(ctypes.Structure):
     """include/hiseg_distill.h hiseg_distill_cfg"""
     _fields_ = [(n, c_float) for n in ("temperature", "kl_weight", "task_weight", "pos_weight")] + \
-               [(n, c_int) for n in ("distill_terms", "distill_in_total", "use_dice", "has_target")]
+               [(n, c_int) for n in ("distill_terms", "distill_in_total", "use_dice", "has_target")] + \
+               [("dev_scalars", c_void_p)]
 
 
 DISTILL_NOUT = 5  # include/hiseg_distill.h HISEG_DISTILL_NOUT
@@ -257,6 +258,11 @@ def _declare(lib):
         "hiseg_built_for_gfx950": ([], c_int),
         "hiseg_stream_create_cu_mask": ([ctypes.POINTER(ctypes.c_uint), c_int, ctypes.POINTER(c_void_p)], c_int),
         "hiseg_stream_destroy": ([P], c_int),
+        "hiseg_comm_load": ([ctypes.c_char_p], c_int),
+        "hiseg_comm_unique_id": ([P], c_int),
+        "hiseg_comm_init": ([ctypes.POINTER(c_void_p), c_int, P, c_int, c_int], c_int),
+        "hiseg_comm_all_reduce": ([P, P, c_ll, c_int, c_int, P], c_int),
+        "hiseg_comm_destroy": ([P], c_int),
         "hiseg_roi_align_fwd": ([ctypes.POINTER(RoiAlignDesc), P], c_int),
         "hiseg_conv2d_fwd": ([ctypes.POINTER(Conv2dDesc), P], c_int),
         "hiseg_conv2d_fwd_variant": ([ctypes.POINTER(Conv2dDesc), c_int, P], c_int),
@@ -369,6 +375,8 @@ def _declare(lib):
         "hiseg_placement_stats": ([ctypes.POINTER(c_ll), ctypes.POINTER(c_ll), c_int], c_int),
         "hiseg_adamw_step_segmented": ([P, P, P, P, c_ll, c_float, c_float, c_float, c_float, c_float, c_float,
                                         c_float, P, c_float, P, P, c_int, P, c_int, P, P], c_int),
+        "hiseg_adamw_step_segmented_dev": ([P, P, P, P, c_ll, P, c_float, c_float, c_float, c_float, c_float, P,
+                                            c_float, P, P, c_int, P, c_int, P, P], c_int),
     }
     for name, (argtypes, restype) in sigs.items():
         fn = getattr(lib, name)

@@ -26,6 +26,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib as L
+from . import graphs as _graphs
 
 _DICT_KEYS = ("total_loss", "kl_loss", "mse_loss", "bce_loss", "dice_loss")
 
@@ -102,6 +103,8 @@ class UNetDistillationLoss(nn.Module):
         self.performance_ratio = 1.0
         self.distillation_eliminated = False
         self.pos_weight_value = float(np.sqrt((1.0 - fg_ratio) / fg_ratio))
+        self._dev: Optional[torch.Tensor] = None   # device f32 [T, kl_weight, task_weight, pos_weight]
+        self._dev_vals = None
 
     # -- schedules (host state, once per epoch: :366-469)
     def update_temperature(self, current_epoch: int, total_epochs: int, final_temperature: float = 1.0,
@@ -164,6 +167,28 @@ class UNetDistillationLoss(nn.Module):
         c.has_target = int(has_target)
         return c
 
+    # ---------------------------------------------------------------- device scalars (hiseg.graphs)
+    def sync_device_scalars(self, device=None):
+        """Write the schedule values (temperature, effective KL weight, task weight, pos weight) into the device
+        buffer the loss kernels read, when they changed; GraphedStep calls this before every replay, so the
+        per-epoch temperature schedule (train_distillation_staged.py:1597-1610) replays one captured graph."""
+        c = self._cfg(True)
+        vals = (c.temperature, c.kl_weight, c.task_weight, c.pos_weight)   # already rounded to f32
+        if self._dev is None or (device is not None and self._dev.device != torch.device(device)):
+            self._dev = torch.empty(4, dtype=torch.float32, device=device)
+            self._dev_vals = None
+        if vals != self._dev_vals:
+            for i, v in enumerate(vals):
+                self._dev[i].fill_(v)
+            self._dev_vals = vals
+        return self._dev
+
+    def graph_key(self):
+        """What a captured step bakes in: which terms run and enter the total (structure, not values)."""
+        c = self._cfg(True)
+        return (c.distill_terms, c.distill_in_total, c.use_dice,
+                self._dev.data_ptr() if self._dev is not None else None)
+
     def forward(self, student_output: torch.Tensor, teacher_output: torch.Tensor,
                 target_masks: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Dict[str, float]]:
         if not student_output.is_cuda:
@@ -174,7 +199,15 @@ class UNetDistillationLoss(nn.Module):
         if s.dim() != 4 or s.shape[1] != 1 or t.shape != s.shape or (y is not None and y.numel() != s.numel()):
             raise ValueError(f"distillation loss: student {tuple(s.shape)} teacher {tuple(t.shape)} "
                              f"target {None if y is None else tuple(y.shape)} (expect [B,1,H,W])")
-        total, out = _DistillLossFn.apply(self._cfg(y is not None), s, t, y)
+        cfg = self._cfg(y is not None)
+        if torch.cuda.is_current_stream_capturing():
+            if self._dev is None or self._dev.device != s.device:
+                raise RuntimeError("UNetDistillationLoss: the first call cannot be captured (run it eagerly first)")
+            _graphs.note_device_scalars(self)
+        else:
+            self.sync_device_scalars(s.device)
+        cfg.dev_scalars = self._dev.data_ptr()
+        total, out = _DistillLossFn.apply(cfg, s, t, y)
         return total, _LazyDict(out, _DICT_KEYS)
 
     def dice_loss(self, pred: torch.Tensor, target: torch.Tensor) -> torch.Tensor:

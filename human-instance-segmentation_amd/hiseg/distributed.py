@@ -27,6 +27,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from . import comm as _comm
 from .streams import role_stream
 
 _SYNC_KEY = "_hiseg_grad_sync"
@@ -50,6 +51,7 @@ class GradBucketSync:
         self.recording: Optional[Dict[int, int]] = None
         self.launched: List[int] = []                     # bucket launch order of the last backward
         self.comm_stream = None
+        self.comm: Optional[_comm.Communicator] = None   # libhiseg's RCCL communicator (nccl groups, GPU grads)
         self.steps = 0
 
     # -- layout
@@ -73,6 +75,8 @@ class GradBucketSync:
         self.last_op, self.launch_after = None, {}
         dev = flat.grad.device
         self.comm_stream = role_stream("comm", dev) if dev.type == "cuda" else None
+        if self.comm is None and _comm.uses_rccl(self.pg, flat.grad):
+            self.comm = _comm.communicator(self.pg, dev)
 
     # -- tape callbacks (train_engine.Tape.run_backward)
     def begin(self, n_ops: int):
@@ -105,7 +109,9 @@ class GradBucketSync:
         self.steps += 1
 
     def _reduce(self, view: torch.Tensor):
-        if self.avg_in_collective:
+        if self.comm is not None:   # RCCL through libhiseg: an enqueue on the current stream, nothing tracked
+            self.comm.all_reduce_(view, _comm.AVG)
+        elif self.avg_in_collective:
             dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.pg)
         else:
             dist.all_reduce(view, group=self.pg)
@@ -136,13 +142,20 @@ def enable_grad_sync(model: nn.Module, process_group=None, bucket_mb: float = 25
             for t in list(model.parameters()) + list(model.buffers()):
                 dist.broadcast(t.data, broadcast_from, group=process_group)
     sync = GradBucketSync(process_group, bucket_mb)
+    p0 = next(iter(model.parameters()), None)
+    if p0 is not None and _comm.uses_rccl(process_group, p0):   # collective: every rank is here together
+        sync.comm = _comm.communicator(process_group, p0.device)
     model.__dict__[_SYNC_KEY] = sync
     return sync
 
 
 def all_reduce_counts(counts: torch.Tensor, process_group=None) -> torch.Tensor:
-    """Sum a count vector over the process group in place (float64; RCCL on the GPU, gloo on the CPU)."""
-    dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=process_group)
+    """Sum a count vector over the process group in place (float64; libhiseg's RCCL communicator on the GPU -- the
+    step that calls this may be under graph capture -- gloo on the CPU)."""
+    if _comm.uses_rccl(process_group, counts):
+        _comm.communicator(process_group, counts.device).all_reduce_(counts, _comm.SUM)
+    else:
+        dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=process_group)
     return counts
 
 
@@ -154,6 +167,8 @@ def sync_loss_class_weights(loss_fn: nn.Module, process_group=None) -> nn.Module
     weights a single process would compute on the concatenated batch."""
     if not dist.is_initialized():
         raise RuntimeError("hiseg.distributed: torch.distributed is not initialised")
+    if _comm.uses_rccl(process_group) and torch.cuda.is_available():
+        _comm.communicator(process_group)   # collective creation here, where every rank calls together
     loss_fn.count_sync = lambda c: all_reduce_counts(c, process_group)
     return loss_fn
 

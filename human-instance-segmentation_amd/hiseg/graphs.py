@@ -8,8 +8,14 @@ into a HIP graph (torch.cuda.graph on the step's stream) and replays it: one lau
 Every piece of per-step state the kernels use lives on the device, so a replayed step is the next step:
 the Dropout2d seed base (TrainState.begin_step), the loss's dynamic-weight EMA, FusedAdamW's step count and
 skip counter (fixed slot, committed by the library).  Host-side values are frozen into the graph: the
-learning rate, the inputs' addresses (the step must read the same input tensors, refilled in place between
-steps) and the shapes -- GraphedStep re-captures when the optimizer's learning rate changes.
+inputs' addresses (the step must read the same input tensors, refilled in place between steps) and the shapes.
+Schedule values are not host-side: FusedAdamW's learning rate (and decay factor) and UNetDistillationLoss's
+temperature / weights live in small device buffers the kernels read at run time ("device-scalar owners").  An owner
+used while a step is being captured registers with it (note_device_scalars); before every replay GraphedStep has
+each owner write its current values (sync_device_scalars: a fill on the replay stream when they changed), so a
+per-epoch LR or temperature schedule replays the same graph.  Only an owner's structural state (graph_key: e.g.
+the distillation terms switched off) and an optimizer without device scalars (its learning rate) force a
+re-capture.
 
 The graph also holds raw pointers to the optimizer's buffers (moments, step counts, norm partials), the
 model's flat parameters and its conv packing table.  Anything that re-allocates them -- a new optimizer
@@ -27,24 +33,32 @@ process groups cannot be captured (host-side reduction): keep such steps eager.
 """
 from __future__ import annotations
 
-from typing import Callable, Optional
+from typing import Callable, List, Optional
 
 import torch
 
 from .streams import role_stream
 
+_capture_owners: Optional[List] = None
 
-def _drain_rccl_watchdog():
-    """Before a capture in a process with an RCCL process group: give its watchdog thread one poll (every 100 ms) to
-    retire the finished eager collectives.  It queries each tracked collective's end event, and the process group
-    reuses finished collectives' events for the ones recorded during the capture: a poll that reaches a retired
-    collective after its event was re-recorded in the capturing stream fails with hipErrorCapturedEvent and aborts
-    the process (seen once in a full GPU suite run, test_graphed_ddp_step_rccl_world1_equals_eager after 150 other
-    tests; profiles/r5_gpu_suite.txt)."""
-    import time
-    import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
-        time.sleep(0.3)
+
+def note_device_scalars(owner) -> None:
+    """Called by a device-scalar owner (``sync_device_scalars()`` / ``graph_key()``) whenever its kernels are
+    enqueued: during a GraphedStep capture it joins that step's owners (synced before every replay)."""
+    if _capture_owners is not None and all(o is not owner for o in _capture_owners):
+        _capture_owners.append(owner)
+
+
+class _CaptureOwners:
+    def __enter__(self):
+        global _capture_owners
+        self.prev, _capture_owners = _capture_owners, []
+        return _capture_owners
+
+    def __exit__(self, *exc):
+        global _capture_owners
+        _capture_owners = self.prev
+        return False
 
 
 class GraphedStep:
@@ -66,13 +80,34 @@ class GraphedStep:
         self.lr = None
         self.captures = 0
         self.fp = None
+        self.owners: List = []
+        self.keys = None
 
     def _opt(self):
         return self.opt_fn() if self.opt_fn is not None else None
 
+    def invalidate(self):
+        """Drop the captured graph(s): the next call captures anew (after no further eager steps)."""
+        self.graph = None
+        if hasattr(self, "graphs"):
+            self.graphs = None
+
     def _lr(self):
+        """The host learning rates baked into a capture: none for an optimizer that keeps them on the device."""
         o = self._opt()
-        return None if o is None else tuple(g["lr"] for g in o.param_groups)
+        if o is None or hasattr(o, "sync_device_scalars"):
+            return None
+        return tuple(g["lr"] for g in o.param_groups)
+
+    def _keys(self):
+        return tuple(o.graph_key() for o in self.owners)
+
+    def _stale(self, captured) -> bool:
+        return captured is None or self._lr() != self.lr or self._keys() != self.keys
+
+    def _sync_owners(self):
+        for o in self.owners:
+            o.sync_device_scalars()
 
     def _fingerprint(self):
         """Identities / addresses of the device state a captured step reads and writes."""
@@ -109,22 +144,24 @@ class GraphedStep:
                 out = self.fn()
             torch.cuda.current_stream().wait_stream(s)
             return out
-        if self.graph is None or self._lr() != self.lr:
+        if self._stale(self.graph):
             self.graph = None
             torch.cuda.synchronize()
-            _drain_rccl_watchdog()
             before = self._fingerprint()
             g = torch.cuda.CUDAGraph()
-            # thread-local capture: RCCL's watchdog thread polls the events of earlier collectives while the step
-            # is being captured, which the default (global) mode turns into a capture error in that thread
-            with torch.cuda.graph(g, stream=role_stream("capture"), capture_error_mode="thread_local"):
-                self.out = self.fn()
+            # thread-local capture: another thread's CUDA calls (a process group's watchdog, a data loader) are not
+            # a capture error; the step itself issues no torch.distributed call (hiseg.comm)
+            with _CaptureOwners() as owners:
+                with torch.cuda.graph(g, stream=role_stream("capture"), capture_error_mode="thread_local"):
+                    self.out = self.fn()
+            self.owners, self.keys = owners, tuple(o.graph_key() for o in owners)
             self.fp = self._fingerprint()
             if self.fp != before:
                 raise RuntimeError("GraphedStep: the step re-allocated optimizer / model state while it was being "
                                    "captured; run more eager steps first (GraphedStep(..., eager=N))")
             self.graph, self.lr = g, self._lr()
             self.captures += 1
+        self._sync_owners()
         self.graph.replay()
         o = self._opt()
         bump = getattr(o, "_bump", None)
@@ -193,18 +230,19 @@ class GraphedBranchStep(GraphedStep):
                 out = self.fn()
             main.wait_stream(s)
             return out
-        if self.graphs is None or self._lr() != self.lr:
+        if self._stale(self.graphs):
             self.graphs = None
             torch.cuda.synchronize()
-            _drain_rccl_watchdog()
             before = self._fingerprint()
             gb, gh, gt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gb, stream=side, capture_error_mode="thread_local"):
-                self.branch_fn()
-            with torch.cuda.graph(gh, stream=role_stream("capture"), capture_error_mode="thread_local"):
-                self.head_fn()
-            with torch.cuda.graph(gt, stream=role_stream("capture"), capture_error_mode="thread_local"):
-                self.out = self.fn()
+            with _CaptureOwners() as owners:
+                with torch.cuda.graph(gb, stream=side, capture_error_mode="thread_local"):
+                    self.branch_fn()
+                with torch.cuda.graph(gh, stream=role_stream("capture"), capture_error_mode="thread_local"):
+                    self.head_fn()
+                with torch.cuda.graph(gt, stream=role_stream("capture"), capture_error_mode="thread_local"):
+                    self.out = self.fn()
+            self.owners, self.keys = owners, tuple(o.graph_key() for o in owners)
             self.fp = self._fingerprint()
             if self.fp != before:
                 raise RuntimeError("GraphedBranchStep: the step re-allocated optimizer / model state while it was "
@@ -212,6 +250,7 @@ class GraphedBranchStep(GraphedStep):
             self.graphs, self.lr = (gb, gh, gt), self._lr()
             self.captures += 1
         gb, gh, gt = self.graphs
+        self._sync_owners()   # on the caller's stream: before the head / tail graphs that read them
         side.wait_stream(main)   # the previous step's tail (or this step's handoff) is done with the branch buffers
         with torch.cuda.stream(side):
             gb.replay()

@@ -16,6 +16,7 @@ from typing import Optional
 import torch
 
 from . import _lib as L
+from . import graphs as _graphs
 
 
 def flat_params_of(model: torch.nn.Module):
@@ -157,6 +158,27 @@ class FusedAdamW(torch.optim.Optimizer):
         self._skipped: Optional[torch.Tensor] = None
         self._pending_state = None
         self._bump = None
+        self._hyper: Optional[torch.Tensor] = None    # device f32 [lr, 1 - lr wd] (hiseg_adamw_step_segmented_dev)
+        self._hyper_vals = None
+
+    # ---------------------------------------------------------------- device scalars (hiseg.graphs)
+    def sync_device_scalars(self):
+        """Write the current learning rate and decay factor into the device buffer the step kernel reads, when they
+        changed (a fill on the current stream: no host sync); GraphedStep calls this before every replay."""
+        g0 = self.param_groups[0]
+        lr = float(g0["lr"])
+        vals = (lr, 1.0 - lr * float(g0["weight_decay"]))   # rounded to f32 by the fill, as by a c_float argument
+        dev = self._flat.data.device if self._flat is not None else None
+        if self._hyper is None or (dev is not None and self._hyper.device != dev):
+            self._hyper = torch.empty(2, dtype=torch.float32, device=dev)
+            self._hyper_vals = None
+        if vals != self._hyper_vals:
+            self._hyper[0].fill_(vals[0])
+            self._hyper[1].fill_(vals[1])
+            self._hyper_vals = vals
+
+    def graph_key(self):
+        return (self._hyper.data_ptr() if self._hyper is not None else None,)
 
     @property
     def lr(self) -> float:
@@ -311,20 +333,26 @@ class FusedAdamW(torch.optim.Optimizer):
         f.prepare_backward()  # adopt any .grad tensors replaced since the backward
         lib = L.lib()
         g0 = self.param_groups[0]
-        lr = g0["lr"]
         b1, b2 = g0["betas"]
-        eps, wd = g0["eps"], g0["weight_decay"]
+        eps = g0["eps"]
         s = L.stream_ptr()
         clip = self.max_grad_norm is not None and self.max_grad_norm > 0
         b, e = self._range
         gp, dp = f.grad.data_ptr() + 4 * b, f.data.data_ptr() + 4 * b
         L.check(lib.hiseg_grad_norm_partials(gp, e - b, self.partial.data_ptr(), s), "grad_norm")
-        L.check(lib.hiseg_adamw_step_segmented(dp, gp, self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), e - b,
-                                               float(lr), float(b1), float(b2), 1.0 - float(b1), 1.0 - float(b2),
-                                               1.0 - float(lr) * float(wd), float(eps),
-                                               self.partial.data_ptr(), float(self.max_grad_norm) if clip else 0.0,
-                                               self.last_norm.data_ptr(), self._seg_start.data_ptr(), self._nseg,
-                                               self._steps.data_ptr(), self._parity, self._skipped.data_ptr(), s),
+        # lr and 1 - lr wd come from the device buffer: a captured step follows the schedule without a re-capture
+        if torch.cuda.is_current_stream_capturing():
+            if self._hyper is None:
+                raise RuntimeError("FusedAdamW: the first step cannot be captured (run it eagerly first)")
+            _graphs.note_device_scalars(self)
+        else:
+            self.sync_device_scalars()
+        L.check(lib.hiseg_adamw_step_segmented_dev(dp, gp, self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), e - b,
+                                                   self._hyper.data_ptr(), float(b1), float(b2), 1.0 - float(b1),
+                                                   1.0 - float(b2), float(eps), self.partial.data_ptr(),
+                                                   float(self.max_grad_norm) if clip else 0.0,
+                                                   self.last_norm.data_ptr(), self._seg_start.data_ptr(), self._nseg,
+                                                   self._steps.data_ptr(), self._parity, self._skipped.data_ptr(), s),
                 "adamw_step")
         # the count stays in slot _parity (the library commits it): no host-side state changes per step, so the
         # whole step can be captured into a HIP graph (hiseg.graphs.GraphedStep)

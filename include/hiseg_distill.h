@@ -34,6 +34,10 @@ typedef struct hiseg_distill_cfg {
   int distill_in_total;   /* 0: distillation_loss = 0 in the total (alpha == 0 with adaptive, or tw >= 0.99) */
   int use_dice;
   int has_target;
+  /* optional device f32[4] {temperature, kl_weight, task_weight, pos_weight}: when non-null the kernels read these
+   * four at run time instead of the fields above (a captured distillation step follows the per-epoch temperature
+   * schedule, train_distillation_staged.py:1597-1610, without a re-capture); the host fields still pass the checks */
+  const float* dev_scalars;
 } hiseg_distill_cfg;
 
 enum { HISEG_DISTILL_TOTAL = 0, HISEG_DISTILL_KL, HISEG_DISTILL_MSE, HISEG_DISTILL_BCE, HISEG_DISTILL_DICE,

@@ -297,6 +297,14 @@ int hiseg_adamw_step_segmented(float* p, float* g, float* m, float* v, long long
                                float beta2, float one_minus_beta1, float one_minus_beta2, float decay, float eps,
                                const float* partial, float max_norm, float* norm_out, const long long* seg_start,
                                int nseg, int* steps, int parity, int* skipped, hiseg_stream_t stream);
+/* The segmented step with the learning rate and the decoupled decay factor on the device: lr_decay[0] = lr,
+ * lr_decay[1] = 1 - lr * weight_decay (rounded from double on the host), read by the kernel at run time, so a HIP
+ * graph that captured the step follows a learning-rate schedule (CosineAnnealingLR, train_advanced.py:1126-1131,
+ * stepped per epoch at :1633) by a device write before its replay, without a re-capture. */
+int hiseg_adamw_step_segmented_dev(float* p, float* g, float* m, float* v, long long n, const float* lr_decay,
+                                   float beta1, float beta2, float one_minus_beta1, float one_minus_beta2, float eps,
+                                   const float* partial, float max_norm, float* norm_out, const long long* seg_start,
+                                   int nseg, int* steps, int parity, int* skipped, hiseg_stream_t stream);
 
 #ifdef __cplusplus
 }

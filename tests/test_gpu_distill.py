@@ -401,3 +401,77 @@ def test_pipelined_teacher_equals_serial_step():
     assert len(set(l0.tolist())) == nstep   # different batches, different losses
     assert torch.equal(l0, l1), (l0, l1)
     assert all(torch.equal(a, b) for a, b in zip(p0, p1))
+
+
+@pytest.mark.parametrize("branch", [False, True])
+def test_temperature_and_lr_schedule_replay_one_graph(branch, monkeypatch):
+    """the staged distillation's per-epoch schedules -- temperature 4 -> 1
+    (UNetDistillationLoss.update_temperature, train_distillation_staged.py:1597-1610) and a cosine learning rate
+    (:1126-1131 style) -- are device scalars a captured step reads, so 4 epochs x 2 steps replay ONE graph
+    (GraphedStep and GraphedBranchStep), with losses and student parameters bit-identical to eager steps."""
+    import math
+    import filler
+    import hiseg
+    from hiseg.distill import DistillationUNetWrapper
+    x = torch.from_numpy(filler.normal(45, (2, 3, 128, 128))).to(DEV)
+    _, _, m = __import__("oracle.distill", fromlist=["np_inputs"]).np_inputs(46, 2, 128, 128)
+    m = m.to(DEV)
+    epochs, per_epoch = 4, 2
+    res = {}
+    for graphed in (False, True):
+        monkeypatch.setattr(DistillationUNetWrapper, "concurrent_teacher", False)
+        model, loss_fn = _distill_model(torch.bfloat16)
+        loss_fn.initial_temperature = loss_fn.temperature = 4.0
+        loss_fn.alpha = loss_fn.initial_alpha = 0.5
+        loss_fn.task_weight = loss_fn.initial_task_weight = 0.5
+        model = model.to(DEV).train()
+        state = {"opt": None}
+        fwd = {}
+
+        def opt():
+            if state["opt"] is None:
+                state["opt"] = hiseg.FusedAdamW(model.student, lr=1e-3, weight_decay=1e-4, max_grad_norm=1.0,
+                                                params=model.student.get_decoder_parameters())
+            return state["opt"]
+
+        def tail():
+            loss, _ = loss_fn(fwd["s"], fwd["t"], m)
+            o = opt()
+            o.zero_grad()
+            loss.backward()
+            o.step()
+            return loss
+
+        def teacher():
+            fwd["t"] = model.teacher(x)
+
+        def student():
+            fwd["s"] = model.student(x)
+
+        def serial():
+            fwd["s"], fwd["t"] = model(x)
+            return tail()
+
+        if not graphed:
+            run = serial
+        elif branch:
+            run = hiseg.GraphedBranchStep(teacher, student, tail, lambda: state["opt"])
+        else:
+            run = hiseg.GraphedStep(serial, lambda: state["opt"])
+        losses, temps = [], []
+        for e in range(epochs):
+            temps.append(loss_fn.update_temperature(e, epochs, final_temperature=1.0))
+            if state["opt"] is not None:
+                for g in state["opt"].param_groups:
+                    g["lr"] = 1e-3 * 0.5 * (1 + math.cos(math.pi * e / epochs))
+            for _ in range(per_epoch):
+                losses.append(run().detach().clone())
+        torch.cuda.synchronize()
+        if graphed:
+            assert run.captures == 1, run.captures
+        res[graphed] = (torch.stack(losses), [p.detach().clone() for p in model.student.parameters()])
+    assert temps == [4.0, 3.0, 2.0, 1.0]
+    (l0, p0), (l1, p1) = res[False], res[True]
+    assert torch.isfinite(l0).all()
+    assert torch.equal(l0, l1), (l0, l1)
+    assert all(torch.equal(a, b) for a, b in zip(p0, p1))
