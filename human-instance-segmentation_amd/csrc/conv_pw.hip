@@ -73,20 +73,57 @@ __global__ void __launch_bounds__(256, 1) conv_pw_kernel(ConvArgs a, int nct, in
   float* ssc = reinterpret_cast<float*>(smem + CT * ROWC);
   float* ssh = ssc + CT;
   float* gl = ssh + CT;
-  const uint4* wg = reinterpret_cast<const uint4*>(d.weight);
+  // Staged kPwStage chunks per thread at a time, all loads of a round issued before its LDS stores: a rolled
+  // load -> store loop waits out one L2/HBM latency per 16-B chunk, 28 times over for a 224-channel 256-column
+  // tile, which cost the EfficientNet layers (a few 32-pixel blocks per wave) 20-40 us per launch.  Loads past
+  // the tile (or past Cout_pad) are OOB buffer reads: zeros, no branches.
+  constexpr int kPwStage = 8;
   const int kc = d.K_pad >> 3;                 // 16-B chunks per global weight row
   const int wch = nks * 4;                     // chunks per row that are used
-  for (int i = t; i < CT * wch; i += 256) {
-    const int r = i / wch, c = i - r * wch;
-    wl[r * ROWC + c] = c0 + r < d.Cout_pad ? wg[(long long)(c0 + r) * kc + c] : make_uint4(0u, 0u, 0u, 0u);
+  const int nchunk = CT * wch;
+  {
+    const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<void*>(d.weight), (short)0, (int)((long long)d.Cout_pad * kc * 16), 0x00020000);
+    for (int i0 = t; i0 < nchunk; i0 += 256 * kPwStage) {
+      pw_u4 v[kPwStage];
+#pragma unroll
+      for (int u = 0; u < kPwStage; ++u) {
+        const int i = i0 + 256 * u;
+        const int r = i / wch, c = i - r * wch;
+        const unsigned off = i < nchunk ? (unsigned)(((c0 + r) * kc + c) * 16) : 0x80000000u;
+        v[u] = __builtin_amdgcn_raw_buffer_load_b128(rW, off, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < kPwStage; ++u) {
+        const int i = i0 + 256 * u;
+        const int r = i / wch, c = i - r * wch;
+        if (i < nchunk) wl[r * ROWC + c] = make_uint4(v[u].x, v[u].y, v[u].z, v[u].w);
+      }
+    }
   }
   for (int i = t; i < CT; i += 256) {
     const int j = c0 + i < d.Cout ? c0 + i : 0;
     ssc[i] = d.scale[j];
     ssh[i] = d.shift[j];
   }
-  if constexpr (INS) {
-    for (int i = t; i < d.N * d.Ca; i += 256) gl[i] = d.in_scale[i];
+  if constexpr (INS) {   // the gate table [N][Ca] f32, 16-B aligned, N Ca a multiple of 8: float4 chunks, staged
+    const int n4 = d.N * d.Ca / 4;
+    const __amdgpu_buffer_rsrc_t rG = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(d.in_scale), (short)0, (int)(n4 * 16), 0x00020000);
+    float4* gl4 = reinterpret_cast<float4*>(gl);
+    for (int i0 = t; i0 < n4; i0 += 256 * kPwStage) {
+      pw_u4 v[kPwStage];
+#pragma unroll
+      for (int u = 0; u < kPwStage; ++u) {
+        const int i = i0 + 256 * u;
+        v[u] = __builtin_amdgcn_raw_buffer_load_b128(rG, i < n4 ? (unsigned)(i * 16) : 0x80000000u, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < kPwStage; ++u) {
+        const int i = i0 + 256 * u;
+        if (i < n4) gl4[i] = __builtin_bit_cast(float4, v[u]);
+      }
+    }
   }
   __syncthreads();
 

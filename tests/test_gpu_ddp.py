@@ -471,7 +471,7 @@ def test_hiseg_comm_all_reduce_world1_eager_and_captured():
             for _ in range(3):
                 g.replay()
             torch.cuda.synchronize()
-            assert torch.equal(x, ref * 16)
+            assert torch.equal(x, ref * 8)   # three replays of x *= 2 (capture itself runs nothing)
         with pytest.raises(RuntimeError, match="f32/f64"):
             c.all_reduce_(torch.zeros(4, dtype=torch.bfloat16, device=DEV))
     finally:
