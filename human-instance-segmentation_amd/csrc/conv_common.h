@@ -16,6 +16,7 @@ struct ConvArgs {
   int kper;    // split-K: K blocks per split (grid.z = splits); nK when unsplit
   int ins_vec; // in_scale rows 16-B aligned (vector gate loads)
   float* ws;   // split-K workspace [splits][M][Cout_pad] f32
+  int abl = 0; // DIAG builds only: ablation bits of a timing variant (parts of a kernel switched off)
 };
 
 template <typename T>

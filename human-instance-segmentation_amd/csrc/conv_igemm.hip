@@ -699,7 +699,7 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
   if (variant == 98) {
     const int r = conv_rows_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
-  } else if (variant == 90) {
+  } else if (variant == 90 || (variant >= 190 && variant < 222)) {
     const int r = conv_pw_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
   } else if ((variant >= 92 && variant <= 97) || variant == 100 || variant == 101 || (variant >= 110 && variant < 142)) {

@@ -66,6 +66,11 @@ __global__ void __launch_bounds__(256, 1) conv_pw_kernel(ConvArgs a, int nct, in
   const int grp = blockIdx.x / nct, ngrp = gridDim.x / nct;
   const int c0 = ct * CT;
   const int act = ACT == kPwActRt ? d.act : ACT;
+#ifdef HISEG_DIAG
+  const int abl = a.abl;   // timing ablations (variants 190-221): 1 staging, 2 loads, 4 MFMAs, 8 epilogue math, 16 stores
+#else
+  constexpr int abl = 0;
+#endif
 
   // ---- weights of the column tile -> LDS (row r, chunk c at r * ROWC + c; rows past Cout_pad zero); scale /
   // shift after them, then (INS) the gate table [N][Ca]
@@ -84,7 +89,7 @@ __global__ void __launch_bounds__(256, 1) conv_pw_kernel(ConvArgs a, int nct, in
   {
     const __amdgpu_buffer_rsrc_t rW = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<void*>(d.weight), (short)0, (int)((long long)d.Cout_pad * kc * 16), 0x00020000);
-    for (int i0 = t; i0 < nchunk; i0 += 256 * kPwStage) {
+    for (int i0 = t; i0 < ((abl & 1) ? 0 : nchunk); i0 += 256 * kPwStage) {
       pw_u4 v[kPwStage];
 #pragma unroll
       for (int u = 0; u < kPwStage; ++u) {
@@ -147,6 +152,10 @@ __global__ void __launch_bounds__(256, 1) conv_pw_kernel(ConvArgs a, int nct, in
 
   // B fragments of block b: lane (g, pl) holds pixel b*32 + 16j + pl, channels 32 ks + 8 g .. + 7
   auto load_ks = [&](int b, int ks, uint4 (&bk)[2]) __attribute__((always_inline)) {
+    if (abl & 2) {
+      bk[0] = bk[1] = make_uint4(0u, 0u, 0u, 0u);
+      return;
+    }
     const bool ch_ok = 32 * ks + 8 * g < d.Ca;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -250,6 +259,7 @@ __global__ void __launch_bounds__(256, 1) conv_pw_kernel(ConvArgs a, int nct, in
       if (ks >= nks) continue;
 #pragma unroll
       for (int i = 0; i < RB; ++i) {
+        if (abl & 4) continue;
         const uint4 af = wrow[16 * i * ROWC + 4 * ks];
         acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af),
                                                             __builtin_bit_cast(bf16x8_t, bf[ks][0]), acc[i][0], 0, 0, 0);
@@ -268,6 +278,10 @@ __global__ void __launch_bounds__(256, 1) conv_pw_kernel(ConvArgs a, int nct, in
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
+          if (abl & 8) {
+            v[e] = acc[i][j][e];
+            continue;
+          }
           v[e] = acc[i][j][e] * sc[e] + sh[e];
           if constexpr (RES) v[e] += Quad<bf16_t>::get(make_uint2(rv[i][j].x, rv[i][j].y), e);
           v[e] = apply_act(v[e], act);
@@ -276,7 +290,7 @@ __global__ void __launch_bounds__(256, 1) conv_pw_kernel(ConvArgs a, int nct, in
         pw_u2 q;
         q.x = f2bf2(v[0], v[1]);
         q.y = f2bf2(v[2], v[3]);
-        __builtin_amdgcn_raw_buffer_store_b64(q, rO, offset(j, i, d.o_cstride, d.o_coff), 0, 0);
+        if (!(abl & 16)) __builtin_amdgcn_raw_buffer_store_b64(q, rO, offset(j, i, d.o_cstride, d.o_coff), 0, 0);
       }
     }
   };
@@ -406,6 +420,13 @@ static bool pw_plan(const ConvArgs& a, int& rb, int& nks, int& nks_max) {
   // up to 320 channels (the B7 encoder's 288-channel SE-gated projections)
   rb = 16;
   if (d.Cout_pad <= 128) rb = d.Cout_pad <= 16 ? 1 : d.Cout_pad <= 32 ? 2 : d.Cout_pad <= 64 ? 4 : 8;
+  {
+    // HISEG_PW_RB=1|2|4|8 (read once; A/B timing): wide layers on narrow column tiles where that form exists
+    static const int force_rb = [] { const char* e = getenv("HISEG_PW_RB"); return e ? atoi(e) : 0; }();
+    if (rb == 16 && (force_rb == 1 || force_rb == 2 || force_rb == 4 || force_rb == 8) && !d.convT && !d.mul &&
+        d.act != HISEG_ACT_SWISH && d.Cb == 0 && !(force_rb > 4 && nks > 8))
+      rb = force_rb;
+  }
   const bool comb = rb == 16 && nks == 9;
   if ((rb == 16 && nks > 9) || (rb > 4 && nks > 8)) return false;   // (registers: 2 x 10 B fragment sets)
   if (comb ? (d.Ca != 256 || d.Cb > 32 || d.convT || d.residual || d.mul || d.in_scale ||
@@ -466,8 +487,15 @@ int conv_pw_gate_images(const ConvArgs& a) {
 }
 
 // Returns 1 if launched, 0 if the layer does not qualify (caller falls back), <0 on error.  variant 90.
-int conv_pw_try(const ConvArgs& a, hipStream_t s, int variant) {
-  if (variant != 90) return 0;
+int conv_pw_try(const ConvArgs& a0, hipStream_t s, int variant) {
+#ifdef HISEG_DIAG
+  const bool diag = variant >= 190 && variant < 222;   // variant 90 with ablation bits variant - 190
+#else
+  const bool diag = false;
+#endif
+  if (variant != 90 && !diag) return 0;
+  ConvArgs a = a0;
+  a.abl = diag ? variant - 190 : 0;
   int rb, nks, nks_max;
   if (!pw_plan(a, rb, nks, nks_max)) return 0;
   int r;

@@ -764,6 +764,47 @@ def test_c2_shape_bf16_properties_and_oracle():
     assert max_abs(binary[:1].cpu(), O.binary_masks(sd, ref_u)) < 0.05
 
 
+def test_c2_size_bf16_within_torch_bf16(monkeypatch):
+    """the bf16 bar at the benchmark's own size.  One 480x640 image with 8 ROIs from the C2 ROI
+    generator (bench.py synthetic_batch), B0-std in bf16 through the exported contract, against the f32 oracle; the
+    same network run by torch in bf16 on the GPU sets what bf16 execution costs.  hiseg's instance masks must agree
+    with the f32 oracle's at least as well as torch-bf16's do, less 0.5 points, and its ROI logits and full-image
+    UNet logits must stay within 1.5x (+1e-3) of torch-bf16's relative error."""
+    from oracle import rgb_model as O
+    from oracle.roi_align import roi_align as roi_np
+    from hiseg import RGBHierarchicalExportWrapper
+    model, kw = _preset_model("b0", torch.bfloat16)
+    cfg = O.cfg_from_kwargs(kw)
+    for m in (model.roi_align_mask, model.roi_align_rgb):
+        m.spatial_scale_h, m.spatial_scale_w = 480, 640
+    images = torch.from_numpy(filler.uniform(1, (1, 3, 480, 640)))
+    rois = torch.from_numpy(filler.box_rois(1, 1, 8))
+    sd = O.np_state(model)
+    with torch.no_grad():
+        inst, _ = RGBHierarchicalExportWrapper(model)(images.to(DEV), rois.to(DEV))
+        logits, aux = model(images.to(DEV), rois.to(DEV))
+        ref_logits, ref_aux, _ = O.rgb_model(sd, images, rois, cfg, (480, 640), "b0")
+
+        def roi_bf16(feat, r, oh, ow, sh, sw, aligned=True):
+            out = roi_np(feat.float().cpu().numpy(), r.float().cpu().numpy(), oh, ow, sh, sw, aligned)
+            return torch.from_numpy(out).to(feat.device, feat.dtype)
+
+        monkeypatch.setattr(O, "roi_align", roi_bf16)
+        sd16 = {k: v.to(DEV, torch.bfloat16) for k, v in sd.items()}
+        t_logits, t_aux, _ = O.rgb_model(sd16, images.to(DEV, torch.bfloat16), rois.to(DEV), cfg, (480, 640), "b0")
+    ref_masks = O.instance_masks(ref_logits)
+    agree_h = (inst.cpu() == ref_masks).float().mean().item()
+    agree_t = (O.instance_masks(t_logits.float().cpu()) == ref_masks).float().mean().item()
+    e_h, e_t = _rel(logits.float().cpu(), ref_logits), _rel(t_logits.float().cpu(), ref_logits)
+    u_h = _rel(aux["full_image_logits"].float().cpu(), ref_aux["full_image_logits"])
+    u_t = _rel(t_aux["full_image_logits"].float().cpu(), ref_aux["full_image_logits"])
+    print(f"C2-size bf16: mask agreement {agree_h:.5f} (torch-bf16 {agree_t:.5f}); logits {e_h:.2e} "
+          f"(torch {e_t:.2e}); UNet logits {u_h:.2e} (torch {u_t:.2e})")
+    assert agree_h >= agree_t - 0.005, (agree_h, agree_t)
+    assert e_h < 1.5 * e_t + 1e-3, (e_h, e_t)
+    assert u_h < 1.5 * u_t + 1e-3, (u_h, u_t)
+
+
 @pytest.mark.parametrize("preset", ["b0", "b1", "b7"])
 def test_bf16_logits_error_within_torch_bf16(monkeypatch, preset):
     """The bf16 inference bar, tied to PyTorch's own bf16: the same network run by torch in bf16 on the GPU

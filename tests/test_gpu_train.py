@@ -1332,3 +1332,73 @@ def test_ubf_backward_two_pixel_loop_bit_identical(monkeypatch):
     (l1, g1), (l0, g0) = res["1"], res["0"]
     assert torch.isfinite(l1) and torch.equal(l1, l0)
     assert len(g1) == len(g0) and all(torch.equal(a, b) for a, b in zip(g1, g0))
+
+
+def test_train_step_bf16_within_torch_bf16_of_oracle(monkeypatch):
+    """the bf16 training bar, tied to PyTorch's own bf16.  The f32 oracle (torch autograd of the
+    restated B0-std model, oracle/train.py) is the reference; the same oracle run by torch in bf16 (bf16 weights,
+    activations and autograd, the loss in f32 as under the reference's autocast, train_advanced.py:693-762) sets
+    the error a bf16 execution incurs.  hiseg's bf16 step -- including the BatchNorm statistics fused into the
+    conv_hwc epilogue and the bf16 weight / data gradient kernels -- must stay within a small multiple of it: loss
+    and logits within 1.5x (+1e-3) of torch-bf16's relative error, the whole gradient's direction within 2x of
+    torch-bf16's (1 - cosine, +1e-4) and its norm within 2x (+1e-2)."""
+    import hiseg
+    from oracle import rgb_model as O
+    from oracle import train as OT
+    from hiseg import train_engine as TE
+    m = _model(torch.bfloat16)
+    sd = OT.params_of(m)
+    m = m.to(DEV).train()
+    cfg = O.cfg_from_kwargs(_kwargs())
+    images = torch.from_numpy(filler.uniform(71, (2, 3, 96, 128)))
+    u = torch.from_numpy(filler.normal(72, (2, 1, 96, 128)) * 2.0)
+    rois = torch.tensor([[0, .10, .10, .40, .90], [1, .35, .15, .80, .95], [0, .55, .05, .95, .70],
+                         [1, .05, .30, .60, .85]])
+    for mm in (m.roi_align_mask, m.roi_align_rgb):
+        mm.spatial_scale_h, mm.spatial_scale_w = 96, 128
+    tgt = torch.from_numpy(filler.ellipse_targets(73, 4, *cfg["mask_hw"]))
+    # hiseg bf16 (the weights are the bf16 roundings of the f32 initialisation: the oracle starts from those too)
+    logits, aux = TE.train_forward(m, images.to(DEV), rois.to(DEV), u_override=u.to(DEV))
+    loss_fn = hiseg.RefinedHierarchicalLoss(use_boundary_aware_loss=True, use_contour_detection=True,
+                                            use_distance_transform=True, boundary_aware_weight=0.1,
+                                            contour_loss_weight=0.1, distance_loss_weight=0.1)
+    loss, _ = loss_fn(logits, tgt.to(DEV), aux)
+    loss.backward()
+
+    def oracle_step(params, dt):
+        if dt == torch.bfloat16:
+            orig = OT.roi_align_torch
+            monkeypatch.setattr(OT, "roi_align_torch", lambda feat, *a, **k: orig(feat.float(), *a, **k).to(feat.dtype))
+        rlog, raux = OT.forward_train(params, images.to(dt), rois, u.to(dt), cfg, (96, 128))
+        rloss, _ = OT.RefinedHierarchicalLoss()(rlog.float(), tgt, {k: v.float() for k, v in raux.items()})
+        rloss.backward()
+        monkeypatch.undo()
+        return rloss.item(), rlog.detach().float()
+
+    sd16 = {k: (v.detach().bfloat16().requires_grad_(True) if v.requires_grad else v.detach().bfloat16())
+            for k, v in sd.items()}
+    l32, g32 = oracle_step(sd, torch.float32)
+    l16, g16 = oracle_step(sd16, torch.bfloat16)
+
+    def flat_grads(get):
+        out = []
+        for n, p in m.named_parameters():
+            if n in sd and sd[n].requires_grad and sd[n].grad is not None:
+                out.append(get(n, p).double().reshape(-1))
+        return torch.cat(out)
+    gr = flat_grads(lambda n, p: sd[n].grad)
+    gt = flat_grads(lambda n, p: sd16[n].grad.float())
+    gh = flat_grads(lambda n, p: p.grad.detach().float().cpu())
+
+    def cos(a, b):
+        return float((a * b).sum() / (a.norm() * b.norm()))
+    e_loss_h, e_loss_t = abs(loss.item() - l32) / abs(l32), abs(l16 - l32) / abs(l32)
+    e_log_h, e_log_t = rel(logits.detach().float(), g32), rel(g16, g32)
+    c_h, c_t = 1 - cos(gh, gr), 1 - cos(gt, gr)
+    n_h, n_t = abs(float(gh.norm() / gr.norm()) - 1), abs(float(gt.norm() / gr.norm()) - 1)
+    print(f"bf16 train vs f32 oracle: loss {e_loss_h:.2e} (torch {e_loss_t:.2e}), logits {e_log_h:.2e} "
+          f"(torch {e_log_t:.2e}), 1-cos {c_h:.2e} (torch {c_t:.2e}), norm {n_h:.2e} (torch {n_t:.2e})")
+    assert e_loss_h < 1.5 * e_loss_t + 1e-3
+    assert e_log_h < 1.5 * e_log_t + 1e-3
+    assert c_h < 2 * c_t + 1e-4
+    assert n_h < 2 * n_t + 1e-2
