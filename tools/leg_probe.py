@@ -23,7 +23,30 @@ def main():
     t0 = time.perf_counter()
     for act in a.seq.split(","):
         ts = f"[{time.perf_counter() - t0:6.1f}s]"
-        if act in ("infer", "infer_serial"):
+        if act == "hp":   # bind a high-priority stream to a hardware queue (one tiny kernel on it), nothing else
+            hs = torch.cuda.Stream(priority=-1)
+            with torch.cuda.stream(hs):
+                torch.ones(1, device=dev).add_(1)
+            torch.cuda.synchronize()
+            print(f"{ts} hp stream bound", flush=True)
+        elif act == "hp_destroyed":   # the same through a raw HIP stream that is destroyed again
+            import ctypes
+            hip = ctypes.CDLL("libamdhip64.so")
+            h = ctypes.c_void_p()
+            assert hip.hipStreamCreateWithPriority(ctypes.byref(h), 0, -1) == 0
+            with torch.cuda.stream(torch.cuda.ExternalStream(h.value)):
+                torch.ones(1, device=dev).add_(1)
+            torch.cuda.synchronize()
+            assert hip.hipStreamDestroy(h) == 0
+            print(f"{ts} hp stream bound and destroyed", flush=True)
+        elif act == "infer_normal":   # the inference leg with its head on a normal-priority stream
+            from hiseg import streams as HS
+            HS._PRIORITY.pop("head", None)
+            ia = argparse.Namespace(steps=20, warmup=5, serial=False, no_cpu_baseline=True, gpus=1, dtype="bf16")
+            r = bench.infer_bench(ia, dev, torch.bfloat16, 0, 1, None)
+            gc.collect()
+            print(f"{ts} {act}: {r['value']} ROI-masks/s, dominant {r['roofline']['avg_launch_ms']} ms", flush=True)
+        elif act in ("infer", "infer_serial"):
             ia = argparse.Namespace(steps=20, warmup=5, serial=act == "infer_serial", no_cpu_baseline=True, gpus=1,
                                     dtype="bf16")
             r = bench.infer_bench(ia, dev, torch.bfloat16, 0, 1, None)
