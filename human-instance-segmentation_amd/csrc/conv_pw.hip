@@ -421,11 +421,20 @@ static bool pw_plan(const ConvArgs& a, int& rb, int& nks, int& nks_max) {
   rb = 16;
   if (d.Cout_pad <= 128) rb = d.Cout_pad <= 16 ? 1 : d.Cout_pad <= 32 ? 2 : d.Cout_pad <= 64 ? 4 : 8;
   {
-    // HISEG_PW_RB=1|2|4|8 (read once; A/B timing): wide layers on narrow column tiles where that form exists
+    // Wide layers over few pixels (the EfficientNet expansions of the distillation teacher / student, M <= 128 Ki
+    // pixels: a 256-column tile gives each wave one or two 32-pixel blocks behind a 115-135 KiB weight staging, one
+    // workgroup per CU) take 64-column tiles: four workgroups per CU, a quarter of the staging each, and less
+    // padding in the last column tile (288 = 4.5 x 64, not 1.1 x 256).  Same accumulation order per output element,
+    // so bit-identical (tools/pw_probe.py, profiles/r6_pw_rb_sweep.txt: 224 -> 1344 @ 4 x 40 x 40 25.1 -> 17.9 us,
+    // 48 -> 288 @ 4 x 160 x 160 29.6 -> 24.6, 160 -> 960 @ 4 x 40 x 40 13.6 -> 12.1; the head's 786 Ki-pixel layers keep
+    // 256 columns, 193 vs 318 us).  HISEG_PW_RB=1|2|4|8|16 (read once; A/B timing) forces the width.
     static const int force_rb = [] { const char* e = getenv("HISEG_PW_RB"); return e ? atoi(e) : 0; }();
-    if (rb == 16 && (force_rb == 1 || force_rb == 2 || force_rb == 4 || force_rb == 8) && !d.convT && !d.mul &&
-        d.act != HISEG_ACT_SWISH && d.Cb == 0 && !(force_rb > 4 && nks > 8))
-      rb = force_rb;
+    const bool narrow_ok = !d.convT && !d.mul && d.act != HISEG_ACT_SWISH && d.Cb == 0;
+    if (rb == 16 && narrow_ok) {
+      int want = force_rb ? force_rb : (a.M <= 131072 ? 4 : 16);
+      if (want != 1 && want != 2 && want != 4 && want != 8) want = 16;
+      if (!(want > 4 && nks > 8)) rb = want;
+    }
   }
   const bool comb = rb == 16 && nks == 9;
   if ((rb == 16 && nks > 9) || (rb > 4 && nks > 8)) return false;   // (registers: 2 x 10 B fragment sets)

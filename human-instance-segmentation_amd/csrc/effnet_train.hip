@@ -163,13 +163,14 @@ __global__ void __launch_bounds__(256) dw_bwd_weight_kernel(const void* x, const
 }
 
 // dw[i] += sum_s ws[s][i]: a block = 64 outputs x 4 split groups (group g sums splits g, g + 4, ... in order, four
-// loads in flight), the groups combined in LDS in order.  (One thread per output walking every split in double was
-// 33 us per call on the 288-output layers.)
+// loads in flight), the groups combined in LDS in order.  The sums run in double (up to 1024 split partials per weight
+// on the large-pixel layers of the unfrozen encoder; the loads, not the adds, bound this pass).  (One thread per output
+// walking every split in double was 33 us per call on the 288-output layers.)
 __global__ void __launch_bounds__(256) dw_weight_reduce_kernel(const float* ws, int S, int n, float* dw) {
-  __shared__ float red[4][64];
+  __shared__ double red[4][64];
   const int ol = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + ol;
-  float acc = 0.f;
+  double acc = 0.0;
   if (i < n) {
     int sp = g;
     for (; sp + 12 < S; sp += 16) {
@@ -181,7 +182,7 @@ __global__ void __launch_bounds__(256) dw_weight_reduce_kernel(const float* ws, 
   }
   red[g][ol] = acc;
   __syncthreads();
-  if (g == 0 && i < n) dw[i] += ((red[0][ol] + red[1][ol]) + red[2][ol]) + red[3][ol];
+  if (g == 0 && i < n) dw[i] = (float)((double)dw[i] + (((red[0][ol] + red[1][ol]) + red[2][ol]) + red[3][ol]));
 }
 
 // pixel splits of the weight gradient: about 32 pixels per thread (R pixel lanes per task), at most kDwMaxSplits

@@ -1341,7 +1341,12 @@ def test_train_step_bf16_within_torch_bf16_of_oracle(monkeypatch):
     the error a bf16 execution incurs.  hiseg's bf16 step -- including the BatchNorm statistics fused into the
     conv_hwc epilogue and the bf16 weight / data gradient kernels -- must stay within a small multiple of it: loss
     and logits within 1.5x (+1e-3) of torch-bf16's relative error, the whole gradient's direction within 2x of
-    torch-bf16's (1 - cosine, +1e-4) and its norm within 2x (+1e-2)."""
+    torch-bf16's (1 - cosine, +1e-4) and its norm within 2x (+1e-2).
+    Why not an absolute bar: at this random initialisation the train-mode head is chaotic -- rounding only the
+    WEIGHTS to bf16 and running the f32 oracle moves its logits by ~30 % (max-relative) and its gradient's cosine to
+    ~0.4 (measured on the CPU oracle, round 6), torch-bf16 lands at ~0.5 / ~0.2 (GPU run: hiseg 0.52 / 0.20, torch
+    0.62 / 0.16; loss 6.0e-4 vs 1.2e-3).  So no bf16 execution is within a fixed tolerance of f32 here; the claim
+    tested is that hiseg's bf16 step is no further from f32 than PyTorch's own bf16 step."""
     import hiseg
     from oracle import rgb_model as O
     from oracle import train as OT
@@ -1402,3 +1407,32 @@ def test_train_step_bf16_within_torch_bf16_of_oracle(monkeypatch):
     assert e_log_h < 1.5 * e_log_t + 1e-3
     assert c_h < 2 * c_t + 1e-4
     assert n_h < 2 * n_t + 1e-2
+
+
+@pytest.mark.parametrize("case", [(4, 32, 320, 320, 3, 1), (4, 96, 320, 320, 3, 2), (4, 144, 160, 160, 5, 1),
+                                  (4, 240, 80, 80, 5, 2)])
+def test_depthwise_weight_gradient_matches_f64_at_encoder_scale(case):
+    """The depthwise weight gradient of the unfrozen encoder's largest-pixel layers (B0 at 640 x 640, 4 images: up to
+    409 600 output pixels, 1 024 split partials per weight) against float64 autograd of the same bf16 operands.  The
+    split partials are f32 sums of ~32 exact bf16 products; their reduce runs in double: the result sits
+    within 1e-5 of the float64 gradient's scale."""
+    from hiseg import _lib as L
+    from hiseg.ops import Act, hdtype
+    N, C, H, W, k, st = case
+    g = torch.Generator(device=DEV).manual_seed(123)
+    x = torch.randn(N, C, H, W, device=DEV, generator=g).bfloat16()
+    Ho, Wo = (H + 2 * (k // 2) - k) // st + 1, (W + 2 * (k // 2) - k) // st + 1
+    dy = torch.randn(N, C, Ho, Wo, device=DEV, generator=g).bfloat16()
+    xa, dya = Act.from_nchw(x.float(), torch.bfloat16), Act.from_nchw(dy.float(), torch.bfloat16)
+    lib = L.lib()
+    ws = torch.empty(int(lib.hiseg_dw_bwd_weight_ws(hdtype(torch.bfloat16), N, Ho, Wo, C, k)), dtype=torch.float32,
+                     device=DEV)
+    dw = torch.zeros(C * k * k, dtype=torch.float32, device=DEV)
+    L.check(lib.hiseg_dw_bwd_weight(hdtype(torch.bfloat16), xa.ptr(), dya.ptr(), N, H, W, C, k, st, Ho, Wo,
+                                    ws.data_ptr(), dw.data_ptr(), L.stream_ptr()), "dw_bwd_weight")
+    w64 = torch.zeros(C, 1, k, k, dtype=torch.float64, device=DEV, requires_grad=True)
+    y = F.conv2d(x.double(), w64, stride=st, padding=k // 2, groups=C)
+    y.backward(dy.double())
+    ref = w64.grad.reshape(-1)
+    err = ((dw.double() - ref).abs().max() / ref.abs().max()).item()
+    assert err < 1e-5, err
