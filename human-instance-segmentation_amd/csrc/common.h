@@ -46,8 +46,14 @@ template <> struct Elem<bf16_t> {
 // 11-instruction sequence: sigmoid / SiLU epilogues are VALU-bound on the wide EfficientNet expansions
 __device__ __forceinline__ float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 
-// nn.GELU() (approximate='none'): x * Phi(x) with the exact erf
-__device__ __forceinline__ float gelu_(float v) { return 0.5f * v * (1.f + erff(v * 0.70710678118654752f)); }
+// nn.GELU() (approximate='none'): x * Phi(x) with the exact erf.  Out of line, as its derivative below: the runtime
+// activation switch is inlined per output element into unrolled epilogues, and the erf body was most of their code
+// (conv_igemm's 128x128 kernels 132 -> 93 KB) -- instruction fetch, not arithmetic, bounds the short launches
+// (tools/icache_probe.hip: ~0.6 us per KB of straight-line code run once per wave, profiles/r6_icache_probe.txt)
+__device__ __noinline__ float gelu_(float v) { return 0.5f * v * (1.f + erff(v * 0.70710678118654752f)); }
+__device__ __noinline__ float gelu_grad_(float v) {
+  return 0.5f * (1.f + erff(v * 0.70710678118654752f)) + v * 0.39894228040143268f * __expf(-0.5f * v * v);
+}
 
 // Activation of the pre-activation v (advanced/activation_utils.py:71-101); beta is Swish's.
 __device__ __forceinline__ float apply_act(float v, int act, float beta = 1.f) {
@@ -69,7 +75,7 @@ __device__ __forceinline__ float act_grad_pre(float v, int act, float beta = 1.f
     case HISEG_ACT_SILU: { const float s = sigmoidf_(v); return s * (1.f + v * (1.f - s)); }
     case HISEG_ACT_SWISH: { const float s = sigmoidf_(beta * v); return s * (1.f + beta * v * (1.f - s)); }
     case HISEG_ACT_GELU:
-      return 0.5f * (1.f + erff(v * 0.70710678118654752f)) + v * 0.39894228040143268f * __expf(-0.5f * v * v);
+      return gelu_grad_(v);
     default: return 1.f;
   }
 }

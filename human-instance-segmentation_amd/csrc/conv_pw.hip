@@ -343,14 +343,28 @@ static int launch_pw(const ConvArgs& a, hipStream_t s, int nks) {
 int launch_pw_narrow(const ConvArgs& a, hipStream_t s, int rb, int nks_max, int nks);
 
 #if HISEG_PW_PART == 2
+// The activation is a template argument for the forms the encoder / head layers use (identity: the projections,
+// SE-gated or not; ReLU: the head; SiLU: the EfficientNet expansions) and a run-time switch otherwise: with the switch
+// inlined per output element the RB 4 kernels were 40-50 KB of code against ~15 KB.
 template <int RB, int NKS>
 static int launch_pw_n2(const ConvArgs& a, hipStream_t s, int nks) {
   const hiseg_conv2d_desc& d = a.d;
+  constexpr int N = HISEG_ACT_NONE, R = HISEG_ACT_RELU, SI = HISEG_ACT_SILU, RT = kPwActRt;
   const bool ins = d.in_scale != nullptr;
-  if (d.residual) return ins ? launch_pw<-NKS, 1, kPwActRt, false, RB, true>(a, s, nks)
-                             : launch_pw<-NKS, 1, kPwActRt, false, RB, false>(a, s, nks);
-  return ins ? launch_pw<-NKS, 0, kPwActRt, false, RB, true>(a, s, nks)
-             : launch_pw<-NKS, 0, kPwActRt, false, RB, false>(a, s, nks);
+  const int act = d.act;
+  if (ins) {
+    if (d.residual) return act == N ? launch_pw<-NKS, 1, N, false, RB, true>(a, s, nks)
+                                    : launch_pw<-NKS, 1, RT, false, RB, true>(a, s, nks);
+    return act == N ? launch_pw<-NKS, 0, N, false, RB, true>(a, s, nks)
+                    : launch_pw<-NKS, 0, RT, false, RB, true>(a, s, nks);
+  }
+  if (d.residual) return act == N ? launch_pw<-NKS, 1, N, false, RB, false>(a, s, nks)
+                       : act == R ? launch_pw<-NKS, 1, R, false, RB, false>(a, s, nks)
+                                  : launch_pw<-NKS, 1, RT, false, RB, false>(a, s, nks);
+  return act == N ? launch_pw<-NKS, 0, N, false, RB, false>(a, s, nks)
+       : act == R ? launch_pw<-NKS, 0, R, false, RB, false>(a, s, nks)
+       : act == SI ? launch_pw<-NKS, 0, SI, false, RB, false>(a, s, nks)
+                   : launch_pw<-NKS, 0, RT, false, RB, false>(a, s, nks);
 }
 template <int RB>
 static int launch_pw_n1(const ConvArgs& a, hipStream_t s, int nks_max, int nks) {

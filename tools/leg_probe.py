@@ -59,9 +59,13 @@ def main():
             gc.collect()
             print(f"{ts} {act}: {r['ms_per_step']} ms", flush=True)
         elif act == "distill":
+            from hiseg import _lib as HL
+            HL.placement_stats(reset=True)
             r = bench.distill_bench(dev, torch.bfloat16, 0, 1, None, 10, 3)
             gc.collect()
-            print(f"{ts} distill: {r['ms_per_step']} ms", flush=True)
+            dec, far = HL.placement_stats(reset=True)
+            print(f"{ts} distill: {r['ms_per_step']} ms (placement-dependent choices: {dec} declined, {far} far; "
+                  f"reserved {torch.cuda.memory_reserved() / 2**30:.1f} GB)", flush=True)
         elif act == "empty":
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
