@@ -55,29 +55,27 @@ __device__ __noinline__ float gelu_grad_(float v) {
   return 0.5f * (1.f + erff(v * 0.70710678118654752f)) + v * 0.39894228040143268f * __expf(-0.5f * v * v);
 }
 
-// Activation of the pre-activation v (advanced/activation_utils.py:71-101); beta is Swish's.
+// Activation of the pre-activation v (advanced/activation_utils.py:71-101); beta is Swish's.  The sigmoid family
+// shares one exp / rcp sequence (a switch inlined per output element into the unrolled epilogues carried three of
+// them; same arithmetic per activation, so the same bits).
 __device__ __forceinline__ float apply_act(float v, int act, float beta = 1.f) {
-  switch (act) {
-    case HISEG_ACT_RELU: return v > 0.f ? v : 0.f;
-    case HISEG_ACT_SIGMOID: return sigmoidf_(v);
-    case HISEG_ACT_SILU: return v * sigmoidf_(v);
-    case HISEG_ACT_GELU: return gelu_(v);
-    case HISEG_ACT_SWISH: return v * sigmoidf_(beta * v);
-    default: return v;
-  }
+  if (act == HISEG_ACT_NONE) return v;
+  if (act == HISEG_ACT_RELU) return v > 0.f ? v : 0.f;
+  if (act == HISEG_ACT_GELU) return gelu_(v);
+  if (act != HISEG_ACT_SIGMOID && act != HISEG_ACT_SILU && act != HISEG_ACT_SWISH) return v;
+  const float s = sigmoidf_(act == HISEG_ACT_SWISH ? beta * v : v);
+  return act == HISEG_ACT_SIGMOID ? s : v * s;
 }
 
 // d act / d v at the pre-activation v.
 __device__ __forceinline__ float act_grad_pre(float v, int act, float beta = 1.f) {
-  switch (act) {
-    case HISEG_ACT_RELU: return v > 0.f ? 1.f : 0.f;
-    case HISEG_ACT_SIGMOID: { const float s = sigmoidf_(v); return s * (1.f - s); }
-    case HISEG_ACT_SILU: { const float s = sigmoidf_(v); return s * (1.f + v * (1.f - s)); }
-    case HISEG_ACT_SWISH: { const float s = sigmoidf_(beta * v); return s * (1.f + beta * v * (1.f - s)); }
-    case HISEG_ACT_GELU:
-      return gelu_grad_(v);
-    default: return 1.f;
-  }
+  if (act == HISEG_ACT_NONE) return 1.f;
+  if (act == HISEG_ACT_RELU) return v > 0.f ? 1.f : 0.f;
+  if (act == HISEG_ACT_GELU) return gelu_grad_(v);
+  if (act != HISEG_ACT_SIGMOID && act != HISEG_ACT_SILU && act != HISEG_ACT_SWISH) return 1.f;
+  const float b = act == HISEG_ACT_SWISH ? beta : 1.f;
+  const float s = sigmoidf_(act == HISEG_ACT_SWISH ? beta * v : v);
+  return act == HISEG_ACT_SIGMOID ? s * (1.f - s) : s * (1.f + b * v * (1.f - s));
 }
 
 // Activations whose derivative needs the pre-activation (not recoverable from the output).

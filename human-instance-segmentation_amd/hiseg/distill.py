@@ -56,7 +56,7 @@ class _LazyDict(Mapping):
 
 class _DistillLossFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, cfg, student, teacher, target):
+    def forward(ctx, cfg, student, teacher, target, dev_scalars=None):
         lib = L.lib()
         B, _, H, W = student.shape
         dev = student.device
@@ -66,6 +66,7 @@ class _DistillLossFn(torch.autograd.Function):
                                            target.data_ptr() if target is not None else None, ws.data_ptr(),
                                            out.data_ptr(), L.stream_ptr()), "distill_loss_fwd")
         ctx.cfg = cfg
+        ctx.dev_scalars = dev_scalars   # cfg.dev_scalars points into it: alive until the backward ran
         ctx.save_for_backward(student, teacher, target, ws)
         ctx.mark_non_differentiable(out)
         return out[0].clone(), out
@@ -79,7 +80,7 @@ class _DistillLossFn(torch.autograd.Function):
         L.check(L.lib().hiseg_distill_loss_bwd(ctypes.byref(ctx.cfg), B, H, W, student.data_ptr(), teacher.data_ptr(),
                                                target.data_ptr() if target is not None else None, ws.data_ptr(),
                                                g.data_ptr(), ds.data_ptr(), L.stream_ptr()), "distill_loss_bwd")
-        return None, ds, None, None
+        return None, ds, None, None, None
 
 
 class UNetDistillationLoss(nn.Module):
@@ -207,7 +208,7 @@ class UNetDistillationLoss(nn.Module):
         else:
             self.sync_device_scalars(s.device)
         cfg.dev_scalars = self._dev.data_ptr()
-        total, out = _DistillLossFn.apply(cfg, s, t, y)
+        total, out = _DistillLossFn.apply(cfg, s, t, y, self._dev)
         return total, _LazyDict(out, _DICT_KEYS)
 
     def dice_loss(self, pred: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
