@@ -1157,7 +1157,8 @@ def infer_bench(args, device, dtype, rank, world, dist):
     wrapper = hiseg.RGBHierarchicalExportWrapper(model)
     images, rois = synthetic_batch(device, rank)
 
-    runner = None if args.serial else hiseg.StreamPipelinedExport(wrapper)
+    gate = os.environ.get("HISEG_PIPE_GATE", "0") == "1"
+    runner = None if args.serial else hiseg.StreamPipelinedExport(wrapper, gate=gate)
 
     def steps(k):
         if runner is None:

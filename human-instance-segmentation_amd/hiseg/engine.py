@@ -356,21 +356,42 @@ def _block_out_channels(blk: nn.Module) -> int:
     return (blk.conv_pw if isinstance(blk, DepthwiseSeparableConv) else blk.conv_pwl).out_channels
 
 
+def _drain(gen):
+    """Run a forward generator (below) to its end and return its value."""
+    while True:
+        try:
+            next(gen)
+        except StopIteration as e:
+            return e.value
+
+
 def unet_logit(E: Ctx, pre: nn.Module, images: torch.Tensor) -> torch.Tensor:
     """PreTrainedPeopleSegmentationUNet.forward (unet.py:1901-1916): normalise, smp.Unet -> u [B,1,H,W] f32."""
+    return _drain(unet_logit_iter(E, pre, images))
+
+
+def unet_logit_iter(E: Ctx, pre: nn.Module, images: torch.Tensor):
+    """unet_logit as a generator: yields after each encoder block / decoder block (the serving schedule's chunks,
+    hiseg.model.StreamPipelinedExport(gate=True)), returns u."""
     B, _, H, W = images.shape
     if H % 32 or W % 32:
         raise NotImplementedError(f"image size {H}x{W} must be a multiple of 32 for the EfficientNet-UNet")
     x = ops.input_norm(images, E.f32(pre.norm_mean, (3,)), E.f32(pre.norm_std, (3,)), E.dtype)
-    return effunet_forward(E, pre.model, x)
+    return (yield from effunet_forward_iter(E, pre.model, x))
 
 
 def effunet_forward(E: Ctx, net: nn.Module, x: Act) -> torch.Tensor:
     """smp.Unet('timm-efficientnet-bX') forward (eval) on an NHWC input -> logits [B,1,H,W] f32."""
+    return _drain(effunet_forward_iter(E, net, x))
+
+
+def effunet_forward_iter(E: Ctx, net: nn.Module, x: Act):
+    """effunet_forward as a generator: yields after the stem, each MBConv block and each decoder block."""
     B, H, W = x.N, x.H, x.W
     enc = net.encoder
     x = ops.conv2d(E.conv(enc.conv_stem, enc.bn1, ACT_SILU), x)
     feats = [x]
+    yield
     for si, stage in enumerate(enc.blocks):
         for bi, blk in enumerate(stage):
             # the skip features of decoder blocks 0-2 (stage 2 / 3 / 5 outputs: 24 / 40 / 112 channels for B0-B1,
@@ -382,6 +403,7 @@ def effunet_forward(E: Ctx, net: nn.Module, x: Act) -> torch.Tensor:
                 c = _block_out_channels(blk)
                 cpad = round_up(c, 64) if c % 64 else None
             x = mbconv(E, blk, x, out_cpad=cpad)
+            yield
         if si + 1 in (2, 3, 5, 7):
             feats.append(x)
     skips = feats[-2::-1]
@@ -391,6 +413,7 @@ def effunet_forward(E: Ctx, net: nn.Module, x: Act) -> torch.Tensor:
         split = (x.C, skip.C, skip.cstride) if skip is not None else None
         x = ops.conv2d(E.conv(blk.conv1[0], blk.conv1[1], ACT_RELU, split=split), x, skip, a_up=2)
         x = ops.conv2d(E.conv(blk.conv2[0], blk.conv2[1], ACT_RELU), x)
+        yield
     u = Act.new(B, H, W, 1, torch.float32, E.device, cpad=1, zero=False)
     ops.conv2d(E.conv(net.segmentation_head[0]), x, out=u)
     return u.t.view(B, 1, H, W)
@@ -490,9 +513,14 @@ def export_forward(model: nn.Module, images: torch.Tensor, rois: torch.Tensor, d
 
 def export_unet_phase(model: nn.Module, images: torch.Tensor):
     """First half of the exported contract: full-image UNet logit u and binary_masks."""
+    return _drain(export_unet_phase_iter(model, images))
+
+
+def export_unet_phase_iter(model: nn.Module, images: torch.Tensor):
+    """export_unet_phase as a generator (yields between UNet blocks), returns (u, binary_masks)."""
     _check_input(images, "RGBHierarchicalExportWrapper")
     E = Ctx(model, _root_dtype(model), images.device)
-    u = unet_logit(E, model.pretrained_unet.model, images.contiguous().float())
+    u = yield from unet_logit_iter(E, model.pretrained_unet.model, images.contiguous().float())
     oc = model.pretrained_unet.output_conv
     return u, ops.binary_masks(u, E.f32(oc.weight, (2,)), E.f32(oc.bias))
 

@@ -240,7 +240,8 @@ class StreamPipelinedExport:
     ready on the caller's current stream when it returns (the caller synchronises as usual).
     """
 
-    def __init__(self, wrapper: "RGBHierarchicalExportWrapper", unet_cu_mask=None, head_priority: bool = True):
+    def __init__(self, wrapper: "RGBHierarchicalExportWrapper", unet_cu_mask=None, head_priority: bool = True,
+                 gate: bool = False, gate_min_gflop: float = 300.0):
         """``unet_cu_mask``: optional list of 32-bit words; the UNet stream then runs only on the CUs whose bits
         are set (hiseg_stream_create_cu_mask), leaving the rest to the head.  ``head_priority``: the head -- the
         critical path once the UNet got cheaper -- runs on a high-priority stream, so its workgroups are dispatched
@@ -259,6 +260,9 @@ class StreamPipelinedExport:
             self._raw_unet = h.value
             self.s_unet = torch.cuda.ExternalStream(h.value)
         self.s_head = streams.role_stream("head" if head_priority else "head_normal")
+        self.gate = gate
+        self.gate_min_flops = gate_min_gflop * 1e9
+        self._windows = None   # learned: light conv launches of the head between its heavy ones (gate=True)
 
     def __del__(self):
         if getattr(self, "_raw_unet", None):
@@ -269,6 +273,8 @@ class StreamPipelinedExport:
                 pass
 
     def run(self, batches):
+        if self.gate:
+            return self._run_gated(list(batches))
         w = self.wrapper
         caller = torch.cuda.current_stream()
         self.s_unet.wait_stream(caller)
@@ -294,6 +300,135 @@ class StreamPipelinedExport:
             inst.record_stream(caller)
             binary.record_stream(caller)
         return outs
+
+    def _set_scale(self, images):
+        w = self.wrapper
+        H, W = images.shape[-2:] if w.image_size is None else w.image_size
+        for m in (w.model.roi_align_mask, w.model.roi_align_rgb):
+            m.spatial_scale = (H, W)
+            m.spatial_scale_h, m.spatial_scale_w = H, W
+
+    def _run_gated(self, batches):
+        """gate=True: the UNet of batch k+1 is issued in chunks (one per encoder / decoder block) from inside the head
+        of batch k, into the windows between the head's heavy convs (>= gate_min_gflop: the 256-channel 3x3 layers
+        at the ROI grid), and each heavy conv first waits for the chunks issued so far -- so the MFMA-bound heavy convs
+        run with the chip to themselves and the latency-bound UNet kernels share it with the head's light kernels.
+        Chunks are spread over the windows in proportion to the light conv launches each window held in the first
+        batch (learned once).  Same kernels on the same inputs as run(): identical results."""
+        from . import ops
+        w = self.wrapper
+        caller = torch.cuda.current_stream()
+        self.s_unet.wait_stream(caller)
+        self.s_head.wait_stream(caller)
+        outs = []
+        if not batches:
+            return outs
+        self._set_scale(batches[0][0])
+        with torch.cuda.stream(self.s_unet):
+            u, binary = engine._drain(engine.export_unet_phase_iter(w.model, batches[0][0]))
+        for k, (images, rois) in enumerate(batches):
+            ready = torch.cuda.Event()
+            ready.record(self.s_unet)
+            nxt = None
+            if k + 1 < len(batches):
+                self._set_scale(batches[k + 1][0])
+                nxt = engine.export_unet_phase_iter(w.model, batches[k + 1][0])
+            self._set_scale(images)
+            g = _HeadGate(self, nxt)
+            with torch.cuda.stream(self.s_head):
+                self.s_head.wait_event(ready)
+                u.record_stream(self.s_head)
+                ops.GATE = g
+                try:
+                    inst = engine.export_head_phase(w.model, images, rois, u, w.dilation_pixels)
+                finally:
+                    ops.GATE = None
+            outs.append((inst, binary))
+            if nxt is not None:
+                u, binary = g.finish()
+            if self._windows is None:
+                self._windows = g.counts + [0]
+        caller.wait_stream(self.s_unet)
+        caller.wait_stream(self.s_head)
+        for inst, binary in outs:
+            inst.record_stream(caller)
+            binary.record_stream(caller)
+        return outs
+
+
+class _HeadGate:
+    """ops.GATE during one head phase of StreamPipelinedExport(gate=True): feeds the next batch's UNet chunks into
+    the windows between heavy convs (see StreamPipelinedExport._run_gated)."""
+
+    def __init__(self, runner: StreamPipelinedExport, gen):
+        self.r, self.gen = runner, gen
+        self.min_flops = runner.gate_min_flops
+        self.counts = [0]            # light launches per window (window i ends at heavy conv i)
+        self.window = 0
+        self.done = gen is None
+        self.result = None
+        self.issued = 0
+        self.last = None             # event after the latest chunk on the UNet stream
+        w = runner._windows
+        if w is not None and gen is not None:   # chunk budget per window, proportional to its light launches
+            tot = max(sum(w), 1)
+            self.share = [c / tot for c in w]
+        else:
+            self.share = None
+        self._issue_window()         # window 0: the head's opening (RoIAlign, feature extractor, ...)
+
+    def _chunks_for(self, i):
+        if self.share is None:       # first batch: one chunk per window
+            return 1
+        # cumulative target after window i, against ~24 chunks of a B0 UNet (the rest drains after the head)
+        return max(0, round(24 * sum(self.share[:i + 1])) - self.issued)
+
+    def _issue(self, n):
+        from . import ops
+        if self.done or n <= 0:
+            return
+        s = self.r.s_unet
+        prev, ops.GATE = ops.GATE, None
+        try:
+            with torch.cuda.stream(s):
+                for _ in range(n):
+                    try:
+                        next(self.gen)
+                        self.issued += 1
+                    except StopIteration as e:
+                        self.result = e.value
+                        self.done = True
+                        break
+                self.last = torch.cuda.Event()
+                self.last.record(s)
+        finally:
+            ops.GATE = prev
+
+    def _issue_window(self):
+        self._issue(self._chunks_for(self.window))
+
+    def light(self):
+        self.counts[-1] += 1
+
+    def before(self):
+        if self.last is not None:   # the chunks issued so far finish before the heavy conv starts
+            torch.cuda.current_stream().wait_event(self.last)
+
+    def after(self):
+        self.window += 1
+        self.counts.append(0)
+        if self.done:
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        self.r.s_unet.wait_event(ev)
+        self._issue_window()
+
+    def finish(self):
+        """Issue the rest of the UNet (after the head) and return (u, binary_masks) of the next batch."""
+        while not self.done:
+            self._issue(64)
+        return self.result
 
 
 def create_rgb_hierarchical_model(roi_size=28, mask_size=56, multi_scale: bool = False,

@@ -160,6 +160,9 @@ class LaunchProbe:
 
 
 PROBE: Optional[LaunchProbe] = None
+# Serving-schedule hook (hiseg.model.StreamPipelinedExport(gate=True)): ``GATE.before()`` / ``GATE.after()`` run on the
+# host around every conv launch of at least ``GATE.min_flops``, on the launching stream.
+GATE = None
 # Developer hook (tools/layer_profile.py): when a list, every conv launch appends
 # (descriptor copy, tensors kept alive, flops).
 RECORD: Optional[list] = None
@@ -338,18 +341,31 @@ def conv2d(p: ConvPlan, xa: Act, xb: Optional[Act] = None, out: Optional[Act] = 
         keep = [t for t in (xa, xb, out, residual, mul, out2, ws) if t is not None]
         flops = 2.0 * d.N * d.Ho * d.Wo * p.gemm_cols * p.kh * p.kw * (xa.C + (xb.C if xb is not None else 0))
         RECORD.append((dc, keep, p, flops))
+    gate = GATE
+    if gate is not None:
+        flops = 2.0 * d.N * d.Ho * d.Wo * p.gemm_cols * p.kh * p.kw * (xa.C + (xb.C if xb is not None else 0))
+        if flops >= gate.min_flops and not variant:
+            gate.before()
+            _launch_conv(d, p, xa, xb)
+            gate.after()
+            return out
+        gate.light()
+    _launch_conv(d, p, xa, xb, variant)
+    return out
+
+
+def _launch_conv(d, p, xa, xb, variant=0):
     if PROBE is not None:
         key = PROBE.select(d)
         if key is not None:
             flops = 2.0 * d.N * d.Ho * d.Wo * p.gemm_cols * p.kh * p.kw * (xa.C + (xb.C if xb is not None else 0))
             L.check(PROBE.around(key, flops, lambda: L.lib().hiseg_conv2d_fwd(ctypes.byref(d), L.stream_ptr())),
                     "conv2d")
-            return out
+            return
     if variant:
         L.check(L.lib().hiseg_conv2d_fwd_variant(ctypes.byref(d), variant, L.stream_ptr()), "conv2d")
     else:
         L.check(L.lib().hiseg_conv2d_fwd(ctypes.byref(d), L.stream_ptr()), "conv2d")
-    return out
 
 
 # ---------------------------------------------------------------------------------------- misc

@@ -653,9 +653,12 @@ def test_bf16_pipeline_instance_mask_agreement():
     assert max_abs(binary.cpu(), O.binary_masks(sd, ref_u)) < 0.05
 
 
-def test_stream_pipelined_export_matches_serial():
+@pytest.mark.parametrize("gate", [None, 0.001, 0.05])
+def test_stream_pipelined_export_matches_serial(gate):
     """hiseg.StreamPipelinedExport (UNet of batch k+1 on a second stream beside the head of batch k) returns
-    exactly the per-batch outputs of the serial RGBHierarchicalExportWrapper."""
+    exactly the per-batch outputs of the serial RGBHierarchicalExportWrapper -- also with gate=True (the UNet issued
+    in chunks into the windows between the head's heavy convs; thresholds here small enough that most / some of this
+    small model's convs count as heavy), over 4 batches (the first learns the windows, the rest use them)."""
     import filler
     import hiseg
     from helpers import b0_kwargs, hiseg_kwargs
@@ -663,13 +666,20 @@ def test_stream_pipelined_export_matches_serial():
     hiseg.set_compute_dtype(m, torch.bfloat16)
     w = hiseg.RGBHierarchicalExportWrapper(m)
     batches = []
-    for k in range(3):
+    for k in range(4):
         images = torch.from_numpy(filler.uniform(200 + k, (2, 3, 96, 128))).cuda()
         rois = torch.from_numpy(filler.box_rois(300 + k, 2, 3)).cuda()
         batches.append((images, rois))
     with torch.no_grad():
         serial = [w(i, r) for i, r in batches]
-        piped = hiseg.StreamPipelinedExport(w).run(batches)
+        runner = (hiseg.StreamPipelinedExport(w) if gate is None
+                  else hiseg.StreamPipelinedExport(w, gate=True, gate_min_gflop=gate))
+        piped = runner.run(batches)
+        if gate is not None:
+            assert runner._windows is not None and len(runner._windows) > 2, runner._windows
+            piped2 = runner.run(batches)   # learned windows from the first call on
+            for (a, b), (c, d) in zip(piped, piped2):
+                assert torch.equal(a, c) and torch.equal(b, d)
     torch.cuda.synchronize()
     for (a, b), (c, d) in zip(serial, piped):
         assert torch.equal(a, c) and torch.equal(b, d)
