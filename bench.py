@@ -1158,7 +1158,8 @@ def infer_bench(args, device, dtype, rank, world, dist):
     images, rois = synthetic_batch(device, rank)
 
     gate = os.environ.get("HISEG_PIPE_GATE", "0") == "1"
-    runner = None if args.serial else hiseg.StreamPipelinedExport(wrapper, gate=gate)
+    head_prio = os.environ.get("HISEG_PIPE_HEAD_PRIO", "1") == "1"
+    runner = None if args.serial else hiseg.StreamPipelinedExport(wrapper, head_priority=head_prio, gate=gate)
 
     def steps(k):
         if runner is None:
