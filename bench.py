@@ -930,10 +930,8 @@ def main():
     ap.add_argument("--eager-train", action="store_true", help="train / distill legs as eager launches (default on one "
                                                                 "GPU: one replayed HIP graph per step)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
-    ap.add_argument("--child-legs", action="store_true",
-                    help="one GPU: run each leg in a child process of its own (round-5 default; default now: every leg "
-                         "in this process)")
-    ap.add_argument("--in-process", action="store_true", help="(default; kept for old command lines)")
+    ap.add_argument("--in-process", action="store_true",
+                    help="one GPU: run every leg in this process (default: each leg in a child process of its own)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher + rendezvous check only (no GPU work): CPU tests of the multi-rank path")
     args = ap.parse_args()
@@ -1000,10 +998,12 @@ def main():
     if args.distill_only:
         args.train_only, args.no_train = True, True
     # The legs run in the order --order names (default: inference, B0 train, C3, C4, distillation, unfrozen
-    # distillation), all in this process.  Round 5 ran each leg in a child process because the distillation step took
-    # 16.8 ms after the inference leg in one process against 8.9 alone; on the round-6 tree every leg is within 1.4 % of
-    # its child-process time in either order (profiles/r6_leg_order_inprocess.txt), so the isolation is off by default
-    # (--child-legs restores it).  The multi-rank run always uses one process per rank.
+    # distillation).  On one GPU each leg runs in a child process of its own (`bench.py --leg L`, whose JSON object this
+    # process merges), so no leg inherits another's device state.  Round 6 measured every leg within 1.4 % of its
+    # child-process time in one process, in either order -- and in a later run on the same tree the unfrozen
+    # distillation leg at 18.6 ms after the others against 14.7 (profiles/r6_leg_order_inprocess.txt): the
+    # stream-to-hardware-queue binding a process keeps still decides it now and then, so the isolation
+    # stays the default.  --in-process runs all legs in this process; the multi-rank run always uses one process per rank.
     half, eager = max(2, args.steps // 2), args.eager_train
     legs = {
         "infer": (not args.train_only, lambda: out.update(infer_bench(args, device, dtype, rank, world, dist))),
@@ -1032,7 +1032,7 @@ def main():
         on, fn = legs[k]
         if not on:
             continue
-        if world == 1 and args.child_legs:
+        if world == 1 and not args.in_process:
             out.update(_leg_in_child(k, args))
         else:
             if not first:
