@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 #include "hiseg.h"
 
 namespace hiseg {
@@ -76,6 +77,22 @@ __device__ __forceinline__ float act_grad_pre(float v, int act, float beta = 1.f
   const float b = act == HISEG_ACT_SWISH ? beta : 1.f;
   const float s = sigmoidf_(act == HISEG_ACT_SWISH ? beta * v : v);
   return act == HISEG_ACT_SIGMOID ? s * (1.f - s) : s * (1.f + b * v * (1.f - s));
+}
+
+// Run `f` with the activation as a compile-time constant when it is identity / ReLU / SiLU (kActRt: the run-time switch
+// for the others): an unrolled epilogue then holds one compact branch-free body per form instead of the activation
+// switch once per output element -- less code to fetch cold on short launches (tools/icache_probe.hip), same bits.
+constexpr int kActRt = -1;
+template <typename F>
+__device__ __forceinline__ void with_act(int act, F&& f) {
+  if (act == HISEG_ACT_NONE) f(std::integral_constant<int, HISEG_ACT_NONE>{});
+  else if (act == HISEG_ACT_RELU) f(std::integral_constant<int, HISEG_ACT_RELU>{});
+  else if (act == HISEG_ACT_SILU) f(std::integral_constant<int, HISEG_ACT_SILU>{});
+  else f(std::integral_constant<int, kActRt>{});
+}
+template <int A>
+__device__ __forceinline__ float act_c(float v, int act, float beta) {
+  return A == kActRt ? apply_act(v, act, beta) : apply_act(v, A);
 }
 
 // Activations whose derivative needs the pre-activation (not recoverable from the output).

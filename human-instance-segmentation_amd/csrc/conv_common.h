@@ -192,31 +192,34 @@ struct TileEpi {
 
   __device__ __forceinline__ void store(const hiseg_conv2d_desc& d, int M, const int (&px)[TN], const int (&co)[TM],
                                         const floatx4 (&acc)[TM][TN], bool write_out2 = true) {
+    with_act(d.act, [&](auto ac) __attribute__((always_inline)) {
+      constexpr int A = decltype(ac)::value;
 #pragma clang loop unroll(full)
-    for (int i = 0; i < TM; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma clang loop unroll(full)
-      for (int j = 0; j < TN; ++j) {
-        if (px[j] >= M || co[i] >= d.Cout) continue;
-        long long op;
-        int oc;
-        out_site(d, px[j], co[i], op, oc);
-        float v[4];
+        for (int j = 0; j < TN; ++j) {
+          if (px[j] >= M || co[i] >= d.Cout) continue;
+          long long op;
+          int oc;
+          out_site(d, px[j], co[i], op, oc);
+          float v[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * sc[i][e] + sh[i][e];
-        if (d.residual) {
+          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * sc[i][e] + sh[i][e];
+          if (d.residual) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += Quad<T>::get(res[i][j], e);
+            for (int e = 0; e < 4; ++e) v[e] += Quad<T>::get(res[i][j], e);
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = act_c<A>(v[e], d.act, d.act_beta);
+          if (d.mul) {
+            const typename Quad<T>::V m = Quad<T>::load(d.mul, op * d.m_cstride + d.m_coff + oc);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] *= Quad<T>::get(m, e);
+          }
+          Quad<TO>::store(d.out, op * d.o_cstride + d.o_coff + oc, v);
+          if (write_out2 && d.out2) Quad<T>::store(d.out2, op * d.o2_cstride + d.o2_coff + oc, v);
         }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], d.act, d.act_beta);
-        if (d.mul) {
-          const typename Quad<T>::V m = Quad<T>::load(d.mul, op * d.m_cstride + d.m_coff + oc);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] *= Quad<T>::get(m, e);
-        }
-        Quad<TO>::store(d.out, op * d.o_cstride + d.o_coff + oc, v);
-        if (write_out2 && d.out2) Quad<T>::store(d.out2, op * d.o2_cstride + d.o2_coff + oc, v);
-      }
+    });
   }
 };
 

@@ -213,24 +213,27 @@ __global__ void __launch_bounds__(64 * WCO * WPX) conv_fast_kernel(ConvArgs a) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __syncthreads();                                      // every wave is done with the ring (no DMA in flight)
       float* st = reinterpret_cast<float*>(smem);
+      with_act(d.act, [&](auto ac) __attribute__((always_inline)) {
+        constexpr int A = decltype(ac)::value;
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int rl = wpx * TN * 16 + j * 16 + (lane & 15);
-          const int cl = wco * TM * 16 + i * 16 + (lane >> 4) * 4;
-          float v[4];
+          for (int j = 0; j < TN; ++j) {
+            const int rl = wpx * TN * 16 + j * 16 + (lane & 15);
+            const int cl = wco * TM * 16 + i * 16 + (lane >> 4) * 4;
+            float v[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * ep.sc[i][e] + ep.sh[i][e];
-          if (d.residual) {
+            for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * ep.sc[i][e] + ep.sh[i][e];
+            if (d.residual) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += Quad<bf16_t>::get(ep.res[i][j], e);
+              for (int e = 0; e < 4; ++e) v[e] += Quad<bf16_t>::get(ep.res[i][j], e);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = act_c<A>(v[e], d.act, d.act_beta);
+            *reinterpret_cast<float4*>(st + rl * BCO + (((cl >> 2) ^ (rl & (NCH - 1))) << 2)) =
+                make_float4(v[0], v[1], v[2], v[3]);
           }
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], d.act, d.act_beta);
-          *reinterpret_cast<float4*>(st + rl * BCO + (((cl >> 2) ^ (rl & (NCH - 1))) << 2)) =
-              make_float4(v[0], v[1], v[2], v[3]);
-        }
+      });
       __syncthreads();
       for (int idx = t; idx < BPX * NCH; idx += 64 * NW) {
         const int rl = idx / NCH, k = idx - (idx / NCH) * NCH;
