@@ -65,8 +65,11 @@ __device__ __forceinline__ void hc_dma16(__amdgpu_buffer_rsrc_t rsrc, unsigned l
 // channels, g masked by the ReLU of that BatchNorm's forward (bnb_z * bnb_scale + bnb_shift > 0, bnb_z loaded beside
 // the store), summed as g, g * xhat and xhat (xhat = (bnb_z - mean) * invstd); the wave's threads of one chunk are
 // added in a fixed butterfly order and each wave writes one split [3][Cout] -- the reduction pass over (dy, z) is gone.
+// R3 (variant 108, round 6): a ring of three halo buffers (72 KiB of LDS, two workgroups per CU still fit): slice
+// sl + 2's halo is LDS-DMA'd during slice sl, so each slice's pieces have a whole slice more to land before the barrier
+// that needs them.
 template <int ACT, bool RES, int NW, bool UP = false, int ABL = 0, bool RP = false, bool ST = false, int TWB = 1,
-          bool BR = false>
+          bool BR = false, bool R3 = false>
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(ConvArgs a) {
   constexpr int NCG = NW / TWB;                      // Cout groups of 32
   constexpr int BCO = 32 * NCG, TM = 2, NR = 16;    // wave tile: 32 Cout x (16 rows x 16 columns)
@@ -79,6 +82,10 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
   constexpr int HB = PPW * NW * 1024;                 // bytes of one halo buffer
   constexpr int NPX = 256 * TWB;                      // output pixels of the tile
   static_assert((NW == 4 || NW == 8) && (TWB == 1 || (TWB == 2 && NW == 4 && !RP)), "configuration");
+  static_assert(!R3 || (NW == 4 && !RP && TWB == 1 && !ST && !BR), "R3: the plain / residual 128-Cout form");
+  // halo pieces the last wave issues per slice (the fewest of any wave): the vmcnt bound that still waits for every
+  // piece of an older slice
+  constexpr int NPMIN = ((NHR + 15) / 16 - 1 - (NW - 1)) / NW + 1;
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];
   const hiseg_conv2d_desc& d = a.d;
   const int t = threadIdx.x;
@@ -138,6 +145,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
   // halo buffer of slice sl (byte offset in LDS)
   auto hbuf = [&](int sl) __attribute__((always_inline)) -> int {
     if constexpr (RP) return ((nsl - 1 - sl) & 1) ? 32 * 1024 : 56 * 1024;
+    else if constexpr (R3) return (sl % 3) * HB;
     else return (sl & 1) * HB;
   };
   auto halo_dma = [&](int p, int sl, int boff) __attribute__((always_inline)) {
@@ -220,8 +228,19 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
   hc_u4 af[3][TM], an[3][TM];
 #pragma unroll
   for (int p = 0; p < PPW; ++p) halo_dma(p, 0, hbuf(0));
+  if constexpr (R3) {
+    if (nsl > 1) {
+#pragma unroll
+      for (int p = 0; p < PPW; ++p) halo_dma(p, 1, hbuf(1));
+    }
+  }
   load_blk(af, 0, 0);
-  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");    // the halo pieces (older than the 6 weight loads)
+  if constexpr (R3) {   // slice 0's pieces (slice 1's, younger, may fly)
+    if (nsl > 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + NPMIN) : "memory");
+    else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");    // the halo pieces (older than the 6 weight loads)
+  }
   __syncthreads();
 
   // One (slice, kx) block: the next block's weights are loaded first; halo pieces of slice sl + 1 ride in blocks
@@ -239,6 +258,11 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
     // this block to land (they are older than the next block's weight loads).
     auto pieces = [&]() __attribute__((always_inline)) {
       if constexpr ((ABL & 2) != 0) {
+      } else if constexpr (R3 && KX < 2) {   // slice sl + 2's halo into the third buffer
+        if (sl + 2 < nsl) {
+#pragma unroll
+          for (int p = KX * PH; p < (KX == 0 ? PH : PPW); ++p) halo_dma(p, sl + 2, hbuf(sl + 2));
+        }
       } else if constexpr (KX < 2) {
         if (more) {
 #pragma unroll
@@ -294,8 +318,16 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
     }
     __builtin_amdgcn_s_setprio(0);
     if constexpr (KX == 2 && (ABL & 8) == 0) {
-      if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // every halo piece (the next weights may fly)
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (R3) {
+        // slice sl + 1's pieces were issued during slice sl - 1: older than this slice's 18 weight loads and its
+        // slice-(sl + 2) pieces, which may fly
+        if (sl + 2 < nsl) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(18 + NPMIN) : "memory");
+        else if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // every halo piece (the next weights may fly)
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       __syncthreads();   // slice sl+1's halo is in LDS; every wave is done reading slice sl's buffer
     }
     if constexpr ((ABL & 1) == 0) {
@@ -520,7 +552,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
 }
 
 template <int ACT, bool RES, int NW, bool UP = false, int ABL = 0, bool RP = false, bool ST = false, int TWB = 1,
-          bool BR = false>
+          bool BR = false, bool R3 = false>
 static int launch_hwc(const ConvArgs& a, hipStream_t s) {
   const hiseg_conv2d_desc& d = a.d;
   constexpr int BCO = 32 * NW / TWB, TW = 16 * TWB;
@@ -528,8 +560,9 @@ static int launch_hwc(const ConvArgs& a, hipStream_t s) {
   constexpr size_t halo2 = (size_t)2 * PPW * NW * 1024, epi = (size_t)256 * TWB * BCO * 2;
   const int tiles = d.N * ((d.H + 15) / 16) * ((d.W + TW - 1) / TW);
   const int nco = d.Cout_pad / BCO;
-  const size_t lds = RP ? (size_t)80 * 1024 : (halo2 > epi ? halo2 : epi);
-  auto kern = conv_hwc_kernel<ACT, RES, NW, UP, ABL, RP, ST, TWB, BR>;
+  const size_t halo = R3 ? halo2 / 2 * 3 : halo2;
+  const size_t lds = RP ? (size_t)80 * 1024 : (halo > epi ? halo : epi);
+  auto kern = conv_hwc_kernel<ACT, RES, NW, UP, ABL, RP, ST, TWB, BR, R3>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -539,23 +572,23 @@ static int launch_hwc(const ConvArgs& a, hipStream_t s) {
   return hiseg_check_launch("conv_hwc");
 }
 
-template <int NW, bool RP = false, int TWB = 1>
+template <int NW, bool RP = false, int TWB = 1, bool R3 = false>
 static int launch_hwc_nw(const ConvArgs& a, hipStream_t s) {
   const hiseg_conv2d_desc& d = a.d;
   if (d.a_up == 2)   // (conv_hwc_try checked the form)
-    return launch_hwc<HISEG_ACT_RELU, false, NW, true, 0, false, false, TWB>(a, s);
+    return launch_hwc<HISEG_ACT_RELU, false, NW, true, 0, false, false, TWB, false, R3>(a, s);
   const bool res = d.residual != nullptr, relu = d.act == HISEG_ACT_RELU;
-  return res ? (relu ? launch_hwc<HISEG_ACT_RELU, true, NW, false, 0, RP, false, TWB>(a, s)
-                     : launch_hwc<HISEG_ACT_NONE, true, NW, false, 0, RP, false, TWB>(a, s))
-             : (relu ? launch_hwc<HISEG_ACT_RELU, false, NW, false, 0, false, false, TWB>(a, s)
-                     : launch_hwc<HISEG_ACT_NONE, false, NW, false, 0, false, false, TWB>(a, s));
+  return res ? (relu ? launch_hwc<HISEG_ACT_RELU, true, NW, false, 0, RP, false, TWB, false, R3>(a, s)
+                     : launch_hwc<HISEG_ACT_NONE, true, NW, false, 0, RP, false, TWB, false, R3>(a, s))
+             : (relu ? launch_hwc<HISEG_ACT_RELU, false, NW, false, 0, false, false, TWB, false, R3>(a, s)
+                     : launch_hwc<HISEG_ACT_NONE, false, NW, false, 0, false, false, TWB, false, R3>(a, s));
 }
 
 // Whether variant `variant` takes the layer (the layer rules are conv_hwr_try's: the same operands, weight fragments and
 // halo; with d.stats_partial the fused-statistics form: variant 104 / 107, no activation, no residual).
 static bool conv_hwc_applies(const ConvArgs& a, int variant) {
   const hiseg_conv2d_desc& d = a.d;
-  if ((variant < 104 || variant > 107) || d.weight_frag == nullptr) return false;
+  if ((variant < 104 || variant > 108) || d.weight_frag == nullptr) return false;
   if (d.dtype != HISEG_BF16 || d.out_dtype != HISEG_BF16) return false;
   if ((d.a_up != 1 && d.a_up != 2) || d.in_scale != nullptr || d.convT || d.mul != nullptr || d.out2 != nullptr)
     return false;
@@ -650,6 +683,7 @@ int conv_hwc_try(const ConvArgs& a, hipStream_t s, int variant) {
     return r < 0 ? r : 1;
   }
   const int r = variant == 107 ? launch_hwc_nw<4, false, 2>(a, s)
+              : variant == 108 ? launch_hwc_nw<4, false, 1, true>(a, s)
               : variant == 105 ? launch_hwc_nw<8>(a, s)
               : variant == 106 ? launch_hwc_nw<4, true>(a, s)
                                : launch_hwc_nw<4>(a, s);

@@ -530,7 +530,7 @@ static bool hwc64_mode() {
 static bool release_variant(int v) {
   return v == -1 || v == 0 || (v >= 1 && v <= 8) || v == 50 || v == 51 || v == 52 || v == 54 || v == 58 ||
          (v >= 60 && v <= 69) || v == 70 || v == 71 || v == 72 || v == 74 || v == 80 || v == 82 || v == 84 || v == 86 ||
-         v == 88 || v == 89 || v == 90 || (v >= 92 && v <= 101) || v == 103 || (v >= 104 && v <= 107);
+         v == 88 || v == 89 || v == 90 || (v >= 92 && v <= 101) || v == 103 || (v >= 104 && v <= 108);
 }
 
 // Workspace bytes the automatic choice uses for this layer (split-K generic kernel), 0 when it needs none.
@@ -705,7 +705,7 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
   } else if ((variant >= 92 && variant <= 97) || variant == 100 || variant == 101 || (variant >= 110 && variant < 142)) {
     const int r = conv_hwr_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
-  } else if ((variant >= 104 && variant <= 107) || (variant >= 150 && variant < 4300)) {
+  } else if ((variant >= 104 && variant <= 108) || (variant >= 150 && variant < 4300)) {
     const int r = conv_hwc_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
   } else if (variant == 103) {
