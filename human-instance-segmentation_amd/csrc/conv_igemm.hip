@@ -527,6 +527,12 @@ static bool hwc64_mode() {
   return !(e && atoi(e) == 0);
 }
 
+// HISEG_CONV_HWC_R3=0 (read per call; A/B timing): the 128-Cout layers on variant 104 (two halo buffers) instead of 108
+static bool hwc_r3_mode() {
+  const char* e = getenv("HISEG_CONV_HWC_R3");
+  return !(e && atoi(e) == 0);
+}
+
 static bool release_variant(int v) {
   return v == -1 || v == 0 || (v >= 1 && v <= 8) || v == 50 || v == 51 || v == 52 || v == 54 || v == 58 ||
          (v >= 60 && v <= 69) || v == 70 || v == 71 || v == 72 || v == 74 || v == 80 || v == 82 || v == 84 || v == 86 ||
@@ -771,8 +777,11 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
     // of the tile -- half the weight-fragment loads, each halo row's B fragment reused across the 3 ky taps;
     // tools/conv_bench.py, profiles/r5_conv_hwc.txt: 256->256 @64x48 x256 ROIs 0.736 -> 0.678 ms, 128->128 @128x96
     // 0.875 -> 0.799, 128->256 0.369 -> 0.345; bit-identical to variant 97 / 86)
+    // Round 6: variant 108, the same kernel with a ring of three halo buffers (slice sl + 2's halo in flight during
+    // slice sl; 72 KiB of LDS, two workgroups per CU): bit-identical, 256->256 @64x48 x256 ROIs 0.709 -> 0.701 ms,
+    // 128->128 @128x96 0.829 -> 0.814, 128->256 0.364 -> 0.351 (tools/conv_bench.py, profiles/r6_conv_hwc_r3.txt)
     if (v == 0 && !four_waves && halo && d->weight_frag != nullptr && d->Cout % 128 == 0) {
-      const int r = conv_hwc_try(a, s, 104);
+      const int r = conv_hwc_try(a, s, hwc_r3_mode() ? 108 : 104);
       if (r != 0) return r < 0 ? r : HISEG_OK;
     }
     if (v == 0 && !four_waves && halo && d->weight_frag != nullptr && d->Cout % 128 == 0) {

@@ -601,8 +601,13 @@ __global__ void __launch_bounds__(256) dwconv_q_kernel(const void* in, int H, in
 // Per output the arithmetic is dwconv_q_kernel's exactly -- same taps skipped outside the image, same tap order, same
 // fused multiply-adds and epilogue -- so the outputs are bit-identical to it.  SE pool: one partial per (image, tile)
 // (hiseg_dw_gap_tiles = ceil(Ho / 8) x ceil(Wo / 16), independent of the batch).
+//
+// CP (round 6): channels per thread.  CP 4: a thread = one channel quad x 2 strips (16 quads x 16 strip groups per
+// block); CP 2: one channel pair x 4 strips (32 pairs x 8 groups).  The k5 form's 25 taps x CP f32 weights live in
+// registers: at CP 4 that is 100 VGPRs and the kernel held 256 + 6 AGPRs (one wave per SIMD, one block per CU, the
+// window load of the next block never overlapped this one's compute); at CP 2, 50.  Same per-output arithmetic.
 constexpr int kDwTH = 8, kDwTW = 16, kDwCG = 64, kDwPS = kDwCG * 2 + 8;
-template <int KS, int ST, bool ZP = false>
+template <int KS, int ST, bool ZP = false, int CP = 4>
 __global__ void __launch_bounds__(256) dwconv_t_kernel(const void* in, int H, int W, int C, const float* w,
                                                        const float* scale, const float* shift, int act, void* out,
                                                        int Ho, int Wo, float* gap, int xcd) {
@@ -666,123 +671,157 @@ __global__ void __launch_bounds__(256) dwconv_t_kernel(const void* in, int H, in
         *reinterpret_cast<uint4*>(dws + (idx >> 3) * kDwPS + (idx & 7) * 16) = v[u];
     }
   }
-  // ---- compute: thread = channel quad qd (16 per block) x strips it, it + 16 (two per thread)
-  const int qd = t & 15, it = t >> 4;
-  const int c = g0 + qd * 4;
+  // ---- compute: thread = channel group qd of CP channels (64 / CP per block) x strips it, it + NG, ... (NG groups)
+  static_assert(CP == 2 || CP == 4, "CP: 2 or 4 channels per thread");
+  constexpr int NQ = kDwCG / CP, NG = 256 / NQ, NP = CP / 2;
+  const int qd = t % NQ, it = t / NQ;
+  const int c = g0 + qd * CP;
   const bool live = c < C;
   const int cc = live ? c : 0;
   typedef float f2v __attribute__((ext_vector_type(2)));
-  float wk[ZP ? 1 : KS * KS][4], sc[4], sh[4], gs[4] = {0.f, 0.f, 0.f, 0.f};
-  f2v wp[ZP ? KS * KS : 1][2];   // ZP: the weights as channel pairs (packed-FMA operands)
+  float wk[ZP ? 1 : KS * KS][CP], sc[CP], sh[CP], gs[CP];
+  f2v wp[ZP ? KS * KS : 1][NP];   // ZP: the weights as channel pairs (packed-FMA operands)
 #pragma unroll
   for (int k = 0; k < KS * KS; ++k) {
-    const float4 f = *reinterpret_cast<const float4*>(w + k * C + cc);
-    if constexpr (ZP) {
-      wp[k][0] = f2v{f.x, f.y};
-      wp[k][1] = f2v{f.z, f.w};
+    float f[CP];
+    if constexpr (CP == 4) {
+      const float4 q = *reinterpret_cast<const float4*>(w + k * C + cc);
+      f[0] = q.x; f[1] = q.y; f[2] = q.z; f[3] = q.w;
     } else {
-      wk[k][0] = f.x; wk[k][1] = f.y; wk[k][2] = f.z; wk[k][3] = f.w;
+      const float2 q = *reinterpret_cast<const float2*>(w + k * C + cc);
+      f[0] = q.x; f[1] = q.y;
+    }
+#pragma unroll
+    for (int e = 0; e < CP; ++e) {
+      if constexpr (ZP) wp[k][e >> 1][e & 1] = f[e];
+      else wk[k][e] = f[e];
     }
   }
 #pragma unroll
-  for (int e = 0; e < 4; ++e) { sc[e] = scale[cc + e]; sh[e] = shift[cc + e]; }
-  // held in registers for both strips (the compiler otherwise re-loads each tap's weights at its use)
+  for (int e = 0; e < CP; ++e) { sc[e] = scale[cc + e]; sh[e] = shift[cc + e]; gs[e] = 0.f; }
+  // held in registers for every strip (the compiler otherwise re-loads each tap's weights at its use)
 #pragma unroll
   for (int k = 0; k < KS * KS; ++k) {
-    if constexpr (ZP) asm volatile("" : "+v"(wp[k][0]), "+v"(wp[k][1]));
-    else asm volatile("" : "+v"(wk[k][0]), "+v"(wk[k][1]), "+v"(wk[k][2]), "+v"(wk[k][3]));
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      if constexpr (ZP) asm volatile("" : "+v"(wp[k][p]));
+      else asm volatile("" : "+v"(wk[k][2 * p]), "+v"(wk[k][2 * p + 1]));
+    }
   }
   __syncthreads();
-  const int nq = C >> 2;
-  uint2* dst = reinterpret_cast<uint2*>(out) + (long long)n * Ho * Wo * nq;
+  const int nq = C / CP;
+  // one uint per channel pair of the output (bf16 x 2)
+  unsigned* dst = reinterpret_cast<unsigned*>(out) + (long long)n * Ho * Wo * (C >> 1);
 #pragma unroll
-  for (int sj = 0; sj < NSTRIP / 16; ++sj) {
-    const int st = it + 16 * sj;
+  for (int sj = 0; sj < NSTRIP / NG; ++sj) {
+    const int st = it + NG * sj;
     const int ry = st / (kDwTW / kDwXS), rx = (st - ry * (kDwTW / kDwXS)) * kDwXS;
     const int oy = oy0 + ry, ox = ox0 + rx;
     if (!live || oy >= Ho) continue;
-    float acc[kDwXS][4];
+    float acc[kDwXS][CP];
 #pragma unroll
     for (int xo = 0; xo < kDwXS; ++xo)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) acc[xo][e] = 0.f;
+      for (int e = 0; e < CP; ++e) acc[xo][e] = 0.f;
     if constexpr (ZP) {
       // no per-tap bounds test -- the window holds zeros outside the image, and fma(w, 0, acc) == acc in value (the
       // sign of an all-zero sum may differ from skipping the tap): straight-line packed FMAs, no exec-mask branches.
       // Per element the same fma(w, v, acc) chain in the same tap order as below.
-      f2v a2[kDwXS][2];
+      f2v a2[kDwXS][NP];
 #pragma unroll
-      for (int xo = 0; xo < kDwXS; ++xo) a2[xo][0] = a2[xo][1] = f2v{0.f, 0.f};
+      for (int xo = 0; xo < kDwXS; ++xo)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) a2[xo][p] = f2v{0.f, 0.f};
 #pragma unroll
       for (int ky = 0; ky < KS; ++ky) {
-        const char* row = dws + ((ry * ST + ky) * IW + rx * ST) * kDwPS + qd * 8;
+        const char* row = dws + ((ry * ST + ky) * IW + rx * ST) * kDwPS + qd * 2 * CP;
 #pragma unroll
         for (int j = 0; j < NIN; ++j) {
-          const uint2 raw = *reinterpret_cast<const uint2*>(row + j * kDwPS);
-          const f2v v01{__uint_as_float(raw.x << 16), __uint_as_float(raw.x & 0xffff0000u)};
-          const f2v v23{__uint_as_float(raw.y << 16), __uint_as_float(raw.y & 0xffff0000u)};
+          unsigned raw[NP];
+          if constexpr (CP == 4) {
+            const uint2 r2 = *reinterpret_cast<const uint2*>(row + j * kDwPS);
+            raw[0] = r2.x; raw[NP - 1] = r2.y;
+          } else {
+            raw[0] = *reinterpret_cast<const unsigned*>(row + j * kDwPS);
+          }
+          f2v v[NP];
+#pragma unroll
+          for (int p = 0; p < NP; ++p) v[p] = f2v{__uint_as_float(raw[p] << 16), __uint_as_float(raw[p] & 0xffff0000u)};
 #pragma unroll
           for (int xo = 0; xo < kDwXS; ++xo) {
             const int kx = j - xo * ST;
             if (kx < 0 || kx >= KS) continue;
-            a2[xo][0] = __builtin_elementwise_fma(wp[ky * KS + kx][0], v01, a2[xo][0]);
-            a2[xo][1] = __builtin_elementwise_fma(wp[ky * KS + kx][1], v23, a2[xo][1]);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) a2[xo][p] = __builtin_elementwise_fma(wp[ky * KS + kx][p], v[p], a2[xo][p]);
           }
         }
-        // k5: one window row's reads live at a time (hoisting all 5 rows' reads took 251-256 VGPRs)
-        if constexpr (KS == 5) __builtin_amdgcn_sched_barrier(0);
+        // k5 at CP 4: one window row's reads live at a time (hoisting all 5 rows' reads took 251-256 VGPRs)
+        if constexpr (KS == 5 && CP == 4) __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
-      for (int xo = 0; xo < kDwXS; ++xo) {
-        acc[xo][0] = a2[xo][0].x; acc[xo][1] = a2[xo][0].y; acc[xo][2] = a2[xo][1].x; acc[xo][3] = a2[xo][1].y;
-      }
+      for (int xo = 0; xo < kDwXS; ++xo)
+#pragma unroll
+        for (int e = 0; e < CP; ++e) acc[xo][e] = a2[xo][e >> 1][e & 1];
     }
 #pragma unroll
     for (int ky = 0; ky < (ZP ? 0 : KS); ++ky) {
       const int iy = oy * ST - KS / 2 + ky;
       if ((unsigned)iy >= (unsigned)H) continue;
-      const char* row = dws + ((ry * ST + ky) * IW + rx * ST) * kDwPS + qd * 8;
+      const char* row = dws + ((ry * ST + ky) * IW + rx * ST) * kDwPS + qd * 2 * CP;
 #pragma unroll
       for (int j = 0; j < NIN; ++j) {
         const int ix = ox * ST - KS / 2 + j;
         if ((unsigned)ix >= (unsigned)W) continue;
-        const uint2 raw = *reinterpret_cast<const uint2*>(row + j * kDwPS);
-        const float v[4] = {__uint_as_float(raw.x << 16), __uint_as_float(raw.x & 0xffff0000u),
-                            __uint_as_float(raw.y << 16), __uint_as_float(raw.y & 0xffff0000u)};
+        unsigned raw[NP];
+        if constexpr (CP == 4) {
+          const uint2 r2 = *reinterpret_cast<const uint2*>(row + j * kDwPS);
+          raw[0] = r2.x; raw[NP - 1] = r2.y;
+        } else {
+          raw[0] = *reinterpret_cast<const unsigned*>(row + j * kDwPS);
+        }
+        float v[CP];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          v[2 * p] = __uint_as_float(raw[p] << 16);
+          v[2 * p + 1] = __uint_as_float(raw[p] & 0xffff0000u);
+        }
 #pragma unroll
         for (int xo = 0; xo < kDwXS; ++xo) {
           const int kx = j - xo * ST;
           if (kx < 0 || kx >= KS) continue;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) acc[xo][e] += wk[ZP ? 0 : ky * KS + kx][e] * v[e];
+          for (int e = 0; e < CP; ++e) acc[xo][e] += wk[ZP ? 0 : ky * KS + kx][e] * v[e];
         }
       }
     }
 #pragma unroll
     for (int xo = 0; xo < kDwXS; ++xo) {
       if (ox + xo >= Wo) break;
-      float o[4];
+      float o[CP];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
+      for (int e = 0; e < CP; ++e) {
         o[e] = apply_act(acc[xo][e] * sc[e] + sh[e], act);
         gs[e] += o[e];
       }
-      dst[((long long)oy * Wo + ox + xo) * nq + (c >> 2)] = make_uint2(f2bf2(o[0], o[1]), f2bf2(o[2], o[3]));
+      unsigned* d = dst + ((long long)oy * Wo + ox + xo) * (C >> 1) + (c >> 1);
+      if constexpr (CP == 4) *reinterpret_cast<uint2*>(d) = make_uint2(f2bf2(o[0], o[1]), f2bf2(o[2], o[3]));
+      else *d = f2bf2(o[0], o[1]);
     }
   }
+  (void)nq;
   if (gap == nullptr) return;
-  __syncthreads();   // the window is no longer read: its LDS takes the 16 x 64 pool partials
+  __syncthreads();   // the window is no longer read: its LDS takes the NG x 64 pool partials
   float* red = reinterpret_cast<float*>(dws);
 #pragma unroll
-  for (int e = 0; e < 4; ++e) red[t * 4 + e] = gs[e];
+  for (int e = 0; e < CP; ++e) red[t * CP + e] = gs[e];
   __syncthreads();
   if (it == 0 && live) {
-    for (int r = 1; r < 16; ++r)
+    for (int r = 1; r < NG; ++r)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) gs[e] += red[(r * 16 + qd) * 4 + e];
+      for (int e = 0; e < CP; ++e) gs[e] += red[(r * NQ + qd) * CP + e];
     float* gp = gap + ((long long)n * gridDim.x + bt) * C + c;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) gp[e] = gs[e];
+    for (int e = 0; e < CP; ++e) gp[e] = gs[e];
   }
 }
 
@@ -1181,6 +1220,10 @@ static void dw_t_attr() {
                               (int)dw_lds(KS, ST));
     (void)hipFuncSetAttribute((const void*)dwconv_t_kernel<KS, ST, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)dw_lds(KS, ST));
+    (void)hipFuncSetAttribute((const void*)dwconv_t_kernel<KS, ST, false, 2>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)dw_lds(KS, ST));
+    (void)hipFuncSetAttribute((const void*)dwconv_t_kernel<KS, ST, true, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)dw_lds(KS, ST));
     done = true;
   }
 }
@@ -1192,6 +1235,16 @@ static bool dw_zero_pad(int K) {
   const char* e = getenv("HISEG_DWCONV_ZP");
   const int m = e ? atoi(e) : 2;
   return m == 2 || (K == 3 && m == 1);
+}
+
+// channels per thread of the LDS-tiled kernel (HISEG_DWCONV_CP, read per call: 4 or 2 everywhere; default: 2 on the
+// k5 layers, whose CP-4 form holds 256 VGPRs + AGPRs, and on the k3 layers of < 512 channels).  tools/dw_bench.py,
+// profiles/r6_dw_cp.txt: k5 stride 1 1.7-2.1x faster (B7 480 ch @80x80 53.0 -> 30.0 us, 1344 @40x40 37.6 -> 21.7, C2
+// 240 @60x80 142 -> 69, 1152 @15x20 64.5 -> 32.8), k3 stride 1 3-7 % faster up to 288 channels, 6 % slower at 960
+static int dw_cp(int K, int C) {
+  const char* e = getenv("HISEG_DWCONV_CP");
+  const int m = e ? atoi(e) : 0;
+  return m == 2 || m == 4 ? m : (K == 5 || C < 512 ? 2 : 4);
 }
 
 static int dwconv_launch(int dtype, const void* in, int N, int H, int W, int C, int K, int stride, const float* w,
@@ -1219,9 +1272,16 @@ static int dwconv_launch(int dtype, const void* in, int N, int H, int W, int C, 
   do {                                                                                                        \
     if (dtype == HISEG_BF16 && dwt) {                                                                         \
       dw_t_attr<KS, ST>();                                                                                    \
-      if (dw_zero_pad(KS))                                                                                    \
+      const bool zp = dw_zero_pad(KS), cp2 = dw_cp(KS, C) == 2;                                                    \
+      if (zp && cp2)                                                                                          \
+        hipLaunchKernelGGL((dwconv_t_kernel<KS, ST, true, 2>), gridt, dim3(256), dw_lds(KS, ST), s, in, H, W, \
+                           C, w, scale, shift, act, out, Ho, Wo, gap, dw_xcd_remap());                        \
+      else if (zp)                                                                                            \
         hipLaunchKernelGGL((dwconv_t_kernel<KS, ST, true>), gridt, dim3(256), dw_lds(KS, ST), s, in, H, W, C, \
                            w, scale, shift, act, out, Ho, Wo, gap, dw_xcd_remap());                           \
+      else if (cp2)                                                                                           \
+        hipLaunchKernelGGL((dwconv_t_kernel<KS, ST, false, 2>), gridt, dim3(256), dw_lds(KS, ST), s, in, H,   \
+                           W, C, w, scale, shift, act, out, Ho, Wo, gap, dw_xcd_remap());                     \
       else                                                                                                    \
         hipLaunchKernelGGL((dwconv_t_kernel<KS, ST, false>), gridt, dim3(256), dw_lds(KS, ST), s, in, H, W,   \
                            C, w, scale, shift, act, out, Ho, Wo, gap, dw_xcd_remap());                        \

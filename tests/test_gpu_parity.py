@@ -1179,7 +1179,8 @@ def test_conv_hwc_bit_identical_to_hwr(shape):
     fragment reused across the 3 ky taps; 106 with the residual tile prefetched into LDS) and 105 (256-Cout workgroups):
     conv_hwr's per-element accumulation order (channel-major slices, kx-major / ky-inner taps, one 32-channel MFMA per
     (slice, tap)) -- equal to variant 97 bit for bit: ragged pixel tiles, residual / ReLU / none, two sources, Cout
-    128 / 256 / 384; the automatic choice takes 104 for 128-multiple Cout.  Outputs NaN-prefilled."""
+    128 / 256 / 384; the automatic choice takes 108 (round 6: 104 with a ring of three halo buffers) for 128-multiple
+    Cout.  Outputs NaN-prefilled."""
     from hiseg import ops
     N, Ca, Cb, Cout, H, W, res, relu = shape
     dt = torch.bfloat16
@@ -1192,7 +1193,7 @@ def test_conv_hwc_bit_identical_to_hwr(shape):
     assert p.weight_frag is not None
     R = ops.Act.from_nchw(torch.randn(N, Cout, H, W, device=DEV, generator=g), dt) if res else None
     outs = {}
-    vs = (97, 104, 106, 0) + ((105,) if Cout % 256 == 0 else ())
+    vs = (97, 104, 106, 108, 0) + ((105,) if Cout % 256 == 0 else ())
     for v in vs:
         o = ops.Act.new(N, H, W, Cout, dt, torch.device(DEV))
         o.t.fill_(float("nan"))
@@ -1256,7 +1257,7 @@ def test_conv_hwc64_upsampled_decoder_bit_identical(shape):
 @pytest.mark.parametrize("shape", [(2, 320, 128, 256, 30, 40), (2, 256, 64, 128, 20, 24), (1, 128, 64, 128, 18, 34)])
 def test_conv_hwc_upsampled_decoder_bit_identical(shape):
     """The smp decoder's conv1 form (src A nearest-x2 upsampled, src B the encoder skip; ReLU, no residual) on
-    conv_hwc (variant 104) equals conv_hwr (97) bit for bit."""
+    conv_hwc (variants 104, 108) equals conv_hwr (97) bit for bit."""
     from hiseg import ops
     N, Ca, Cb, Cout, H, W = shape
     dt = torch.bfloat16
@@ -1266,20 +1267,20 @@ def test_conv_hwc_upsampled_decoder_bit_identical(shape):
     w = torch.randn(Cout, Ca + Cb, 3, 3, device=DEV, generator=g) / ((Ca + Cb) * 9) ** 0.5
     p = ops.pack_conv(w, torch.randn(Cout, device=DEV, generator=g) * 0.1, None, 1, dt, DEV, pad=1, split=(Ca, Cb))
     outs = {}
-    for v in (97, 104, 0):
+    for v in (97, 104, 108, 0):
         o = ops.Act.new(N, H, W, Cout, dt, torch.device(DEV))
         o.t.fill_(float("nan"))
         outs[v] = ops.conv2d(p, xa, xb, out=o, a_up=2, variant=v).t.clone()
     torch.cuda.synchronize()
     assert torch.isfinite(outs[97].float()).all()
-    assert torch.equal(outs[104], outs[97]) and torch.equal(outs[0], outs[97])
+    assert torch.equal(outs[104], outs[97]) and torch.equal(outs[108], outs[97]) and torch.equal(outs[0], outs[97])
 
 
 @pytest.mark.parametrize("shape", [(2, 37, 45, 240, 5, 1), (3, 20, 20, 2304, 5, 1), (2, 33, 47, 144, 3, 2),
                                    (2, 40, 40, 480, 5, 2), (1, 9, 7, 192, 3, 1), (2, 64, 48, 200, 3, 1)])
 def test_dwconv_lds_tile_bit_identical_to_gather_kernel(shape, monkeypatch):
     """The LDS-tiled depthwise conv (dwconv_t_kernel: 8 x 16 output tiles x 64 channels, the input window loaded
-    once; bf16 stride-1 layers of >= 192 channels) against the register-gather kernel (dwconv_q_kernel,
+    once; bf16 stride-1 layers of >= 192 channels; 4 and 2 channels per thread, HISEG_DWCONV_CP) against the register-gather kernel (dwconv_q_kernel,
     HISEG_DWCONV_T=0): bit-identical outputs (same taps, order and epilogue) at ragged tiles and partial channel
     groups, k3 / k5; the fused SE pool and gate within f32 re-association (one partial per tile instead of per strip
     range), the gate batch-invariant (the automatic choice's tiled layers).  HISEG_DWCONV_T=2 forces the tiled kernel
@@ -1295,16 +1296,22 @@ on the stride-2 and narrow layers the automatic choice gives the gather kernel."
     w1, b1 = torch.randn(cr, C, device=DEV, generator=g) * 0.1, torch.randn(cr, device=DEV, generator=g) * 0.1
     w2, b2 = torch.randn(C, cr, device=DEV, generator=g) * 0.1, torch.randn(C, device=DEV, generator=g) * 0.1
     res = {}
-    for mode in ("2", "0"):   # 2: the LDS-tiled kernel for every bf16 layer, stride 2 and narrow ones included
+    # 2: the LDS-tiled kernel for every bf16 layer, stride 2 and narrow ones included, at 4 and 2 channels per thread
+    for mode, cp in (("2", "4"), ("2", "2"), ("0", "4")):
         monkeypatch.setenv("HISEG_DWCONV_T", mode)
+        monkeypatch.setenv("HISEG_DWCONV_CP", cp)
         plain = ops.dwconv(A, wd, sc, sh, k, stride, 3).t.clone()
         h, gate = ops.dwconv_se_gate(A, wd, sc, sh, k, stride, 3, w1, b1, w2, b2, 3)
-        res[mode] = (plain, h.t.clone(), gate.clone())
+        res[mode + cp] = (plain, h.t.clone(), gate.clone())
+    monkeypatch.delenv("HISEG_DWCONV_CP")
     torch.cuda.synchronize()
-    (p1, h1, g1), (p0, h0, g0) = res["2"], res["0"]
-    assert torch.isfinite(p1.float()).all()
-    assert torch.equal(p1, p0) and torch.equal(h1, h0) and torch.equal(p1, h1)
-    assert (g1 - g0).abs().max().item() < 1e-5
+    (p0, h0, g0) = res["04"]
+    for key in ("24", "22"):
+        p1, h1, g1 = res[key]
+        assert torch.isfinite(p1.float()).all()
+        assert torch.equal(p1, p0) and torch.equal(h1, h0) and torch.equal(p1, h1), key
+        assert (g1 - g0).abs().max().item() < 1e-5, key
+    g1 = res["22" if k == 5 or C < 512 else "24"][2]   # the default channels per thread (dw_cp): the pool sums' order
     if not (192 <= C < 2048 and (stride == 1 or k == 5)):   # the automatic choice's tiled layers (dw_use_tiles)
         return
     # batch invariance of the pooled gate (tile partials do not depend on the batch): image 0 alone

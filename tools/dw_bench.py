@@ -1,7 +1,8 @@
 """Depthwise conv timing per EfficientNet layer shape (developer tool, GPU): the automatic choice, the LDS-tiled kernel
 forced for every layer (HISEG_DWCONV_T=2) and the register-gather kernel (HISEG_DWCONV_T=0), HIP events, algorithmic GB/s (input + output read / written once).
 
-Usage: python tools/dw_bench.py [--reps 20] [--shapes a,b] [--modes 1,2,0]"""
+Usage: python tools/dw_bench.py [--reps 20] [--shapes a,b] [--modes 1,2,0] [--ab HISEG_DWCONV_FW=0,HISEG_DWCONV_FW=1]
+(--ab: each mode timed once per listed environment setting, in order; the launcher reads them per call)"""
 import argparse
 import os
 import sys
@@ -28,6 +29,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--shapes", default="", help="comma-separated shape names (default: all)")
     ap.add_argument("--modes", default="1,2,0", help="HISEG_DWCONV_T values: 1 auto, 2 LDS tile, 0 gather")
+    ap.add_argument("--ab", default="", help="comma-separated KEY=VALUE settings, each mode timed under each")
     a = ap.parse_args()
     dt = torch.bfloat16
     for name, N, H, W, C, k, st in SHAPES:
@@ -42,8 +44,11 @@ def main():
         Ho, Wo = (H + 2 * (k // 2) - k) // st + 1, (W + 2 * (k // 2) - k) // st + 1
         nbytes = (N * H * W * C + N * Ho * Wo * C) * 2
         row = []
-        for mode in a.modes.split(","):
+        settings = [kv.split("=", 1) for kv in a.ab.split(",")] if a.ab else [None]
+        for mode, kv in [(m, kv) for m in a.modes.split(",") for kv in settings]:
             os.environ["HISEG_DWCONV_T"] = mode
+            if kv is not None:
+                os.environ[kv[0]] = kv[1]
             for _ in range(3):
                 ops.dwconv_se_gate(x, w, sc, sh, k, st, 3, w1, b1, w2, b2, 3)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -53,7 +58,8 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / a.reps
-            row.append(f"{ {'1': 'auto', '2': 'lds', '0': 'gather'}[mode]} {ms * 1e3:8.1f} us {nbytes / ms / 1e6:7.0f} GB/s")
+            tag = {'1': 'auto', '2': 'lds', '0': 'gather'}[mode] + (f"[{kv[1]}]" if kv is not None else "")
+            row.append(f"{tag} {ms * 1e3:8.1f} us {nbytes / ms / 1e6:7.0f} GB/s")
         print(f"{name:22s} " + "   ".join(row), flush=True)
 
 
