@@ -1409,15 +1409,20 @@ def test_train_step_bf16_within_torch_bf16_of_oracle(monkeypatch):
     assert n_h < 2 * n_t + 1e-2
 
 
+@pytest.mark.parametrize("tiled", ["1", "0"])
 @pytest.mark.parametrize("case", [(4, 32, 320, 320, 3, 1), (4, 96, 320, 320, 3, 2), (4, 144, 160, 160, 5, 1),
-                                  (4, 240, 80, 80, 5, 2)])
-def test_depthwise_weight_gradient_matches_f64_at_encoder_scale(case):
+                                  (4, 240, 80, 80, 5, 2), (4, 1152, 20, 20, 5, 1), (2, 200, 37, 45, 5, 1),
+                                  (3, 104, 33, 21, 3, 2), (1, 40, 9, 7, 5, 2)])
+def test_depthwise_weight_gradient_matches_f64_at_encoder_scale(case, tiled, monkeypatch):
     """The depthwise weight gradient of the unfrozen encoder's largest-pixel layers (B0 at 640 x 640, 4 images: up to
     409 600 output pixels, 1 024 split partials per weight) against float64 autograd of the same bf16 operands.  The
     split partials are f32 sums of ~32 exact bf16 products; their reduce runs in double: the result sits
-    within 1e-5 of the float64 gradient's scale."""
+    within 1e-5 of the float64 gradient's scale.  Both forms (HISEG_DW_WGRAD_TILE: 1 the LDS-tiled kernel of round 6,
+    per-tile-row f32 partials of 16 x K products, one- or two-pass double reduce; 0 the split kernel), ragged tiles,
+    partial channel groups, and the gradient accumulated onto a non-zero buffer."""
     from hiseg import _lib as L
     from hiseg.ops import Act, hdtype
+    monkeypatch.setenv("HISEG_DW_WGRAD_TILE", tiled)
     N, C, H, W, k, st = case
     g = torch.Generator(device=DEV).manual_seed(123)
     x = torch.randn(N, C, H, W, device=DEV, generator=g).bfloat16()
@@ -1427,12 +1432,51 @@ def test_depthwise_weight_gradient_matches_f64_at_encoder_scale(case):
     lib = L.lib()
     ws = torch.empty(int(lib.hiseg_dw_bwd_weight_ws(hdtype(torch.bfloat16), N, Ho, Wo, C, k)), dtype=torch.float32,
                      device=DEV)
-    dw = torch.zeros(C * k * k, dtype=torch.float32, device=DEV)
+    dw0 = torch.randn(C * k * k, dtype=torch.float32, device=DEV, generator=g)
+    dw = dw0.clone()
     L.check(lib.hiseg_dw_bwd_weight(hdtype(torch.bfloat16), xa.ptr(), dya.ptr(), N, H, W, C, k, st, Ho, Wo,
                                     ws.data_ptr(), dw.data_ptr(), L.stream_ptr()), "dw_bwd_weight")
     w64 = torch.zeros(C, 1, k, k, dtype=torch.float64, device=DEV, requires_grad=True)
     y = F.conv2d(x.double(), w64, stride=st, padding=k // 2, groups=C)
     y.backward(dy.double())
-    ref = w64.grad.reshape(-1)
+    ref = w64.grad.reshape(-1) + dw0.double()
     err = ((dw.double() - ref).abs().max() / ref.abs().max()).item()
     assert err < 1e-5, err
+
+
+@pytest.mark.parametrize("case", [(4, 96, 320, 320, 3), (4, 144, 160, 160, 5), (4, 240, 80, 80, 3), (4, 672, 40, 40, 5),
+                                  (2, 200, 37, 45, 5), (3, 104, 33, 21, 3), (1, 40, 9, 7, 5)])
+def test_depthwise_stride2_data_gradient_tiled_matches_per_pixel_and_f64(case, monkeypatch):
+    """The stride-2 depthwise data gradient: the LDS-tiled kernel (dw_dgrad_s2_tile_kernel, round 6; dy window in
+    LDS, wave-uniform row parity) against the per-pixel kernel (HISEG_DW_DGRAD_TILE=0) and float64 autograd of the
+    same bf16 operands -- the B0 student's four stride-2 layers at 640 x 640 plus ragged tiles, odd sizes and partial
+    channel groups; written over and accumulated onto a bf16 buffer."""
+    from hiseg import _lib as L
+    from hiseg.ops import Act, hdtype
+    N, C, H, W, k = case
+    g = torch.Generator(device=DEV).manual_seed(321)
+    Ho, Wo = (H + 2 * (k // 2) - k) // 2 + 1, (W + 2 * (k // 2) - k) // 2 + 1
+    dy = torch.randn(N, C, Ho, Wo, device=DEV, generator=g).bfloat16()
+    w = torch.randn(C, k * k, device=DEV, generator=g) * 0.3
+    prev = torch.randn(N, C, H, W, device=DEV, generator=g).bfloat16()
+    dya = Act.from_nchw(dy.float(), torch.bfloat16)
+    lib = L.lib()
+    out = {}
+    for tiled in ("1", "0"):
+        monkeypatch.setenv("HISEG_DW_DGRAD_TILE", tiled)
+        for acc in (0, 1):
+            gx = Act.from_nchw(prev.float(), torch.bfloat16)
+            L.check(lib.hiseg_dw_bwd_data(hdtype(torch.bfloat16), dya.ptr(), N, H, W, C, k, 2, w.data_ptr(), Ho, Wo,
+                                          gx.ptr(), acc, L.stream_ptr()), "dw_bwd_data")
+            out[tiled, acc] = gx.to_nchw().float()
+    x64 = torch.zeros(N, C, H, W, dtype=torch.float64, device=DEV, requires_grad=True)
+    y = F.conv2d(x64, w.double().reshape(C, 1, k, k), stride=2, padding=k // 2, groups=C)
+    y.backward(dy.double())
+    ref = x64.grad
+    for acc in (0, 1):
+        r = ref + (prev.double() if acc else 0)
+        t, p = out["1", acc].double(), out["0", acc].double()
+        scale = r.abs().max().item()
+        # bf16 output rounding: within one bf16 ulp of the f64 value, and the two kernels within one ulp of each other
+        assert ((t - r).abs() <= r.abs() * 2 ** -8 + 1e-6 * scale).all(), acc
+        assert ((t - p).abs() <= p.abs() * 2 ** -7 + 1e-6 * scale).all(), acc
