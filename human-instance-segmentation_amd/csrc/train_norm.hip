@@ -352,6 +352,63 @@ __global__ void __launch_bounds__(256) bn_finalize_par_kernel(const float* parti
   }
 }
 
+// The same merge as 16 channel lanes x 16 split rows per block (round 6): row r sums splits r, r + 16, ... of its
+// channel as (n, sum n mean, sum M2 + n mean^2) in double, four splits' loads in flight, no division in the loop
+// (bn_premerge_kernel's form); the 16 rows are added in a fixed order.  C / 16 blocks instead of C: the per-channel
+// kernel's 256-thread block and eight-level double Chan tree per channel cost ~7 us a call whatever S, on ~58 calls
+// of the distillation student's forward.  Within f32 rounding of the Chan merge (test_bn_finalize_n_matches_f64_merge).
+__global__ void __launch_bounds__(256) bn_finalize_rows_kernel(const float* partial, int S, int C, long long P,
+                                                               const float* gamma, const float* beta, float eps,
+                                                               float momentum, float* rm, float* rv, float* mean_o,
+                                                               float* invstd_o, float* scale, float* shift,
+                                                               long long rs) {
+  __shared__ double sn[16][16], sa[16][16], sb[16][16];
+  const int l = threadIdx.x & 15, r = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + l;
+  double n = 0, a = 0, b = 0;
+  if (c < C) {
+    int s = r;
+    for (; s + 48 < S; s += 64) {
+      float pn[4], pm[4], pq[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float* p = partial + (long long)(s + 16 * u) * rs;
+        pn[u] = p[c];
+        pm[u] = p[C + c];
+        pq[u] = p[2 * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const double ni = pn[u], mi = pm[u];
+        n += ni;
+        a = fma(ni, mi, a);
+        b += (double)pq[u] + ni * mi * mi;
+      }
+    }
+    for (; s < S; s += 16) {
+      const float* p = partial + (long long)s * rs;
+      const double ni = p[c], mi = p[C + c];
+      n += ni;
+      a = fma(ni, mi, a);
+      b += (double)p[2 * C + c] + ni * mi * mi;
+    }
+  }
+  sn[r][l] = n; sa[r][l] = a; sb[r][l] = b;
+  __syncthreads();
+  if (r != 0 || c >= C) return;
+  for (int q = 1; q < 16; ++q) { n += sn[q][l]; a += sa[q][l]; b += sb[q][l]; }
+  const double mu = n > 0 ? a / n : 0.0;
+  const double var = n > 0 ? fmax(b - a * mu, 0.0) / n : 0.0;
+  const double inv = 1.0 / sqrt(var + (double)eps);
+  const float g = gamma ? gamma[c] : 1.f, bb = beta ? beta[c] : 0.f;
+  mean_o[c] = (float)mu;
+  invstd_o[c] = (float)inv;
+  scale[c] = (float)(g * inv);
+  shift[c] = (float)(bb - mu * g * inv);
+  if (rm) rm[c] = (float)((1.0 - momentum) * rm[c] + momentum * mu);
+  if (rv) rv[c] = (float)((1.0 - momentum) * rv[c] + momentum * (P > 1 ? var * (double)P / (double)(P - 1) : var));
+}
+
 // Element-wise passes: block = CT chunk lanes x R pixel rows (as the reductions), blocks stride over pixel
 // rows; 32-bit pixel indices (P < 2^31, checked on the host), no per-element 64-bit division.
 template <typename T, int U = 1>
@@ -1159,6 +1216,25 @@ static int stat_splits(long long P) {
 }
 static dim3 fin_grid(int C) { return dim3((unsigned)C); }   // one block per channel
 
+// HISEG_BN_FIN (read per call): 1 bn_finalize_rows_kernel, 0 the per-channel Chan-tree kernel, 2 (default) the rows
+// kernel up to 256 splits (a row walks S / 16 of them; more take the per-channel kernel's one round of loads)
+static bool bn_fin_rows(int S) {
+  const char* e = getenv("HISEG_BN_FIN");
+  const int m = e ? atoi(e) : 2;
+  return m == 1 || (m == 2 && S <= 256);
+}
+
+static void bn_fin_launch(const float* partial, int S, int C, long long P, const float* gamma, const float* beta,
+                          float eps, float momentum, float* rm, float* rv, float* mean, float* invstd, float* scale,
+                          float* shift, hipStream_t stream, long long rs) {
+  if (bn_fin_rows(S))
+    hipLaunchKernelGGL(bn_finalize_rows_kernel, dim3((unsigned)((C + 15) / 16)), dim3(256), 0, stream, partial, S, C,
+                       P, gamma, beta, eps, momentum, rm, rv, mean, invstd, scale, shift, rs);
+  else
+    hipLaunchKernelGGL(bn_finalize_par_kernel, fin_grid(C), dim3(256), 0, stream, partial, S, C, P, gamma, beta, eps,
+                       momentum, rm, rv, mean, invstd, scale, shift, rs);
+}
+
 extern "C" int hiseg_bn_stats(int dtype, const void* z, long long P, int C, int cstride, int coff, float* partial,
                               hiseg_stream_t stream) {
   HISEG_REQUIRE(z && partial && P > 0 && C > 0 && cstride >= C, HISEG_ERR_BAD_ARG, "bn_stats: bad arguments");
@@ -1181,9 +1257,8 @@ extern "C" int hiseg_bn_finalize(const float* partial, int C, long long P, const
                                  float eps, float momentum, float* running_mean, float* running_var, float* mean,
                                  float* invstd, float* scale, float* shift, hiseg_stream_t stream) {
   HISEG_REQUIRE(partial && mean && invstd && scale && shift && C > 0, HISEG_ERR_BAD_ARG, "bn_finalize: null");
-  hipLaunchKernelGGL(bn_finalize_par_kernel, fin_grid(C), dim3(256), 0, (hipStream_t)stream, partial, stat_splits(P), C,
-                     P, gamma, beta, eps, momentum, running_mean, running_var, mean, invstd, scale, shift,
-                     3ll * C);
+  bn_fin_launch(partial, stat_splits(P), C, P, gamma, beta, eps, momentum, running_mean, running_var, mean, invstd, scale,
+                shift, (hipStream_t)stream, 3ll * C);
   return hiseg_check_launch("bn_finalize");
 }
 
@@ -1191,8 +1266,8 @@ extern "C" int hiseg_bn_finalize(const float* partial, int C, long long P, const
 int bn_finalize_splits(const float* partial, int S, int C, long long P, const float* gamma, const float* beta,
                        float eps, float momentum, float* running_mean, float* running_var, float* mean, float* invstd,
                        float* scale, float* shift, hipStream_t stream, long long rs = 0) {
-  hipLaunchKernelGGL(bn_finalize_par_kernel, fin_grid(C), dim3(256), 0, stream, partial, S, C, P, gamma, beta, eps,
-                     momentum, running_mean, running_var, mean, invstd, scale, shift, rs ? rs : 3ll * C);
+  bn_fin_launch(partial, S, C, P, gamma, beta, eps, momentum, running_mean, running_var, mean, invstd, scale, shift, stream,
+                rs ? rs : 3ll * C);
   return hiseg_check_launch("bn_finalize");
 }
 
