@@ -33,6 +33,7 @@ process groups cannot be captured (host-side reduction): keep such steps eager.
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, List, Optional
 
 import torch
@@ -170,6 +171,12 @@ class GraphedStep:
         return self.out
 
 
+def _branch_priority() -> str:
+    """HISEG_BRANCH_PRIO (read per call): "head" -- GraphedBranchStep replays its head and tail graphs on the
+    high-priority stream; "branch" -- the branch graph there instead of the side stream; unset: neither (A/B)."""
+    return os.environ.get("HISEG_BRANCH_PRIO", "")
+
+
 class GraphedBranchStep(GraphedStep):
     """GraphedStep for a step that opens with two independent branches: ``branch_fn`` on the side stream (the frozen
     distillation teacher's forward), ``head_fn`` on the caller's stream beside it (the student's forward), then
@@ -251,14 +258,29 @@ class GraphedBranchStep(GraphedStep):
             self.captures += 1
         gb, gh, gt = self.graphs
         self._sync_owners()   # on the caller's stream: before the head / tail graphs that read them
+        prio = _branch_priority()
+        if prio == "branch":   # the branch replayed on the high-priority stream instead of the side stream
+            side = role_stream("priority")
         side.wait_stream(main)   # the previous step's tail (or this step's handoff) is done with the branch buffers
         with torch.cuda.stream(side):
             gb.replay()
         self._ev.record(side)
-        gh.replay()
-        if not piped:
-            main.wait_event(self._ev)
-        gt.replay()
+        if prio == "head":
+            # the head and tail -- the step's critical path -- replayed on the high-priority stream, the branch
+            # filling what they leave (event-ordered with the caller's stream on both sides)
+            hp = role_stream("priority")
+            hp.wait_stream(main)
+            with torch.cuda.stream(hp):
+                gh.replay()
+                if not piped:
+                    hp.wait_event(self._ev)
+                gt.replay()
+            main.wait_stream(hp)
+        else:
+            gh.replay()
+            if not piped:
+                main.wait_event(self._ev)
+            gt.replay()
         o = self._opt()
         bump = getattr(o, "_bump", None)
         if bump:

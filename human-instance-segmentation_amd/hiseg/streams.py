@@ -16,7 +16,8 @@ normal-priority streams, each with a queue of its own whatever ran before:
 * ``aux``: GraphedStep's eager warm-up steps and its capture stream (never concurrent with anything);
 * ``comm``: GradBucketSync's all-reduces (world > 1 only).
 
-plus ``head``, the high-priority stream of the inference head (its own priority level, so its own queue).  The
+plus ``head``, the high-priority stream of the inference head (its own priority level, so its own queue; also the
+``priority`` role: GraphedBranchStep's head and tail with HISEG_BRANCH_PRIO=head, or its branch with =branch).  The
 roles map onto those streams (``ROLE``); a stream is created on the first request for it, untouched (bound to a queue
 on its first real command, so a process that never uses one never binds it)."""
 from __future__ import annotations
@@ -26,7 +27,7 @@ from typing import Dict, Optional
 import torch
 
 ROLE = {"unet": "side", "teacher": "side", "warm": "aux", "capture": "aux", "comm": "comm", "head": "head",
-        "head_normal": "head_normal"}
+        "head_normal": "head_normal", "priority": "head"}
 _PRIORITY = {"head": -1}
 _by_device: Dict[int, Dict[str, torch.cuda.Stream]] = {}
 
