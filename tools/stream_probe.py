@@ -13,9 +13,9 @@ import bench  # noqa: E402
 
 def main():
     k = int(sys.argv[1])
-    if "--prio" in sys.argv:
-        from hiseg.distill import DistillationUNetWrapper
-        DistillationUNetWrapper._teacher_priority = -1
+    if "--prio" in sys.argv:   # the teacher branch on the high-priority stream (its own queue and priority level)
+        from hiseg import streams
+        streams.ROLE["teacher"] = "head"
     dev = torch.device("cuda", 0)
     keep = []
     if "--hiprio-first" in sys.argv:   # as the C2 inference leg's head stream
