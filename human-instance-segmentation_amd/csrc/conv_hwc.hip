@@ -148,8 +148,8 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
     else if constexpr (R3) return (sl % 3) * HB;
     else return (sl & 1) * HB;
   };
-  auto halo_dma = [&](int p, int sl, int boff) __attribute__((always_inline)) {
-    if (16 * (NW * p + w) >= NHR) return;   // a piece wholly past the halo (wave-uniform): nothing to load
+  // source byte offset of halo piece p's lane at slice sl (src A: sl < Ca / 32; src B: the concatenated rest)
+  auto piece_off = [&](int p, int sl) __attribute__((always_inline)) -> unsigned {
     int ln = lane;
     asm volatile("" : "+v"(ln));
     const int hr = 16 * (NW * p + w) + (ln >> 2);
@@ -159,14 +159,25 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
     const int chunk = (ln & 3) ^ (((hx >> 2) & 1) << 1);
     const bool fb = 32 * sl >= d.Ca;
     const int cs = fb ? d.b_cstride : d.a_cstride, coff = fb ? d.b_coff + 32 * sl - d.Ca : d.a_coff + 32 * sl;
-    unsigned off;
     if constexpr (UP) {
       const int ush = fb ? 0 : 1;
-      off = ok ? (unsigned)((((n * (d.H >> ush) + (iy >> ush)) * (d.W >> ush) + (ix >> ush)) * cs + coff + chunk * 8) * 2)
-               : OOB;
+      return ok ? (unsigned)((((n * (d.H >> ush) + (iy >> ush)) * (d.W >> ush) + (ix >> ush)) * cs + coff + chunk * 8) * 2)
+                : OOB;
     } else {
-      off = ok ? (unsigned)((((n * d.H + iy) * d.W + ix) * cs + coff + chunk * 8) * 2) : OOB;
+      return ok ? (unsigned)((((n * d.H + iy) * d.W + ix) * cs + coff + chunk * 8) * 2) : OOB;
     }
+  };
+  // Each piece's src-A offset at slice 0, computed once: a src-A slice adds 64 B (an out-of-tile lane keeps OOB +
+  // 64 sl >= 2^31 > num_records).  The per-slice address arithmetic (a division by the halo width, three 32-bit
+  // multiplies, the bounds tests: ~30 instructions per piece, issued between two MFMA rows) is gone from the K loop
+  // for every src-A slice; src-B slices (the decoder's concatenated skip) keep it.
+  unsigned pofA[PPW];
+#pragma unroll
+  for (int p = 0; p < PPW; ++p) pofA[p] = 16 * (NW * p + w) < NHR ? piece_off(p, 0) : OOB;
+  auto halo_dma = [&](int p, int sl, int boff) __attribute__((always_inline)) {
+    if (16 * (NW * p + w) >= NHR) return;   // a piece wholly past the halo (wave-uniform): nothing to load
+    const bool fb = 32 * sl >= d.Ca;
+    const unsigned off = fb ? piece_off(p, sl) : pofA[p] + 64u * (unsigned)sl;
     hc_dma16(fb ? rB : rA, lds_base + (unsigned)(boff + 1024 * (NW * p + w)), off);
   };
   const char* lds_c = reinterpret_cast<const char*>(smem);
