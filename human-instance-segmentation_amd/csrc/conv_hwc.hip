@@ -464,14 +464,26 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) conv_hwc_kernel(Conv
 #pragma unroll
     for (int e = 0; e < 8; ++e) sk[e] = s1[e] = s2[e] = 0.f;
   }
-#pragma unroll BR ? NST : 4
+  // All NST chunks leave LDS first (the accumulators are dead, their registers free), then go out by buffer stores
+  // whose out-of-tile lanes carry an offset past num_records (dropped by the hardware): no LDS latency per store, no
+  // branch, 32-bit offsets (conv_hwc_applies bounds the output span).
+  uint4 sv[NST];
+#pragma unroll
+  for (int k = 0; k < NST; ++k) {
+    const int idx = t + NW * 64 * k;
+    const int r = idx / CPR, c = idx % CPR;
+    sv[k] = *reinterpret_cast<const uint4*>(tile + r * EROWB + ((c ^ (r & SWM)) << 4));
+  }
+  const __amdgpu_buffer_rsrc_t rO = __builtin_amdgcn_make_buffer_rsrc(d.out, (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
   for (int k = 0; k < NST; ++k) {
     const int idx = t + NW * 64 * k;
     const int r = idx / CPR, c = idx % CPR;
     const int px = px_of(r), co = co0 + 8 * c;
-    const uint4 v = *reinterpret_cast<const uint4*>(tile + r * EROWB + ((c ^ (r & SWM)) << 4));
-    if (px >= 0 && co < d.Cout)
-      *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(d.out) + (long long)px * d.o_cstride + d.o_coff + co) = v;
+    const uint4 v = sv[k];
+    __builtin_amdgcn_raw_buffer_store_b128(
+        __builtin_bit_cast(hc_u4, v), rO,
+        (px >= 0 && co < d.Cout) ? (unsigned)((px * d.o_cstride + d.o_coff + co) * 2) : OOB, 0, 0);
     if constexpr (BR) {
       if (px >= 0 && co < d.Cout) {
         const uint4 zq = zpre[BR ? k : 0];
@@ -620,7 +632,10 @@ static bool conv_hwc_applies(const ConvArgs& a, int variant) {
   const long long span_b = d.Cb ? (long long)d.N * d.H * d.W * d.b_cstride * 2 : 0;
   const long long span_w = (long long)d.Cout_pad * d.K_pad * 2;
   const long long span_r = d.residual ? (long long)a.M * d.r_cstride * 2 : 0;
-  if (span_a >= 0x7fffffffll || span_b >= 0x7fffffffll || span_w >= 0x7fffffffll || span_r >= 0x7fffffffll) return false;
+  const long long span_o = (long long)a.M * d.o_cstride * 2;   // the epilogue's 32-bit buffer-store offsets
+  if (span_a >= 0x7fffffffll || span_b >= 0x7fffffffll || span_w >= 0x7fffffffll || span_r >= 0x7fffffffll ||
+      span_o >= 0x7fffffffll)
+    return false;
   if ((long long)d.N * d.H * d.W >= (1ll << 29)) return false;
   // upsampled src A: the smp decoder conv1 form only (ReLU, or no activation when the conv feeds a train-mode BN)
   if (d.a_up == 2 && (d.residual || d.act != (d.stats_partial ? HISEG_ACT_NONE : HISEG_ACT_RELU))) return false;
