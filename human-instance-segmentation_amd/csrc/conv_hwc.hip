@@ -26,6 +26,10 @@
 
 namespace hiseg {
 
+#ifndef HISEG_CONV_HWC_MT
+#define HISEG_CONV_HWC_MT 3   // work items per multi-tile workgroup (variants 109 / 102)
+#endif
+
 typedef unsigned hc_u4 __attribute__((ext_vector_type(4)));
 typedef unsigned hc_u2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) void hc_lds_void;
@@ -595,6 +599,332 @@ static int launch_hwc(const ConvArgs& a, hipStream_t s) {
   return hiseg_check_launch("conv_hwc");
 }
 
+// MT (variants 109 / 102, round 6): multi-tile workgroups.  conv_hwc_kernel's wave tile, slice loop and per-element
+// accumulation order (so the outputs are bit-identical to it), but each workgroup walks MT work items (pixel tile x
+// Cout tile) -- item wg, wg + G, wg + 2G, ... (G = the grid: at any moment the concurrent workgroups hold adjacent
+// items, as in the one-tile grid) -- and the tile boundary is pipelined: during the last slice of a tile (odd, buffer
+// 1) the NEXT tile's slice-0 halo is LDS-DMA'd into buffer 0 and its first weight block loaded, so the next tile
+// starts without a prologue.  The epilogue therefore must not touch buffer 0: it runs in two halves of NPX / 2 rows
+// through a 32-KiB region E at [HB, HB + 32K) (over buffer 1, free after the last slice; TWB 1 takes 56 KiB of LDS,
+// TWB 2 the 80 KiB of its two buffers -- two workgroups per CU either way).  No fused statistics / residual prefetch / ring of three.
+template <int ACT, bool RES, int TWB, int MT>
+__global__ void __launch_bounds__(256, 2) conv_hwc_mt_kernel(ConvArgs a) {
+  constexpr int NW = 4, NCG = NW / TWB;
+  constexpr int BCO = 32 * NCG, TM = 2, NR = 16;
+  constexpr int TW = 16 * TWB, HWD = TW + 2;
+  constexpr int NHR = 18 * HWD;
+  constexpr int PPW = ((NHR + 15) / 16 + NW - 1) / NW;
+  constexpr int PH = (PPW + 1) / 2;
+  constexpr int HB = PPW * NW * 1024;
+  constexpr int NPX = 256 * TWB, HALF = NPX / 2;
+  constexpr int EOFF = HB;
+  static_assert(MT >= 2 && (TWB == 1 || TWB == 2), "multi-tile configuration");
+  extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+  const hiseg_conv2d_desc& d = a.d;
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wc = w % NCG, pb = w / NCG;
+
+  const int nco = d.Cout_pad / BCO;
+  const int ntx = (d.W + TW - 1) / TW, nty = (d.H + 15) >> 4;
+  const int total = d.N * nty * ntx * nco;   // work items
+  const int G = gridDim.x;
+  const int orig = blockIdx.x;
+  const int q8 = G >> 3, r8 = G & 7, xcd = orig & 7, loc = orig >> 3;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+
+  const unsigned OOB = 0x80000000u;
+  const int nsl = a.Cin >> 5;
+  const int ncb = a.Cin >> 6;
+  const __amdgpu_buffer_rsrc_t rF = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(d.weight_frag), (short)0, d.Cout_pad * 9 * a.Cin * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(d.srcA), (short)0, d.N * d.H * d.W * d.a_cstride * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(d.Cb ? d.srcB : d.srcA), (short)0, d.Cb ? d.N * d.H * d.W * d.b_cstride * 2 : 0, 0x00020000);
+  const unsigned a_ct_step = (unsigned)ncb * 18u * 1024u;
+
+  // tile geometry of work item i (Cout tiles fastest, as conv_hwc_kernel's remap)
+  struct Geo { int co0, n, y0, x0; unsigned a_ct; };
+  auto geo = [&](int i) __attribute__((always_inline)) -> Geo {
+    Geo g;
+    g.co0 = (i % nco) * BCO;
+    int tl = i / nco;
+    g.x0 = (tl % ntx) * TW;
+    tl /= ntx;
+    g.y0 = (tl % nty) * 16;
+    g.n = tl / nty;
+    g.a_ct = (unsigned)((g.co0 + wc * 32) >> 4) * (unsigned)ncb * 18u * 1024u;
+    return g;
+  };
+  auto load_blk = [&](hc_u4 (&af)[3][TM], unsigned a_ct, int sl, int kx) __attribute__((always_inline)) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const unsigned a_lane = a_ct + (unsigned)ln * 16u;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const unsigned so = __builtin_amdgcn_readfirstlane(
+          (((unsigned)(sl >> 1) * 9u + (unsigned)(ky * 3 + kx)) * 2u + (unsigned)(sl & 1)) * 1024u);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[ky][i] = __builtin_amdgcn_raw_buffer_load_b128(rF, a_lane + (unsigned)i * a_ct_step, so, 0);
+    }
+  };
+  auto piece_off = [&](const Geo& g, int p, int sl) __attribute__((always_inline)) -> unsigned {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int hr = 16 * (NW * p + w) + (ln >> 2);
+    const int hy = hr / HWD, hx = hr - HWD * hy;
+    const int iy = g.y0 + hy - 1, ix = g.x0 + hx - 1;
+    const bool ok = hr < NHR && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+    const int chunk = (ln & 3) ^ (((hx >> 2) & 1) << 1);
+    const bool fb = 32 * sl >= d.Ca;
+    const int cs = fb ? d.b_cstride : d.a_cstride, coff = fb ? d.b_coff + 32 * sl - d.Ca : d.a_coff + 32 * sl;
+    return ok ? (unsigned)((((g.n * d.H + iy) * d.W + ix) * cs + coff + chunk * 8) * 2) : OOB;
+  };
+  const unsigned lds_base = (unsigned)(uintptr_t)(hc_lds_void*)smem;
+  auto hbuf = [&](int sl) __attribute__((always_inline)) -> int { return (sl & 1) * HB; };
+  unsigned pofA[PPW];
+  auto set_pof = [&](const Geo& g) __attribute__((always_inline)) {
+#pragma unroll
+    for (int p = 0; p < PPW; ++p) pofA[p] = 16 * (NW * p + w) < NHR ? piece_off(g, p, 0) : OOB;
+  };
+  auto halo_dma = [&](const Geo& g, int p, int sl, int boff) __attribute__((always_inline)) {
+    if (16 * (NW * p + w) >= NHR) return;
+    const bool fb = 32 * sl >= d.Ca;
+    const unsigned off = fb ? piece_off(g, p, sl) : pofA[p] + 64u * (unsigned)sl;
+    hc_dma16(fb ? rB : rA, lds_base + (unsigned)(boff + 1024 * (NW * p + w)), off);
+  };
+  // the next tile's slice-0 pieces (its offsets computed here, once per tile)
+  auto halo_dma0 = [&](const Geo& g, int p) __attribute__((always_inline)) {
+    if (16 * (NW * p + w) >= NHR) return;
+    hc_dma16(rA, lds_base + (unsigned)(1024 * (NW * p + w)), piece_off(g, p, 0));
+  };
+  const char* lds_c = reinterpret_cast<const char*>(smem);
+  auto rdB = [&](int ln, int boff, int kx, int r) __attribute__((always_inline)) -> hc_u4 {
+    const int hx = (ln & 15) + kx + 16 * pb;
+    return *reinterpret_cast<const hc_u4*>(lds_c + boff + (r * HWD + hx) * 64 +
+                                           (((ln >> 4) ^ (((hx >> 2) & 1) << 1)) << 4));
+  };
+
+  floatx4 acc[TM][NR];
+  constexpr int EROWB = BCO * 2;
+  constexpr int CPR = BCO / 8;
+  constexpr int RPI = 64 / CPR;
+  constexpr int SWM = CPR - 1;
+  constexpr int NRI = NPX / (RPI * NW);
+  static_assert(HALF * EROWB == 32 * 1024 && EOFF + HALF * EROWB <= 80 * 1024 && 2 * HB <= 80 * 1024 && NRI % 2 == 0,
+                "epilogue halves");
+  const __amdgpu_buffer_rsrc_t rR = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(RES ? d.residual : d.out), (short)0, RES ? a.M * d.r_cstride * 2 : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rO = __builtin_amdgcn_make_buffer_rsrc(d.out, (short)0, 0x7fffffff, 0x00020000);
+  char* E = reinterpret_cast<char*>(smem) + EOFF;
+
+  int item = wg;
+  Geo g = geo(item);
+  set_pof(g);
+  hc_u4 af[3][TM], an[3][TM];
+#pragma unroll
+  for (int p = 0; p < PPW; ++p) halo_dma(g, p, 0, hbuf(0));
+  load_blk(af, g.a_ct, 0, 0);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  __syncthreads();
+
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // one loop over (tile, slice): the epilogue runs after each tile's last slice (a single loop level keeps the
+  // compiler from hoisting per-slice scalars out of an outer tile loop -- SGPR spills)
+  int it = 0, sl = 0;
+  int nitem = item + G;
+  bool has_next = 1 < MT && nitem < total;   // workgroup-uniform
+  for (;;) {
+
+    auto block = [&](int sl, auto kxc) __attribute__((always_inline)) {
+      constexpr int KX = decltype(kxc)::value;
+      const int buf = hbuf(sl);
+      const bool more = sl + 1 < nsl;
+      if (KX < 2 || more) load_blk(an, g.a_ct, KX < 2 ? sl : sl + 1, KX < 2 ? KX + 1 : 0);
+      auto pieces = [&]() __attribute__((always_inline)) {
+        if constexpr (KX < 2) {
+          if (more) {
+#pragma unroll
+            for (int p = KX * PH; p < (KX == 0 ? PH : PPW); ++p) halo_dma(g, p, sl + 1, hbuf(sl + 1));
+          } else if (has_next) {   // last slice (buffer 1): the next tile's slice 0 into buffer 0
+            const Geo gn = geo(nitem);
+#pragma unroll
+            for (int p = KX * PH; p < (KX == 0 ? PH : PPW); ++p) halo_dma0(gn, p);
+          }
+        }
+      };
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      hc_u4 bq[3];
+      bq[0] = rdB(ln, buf, KX, 0);
+      bq[1] = rdB(ln, buf, KX, 1);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int r = 0; r < NR + 2; ++r) {
+        if (r == 3) {
+          __builtin_amdgcn_s_setprio(0);
+          pieces();
+          __builtin_amdgcn_s_setprio(1);
+        }
+        if (r + 2 < NR + 2) bq[(r + 2) % 3] = rdB(ln, buf, KX, r + 2);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const int j = r - ky;
+          if (j >= 0 && j < NR) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[ky][i]),
+                                                                 __builtin_bit_cast(bf16x8_t, bq[r % 3]), acc[i][j], 0,
+                                                                 0, 0);
+          }
+        }
+      }
+      __builtin_amdgcn_s_setprio(0);
+      if constexpr (KX == 2) {
+        if (more) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // halo pieces (the next weights may fly)
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (last slice: the next tile's slice-0 pieces)
+        __syncthreads();
+      }
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[ky][i] = an[ky][i];
+    };
+    using K0 = std::integral_constant<int, 0>;
+    using K1 = std::integral_constant<int, 1>;
+    using K2 = std::integral_constant<int, 2>;
+    block(sl, K0{});
+    block(sl, K1{});
+    block(sl, K2{});
+    if (++sl < nsl) continue;
+
+    // ---- epilogue in two halves through E (buffer 0 holds the next tile's slice-0 halo).  Its lane-derived addresses
+    // come from an opaque copy of the lane id, so the compiler cannot hoist them out of the tile loop (live registers)
+    int eln = lane;
+    asm volatile("" : "+v"(eln));
+    const int et = w * 64 + eln;
+    auto px_of = [&](int r) __attribute__((always_inline)) -> int {
+      const int y = g.y0 + r / TW, x = g.x0 + r % TW;
+      return (y < d.Ho && x < d.Wo) ? (g.n * d.Ho + y) * d.Wo + x : -1;
+    };
+    floatx4 sc[TM], sh[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int cl = wc * 32 + i * 16 + (eln >> 4) * 4;
+      const int cc = g.co0 + cl < d.Cout ? g.co0 + cl : 0;
+      sc[i] = *reinterpret_cast<const floatx4*>(d.scale + cc);
+      sh[i] = *reinterpret_cast<const floatx4*>(d.shift + cc);
+    }
+    constexpr int NST = NPX * CPR / (NW * 64);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if constexpr (RES) {
+#pragma unroll
+        for (int k = h * NRI / 2; k < (h + 1) * NRI / 2; ++k) {
+          int ln = lane;
+          asm volatile("" : "+v"(ln));
+          const int c = ln % CPR;
+          const int r = RPI * (w + NW * k) + ln / CPR;
+          const int px = px_of(r);
+          const unsigned off =
+              px >= 0 ? (unsigned)((px * d.r_cstride + d.r_coff + g.co0 + ((c ^ (r & SWM)) * 8)) * 2) : OOB;
+          hc_dma16(rR, lds_base + (unsigned)(EOFF + (RPI * (w + NW * k) - h * HALF) * EROWB), off);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = h * NR / 2; j < (h + 1) * NR / 2; ++j) {
+          const int cl = wc * 32 + i * 16 + (eln >> 4) * 4;
+          const int r = j * TW + 16 * pb + (eln & 15);
+          char* q = E + (r - h * HALF) * EROWB + ((((cl >> 3) ^ (r & SWM)) << 4) | ((cl & 4) << 1));
+          const floatx4 ac = acc[i][j];
+          float v[4];
+          uint2 rv = make_uint2(0u, 0u);
+          if constexpr (RES) rv = *reinterpret_cast<const uint2*>(q);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = ac[e] * sc[i][e] + sh[i][e];
+            if constexpr (RES) v[e] += Quad<bf16_t>::get(rv, e);
+            if constexpr (ACT == HISEG_ACT_RELU) v[e] = v[e] > 0.f ? v[e] : 0.f;
+          }
+          uint2 o;
+          o.x = f2bf2(v[0], v[1]);
+          o.y = f2bf2(v[2], v[3]);
+          *reinterpret_cast<uint2*>(q) = o;
+        }
+      __syncthreads();
+      uint4 sv[NST / 2];
+#pragma unroll
+      for (int k = 0; k < NST / 2; ++k) {
+        const int idx = et + NW * 64 * (k + h * NST / 2);
+        const int r = idx / CPR, c = idx % CPR;
+        sv[k] = *reinterpret_cast<const uint4*>(E + (r - h * HALF) * EROWB + ((c ^ (r & SWM)) << 4));
+      }
+#pragma unroll
+      for (int k = 0; k < NST / 2; ++k) {
+        const int idx = et + NW * 64 * (k + h * NST / 2);
+        const int r = idx / CPR, c = idx % CPR;
+        const int px = px_of(r), co = g.co0 + 8 * c;
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(hc_u4, sv[k]), rO,
+            (px >= 0 && co < d.Cout) ? (unsigned)((px * d.o_cstride + d.o_coff + co) * 2) : OOB, 0, 0);
+      }
+      // the next tile's first weight block, in flight during the second half (its registers were free)
+      if (h == 0 && has_next) load_blk(af, geo(nitem).a_ct, 0, 0);
+      __syncthreads();   // E free again (next half; the next tile's slice-1 halo lands over it)
+    }
+    if (!has_next) break;
+    item = nitem;
+    g = geo(item);
+    set_pof(g);
+    sl = 0;
+    ++it;
+    nitem = item + G;
+    has_next = it + 1 < MT && nitem < total;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < NR; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+template <int ACT, bool RES, int TWB, int MT>
+static int launch_hwc_mt(const ConvArgs& a, hipStream_t s) {
+  const hiseg_conv2d_desc& d = a.d;
+  constexpr int BCO = 128 / TWB, TW = 16 * TWB;
+  constexpr int PPW = ((18 * (TW + 2) + 15) / 16 + 3) / 4;
+  constexpr size_t hb = (size_t)PPW * 4 * 1024;   // one halo buffer; E = [hb, hb + 32K) over buffer 1
+  constexpr size_t lds = 2 * hb > hb + 32 * 1024 ? 2 * hb : hb + 32 * 1024;
+  const long long items = (long long)d.N * ((d.H + 15) / 16) * ((d.W + TW - 1) / TW) * (d.Cout_pad / BCO);
+  const int grid = (int)((items + MT - 1) / MT);
+  auto kern = conv_hwc_mt_kernel<ACT, RES, TWB, MT>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, s, a);
+  return hiseg_check_launch("conv_hwc_mt");
+}
+
+template <int TWB, int MT>
+static int launch_hwc_mt_act(const ConvArgs& a, hipStream_t s) {
+  const bool res = a.d.residual != nullptr, relu = a.d.act == HISEG_ACT_RELU;
+  return res ? (relu ? launch_hwc_mt<HISEG_ACT_RELU, true, TWB, MT>(a, s) : launch_hwc_mt<HISEG_ACT_NONE, true, TWB, MT>(a, s))
+             : (relu ? launch_hwc_mt<HISEG_ACT_RELU, false, TWB, MT>(a, s)
+                     : launch_hwc_mt<HISEG_ACT_NONE, false, TWB, MT>(a, s));
+}
+
 template <int NW, bool RP = false, int TWB = 1, bool R3 = false>
 static int launch_hwc_nw(const ConvArgs& a, hipStream_t s) {
   const hiseg_conv2d_desc& d = a.d;
@@ -611,7 +941,9 @@ static int launch_hwc_nw(const ConvArgs& a, hipStream_t s) {
 // halo; with d.stats_partial the fused-statistics form: variant 104 / 107, no activation, no residual).
 static bool conv_hwc_applies(const ConvArgs& a, int variant) {
   const hiseg_conv2d_desc& d = a.d;
-  if ((variant < 104 || variant > 108) || d.weight_frag == nullptr) return false;
+  if (((variant < 104 || variant > 109) && variant != 102) || d.weight_frag == nullptr) return false;
+  // 109 / 102: the multi-tile workgroups (no upsampled source, no fused statistics / BatchNorm-backward reduction)
+  if ((variant == 109 || variant == 102) && (d.a_up != 1 || d.stats_partial || d.bnb_partial)) return false;
   if (d.dtype != HISEG_BF16 || d.out_dtype != HISEG_BF16) return false;
   if ((d.a_up != 1 && d.a_up != 2) || d.in_scale != nullptr || d.convT || d.mul != nullptr || d.out2 != nullptr)
     return false;
@@ -621,7 +953,7 @@ static bool conv_hwc_applies(const ConvArgs& a, int variant) {
     return false;
   if ((d.a_cstride | d.a_coff) & 7) return false;
   if (d.Cb && (d.srcB == nullptr || ((d.b_cstride | d.b_coff) & 7))) return false;
-  if ((d.Cout & (variant == 105 ? 255 : variant == 107 ? 63 : 127)) || d.Cout_pad != d.Cout ||
+  if ((d.Cout & (variant == 105 ? 255 : (variant == 107 || variant == 102) ? 63 : 127)) || d.Cout_pad != d.Cout ||
       ((d.o_cstride | d.o_coff) & 7) ||
       (d.residual && ((d.r_cstride | d.r_coff) & 7)))
     return false;
@@ -708,7 +1040,9 @@ int conv_hwc_try(const ConvArgs& a, hipStream_t s, int variant) {
                       : launch_hwc<HISEG_ACT_NONE, false, 4, false, 0, false, true>(a, s);
     return r < 0 ? r : 1;
   }
-  const int r = variant == 107 ? launch_hwc_nw<4, false, 2>(a, s)
+  const int r = variant == 109 ? launch_hwc_mt_act<1, HISEG_CONV_HWC_MT>(a, s)
+              : variant == 102 ? launch_hwc_mt_act<2, HISEG_CONV_HWC_MT>(a, s)
+              : variant == 107 ? launch_hwc_nw<4, false, 2>(a, s)
               : variant == 108 ? launch_hwc_nw<4, false, 1, true>(a, s)
               : variant == 105 ? launch_hwc_nw<8>(a, s)
               : variant == 106 ? launch_hwc_nw<4, true>(a, s)

@@ -533,10 +533,21 @@ static bool hwc_r3_mode() {
   return !(e && atoi(e) == 0);
 }
 
+// HISEG_CONV_HWC_MTW=0|1 (read per call; A/B timing): the multi-tile conv_hwc forms (109 for 128-multiple Cout, 102 for
+// the 64-Cout layers) instead of 108 / 107
+#ifndef HISEG_CONV_HWC_MT_DEFAULT
+#define HISEG_CONV_HWC_MT_DEFAULT(bco) false
+#endif
+static bool hwc_mt_mode(int bco) {
+  const char* e = getenv("HISEG_CONV_HWC_MTW");
+  if (e) return atoi(e) != 0;
+  return HISEG_CONV_HWC_MT_DEFAULT(bco);
+}
+
 static bool release_variant(int v) {
   return v == -1 || v == 0 || (v >= 1 && v <= 8) || v == 50 || v == 51 || v == 52 || v == 54 || v == 58 ||
          (v >= 60 && v <= 69) || v == 70 || v == 71 || v == 72 || v == 74 || v == 80 || v == 82 || v == 84 || v == 86 ||
-         v == 88 || v == 89 || v == 90 || (v >= 92 && v <= 101) || v == 103 || (v >= 104 && v <= 108);
+         v == 88 || v == 89 || v == 90 || (v >= 92 && v <= 101) || v == 103 || v == 102 || (v >= 104 && v <= 109);
 }
 
 // Workspace bytes the automatic choice uses for this layer (split-K generic kernel), 0 when it needs none.
@@ -711,7 +722,7 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
   } else if ((variant >= 92 && variant <= 97) || variant == 100 || variant == 101 || (variant >= 110 && variant < 142)) {
     const int r = conv_hwr_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
-  } else if ((variant >= 104 && variant <= 108) || (variant >= 150 && variant < 4300)) {
+  } else if (variant == 102 || (variant >= 104 && variant <= 109) || (variant >= 150 && variant < 4300)) {
     const int r = conv_hwc_try(a, s, variant);
     if (r != 0) return r < 0 ? r : HISEG_OK;
   } else if (variant == 103) {
@@ -780,6 +791,12 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
     // Round 6: variant 108, the same kernel with a ring of three halo buffers (slice sl + 2's halo in flight during
     // slice sl; 72 KiB of LDS, two workgroups per CU): bit-identical, 256->256 @64x48 x256 ROIs 0.709 -> 0.701 ms,
     // 128->128 @128x96 0.829 -> 0.814, 128->256 0.364 -> 0.351 (tools/conv_bench.py, profiles/r6_conv_hwc_r3.txt)
+    // Round 6: variants 109 / 102, multi-tile workgroups (conv_hwc_mt_kernel: the next tile's first halo slice lands
+    // during the last slice, two-half epilogue; bit-identical; HISEG_CONV_HWC_MTW=0|1 overrides the default)
+    if (v == 0 && !four_waves && halo && d->weight_frag != nullptr && d->Cout % 128 == 0 && hwc_mt_mode(128)) {
+      const int r = conv_hwc_try(a, s, 109);
+      if (r != 0) return r < 0 ? r : HISEG_OK;
+    }
     if (v == 0 && !four_waves && halo && d->weight_frag != nullptr && d->Cout % 128 == 0) {
       const int r = conv_hwc_try(a, s, hwc_r3_mode() ? 108 : 104);
       if (r != 0) return r < 0 ? r : HISEG_OK;
@@ -790,6 +807,11 @@ static int conv2d_impl(const hiseg_conv2d_desc* d, hiseg_stream_t stream, int va
     }
     // 64-multiple Cout (the EnhancedUNet's 64-channel layers, the smp decoder's 64-channel block): conv_hwc on 64-Cout
     // x 16 x 32-pixel tiles (variant 107, round 5), else conv_hwr's (variant 100)
+    if (v == 0 && !four_waves && halo && d->weight_frag != nullptr && d->Cout % 64 == 0 && hwc64_mode() &&
+        hwc_mt_mode(64)) {
+      const int r = conv_hwc_try(a, s, 102);
+      if (r != 0) return r < 0 ? r : HISEG_OK;
+    }
     if (v == 0 && !four_waves && halo && d->weight_frag != nullptr && d->Cout % 64 == 0 && hwc64_mode()) {
       const int r = conv_hwc_try(a, s, 107);
       if (r != 0) return r < 0 ? r : HISEG_OK;

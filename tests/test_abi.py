@@ -88,7 +88,7 @@ def test_release_library_refuses_diagnostic_conv_variants():
         d.weight, d.Cout, d.Cout_pad, d.K_pad = fake, 256, 256, 9 * 256
         d.scale, d.shift, d.act = fake, fake, 0
         d.out, d.o_cstride, d.o_coff = fake, 256, 0
-    for v in (9, 10, 18, 19, 20, 30, 40, 41, 44, 59, 73, 75, 76, 77, 79, 102, -5):
+    for v in (9, 10, 18, 19, 20, 30, 40, 41, 44, 59, 73, 75, 76, 77, 79, 142, -5):
         st = L.lib().hiseg_conv2d_fwd_variant(ctypes.byref(d), v, None)
         assert st == -1, v   # HISEG_ERR_BAD_ARG
         assert b"not a release variant" in L.lib().hiseg_last_error_string(), v

@@ -1180,7 +1180,9 @@ def test_conv_hwc_bit_identical_to_hwr(shape):
     conv_hwr's per-element accumulation order (channel-major slices, kx-major / ky-inner taps, one 32-channel MFMA per
     (slice, tap)) -- equal to variant 97 bit for bit: ragged pixel tiles, residual / ReLU / none, two sources, Cout
     128 / 256 / 384; the automatic choice takes 108 (round 6: 104 with a ring of three halo buffers) for 128-multiple
-    Cout.  Outputs NaN-prefilled."""
+    Cout; 109 (round 6): multi-tile workgroups, each walking HISEG_CONV_HWC_MT work items with the next tile's first halo
+    slice DMA'd during the last slice and a two-half epilogue (ragged item counts: the last workgroups take fewer).
+    Outputs NaN-prefilled."""
     from hiseg import ops
     N, Ca, Cb, Cout, H, W, res, relu = shape
     dt = torch.bfloat16
@@ -1193,7 +1195,7 @@ def test_conv_hwc_bit_identical_to_hwr(shape):
     assert p.weight_frag is not None
     R = ops.Act.from_nchw(torch.randn(N, Cout, H, W, device=DEV, generator=g), dt) if res else None
     outs = {}
-    vs = (97, 104, 106, 108, 0) + ((105,) if Cout % 256 == 0 else ())
+    vs = (97, 104, 106, 108, 109, 0) + ((105,) if Cout % 256 == 0 else ())
     for v in vs:
         o = ops.Act.new(N, H, W, Cout, dt, torch.device(DEV))
         o.t.fill_(float("nan"))
@@ -1224,13 +1226,14 @@ def test_conv_hwc64_bit_identical_to_hwr(shape):
     assert p.weight_frag is not None
     R = ops.Act.from_nchw(torch.randn(N, Cout, H, W, device=DEV, generator=g), dt) if res else None
     outs = {}
-    for v in (100, 107, 0):
+    for v in (100, 107, 102, 0):
         o = ops.Act.new(N, H, W, Cout, dt, torch.device(DEV))
         o.t.fill_(float("nan"))
         outs[v] = ops.conv2d(p, xa, xb, out=o, residual=R, variant=v).t.clone()
     torch.cuda.synchronize()
     assert torch.isfinite(outs[100].float()).all()
     assert torch.equal(outs[107], outs[100]) and torch.equal(outs[0], outs[100])
+    assert torch.equal(outs[102], outs[100])   # (round 6: variant 102, the multi-tile form of 107)
 
 
 @pytest.mark.parametrize("shape", [(2, 128, 64, 64, 36, 40), (1, 64, 64, 64, 18, 34)])
